@@ -1,0 +1,94 @@
+/* yolomi — C-ABI of the MI355X-native YOLO11 inference path (gfx950 HIP kernels).
+ *
+ * The reference has no FFI: its hot path is pure Python delegating to Ultralytics
+ * (/root/reference/core/model.py:118-133 `YOLO11Model.predict` → `self.model.predict(source, **kwargs)`;
+ * /root/reference/core/model.py:253-291 `benchmark`).  This header is the boundary that replaces the
+ * Ultralytics engine + ATen/torchvision kernels under that call: the Python facade
+ * (`yolo-infer_amd/core/model.py`) binds it with ctypes; a C/C++ host can link it directly.
+ *
+ * Conventions: every function returns 0 (YM_OK) or a negative YM_E* code and never throws; the message of the
+ * last failure on the calling thread is `ym_last_error()`.  The library owns weights, workspace and captured
+ * graphs; the caller owns input/output device buffers.  One context per device; a context is not re-entrant;
+ * distinct contexts may be used concurrently from different threads or processes.
+ */
+#ifndef YOLOMI_H
+#define YOLOMI_H
+#include <stddef.h>
+#include <stdint.h>
+
+#ifdef __cplusplus
+extern "C" {
+#endif
+
+#define YM_OK 0
+#define YM_EINVAL -1    /* bad argument (shape, pointer, size) */
+#define YM_EBLOB -2     /* malformed model blob */
+#define YM_EHIP -3      /* HIP runtime error */
+#define YM_ENOMEM -4    /* device allocation failed */
+#define YM_ESTATE -5    /* call order (e.g. infer before load) */
+
+typedef struct ym_ctx ym_ctx;
+
+/* Capacity hints (0 = grow on demand). */
+typedef struct {
+  int max_batch;
+  int max_h;
+  int max_w;
+  int reserved[5];
+} ym_model_desc;
+
+/* Per-call predict arguments: the Ultralytics predict kwargs that reach the hot path
+ * (conf, iou, classes, agnostic_nms, max_det; NMS constants max_nms=30000, max_wh=7680;
+ * LoadTensor eps = finfo(input dtype).eps for the /255 rule). */
+typedef struct {
+  float conf;
+  float max_wh;
+  double iou;
+  int max_det;
+  int max_nms;
+  int agnostic;
+  float in_eps;
+  int has_classes;
+  uint32_t classes[4]; /* bit c set = keep class c (c < 128) */
+  int use_graph;       /* 1: capture/replay a HIP graph per (shape, pointers, args); 0: eager launches */
+  int reserved[7];
+} ym_infer_args;
+
+/* Replaces `YOLO(model_path)` construction (core/model.py:100-116): create a context on `device`. */
+int ym_create(int device, const ym_model_desc* desc, ym_ctx** out);
+
+/* Load a model blob (plan + BN-folded packed weights, produced by yolomi.plan.pack_model) from host memory.
+ * Replaces AutoBackend(fuse=True) weight preparation.  Copies to device; the host blob may be freed after. */
+int ym_load_weights(ym_ctx* ctx, const void* blob, size_t bytes);
+
+/* Replaces `YOLO11Model.predict(tensor)` (core/model.py:118-133) for tensor sources: asynchronous on `stream`
+ * (a hipStream_t, NULL = default).  d_input: B×3×H×W fp32 NCHW device tensor (H, W multiples of 32).
+ * d_dets: B×max_det×(6+nm) fp32 [x1,y1,x2,y2,conf,cls,(mask coeffs)], rows ordered by NMS keep order;
+ * d_counts: B int32 kept counts.  d_dets / d_counts must be device pointers. */
+int ym_infer(ym_ctx* ctx, const float* d_input, int B, int H, int W, const ym_infer_args* args, float* d_dets,
+             int* d_counts, void* stream);
+
+/* Eager run with a HIP event pair around every op: op_ms[i] = device time of op i (n_ops entries). */
+int ym_profile(ym_ctx* ctx, const float* d_input, int B, int H, int W, const ym_infer_args* args, float* d_dets,
+               int* d_counts, void* stream, float* op_ms, int n_ops);
+
+/* Introspection for tests / bisecting: op count & names, and the device view of plan buffer `buf` as produced by
+ * the last ym_infer/ym_profile (NHWC; elem_bytes 2 = fp16, 4 = fp32; for the anchor buffer H=1, W=A). */
+int ym_num_ops(ym_ctx* ctx);
+const char* ym_op_name(ym_ctx* ctx, int i);
+int ym_num_buffers(ym_ctx* ctx);
+int ym_buffer_info(ym_ctx* ctx, int buf, void** ptr, int* C, int* H, int* W, int* elem_bytes);
+
+/* Copy the first `bytes` of plan buffer `buf` (as left by the last ym_infer/ym_profile) to `dst` (host or device
+ * pointer); synchronous. */
+int ym_read_buffer(ym_ctx* ctx, int buf, void* dst, size_t bytes);
+
+int ym_sync(ym_ctx* ctx);
+const char* ym_last_error(void);
+void ym_destroy(ym_ctx* ctx);
+int ym_version(void);
+
+#ifdef __cplusplus
+}
+#endif
+#endif /* YOLOMI_H */

@@ -1,0 +1,96 @@
+"""Detection matching protocol for parity.
+
+Per image: for each oracle detection (score-descending) find an unmatched build detection of the SAME class with
+IoU >= 0.99 and require |Δcoord| <= tol_xy, |Δscore| <= tol_score.  Oracle detections whose score is within
+`conf_margin` of the confidence threshold, or that sit in an NMS near-tie (another same-class oracle box with IoU
+within `iou_margin` of the NMS threshold), are EXEMPT: an ulp-level difference can legitimately flip them.
+Build detections left unmatched are checked the same way against the exemption rules from the build side.
+"""
+from __future__ import annotations
+
+from dataclasses import dataclass, field
+from typing import List
+
+import numpy as np
+
+
+def iou_matrix(a: np.ndarray, b: np.ndarray) -> np.ndarray:
+    if len(a) == 0 or len(b) == 0:
+        return np.zeros((len(a), len(b)))
+    x1 = np.maximum(a[:, None, 0], b[None, :, 0])
+    y1 = np.maximum(a[:, None, 1], b[None, :, 1])
+    x2 = np.minimum(a[:, None, 2], b[None, :, 2])
+    y2 = np.minimum(a[:, None, 3], b[None, :, 3])
+    inter = np.clip(x2 - x1, 0, None) * np.clip(y2 - y1, 0, None)
+    aa = (a[:, 2] - a[:, 0]) * (a[:, 3] - a[:, 1])
+    ab = (b[:, 2] - b[:, 0]) * (b[:, 3] - b[:, 1])
+    return inter / np.maximum(aa[:, None] + ab[None, :] - inter, 1e-12)
+
+
+@dataclass
+class MatchReport:
+    matched: int = 0
+    exempt: int = 0
+    unmatched_ref: int = 0
+    unmatched_build: int = 0
+    max_dxy: float = 0.0
+    max_dscore: float = 0.0
+    failures: List[str] = field(default_factory=list)
+
+    @property
+    def ok(self) -> bool:
+        return self.unmatched_ref == 0 and self.unmatched_build == 0
+
+    def __str__(self):
+        return (f"matched={self.matched} exempt={self.exempt} unmatched_ref={self.unmatched_ref} "
+                f"unmatched_build={self.unmatched_build} max|dxy|={self.max_dxy:.3g} "
+                f"max|dscore|={self.max_dscore:.3g}")
+
+
+def _exempt(d: np.ndarray, same: np.ndarray, conf: float, iou_thr: float, conf_margin: float,
+            iou_margin: float) -> np.ndarray:
+    ex = np.abs(d[:, 4] - conf) <= conf_margin
+    if len(d):
+        m = iou_matrix(d[:, :4], same[:, :4]) if len(same) else np.zeros((len(d), 0))
+        if m.size:
+            cls_eq = d[:, None, 5] == same[None, :, 5]
+            near = (np.abs(m - iou_thr) <= iou_margin) & cls_eq
+            ex |= near.any(1)
+    return ex
+
+
+def match_image(ref: np.ndarray, got: np.ndarray, conf: float, iou_thr: float, tol_xy: float, tol_score: float,
+                conf_margin: float = 2e-3, iou_margin: float = 2e-2, rep: MatchReport = None) -> MatchReport:
+    rep = rep or MatchReport()
+    ref = ref[np.argsort(-ref[:, 4], kind="stable")] if len(ref) else ref.reshape(0, 6)
+    got = got[np.argsort(-got[:, 4], kind="stable")] if len(got) else got.reshape(0, 6)
+    used = np.zeros(len(got), bool)
+    ious = iou_matrix(ref[:, :4], got[:, :4])
+    ex_ref = _exempt(ref, ref, conf, iou_thr, conf_margin, iou_margin) if len(ref) else np.zeros(0, bool)
+    for i in range(len(ref)):
+        cand = np.where((~used) & (got[:, 5] == ref[i, 5]) & (ious[i] >= 0.99))[0] if len(got) else []
+        ok = False
+        for j in cand:
+            dxy = float(np.abs(got[j, :4] - ref[i, :4]).max())
+            ds = float(abs(got[j, 4] - ref[i, 4]))
+            if dxy <= tol_xy and ds <= tol_score:
+                used[j] = True
+                rep.matched += 1
+                rep.max_dxy = max(rep.max_dxy, dxy)
+                rep.max_dscore = max(rep.max_dscore, ds)
+                ok = True
+                break
+        if not ok:
+            if ex_ref[i]:
+                rep.exempt += 1
+            else:
+                rep.unmatched_ref += 1
+                rep.failures.append(f"ref det {ref[i].tolist()} unmatched")
+    rest = got[~used]
+    if len(rest):
+        ex_b = _exempt(rest, got, conf, iou_thr, conf_margin, iou_margin)
+        rep.exempt += int(ex_b.sum())
+        rep.unmatched_build += int((~ex_b).sum())
+        for r in rest[~ex_b]:
+            rep.failures.append(f"build det {r.tolist()} unmatched")
+    return rep

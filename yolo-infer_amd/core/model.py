@@ -1,0 +1,242 @@
+"""YOLO11Model / YOLO11Factory — drop-in for /root/reference/core/model.py on MI355X.
+
+Same constructor, `predict`, `benchmark`, `get_model_info`, `.model` surface as the reference
+(`core/model.py:29-295`), but `predict` runs the hand-written gfx950 path (`yolomi.engine.Engine` → libyolomi.so →
+one HIP-graph replay per batch) instead of delegating to `ultralytics.YOLO.predict` (`core/model.py:133`).
+
+Scope: tasks detect/segment, sizes n/s/m/l/x, `torch.Tensor` sources (BCHW or CHW, H,W % 32 == 0,
+LoadTensor's /255 rule).  There is no CPU fallback: a CPU device or a missing libyolomi.so raises.
+"""
+from __future__ import annotations
+
+import logging
+import time
+from pathlib import Path
+from typing import Any, Dict, List, Optional, Union
+
+import numpy as np
+import torch
+
+from yolomi.engine import Engine
+from yolomi.synth import synth_weights
+
+from .results import Results
+
+logger = logging.getLogger(__name__)
+
+COCO_NAMES = dict(enumerate((
+    "person", "bicycle", "car", "motorcycle", "airplane", "bus", "train", "truck", "boat", "traffic light",
+    "fire hydrant", "stop sign", "parking meter", "bench", "bird", "cat", "dog", "horse", "sheep", "cow", "elephant",
+    "bear", "zebra", "giraffe", "backpack", "umbrella", "handbag", "tie", "suitcase", "frisbee", "skis", "snowboard",
+    "sports ball", "kite", "baseball bat", "baseball glove", "skateboard", "surfboard", "tennis racket", "bottle",
+    "wine glass", "cup", "fork", "knife", "spoon", "bowl", "banana", "apple", "sandwich", "orange", "broccoli",
+    "carrot", "hot dog", "pizza", "donut", "cake", "chair", "couch", "potted plant", "bed", "dining table", "toilet",
+    "tv", "laptop", "mouse", "remote", "keyboard", "cell phone", "microwave", "oven", "toaster", "sink",
+    "refrigerator", "book", "clock", "vase", "scissors", "teddy bear", "hair drier", "toothbrush")))
+
+
+class _ModelHandle:
+    """What the reference exposes as `YOLO11Model.model` (an `ultralytics.YOLO`): callers use `.eval()`
+    (speed_benchmark.py:323), `.parameters()` / `.model.parameters()` (model.py:240), `.names`."""
+
+    def __init__(self, state_dict: Dict[str, np.ndarray], engine: Engine, names: Dict[int, str]):
+        self._params = {k: torch.from_numpy(np.asarray(v)) for k, v in state_dict.items()
+                        if not k.endswith("num_batches_tracked")}
+        for p in self._params.values():
+            p.requires_grad_(True)
+        self.engine = engine
+        self.names = names
+        self.model = self
+        self.training = False
+
+    def eval(self):
+        return self
+
+    def parameters(self):
+        return iter(self._params.values())
+
+    def state_dict(self):
+        return dict(self._params)
+
+
+def _load_state_dict(path: Path) -> Dict[str, np.ndarray]:
+    """Weights file → Ultralytics-key state dict. Loaders that execute nothing from the file only."""
+    suf = path.suffix.lower()
+    if suf == ".safetensors":
+        from safetensors.numpy import load_file
+        return dict(load_file(str(path)))
+    if suf == ".npz":
+        with np.load(path, allow_pickle=False) as z:
+            return {k: z[k] for k in z.files}
+    if suf == ".pt":
+        obj = torch.load(path, map_location="cpu", weights_only=True)
+        if isinstance(obj, dict) and "state_dict" in obj:
+            obj = obj["state_dict"]
+        if not isinstance(obj, dict):
+            raise ValueError(f"{path}: expected a state dict of tensors")
+        return {k: v.float().numpy() if v.is_floating_point() else v.numpy() for k, v in obj.items()}
+    raise ValueError(f"unsupported weights file {path} (use .safetensors, .npz or a state-dict .pt)")
+
+
+class YOLO11Model:
+    SUPPORTED_TASKS = {
+        "detect": "yolo11n.pt",
+        "segment": "yolo11n-seg.pt",
+        "classify": "yolo11n-cls.pt",
+        "pose": "yolo11n-pose.pt",
+        "obb": "yolo11n-obb.pt",
+    }
+    SUPPORTED_SIZES = ["n", "s", "m", "l", "x"]
+    HIP_TASKS = ("detect", "segment")
+
+    def __init__(self, model_path: Optional[Union[str, Path]] = None, task: str = "detect", size: str = "n",
+                 device: Optional[str] = None, verbose: bool = True, dtype: str = "f16", seed: int = 0):
+        self.task = task
+        self.size = size
+        self.device = device or self._get_default_device()
+        self.verbose = verbose
+        self.model_path = model_path
+        self.dtype = dtype
+        self.seed = seed
+        self.optimization_history: List[Dict[str, Any]] = []
+        self._validate_inputs()
+        self.model = self._load_model()
+        self.original_model = None
+        logger.info(f"YOLO11 model initialized: task={task}, size={size}, device={self.device}")
+
+    def _get_default_device(self) -> str:
+        return "cuda" if torch.cuda.is_available() else "cpu"
+
+    def _validate_inputs(self):
+        if self.task not in self.SUPPORTED_TASKS:
+            raise ValueError(f"Unsupported task: {self.task}. Supported: {list(self.SUPPORTED_TASKS.keys())}")
+        if self.size not in self.SUPPORTED_SIZES:
+            raise ValueError(f"Unsupported size: {self.size}. Supported: {self.SUPPORTED_SIZES}")
+        if self.task not in self.HIP_TASKS:
+            raise NotImplementedError(f"task {self.task!r} has no MI355X plan (supported: {self.HIP_TASKS})")
+
+    def _load_model(self) -> _ModelHandle:
+        dev = torch.device(self.device)
+        if dev.type != "cuda":
+            raise RuntimeError(f"YOLO11Model runs on MI355X (gfx950) only; device {self.device!r} has no HIP path")
+        if dev.index is None:
+            dev = torch.device("cuda", torch.cuda.current_device())
+        self._dev = dev
+        try:
+            if self.model_path:
+                sd = _load_state_dict(Path(self.model_path))
+            else:  # the reference fetches yolo11{size}.pt by name; offline we synthesise weights of that graph
+                sd = synth_weights(self.size, self.task, self.seed)
+            engine = Engine(self.size, self.task, sd, dev, self.dtype)
+        except Exception as e:
+            logger.error(f"Failed to load model: {e}")
+            raise
+        return _ModelHandle(sd, engine, COCO_NAMES)
+
+    # ------------------------------------------------------------------ hot path
+    def _as_batch(self, source) -> (torch.Tensor, float):
+        if isinstance(source, (list, tuple)) and source and all(isinstance(s, torch.Tensor) for s in source):
+            source = torch.stack(list(source))
+        if not isinstance(source, torch.Tensor):
+            raise NotImplementedError("only torch.Tensor sources (BCHW/CHW) run on the MI355X path this round; "
+                                      "file/ndarray sources need the letterbox kernel (SURVEY §8f)")
+        im = source
+        if im.dim() != 4:
+            if im.dim() != 3:
+                raise ValueError("torch.Tensor inputs should be BCHW i.e. shape(1, 3, 640, 640)")
+            im = im.unsqueeze(0)
+        if im.shape[1] != 3:
+            raise ValueError(f"expected 3 input channels, got shape {tuple(im.shape)}")
+        if im.shape[2] % 32 or im.shape[3] % 32:
+            raise ValueError(f"torch.Tensor inputs should be BCHW divisible by stride 32, got {tuple(im.shape)}")
+        if not im.is_floating_point():
+            raise TypeError(f"tensor source must be floating point, got {im.dtype}")
+        eps = torch.finfo(im.dtype).eps
+        if im.device != self._dev:
+            im = im.to(self._dev)
+        im = im.float().contiguous()
+        return im, eps
+
+    def predict(self, source, **kwargs) -> List[Results]:
+        conf = float(kwargs.get("conf", 0.25))
+        iou = float(kwargs.get("iou", 0.7))
+        max_det = int(kwargs.get("max_det", 300))
+        classes = kwargs.get("classes", None)
+        agnostic = bool(kwargs.get("agnostic_nms", False))
+        im, eps = self._as_batch(source)
+        eng = self.model.engine
+        t0 = time.perf_counter()
+        dets, counts = eng.run(im, conf=conf, iou=iou, max_det=max_det, classes=classes, agnostic=agnostic,
+                               in_eps=eps)
+        B = im.shape[0]
+        out = dets[:B].clone()
+        n = counts[:B].tolist()  # the one device→host sync of a predict call
+        dt = (time.perf_counter() - t0) * 1e3
+        speed = {"preprocess": 0.0, "inference": dt, "postprocess": 0.0}
+        names = self.model.names
+        return [Results(im[b], names, out[b, : n[b], :6], path=f"image{b}.jpg", speed=speed) for b in range(B)]
+
+    def __call__(self, source, **kwargs):
+        return self.predict(source, **kwargs)
+
+    # ------------------------------------------------------------------ reference surface
+    def get_model_info(self) -> Dict[str, Any]:
+        info = {
+            "task": self.task,
+            "size": self.size,
+            "device": self.device,
+            "model_path": self.model_path,
+            "optimization_history": self.optimization_history,
+        }
+        params = list(self.model.model.parameters())
+        total = sum(p.numel() for p in params)
+        info.update({
+            "total_parameters": total,
+            "trainable_parameters": sum(p.numel() for p in params if p.requires_grad),
+            "model_size_mb": total * 4 / (1024 * 1024),
+        })
+        return info
+
+    def benchmark(self, data_source, num_runs: int = 100, warmup_runs: int = 10) -> Dict[str, float]:
+        """Same protocol as the reference (core/model.py:253-291): warm-up, then wall-clock per predict()."""
+        for _ in range(warmup_runs):
+            _ = self.predict(data_source, verbose=False)
+        times = []
+        for _ in range(num_runs):
+            start = time.time()
+            _ = self.predict(data_source, verbose=False)
+            times.append(time.time() - start)
+        avg = sum(times) / len(times)
+        return {"avg_inference_time": avg, "min_inference_time": min(times), "max_inference_time": max(times),
+                "fps": 1.0 / avg}
+
+    def train(self, *a, **k):
+        raise NotImplementedError("training is out of scope for the MI355X inference path (SURVEY §2)")
+
+    val = export = train
+
+    def __repr__(self) -> str:
+        return (f"YOLO11Model(task={self.task}, size={self.size}, "
+                f"device={self.device}, optimized={len(self.optimization_history) > 0})")
+
+
+class YOLO11Factory:
+    @staticmethod
+    def create_detector(size: str = "n", **kwargs) -> YOLO11Model:
+        return YOLO11Model(task="detect", size=size, **kwargs)
+
+    @staticmethod
+    def create_segmenter(size: str = "n", **kwargs) -> YOLO11Model:
+        return YOLO11Model(task="segment", size=size, **kwargs)
+
+    @staticmethod
+    def create_classifier(size: str = "n", **kwargs) -> YOLO11Model:
+        return YOLO11Model(task="classify", size=size, **kwargs)
+
+    @staticmethod
+    def create_pose_estimator(size: str = "n", **kwargs) -> YOLO11Model:
+        return YOLO11Model(task="pose", size=size, **kwargs)
+
+    @staticmethod
+    def create_obb_detector(size: str = "n", **kwargs) -> YOLO11Model:
+        return YOLO11Model(task="obb", size=size, **kwargs)

@@ -1,0 +1,167 @@
+"""Results / Boxes / Masks: the per-image result objects `YOLO11Model.predict` returns.
+
+Mirrors the subset of the Ultralytics Results contract the reference's consumers read
+(/root/reference/demos/detection_demo.py:116-132 `.boxes.xyxy/.conf/.cls` per box, `.cpu().numpy()`;
+/root/reference/utils/visualization.py:46-74, 370-437 `.names`, `len(boxes)`, iteration, `.masks.data`).
+Tensors stay on the model's device, like upstream.
+"""
+from __future__ import annotations
+
+from typing import Dict, Optional
+
+import numpy as np
+import torch
+
+
+class _TensorView:
+    def __init__(self, data):
+        self.data = data
+
+    def cpu(self):
+        return self.__class__(self.data.cpu(), *self._extra()) if isinstance(self.data, torch.Tensor) else self
+
+    def numpy(self):
+        d = self.data.cpu().numpy() if isinstance(self.data, torch.Tensor) else self.data
+        return self.__class__(d, *self._extra())
+
+    def cuda(self):
+        return self.__class__(torch.as_tensor(self.data).cuda(), *self._extra())
+
+    def to(self, *args, **kwargs):
+        return self.__class__(torch.as_tensor(self.data).to(*args, **kwargs), *self._extra())
+
+    def _extra(self):
+        return ()
+
+    @property
+    def shape(self):
+        return self.data.shape
+
+    def __len__(self):
+        return len(self.data)
+
+    def __getitem__(self, idx):
+        return self.__class__(self.data[idx], *self._extra())
+
+    def __iter__(self):
+        for i in range(len(self)):
+            yield self[i]
+
+
+class Boxes(_TensorView):
+    """(n, 6) [x1, y1, x2, y2, conf, cls] detections of one image (upstream `ultralytics.engine.results.Boxes`)."""
+
+    def __init__(self, boxes, orig_shape):
+        if boxes.ndim == 1:
+            boxes = boxes[None, :]
+        super().__init__(boxes)
+        self.orig_shape = orig_shape
+
+    def _extra(self):
+        return (self.orig_shape,)
+
+    @property
+    def xyxy(self):
+        return self.data[:, :4]
+
+    @property
+    def conf(self):
+        return self.data[:, 4]
+
+    @property
+    def cls(self):
+        return self.data[:, 5]
+
+    @property
+    def id(self):
+        return None
+
+    @property
+    def is_track(self):
+        return False
+
+    @property
+    def xywh(self):
+        x = self.xyxy
+        y = x.clone() if isinstance(x, torch.Tensor) else np.copy(x)
+        y[..., 0] = (x[..., 0] + x[..., 2]) / 2
+        y[..., 1] = (x[..., 1] + x[..., 3]) / 2
+        y[..., 2] = x[..., 2] - x[..., 0]
+        y[..., 3] = x[..., 3] - x[..., 1]
+        return y
+
+    @property
+    def xyxyn(self):
+        x = self.xyxy.clone() if isinstance(self.xyxy, torch.Tensor) else np.copy(self.xyxy)
+        x[..., [0, 2]] /= self.orig_shape[1]
+        x[..., [1, 3]] /= self.orig_shape[0]
+        return x
+
+    @property
+    def xywhn(self):
+        x = self.xywh
+        x[..., [0, 2]] /= self.orig_shape[1]
+        x[..., [1, 3]] /= self.orig_shape[0]
+        return x
+
+
+class Masks(_TensorView):
+    """(n, H, W) binary instance masks of one image."""
+
+    def __init__(self, masks, orig_shape=None):
+        super().__init__(masks)
+        self.orig_shape = orig_shape
+
+    def _extra(self):
+        return (self.orig_shape,)
+
+
+class Results:
+    def __init__(self, orig_tensor: Optional[torch.Tensor], names: Dict[int, str], boxes: torch.Tensor,
+                 masks: Optional[torch.Tensor] = None, path: str = "image0.jpg", speed=None):
+        self._orig_tensor = orig_tensor
+        self._orig_img = None
+        self.orig_shape = tuple(orig_tensor.shape[-2:]) if orig_tensor is not None else None
+        self.names = names
+        self.boxes = Boxes(boxes, self.orig_shape)
+        self.masks = Masks(masks, self.orig_shape) if masks is not None else None
+        self.path = path
+        self.speed = speed or {"preprocess": None, "inference": None, "postprocess": None}
+        self.probs = None
+        self.keypoints = None
+        self.obb = None
+
+    @property
+    def orig_img(self) -> np.ndarray:
+        """HWC uint8 copy of the input image, as upstream `convert_torch2numpy_batch` makes it
+        ((x.permute(1,2,0)*255).clamp(0,255).to(uint8)); materialised (one device→host copy) on first access."""
+        if self._orig_img is None and self._orig_tensor is not None:
+            t = self._orig_tensor
+            self._orig_img = (t.permute(1, 2, 0).contiguous() * 255).clamp_(0, 255).to(torch.uint8).cpu().numpy()
+        return self._orig_img
+
+    def __len__(self):
+        return len(self.boxes)
+
+    def __getitem__(self, idx):
+        r = Results(self._orig_tensor, self.names, self.boxes.data[idx],
+                    self.masks.data[idx] if self.masks is not None else None, self.path, self.speed)
+        return r
+
+    def cpu(self):
+        r = Results(self._orig_tensor.cpu() if self._orig_tensor is not None else None, self.names,
+                    self.boxes.data.cpu(), self.masks.data.cpu() if self.masks is not None else None, self.path,
+                    self.speed)
+        return r
+
+    def summary(self, normalize=False, decimals=5):
+        out = []
+        for row in self.boxes.data.tolist():
+            x1, y1, x2, y2, conf, c = row[:6]
+            out.append({"name": self.names[int(c)], "class": int(c), "confidence": round(conf, decimals),
+                        "box": {"x1": round(x1, decimals), "y1": round(y1, decimals), "x2": round(x2, decimals),
+                                "y2": round(y2, decimals)}})
+        return out
+
+    def __repr__(self):
+        return f"Results(boxes={len(self.boxes)}, orig_shape={self.orig_shape})"

@@ -1,0 +1,109 @@
+// Shared device/host definitions for the yolomi HIP runtime (gfx950 / CDNA4 only).
+#pragma once
+#include <hip/hip_runtime.h>
+#include <stdint.h>
+
+typedef _Float16 f16;
+typedef _Float16 f16x8 __attribute__((ext_vector_type(8)));
+typedef _Float16 f16x4 __attribute__((ext_vector_type(4)));
+typedef float f32x4 __attribute__((ext_vector_type(4)));
+typedef float f32x8 __attribute__((ext_vector_type(8)));
+
+#define YM_WAVE 64
+
+// Activation storage precision of a plan: f16 (MFMA 16x16x32 f16) or f32 (exact-f32 MFMA 16x16x4, parity mode).
+enum { YM_DT_F16 = 0, YM_DT_F32 = 1 };
+
+// 8 consecutive channels of one pixel: the unit of every NHWC load in this runtime (16 B in f16, 32 B in f32).
+template <typename T> struct Vec8;
+template <> struct Vec8<f16> {
+  typedef f16x8 type;
+  static __device__ __forceinline__ type load(const f16* p) { return *reinterpret_cast<const f16x8*>(p); }
+  static __device__ __forceinline__ void store(f16* p, type v) { *reinterpret_cast<f16x8*>(p) = v; }
+  static __device__ __forceinline__ type zero() { return type{0, 0, 0, 0, 0, 0, 0, 0}; }
+};
+template <> struct Vec8<float> {
+  typedef f32x8 type;
+  static __device__ __forceinline__ type load(const float* p) {
+    f32x4 a = *reinterpret_cast<const f32x4*>(p);
+    f32x4 b = *reinterpret_cast<const f32x4*>(p + 4);
+    return type{a[0], a[1], a[2], a[3], b[0], b[1], b[2], b[3]};
+  }
+  static __device__ __forceinline__ void store(float* p, type v) {
+    *reinterpret_cast<f32x4*>(p) = f32x4{v[0], v[1], v[2], v[3]};
+    *reinterpret_cast<f32x4*>(p + 4) = f32x4{v[4], v[5], v[6], v[7]};
+  }
+  static __device__ __forceinline__ type zero() { return type{0, 0, 0, 0, 0, 0, 0, 0}; }
+};
+
+__device__ __forceinline__ float ym_silu(float x) { return x / (1.0f + expf(-x)); }
+__device__ __forceinline__ float ym_sigmoid(float x) { return 1.0f / (1.0f + expf(-x)); }
+
+// ------------------------------------------------------------------------------------------------------------
+// Kernel argument blocks (plain structs passed by value).
+
+struct ConvArgs {
+  const void* src0; int s0_ctot, s0_coff, C0, s0_W, s0_P, up0;  // first A source; up0: read at (y>>1, x>>1)
+  const void* src1; int s1_ctot, s1_coff, C1, s1_P;             // optional second A source (concat tail)
+  const void* w; const float* bias;                             // W packed [N][Kpad] (act dtype), bias f32 [N]
+  void* dst; int d_ctot, d_coff, d_P, d_pixoff, d_W;            // output view (d_W: dst row width in pixels)
+  const void* res; int r_ctot, r_coff, r_P;                     // optional residual view (same geometry as dst)
+  int Hin, Win, Ho, Wo, k, s, pad, Cin8, Kc, N, Kpad, act, shuffle, npr, M, tiles_n;
+};
+
+struct DwArgs {
+  const void* src; int s_ctot, s_coff, s_P;
+  void* dst; int d_ctot, d_coff, d_P;
+  const float* w; const float* bias;  // w: [9][C] f32
+  int C, H, W, act, B;
+};
+
+struct PoolArgs {
+  void* buf; int ctot, coff, P;  // y0 at coff, writes y1,y2,y3 at coff+C, +2C, +3C
+  int C, H, W, B;
+};
+
+struct AttnArgs {
+  const void* qkv; int q_ctot, q_coff, q_P;
+  void* dst; int d_ctot, d_coff, d_P;
+  const float* pe_w; const float* pe_b;  // [9][C], [C]
+  int C, nh, kd, hd, H, W, N, B;
+  float scale;
+};
+
+struct DecodeArgs {
+  const float* anchors; int no_tot;      // (B, A, no_tot) fp32
+  float4* boxes; float* scores; int* cls;  // (B, A)
+  unsigned long long* keys; int* counts;   // (B, A) candidate keys, (B) counts
+  int A, kstride, nc, reg_max, B;
+  int lvl_W[4], lvl_off[4], nl; float lvl_stride[4];
+  float conf; int has_classes; unsigned int classes[4];
+};
+
+struct NmsArgs {
+  const float* anchors; int no_tot, mask_off;  // mask coefficients live at [mask_off, mask_off+nm) of each anchor row
+  const float4* boxes; const float* scores; const int* cls;
+  unsigned long long* keys; const int* counts;
+  float4* sboxes; float* sareas; unsigned char* sup;  // per image scratch (A each)
+  float* dets; int* out_counts;                       // (B, max_det, 6 + nm), (B)
+  int A, kstride, nm, max_det, max_nms, agnostic, B;
+  float max_wh, img_h, img_w;
+  double iou;
+};
+
+struct PrepArgs {
+  const float* in; void* out;  // NCHW fp32 → NHWC act dtype, 8 channels (3 real + 5 zero)
+  float* ctl;                  // ctl[0] = running max (ordered-int encoded) of the input
+  int B, C, H, W;
+  float eps;                   // LoadTensor rule: /255 when max > 1 + eps
+};
+
+// ------------------------------------------------------------------------------------------------------------
+// Host-side launchers (defined in the .hip translation units).
+hipError_t ym_launch_conv(int dtype, int out_f32, const ConvArgs& a, hipStream_t st);
+hipError_t ym_launch_dwconv(int dtype, const DwArgs& a, hipStream_t st);
+hipError_t ym_launch_sppf(int dtype, const PoolArgs& a, hipStream_t st);
+hipError_t ym_launch_attn(int dtype, const AttnArgs& a, hipStream_t st);
+hipError_t ym_launch_prep(int dtype, const PrepArgs& a, int* counts, int B, hipStream_t st);
+hipError_t ym_launch_decode(const DecodeArgs& a, hipStream_t st);
+hipError_t ym_launch_nms(const NmsArgs& a, hipStream_t st);

@@ -1,0 +1,499 @@
+// yolomi runtime: model-blob parsing, device weight/workspace arena, per-op launch, HIP-graph cache, C-ABI.
+//
+// This is the native replacement for the Ultralytics predictor loop that `YOLO11Model.predict` delegates to
+// (/root/reference/core/model.py:118-133): per batch it replays ONE captured HIP graph of the whole forward
+// (input /255 rule → 80+ fused conv launches → attention → decode → NMS), so the Python host issues one call.
+#include <hip/hip_runtime.h>
+
+#include <cstdarg>
+#include <cstdio>
+#include <cstring>
+#include <string>
+#include <vector>
+
+#include "../../include/yolomi.h"
+#include "ym_common.h"
+
+namespace {
+
+thread_local std::string g_err;
+
+int fail(int code, const char* fmt, ...) {
+  char buf[512];
+  va_list ap;
+  va_start(ap, fmt);
+  vsnprintf(buf, sizeof(buf), fmt, ap);
+  va_end(ap);
+  g_err = buf;
+  return code;
+}
+
+#define HIPCK(x)                                                                              \
+  do {                                                                                        \
+    hipError_t e_ = (x);                                                                      \
+    if (e_ != hipSuccess) return fail(YM_EHIP, "%s: %s (%s:%d)", #x, hipGetErrorString(e_), __FILE__, __LINE__); \
+  } while (0)
+
+constexpr int32_t kMagic = 0x4C504D59;  // 'YMPL'
+constexpr int kHdr = 32, kBufRec = 8, kOpRec = 32, kNameLen = 48;
+
+enum OpKind { OP_INPUT = 1, OP_CONV = 2, OP_DW = 3, OP_SPPF = 4, OP_ATTN = 5, OP_DECODE = 6, OP_NMS = 7 };
+
+struct BufDesc {
+  int C, f, f32;
+};
+
+struct Op {
+  int32_t r[kOpRec];
+  char name[kNameLen];
+};
+
+struct GraphKey {
+  int B, H, W;
+  const void* in;
+  const void* dets;
+  const void* counts;
+  const void* stream_unused;
+  ym_infer_args args;
+  bool operator==(const GraphKey& o) const { return memcmp(this, &o, sizeof(GraphKey)) == 0; }
+};
+
+struct GraphEntry {
+  GraphKey key;
+  hipGraph_t graph;
+  hipGraphExec_t exec;
+};
+
+}  // namespace
+
+struct ym_ctx {
+  int device = 0;
+  ym_model_desc desc{};
+  bool loaded = false;
+  // plan
+  int dtype = YM_DT_F16, task = 0, nc = 80, nm = 0, reg_max = 16, nl = 3;
+  int strides[4] = {8, 16, 32, 0};
+  int input_buf = -1, anchor_buf = -1, no = 0;
+  std::vector<BufDesc> bufs;
+  std::vector<Op> ops;
+  char* d_weights = nullptr;
+  size_t wbytes = 0;
+  // workspace for the current (B, H, W)
+  int cB = 0, cH = 0, cW = 0;
+  char* d_arena = nullptr;
+  size_t arena_bytes = 0;
+  std::vector<size_t> buf_off;
+  size_t off_boxes = 0, off_scores = 0, off_cls = 0, off_keys = 0, off_counts = 0, off_ctl = 0, off_sboxes = 0,
+         off_sareas = 0, off_sup = 0;
+  int A = 0, kstride = 0;
+  int lvl_W[4] = {0}, lvl_off[4] = {0};
+  hipStream_t cap_stream = nullptr;
+  std::vector<GraphEntry> graphs;
+  std::vector<hipEvent_t> prof_events;
+
+  ~ym_ctx() {
+    (void)hipSetDevice(device);
+    clear_graphs();
+    for (auto e : prof_events) (void)hipEventDestroy(e);
+    if (d_arena) (void)hipFree(d_arena);
+    if (d_weights) (void)hipFree(d_weights);
+    if (cap_stream) (void)hipStreamDestroy(cap_stream);
+  }
+  void clear_graphs() {
+    for (auto& g : graphs) {
+      (void)hipGraphExecDestroy(g.exec);
+      (void)hipGraphDestroy(g.graph);
+    }
+    graphs.clear();
+  }
+  int buf_P(int b) const {
+    const BufDesc& d = bufs[b];
+    if (d.f == 0) return A;
+    return (cH / d.f) * (cW / d.f);
+  }
+  int buf_H(int b) const { return bufs[b].f == 0 ? 1 : cH / bufs[b].f; }
+  int buf_Wd(int b) const { return bufs[b].f == 0 ? A : cW / bufs[b].f; }
+  int elem(int b) const { return (bufs[b].f32 || dtype == YM_DT_F32) ? 4 : 2; }
+  void* bptr(int b) const { return d_arena + buf_off[b]; }
+};
+
+namespace {
+
+size_t align_up(size_t x, size_t a) { return (x + a - 1) / a * a; }
+
+int ensure_workspace(ym_ctx* c, int B, int H, int W) {
+  if (c->d_arena && B <= c->cB && H == c->cH && W == c->cW) return YM_OK;
+  const int nB = (H == c->cH && W == c->cW && B < c->cB) ? c->cB : B;
+  c->clear_graphs();
+  if (c->d_arena) {
+    HIPCK(hipFree(c->d_arena));
+    c->d_arena = nullptr;
+  }
+  c->cB = nB;
+  c->cH = H;
+  c->cW = W;
+  c->A = 0;
+  for (int l = 0; l < c->nl; ++l) {
+    c->lvl_off[l] = c->A;
+    c->lvl_W[l] = W / c->strides[l];
+    c->A += (H / c->strides[l]) * (W / c->strides[l]);
+  }
+  c->kstride = 1;
+  while (c->kstride < c->A) c->kstride <<= 1;
+  size_t off = 0;
+  c->buf_off.assign(c->bufs.size(), 0);
+  for (size_t b = 0; b < c->bufs.size(); ++b) {
+    c->buf_off[b] = off;
+    off = align_up(off + (size_t)nB * c->buf_P((int)b) * c->bufs[b].C * c->elem((int)b), 256);
+  }
+  const size_t BA = (size_t)nB * c->A;
+  c->off_boxes = off;  off = align_up(off + BA * 16, 256);
+  c->off_scores = off; off = align_up(off + BA * 4, 256);
+  c->off_cls = off;    off = align_up(off + BA * 4, 256);
+  c->off_keys = off;   off = align_up(off + (size_t)nB * c->kstride * 8, 256);
+  c->off_counts = off; off = align_up(off + (size_t)nB * 4, 256);
+  c->off_ctl = off;    off = align_up(off + 256, 256);
+  c->off_sboxes = off; off = align_up(off + BA * 16, 256);
+  c->off_sareas = off; off = align_up(off + BA * 4, 256);
+  c->off_sup = off;    off = align_up(off + BA, 256);
+  c->arena_bytes = off;
+  hipError_t e = hipMalloc(&c->d_arena, off);
+  if (e != hipSuccess) {
+    c->d_arena = nullptr;
+    c->cB = 0;
+    return fail(YM_ENOMEM, "workspace hipMalloc(%zu) failed: %s", off, hipGetErrorString(e));
+  }
+  HIPCK(hipMemset(c->d_arena, 0, off));
+  return YM_OK;
+}
+
+int launch_op(ym_ctx* c, const Op& op, int B, const float* d_in, const ym_infer_args* args, float* d_dets,
+              int* d_counts, hipStream_t st) {
+  const int32_t* r = op.r;
+  const int dt = c->dtype;
+  hipError_t e = hipSuccess;
+  switch (r[0]) {
+    case OP_INPUT: {
+      PrepArgs a{};
+      a.in = d_in;
+      a.out = c->bptr(c->input_buf);
+      a.ctl = reinterpret_cast<float*>(c->d_arena + c->off_ctl);
+      a.B = B; a.C = 3; a.H = c->cH; a.W = c->cW;
+      a.eps = args->in_eps;
+      e = ym_launch_prep(dt, a, reinterpret_cast<int*>(c->d_arena + c->off_counts), B, st);
+      break;
+    }
+    case OP_CONV: {
+      ConvArgs a{};
+      const int k = r[1], s = r[2], cin = r[3], cout = r[4];
+      const int b0 = r[6], b1 = r[10], bd = r[13], br = r[17];
+      const int up0 = r[9];
+      a.src0 = c->bptr(b0); a.s0_ctot = c->bufs[b0].C; a.s0_coff = r[7]; a.C0 = r[8];
+      a.s0_W = c->buf_Wd(b0); a.s0_P = c->buf_P(b0); a.up0 = up0;
+      a.Hin = c->buf_H(b0) * (up0 ? 2 : 1);
+      a.Win = c->buf_Wd(b0) * (up0 ? 2 : 1);
+      if (b1 >= 0) {
+        a.src1 = c->bptr(b1); a.s1_ctot = c->bufs[b1].C; a.s1_coff = r[11]; a.C1 = r[12]; a.s1_P = c->buf_P(b1);
+        if (c->buf_H(b1) != a.Hin || c->buf_Wd(b1) != a.Win)
+          return fail(YM_EBLOB, "op %s: concat sources disagree in shape", op.name);
+      }
+      a.k = k; a.s = s; a.pad = k / 2;
+      a.Ho = (a.Hin + 2 * a.pad - k) / s + 1;
+      a.Wo = (a.Win + 2 * a.pad - k) / s + 1;
+      if (cin % 8 || (a.C0 + a.C1) != cin) return fail(YM_EBLOB, "op %s: cin %d not a multiple of 8", op.name, cin);
+      a.Cin8 = cin / 8;
+      a.Kc = k * k * a.Cin8;
+      a.Kpad = r[21];
+      a.N = cout;
+      a.w = c->d_weights + (size_t)(uint32_t)r[19];
+      a.bias = reinterpret_cast<const float*>(c->d_weights + (size_t)(uint32_t)r[20]);
+      a.act = r[5];
+      a.shuffle = r[16];
+      a.npr = a.shuffle ? cout / 4 : cout;
+      a.dst = c->bptr(bd); a.d_ctot = c->bufs[bd].C; a.d_coff = r[14]; a.d_P = c->buf_P(bd);
+      const int lvl = r[15];
+      if (lvl >= 0) {
+        a.d_pixoff = c->lvl_off[lvl];
+        a.d_W = a.Wo;
+        if (a.Wo != c->lvl_W[lvl]) return fail(YM_EBLOB, "op %s: head level width mismatch", op.name);
+      } else {
+        a.d_pixoff = 0;
+        a.d_W = c->buf_Wd(bd);
+        const int expect = a.shuffle ? 2 : 1;
+        if (c->buf_H(bd) != expect * a.Ho || c->buf_Wd(bd) != expect * a.Wo)
+          return fail(YM_EBLOB, "op %s: output %dx%d does not match dst buffer %dx%d", op.name, a.Ho, a.Wo,
+                      c->buf_H(bd), c->buf_Wd(bd));
+      }
+      if (br >= 0) { a.res = c->bptr(br); a.r_ctot = c->bufs[br].C; a.r_coff = r[18]; a.r_P = c->buf_P(br); }
+      a.M = B * a.Ho * a.Wo;
+      e = ym_launch_conv(dt, c->bufs[bd].f32 && dt == YM_DT_F16, a, st);
+      break;
+    }
+    case OP_DW: {
+      DwArgs a{};
+      const int bs = r[6], bd = r[13];
+      a.src = c->bptr(bs); a.s_ctot = c->bufs[bs].C; a.s_coff = r[7]; a.s_P = c->buf_P(bs);
+      a.dst = c->bptr(bd); a.d_ctot = c->bufs[bd].C; a.d_coff = r[14]; a.d_P = c->buf_P(bd);
+      a.w = reinterpret_cast<const float*>(c->d_weights + (size_t)(uint32_t)r[19]);
+      a.bias = reinterpret_cast<const float*>(c->d_weights + (size_t)(uint32_t)r[20]);
+      a.C = r[3]; a.act = r[5]; a.H = c->buf_H(bs); a.W = c->buf_Wd(bs); a.B = B;
+      e = ym_launch_dwconv(dt, a, st);
+      break;
+    }
+    case OP_SPPF: {
+      PoolArgs a{};
+      const int bb = r[13];
+      a.buf = c->bptr(bb); a.ctot = c->bufs[bb].C; a.coff = r[7]; a.P = c->buf_P(bb);
+      a.C = r[3]; a.H = c->buf_H(bb); a.W = c->buf_Wd(bb); a.B = B;
+      e = ym_launch_sppf(dt, a, st);
+      break;
+    }
+    case OP_ATTN: {
+      AttnArgs a{};
+      const int bq = r[6], bd = r[13];
+      a.qkv = c->bptr(bq); a.q_ctot = c->bufs[bq].C; a.q_coff = r[7]; a.q_P = c->buf_P(bq);
+      a.dst = c->bptr(bd); a.d_ctot = c->bufs[bd].C; a.d_coff = r[14]; a.d_P = c->buf_P(bd);
+      a.pe_w = reinterpret_cast<const float*>(c->d_weights + (size_t)(uint32_t)r[19]);
+      a.pe_b = reinterpret_cast<const float*>(c->d_weights + (size_t)(uint32_t)r[20]);
+      a.C = r[3]; a.nh = r[4]; a.kd = r[5]; a.hd = r[9];
+      a.H = c->buf_H(bq); a.W = c->buf_Wd(bq); a.N = a.H * a.W; a.B = B;
+      memcpy(&a.scale, &r[21], 4);
+      e = ym_launch_attn(dt, a, st);
+      break;
+    }
+    case OP_DECODE: {
+      DecodeArgs a{};
+      a.anchors = reinterpret_cast<const float*>(c->bptr(c->anchor_buf));
+      a.no_tot = c->bufs[c->anchor_buf].C;
+      a.boxes = reinterpret_cast<float4*>(c->d_arena + c->off_boxes);
+      a.scores = reinterpret_cast<float*>(c->d_arena + c->off_scores);
+      a.cls = reinterpret_cast<int*>(c->d_arena + c->off_cls);
+      a.keys = reinterpret_cast<unsigned long long*>(c->d_arena + c->off_keys);
+      a.counts = reinterpret_cast<int*>(c->d_arena + c->off_counts);
+      a.A = c->A; a.kstride = c->kstride; a.nc = c->nc; a.reg_max = c->reg_max; a.B = B; a.nl = c->nl;
+      for (int l = 0; l < c->nl; ++l) {
+        a.lvl_W[l] = c->lvl_W[l]; a.lvl_off[l] = c->lvl_off[l]; a.lvl_stride[l] = (float)c->strides[l];
+      }
+      a.conf = args->conf;
+      a.has_classes = args->has_classes;
+      for (int i = 0; i < 4; ++i) a.classes[i] = args->classes[i];
+      e = ym_launch_decode(a, st);
+      break;
+    }
+    case OP_NMS: {
+      NmsArgs a{};
+      a.anchors = reinterpret_cast<const float*>(c->bptr(c->anchor_buf));
+      a.no_tot = c->bufs[c->anchor_buf].C;
+      a.mask_off = c->no;
+      a.boxes = reinterpret_cast<const float4*>(c->d_arena + c->off_boxes);
+      a.scores = reinterpret_cast<const float*>(c->d_arena + c->off_scores);
+      a.cls = reinterpret_cast<const int*>(c->d_arena + c->off_cls);
+      a.keys = reinterpret_cast<unsigned long long*>(c->d_arena + c->off_keys);
+      a.counts = reinterpret_cast<const int*>(c->d_arena + c->off_counts);
+      a.sboxes = reinterpret_cast<float4*>(c->d_arena + c->off_sboxes);
+      a.sareas = reinterpret_cast<float*>(c->d_arena + c->off_sareas);
+      a.sup = reinterpret_cast<unsigned char*>(c->d_arena + c->off_sup);
+      a.dets = d_dets;
+      a.out_counts = d_counts;
+      a.A = c->A; a.kstride = c->kstride; a.nm = c->nm; a.max_det = args->max_det; a.max_nms = args->max_nms;
+      a.agnostic = args->agnostic; a.B = B;
+      a.max_wh = args->max_wh; a.img_h = (float)c->cH; a.img_w = (float)c->cW;
+      a.iou = args->iou;
+      e = ym_launch_nms(a, st);
+      break;
+    }
+    default:
+      return fail(YM_EBLOB, "unknown op kind %d", r[0]);
+  }
+  if (e != hipSuccess) return fail(YM_EHIP, "launch of op %s failed: %s", op.name, hipGetErrorString(e));
+  return YM_OK;
+}
+
+int check_call(ym_ctx* c, const float* d_in, int B, int H, int W, const ym_infer_args* args, float* d_dets,
+               int* d_counts) {
+  if (!c) return fail(YM_EINVAL, "null context");
+  if (!c->loaded) return fail(YM_ESTATE, "ym_infer before ym_load_weights");
+  if (!d_in || !d_dets || !d_counts || !args) return fail(YM_EINVAL, "null pointer argument");
+  if (B < 1 || H < 32 || W < 32 || H % 32 || W % 32)
+    return fail(YM_EINVAL, "input shape (%d,3,%d,%d): H and W must be positive multiples of 32", B, H, W);
+  if (args->max_det < 1 || args->max_nms < 1) return fail(YM_EINVAL, "max_det/max_nms must be >= 1");
+  return YM_OK;
+}
+
+}  // namespace
+
+extern "C" {
+
+int ym_version(void) { return 1; }
+
+const char* ym_last_error(void) { return g_err.c_str(); }
+
+int ym_create(int device, const ym_model_desc* desc, ym_ctx** out) {
+  if (!out) return fail(YM_EINVAL, "null out");
+  int n = 0;
+  HIPCK(hipGetDeviceCount(&n));
+  if (device < 0 || device >= n) return fail(YM_EINVAL, "device %d out of range (%d devices)", device, n);
+  HIPCK(hipSetDevice(device));
+  ym_ctx* c = new ym_ctx();
+  c->device = device;
+  if (desc) c->desc = *desc;
+  hipError_t e = hipStreamCreateWithFlags(&c->cap_stream, hipStreamNonBlocking);
+  if (e != hipSuccess) {
+    delete c;
+    return fail(YM_EHIP, "hipStreamCreate: %s", hipGetErrorString(e));
+  }
+  *out = c;
+  return YM_OK;
+}
+
+int ym_load_weights(ym_ctx* c, const void* blob, size_t bytes) {
+  if (!c || !blob) return fail(YM_EINVAL, "null argument");
+  HIPCK(hipSetDevice(c->device));
+  const int32_t* h = static_cast<const int32_t*>(blob);
+  if (bytes < kHdr * 4 || h[0] != kMagic || h[1] != 1) return fail(YM_EBLOB, "bad blob magic/version");
+  const int nbuf = h[11], nop = h[12];
+  const size_t wbytes = (size_t)(uint32_t)h[13] | ((size_t)(uint32_t)h[14] << 32);
+  const size_t need = (size_t)kHdr * 4 + (size_t)nbuf * kBufRec * 4 + (size_t)nop * (kOpRec * 4 + kNameLen);
+  const size_t woff = align_up(need, 256);
+  if (bytes < woff + wbytes) return fail(YM_EBLOB, "blob truncated (%zu < %zu)", bytes, woff + wbytes);
+  c->dtype = h[2];
+  if (c->dtype != YM_DT_F16 && c->dtype != YM_DT_F32) return fail(YM_EBLOB, "unknown dtype %d", c->dtype);
+  c->task = h[3]; c->nc = h[4]; c->nm = h[5]; c->reg_max = h[6]; c->nl = h[7];
+  if (c->nl < 1 || c->nl > 4) return fail(YM_EBLOB, "bad level count");
+  for (int l = 0; l < c->nl; ++l) c->strides[l] = h[8 + l];
+  c->input_buf = h[15]; c->anchor_buf = h[16]; c->no = h[18];
+  const int32_t* bp = h + kHdr;
+  c->bufs.resize(nbuf);
+  for (int i = 0; i < nbuf; ++i) c->bufs[i] = BufDesc{bp[i * kBufRec], bp[i * kBufRec + 1], bp[i * kBufRec + 2]};
+  const int32_t* op = bp + (size_t)nbuf * kBufRec;
+  const char* names = reinterpret_cast<const char*>(op + (size_t)nop * kOpRec);
+  c->ops.resize(nop);
+  for (int i = 0; i < nop; ++i) {
+    memcpy(c->ops[i].r, op + (size_t)i * kOpRec, kOpRec * 4);
+    memcpy(c->ops[i].name, names + (size_t)i * kNameLen, kNameLen);
+    c->ops[i].name[kNameLen - 1] = 0;
+  }
+  if (c->input_buf < 0 || c->input_buf >= nbuf || c->anchor_buf < 0 || c->anchor_buf >= nbuf)
+    return fail(YM_EBLOB, "bad input/anchor buffer ids");
+  c->clear_graphs();
+  if (c->d_weights) HIPCK(hipFree(c->d_weights));
+  c->d_weights = nullptr;
+  hipError_t e = hipMalloc(&c->d_weights, wbytes ? wbytes : 256);
+  if (e != hipSuccess) return fail(YM_ENOMEM, "weights hipMalloc(%zu): %s", wbytes, hipGetErrorString(e));
+  HIPCK(hipMemcpy(c->d_weights, static_cast<const char*>(blob) + woff, wbytes, hipMemcpyHostToDevice));
+  c->wbytes = wbytes;
+  c->loaded = true;
+  return YM_OK;
+}
+
+int ym_infer(ym_ctx* c, const float* d_in, int B, int H, int W, const ym_infer_args* args, float* d_dets,
+             int* d_counts, void* stream) {
+  int rc = check_call(c, d_in, B, H, W, args, d_dets, d_counts);
+  if (rc) return rc;
+  HIPCK(hipSetDevice(c->device));
+  hipStream_t st = static_cast<hipStream_t>(stream);
+  rc = ensure_workspace(c, B, H, W);
+  if (rc) return rc;
+  if (!args->use_graph) {
+    for (const Op& op : c->ops)
+      if ((rc = launch_op(c, op, B, d_in, args, d_dets, d_counts, st))) return rc;
+    return YM_OK;
+  }
+  GraphKey key;
+  memset(&key, 0, sizeof(key));
+  key.B = B; key.H = H; key.W = W; key.in = d_in; key.dets = d_dets; key.counts = d_counts; key.args = *args;
+  for (auto& g : c->graphs)
+    if (g.key == key) {
+      HIPCK(hipGraphLaunch(g.exec, st));
+      return YM_OK;
+    }
+  if (c->graphs.size() >= 16) {
+    (void)hipGraphExecDestroy(c->graphs.front().exec);
+    (void)hipGraphDestroy(c->graphs.front().graph);
+    c->graphs.erase(c->graphs.begin());
+  }
+  // capture on the private stream (ordered after the caller's stream), replay on the caller's stream
+  HIPCK(hipStreamBeginCapture(c->cap_stream, hipStreamCaptureModeRelaxed));
+  for (const Op& op : c->ops) {
+    if ((rc = launch_op(c, op, B, d_in, args, d_dets, d_counts, c->cap_stream))) {
+      hipGraph_t g = nullptr;
+      (void)hipStreamEndCapture(c->cap_stream, &g);
+      if (g) (void)hipGraphDestroy(g);
+      return rc;
+    }
+  }
+  GraphEntry ge;
+  ge.key = key;
+  HIPCK(hipStreamEndCapture(c->cap_stream, &ge.graph));
+  HIPCK(hipGraphInstantiate(&ge.exec, ge.graph, nullptr, nullptr, 0));
+  c->graphs.push_back(ge);
+  HIPCK(hipGraphLaunch(ge.exec, st));
+  return YM_OK;
+}
+
+int ym_profile(ym_ctx* c, const float* d_in, int B, int H, int W, const ym_infer_args* args, float* d_dets,
+               int* d_counts, void* stream, float* op_ms, int n_ops) {
+  int rc = check_call(c, d_in, B, H, W, args, d_dets, d_counts);
+  if (rc) return rc;
+  if (!op_ms || n_ops < (int)c->ops.size()) return fail(YM_EINVAL, "op_ms must hold %zu entries", c->ops.size());
+  HIPCK(hipSetDevice(c->device));
+  hipStream_t st = static_cast<hipStream_t>(stream);
+  if ((rc = ensure_workspace(c, B, H, W))) return rc;
+  const size_t ne = c->ops.size() + 1;
+  while (c->prof_events.size() < ne) {
+    hipEvent_t e;
+    HIPCK(hipEventCreate(&e));
+    c->prof_events.push_back(e);
+  }
+  HIPCK(hipEventRecord(c->prof_events[0], st));
+  for (size_t i = 0; i < c->ops.size(); ++i) {
+    if ((rc = launch_op(c, c->ops[i], B, d_in, args, d_dets, d_counts, st))) return rc;
+    HIPCK(hipEventRecord(c->prof_events[i + 1], st));
+  }
+  HIPCK(hipEventSynchronize(c->prof_events[ne - 1]));
+  for (size_t i = 0; i < c->ops.size(); ++i)
+    HIPCK(hipEventElapsedTime(&op_ms[i], c->prof_events[i], c->prof_events[i + 1]));
+  return YM_OK;
+}
+
+int ym_num_ops(ym_ctx* c) { return c ? (int)c->ops.size() : fail(YM_EINVAL, "null context"); }
+
+const char* ym_op_name(ym_ctx* c, int i) {
+  if (!c || i < 0 || i >= (int)c->ops.size()) return "";
+  return c->ops[i].name;
+}
+
+int ym_num_buffers(ym_ctx* c) { return c ? (int)c->bufs.size() : fail(YM_EINVAL, "null context"); }
+
+int ym_buffer_info(ym_ctx* c, int b, void** ptr, int* C, int* H, int* W, int* elem_bytes) {
+  if (!c || b < 0 || b >= (int)c->bufs.size()) return fail(YM_EINVAL, "bad buffer id");
+  if (!c->d_arena) return fail(YM_ESTATE, "no workspace yet (run ym_infer first)");
+  if (ptr) *ptr = c->bptr(b);
+  if (C) *C = c->bufs[b].C;
+  if (H) *H = c->buf_H(b);
+  if (W) *W = c->buf_Wd(b);
+  if (elem_bytes) *elem_bytes = c->elem(b);
+  return YM_OK;
+}
+
+int ym_read_buffer(ym_ctx* c, int b, void* dst, size_t bytes) {
+  if (!c || b < 0 || b >= (int)c->bufs.size() || !dst) return fail(YM_EINVAL, "bad buffer id or null dst");
+  if (!c->d_arena) return fail(YM_ESTATE, "no workspace yet (run ym_infer first)");
+  const size_t cap = (size_t)c->cB * c->buf_P(b) * c->bufs[b].C * c->elem(b);
+  if (bytes > cap) return fail(YM_EINVAL, "read of %zu bytes exceeds buffer size %zu", bytes, cap);
+  HIPCK(hipSetDevice(c->device));
+  HIPCK(hipDeviceSynchronize());
+  HIPCK(hipMemcpy(dst, c->bptr(b), bytes, hipMemcpyDefault));
+  return YM_OK;
+}
+
+int ym_sync(ym_ctx* c) {
+  if (!c) return fail(YM_EINVAL, "null context");
+  HIPCK(hipSetDevice(c->device));
+  HIPCK(hipDeviceSynchronize());
+  return YM_OK;
+}
+
+void ym_destroy(ym_ctx* c) { delete c; }
+
+}  // extern "C"

@@ -1,0 +1,351 @@
+"""YOLO11 graph → flat NHWC execution plan for the HIP runtime.
+
+This is the MI355X-side description of the graph the reference reaches through `ultralytics.YOLO(...)`
+(`core/model.py:106-110`; architecture restated in SURVEY Appendix A).  It is *not* a module tree: it is a list of
+fused kernel launches over channel-sliced NHWC buffers:
+
+* every `Conv` (conv2d → BN → SiLU) is one implicit-GEMM launch with BN folded into weight/bias
+  (Ultralytics `fuse_conv_and_bn`, eps 1e-3) and the activation, Bottleneck residual add and concat placement done
+  in the epilogue (producers write straight into a channel slice of the concat buffer: no cat kernels);
+* `Upsample(2, nearest)` + `Concat` never materialise: the consumer conv gets two A-sources, the first read at
+  (y>>1, x>>1) (`up` flag);
+* SPPF's three cascaded MaxPool2d(5,1,2) are one kernel writing three slices (max5∘max5 = max9, max5∘max5∘max5 =
+  max13 exactly, with -inf padding);
+* C2PSA's attention + positional depthwise conv is one kernel; `proj`/`ffn` residuals are conv epilogues;
+* the Detect head's final 1x1 convs write fp32 straight into an anchor-major (B, A, no) buffer, which the decode
+  and NMS kernels consume.
+
+The same walk also enumerates every parameter with its Ultralytics state-dict name and shape, so synthetic weights
+(`yolomi.synth`) and real checkpoints pack the same way.
+"""
+from __future__ import annotations
+
+import math
+from dataclasses import dataclass, field
+from typing import Dict, List, Optional, Tuple
+
+# scale → (depth, width, max_channels); SURVEY Appendix A parse rules
+SCALES = {
+    "n": (0.50, 0.25, 1024),
+    "s": (0.50, 0.50, 1024),
+    "m": (0.50, 1.00, 512),
+    "l": (1.00, 1.00, 512),
+    "x": (1.00, 1.50, 512),
+}
+
+NC = 80
+REG_MAX = 16
+STRIDES = (8, 16, 32)
+
+
+def make_divisible(x: float, d: int = 8) -> int:
+    return int(math.ceil(x / d) * d)
+
+
+@dataclass
+class Buffer:
+    id: int
+    C: int
+    f: int            # spatial down-sampling factor w.r.t. the input (1, 2, ... 32); 0 = anchor-major buffer
+    f32: bool = False  # storage fp32 regardless of activation dtype (head outputs)
+    name: str = ""
+
+
+@dataclass
+class View:
+    buf: Buffer
+    coff: int
+    C: int
+
+
+@dataclass
+class Op:
+    kind: str
+    args: Dict
+    name: str = ""
+
+
+@dataclass
+class Param:
+    name: str
+    shape: Tuple[int, ...]
+    kind: str
+    extra: Dict = field(default_factory=dict)
+
+
+class GraphBuilder:
+    def __init__(self, scale: str = "n", task: str = "detect", nc: int = NC):
+        if scale not in SCALES:
+            raise ValueError(f"Unsupported size: {scale}")
+        if task not in ("detect", "segment"):
+            raise ValueError(f"task {task!r} has no HIP plan (supported: detect, segment)")
+        self.scale, self.task, self.nc = scale, task, nc
+        self.depth, self.width, self.max_ch = SCALES[scale]
+        self.buffers: List[Buffer] = []
+        self.ops: List[Op] = []
+        self.params: List[Param] = []
+        self.flops_per_pixel: List[Tuple[str, int, int]] = []  # (op name, factor, MACs per output pixel)
+        self._build()
+
+    # ------------------------------------------------------------------ helpers
+    def ch(self, c: int) -> int:
+        return make_divisible(min(c, self.max_ch) * self.width, 8)
+
+    def rep(self, n: int) -> int:
+        return max(round(n * self.depth), 1) if n > 1 else n
+
+    def buf(self, C: int, f: int, name: str, f32: bool = False) -> Buffer:
+        b = Buffer(len(self.buffers), C, f, f32, name)
+        self.buffers.append(b)
+        return b
+
+    def full(self, b: Buffer) -> View:
+        return View(b, 0, b.C)
+
+    def _conv_params(self, prefix: str, c1: int, c2: int, k: int, g: int = 1, bn: bool = True, bias_kind=None,
+                     extra=None):
+        w_kind = "conv_w" if bn else "head_w"
+        self.params.append(Param(f"{prefix}.conv.weight" if bn else f"{prefix}.weight", (c2, c1 // g, k, k), w_kind))
+        if bn:
+            for suf, kind in (("weight", "bn_w"), ("bias", "bn_b"), ("running_mean", "bn_mean"),
+                              ("running_var", "bn_var")):
+                self.params.append(Param(f"{prefix}.bn.{suf}", (c2,), kind))
+            self.params.append(Param(f"{prefix}.bn.num_batches_tracked", (), "count"))
+        else:
+            self.params.append(Param(f"{prefix}.bias", (c2,), bias_kind or "bias", extra or {}))
+
+    def conv(self, prefix: str, src: View, c2: int, k: int, s: int, dst: View, act: bool = True,
+             res: Optional[View] = None, src1: Optional[View] = None, up0: bool = False, bn: bool = True,
+             bias_kind=None, extra=None, anchor_level: int = -1, shuffle2x2: bool = False):
+        c1 = src.C + (src1.C if src1 is not None else 0)
+        self._conv_params(prefix, c1, c2, k, 1, bn, bias_kind, extra)
+        assert dst.C == (4 * c2 if shuffle2x2 else c2) or anchor_level >= 0 or shuffle2x2
+        self.ops.append(Op("conv", dict(k=k, s=s, c1=c1, c2=c2, act=act, src0=src, up0=up0, src1=src1, dst=dst,
+                                        res=res, anchor_level=anchor_level, shuffle2x2=shuffle2x2, bn=bn,
+                                        wkey=prefix), prefix))
+        fin = src.buf.f * (2 if s == 2 else 1) // (2 if up0 else 1)
+        self.flops_per_pixel.append((prefix, fin, k * k * c1 * c2))
+
+    def dwconv(self, prefix: str, src: View, dst: View, act: bool = True):
+        C = src.C
+        self._conv_params(prefix, C, C, 3, g=C)
+        self.ops.append(Op("dwconv", dict(C=C, act=act, src=src, dst=dst, wkey=prefix), prefix))
+        self.flops_per_pixel.append((prefix, src.buf.f, 9 * C))
+
+    # ------------------------------------------------------------------ modules
+    def Conv(self, i: int, x: View, c2: int, k: int, s: int) -> View:
+        f = x.buf.f * s
+        out = self.buf(c2, f, f"L{i}")
+        self.conv(f"model.{i}", x, c2, k, s, self.full(out))
+        return self.full(out)
+
+    def bottleneck(self, prefix: str, x: View, c: int, e: float, dst: View, f: int):
+        c_ = int(c * e)
+        h = self.buf(c_, f, prefix + ".h")
+        self.conv(prefix + ".cv1", x, c_, 3, 1, self.full(h))
+        self.conv(prefix + ".cv2", self.full(h), c, 3, 1, dst, res=x)
+
+    def c3k(self, prefix: str, x: View, c: int, dst: View, f: int, n: int = 2):
+        c_ = int(c * 0.5)
+        cat = self.buf(2 * c_, f, prefix + ".cat")
+        t = self.buf(c_, f, prefix + ".t0")
+        self.conv(prefix + ".cv1", x, c_, 1, 1, self.full(t))
+        self.conv(prefix + ".cv2", x, c_, 1, 1, View(cat, c_, c_))
+        cur = self.full(t)
+        for j in range(n):
+            last = j == n - 1
+            nxt = View(cat, 0, c_) if last else self.full(self.buf(c_, f, f"{prefix}.t{j + 1}"))
+            self.bottleneck(f"{prefix}.m.{j}", cur, c_, 1.0, nxt, f)
+            cur = nxt
+        self.conv(prefix + ".cv3", self.full(cat), c, 1, 1, dst)
+
+    def C3k2(self, i: int, x: View, c2: int, n: int, c3k: bool, e: float, x1: Optional[View] = None,
+             up0: bool = False) -> View:
+        if self.scale in "mlx":
+            c3k = True
+        n = self.rep(n)
+        f = x.buf.f // (2 if up0 else 1)
+        c = int(c2 * e)
+        cat = self.buf((2 + n) * c, f, f"L{i}.cat")
+        self.conv(f"model.{i}.cv1", x, 2 * c, 1, 1, View(cat, 0, 2 * c), src1=x1, up0=up0)
+        prev = View(cat, c, c)
+        for j in range(n):
+            dst = View(cat, (2 + j) * c, c)
+            if c3k:
+                self.c3k(f"model.{i}.m.{j}", prev, c, dst, f)
+            else:
+                self.bottleneck(f"model.{i}.m.{j}", prev, c, 0.5, dst, f)
+            prev = dst
+        out = self.buf(c2, f, f"L{i}")
+        self.conv(f"model.{i}.cv2", self.full(cat), c2, 1, 1, self.full(out))
+        return self.full(out)
+
+    def SPPF(self, i: int, x: View, c2: int) -> View:
+        c_ = x.C // 2
+        f = x.buf.f
+        cat = self.buf(4 * c_, f, f"L{i}.cat")
+        self.conv(f"model.{i}.cv1", x, c_, 1, 1, View(cat, 0, c_))
+        self.ops.append(Op("sppf", dict(C=c_, src=View(cat, 0, c_), dst=cat), f"model.{i}.m"))
+        out = self.buf(c2, f, f"L{i}")
+        self.conv(f"model.{i}.cv2", self.full(cat), c2, 1, 1, self.full(out))
+        return self.full(out)
+
+    def C2PSA(self, i: int, x: View, c2: int, n: int) -> View:
+        n = self.rep(n)
+        f = x.buf.f
+        c = int(x.C * 0.5)
+        nh = c // 64
+        hd = c // nh
+        kd = int(hd * 0.5)
+        h = c + 2 * nh * kd
+        cv1 = self.buf(2 * c, f, f"L{i}.cv1")
+        self.conv(f"model.{i}.cv1", x, 2 * c, 1, 1, self.full(cv1))
+        b = View(cv1, c, c)
+        for j in range(n):
+            p = f"model.{i}.m.{j}"
+            qkv = self.buf(h, f, p + ".qkv")
+            self.conv(p + ".attn.qkv", b, h, 1, 1, self.full(qkv), act=False)
+            ao = self.buf(c, f, p + ".attn.o")
+            self._conv_params(p + ".attn.pe", c, c, 3, g=c)
+            self.ops.append(Op("attn", dict(C=c, nh=nh, kd=kd, hd=hd, qkv=self.full(qkv), dst=self.full(ao),
+                                            wkey=p + ".attn.pe"), p + ".attn"))
+            self.flops_per_pixel.append((p + ".attn.pe", f, 9 * c))
+            b1 = self.buf(c, f, p + ".b1")
+            self.conv(p + ".attn.proj", self.full(ao), c, 1, 1, self.full(b1), act=False, res=b)
+            ff = self.buf(2 * c, f, p + ".ffn")
+            self.conv(p + ".ffn.0", self.full(b1), 2 * c, 1, 1, self.full(ff))
+            b2 = self.buf(c, f, p + ".b2")
+            self.conv(p + ".ffn.1", self.full(ff), c, 1, 1, self.full(b2), act=False, res=self.full(b1))
+            b = self.full(b2)
+        out = self.buf(c2, f, f"L{i}")
+        self.conv(f"model.{i}.cv2", View(cv1, 0, c), c2, 1, 1, self.full(out), src1=b)
+        return self.full(out)
+
+    def Detect(self, i: int, xs: List[View]):
+        nc = self.nc
+        no = nc + 4 * REG_MAX
+        nm = 32 if self.task == "segment" else 0
+        self.no, self.nm = no, nm
+        anchor = self.buf(no + nm, 0, "anchors", f32=True)
+        self.anchor_buf = anchor
+        ch0 = xs[0].C
+        c2 = max(16, ch0 // 4, REG_MAX * 4)
+        c3 = max(ch0, min(nc, 100))
+        p = f"model.{i}"
+        if self.task == "segment":  # Proto on P3 (Segment.forward computes it first)
+            npr = make_divisible(min(256, self.max_ch) * self.width, 8)
+            f = xs[0].buf.f
+            p1 = self.buf(npr, f, "proto.cv1")
+            self.conv(f"{p}.proto.cv1", xs[0], npr, 3, 1, self.full(p1))
+            p2 = self.buf(npr, f // 2, "proto.up")
+            # ConvTranspose2d(npr, npr, 2, 2, bias): a 1x1 GEMM with N = 4*npr scattered 2x2 (pixel shuffle)
+            self.params.append(Param(f"{p}.proto.upsample.weight", (npr, npr, 2, 2), "convT_w"))
+            self.params.append(Param(f"{p}.proto.upsample.bias", (npr,), "bias"))
+            self.ops.append(Op("conv", dict(k=1, s=1, c1=npr, c2=4 * npr, act=False, src0=self.full(p1), up0=False,
+                                            src1=None, dst=self.full(p2), res=None, anchor_level=-1,
+                                            shuffle2x2=True, bn=False, wkey=f"{p}.proto.upsample", convT=True),
+                               f"{p}.proto.upsample"))
+            self.flops_per_pixel.append((f"{p}.proto.upsample", f, 4 * npr * npr))
+            p3 = self.buf(npr, f // 2, "proto.cv2")
+            self.conv(f"{p}.proto.cv2", self.full(p2), npr, 3, 1, self.full(p3))
+            proto = self.buf(nm, f // 2, "proto", f32=True)
+            self.conv(f"{p}.proto.cv3", self.full(p3), nm, 1, 1, self.full(proto))
+            self.proto_buf = proto
+        for l, x in enumerate(xs):
+            f = x.buf.f
+            # box branch cv2: Conv(x,c2,3) → Conv(c2,c2,3) → Conv2d(c2, 64, 1)
+            t1 = self.buf(c2, f, f"cv2.{l}.0")
+            self.conv(f"{p}.cv2.{l}.0", x, c2, 3, 1, self.full(t1))
+            t2 = self.buf(c2, f, f"cv2.{l}.1")
+            self.conv(f"{p}.cv2.{l}.1", self.full(t1), c2, 3, 1, self.full(t2))
+            self.conv(f"{p}.cv2.{l}.2", self.full(t2), 4 * REG_MAX, 1, 1, View(anchor, 0, 4 * REG_MAX),
+                      act=False, bn=False, bias_kind="box_b", anchor_level=l)
+            # cls branch cv3: [DWConv(x,x,3) → Conv(x,c3,1)] → [DWConv(c3,c3,3) → Conv(c3,c3,1)] → Conv2d(c3, nc, 1)
+            d1 = self.buf(x.C, f, f"cv3.{l}.0.0")
+            self.dwconv(f"{p}.cv3.{l}.0.0", x, self.full(d1))
+            e1 = self.buf(c3, f, f"cv3.{l}.0.1")
+            self.conv(f"{p}.cv3.{l}.0.1", self.full(d1), c3, 1, 1, self.full(e1))
+            d2 = self.buf(c3, f, f"cv3.{l}.1.0")
+            self.dwconv(f"{p}.cv3.{l}.1.0", self.full(e1), self.full(d2))
+            e2 = self.buf(c3, f, f"cv3.{l}.1.1")
+            self.conv(f"{p}.cv3.{l}.1.1", self.full(d2), c3, 1, 1, self.full(e2))
+            self.conv(f"{p}.cv3.{l}.2", self.full(e2), nc, 1, 1, View(anchor, 4 * REG_MAX, nc), act=False,
+                      bn=False, bias_kind="cls_b",
+                      extra=dict(nc=nc, stride=STRIDES[l], shift=_cls_shift(self.scale)), anchor_level=l)
+            if self.task == "segment":  # mask-coefficient branch cv4: Conv(x,c4,3) → Conv(c4,c4,3) → Conv2d(c4,nm,1)
+                c4 = max(ch0 // 4, nm)
+                m1 = self.buf(c4, f, f"cv4.{l}.0")
+                self.conv(f"{p}.cv4.{l}.0", x, c4, 3, 1, self.full(m1))
+                m2 = self.buf(c4, f, f"cv4.{l}.1")
+                self.conv(f"{p}.cv4.{l}.1", self.full(m1), c4, 3, 1, self.full(m2))
+                self.conv(f"{p}.cv4.{l}.2", self.full(m2), nm, 1, 1, View(anchor, no, nm), act=False, bn=False,
+                          anchor_level=l)
+        self.params.append(Param(f"{p}.dfl.conv.weight", (1, REG_MAX, 1, 1), "dfl"))
+        self.ops.append(Op("decode", dict(anchor=anchor, nc=nc, nm=nm), f"{p}.decode"))
+        self.ops.append(Op("nms", dict(nc=nc, nm=nm), f"{p}.nms"))
+
+    # ------------------------------------------------------------------ the graph
+    def _build(self):
+        self.input = self.buf(8, 1, "input")  # RGB padded to 8 channels (16 B per pixel in fp16)
+        self.ops.append(Op("input", dict(dst=self.input), "input"))
+        x = View(self.input, 0, 3)
+        ch = self.ch
+        L0 = self.Conv(0, x, ch(64), 3, 2)
+        L1 = self.Conv(1, L0, ch(128), 3, 2)
+        L2 = self.C3k2(2, L1, ch(256), 2, False, 0.25)
+        L3 = self.Conv(3, L2, ch(256), 3, 2)
+        L4 = self.C3k2(4, L3, ch(512), 2, False, 0.25)
+        L5 = self.Conv(5, L4, ch(512), 3, 2)
+        L6 = self.C3k2(6, L5, ch(512), 2, True, 0.5)
+        L7 = self.Conv(7, L6, ch(1024), 3, 2)
+        L8 = self.C3k2(8, L7, ch(1024), 2, True, 0.5)
+        L9 = self.SPPF(9, L8, ch(1024))
+        L10 = self.C2PSA(10, L9, ch(1024), 2)
+        # 11 Upsample + 12 Concat[-1, 6] fold into layer 13's cv1 (two-source A loader, first source up-sampled)
+        L13 = self.C3k2(13, L10, ch(512), 2, False, 0.5, x1=L6, up0=True)
+        L16 = self.C3k2(16, L13, ch(256), 2, False, 0.5, x1=L4, up0=True)
+        L17 = self.Conv(17, L16, ch(256), 3, 2)
+        L19 = self.C3k2(19, L17, ch(512), 2, False, 0.5, x1=L13)
+        L20 = self.Conv(20, L19, ch(512), 3, 2)
+        L22 = self.C3k2(22, L20, ch(1024), 2, True, 0.5, x1=L10)
+        self.Detect(23, [L16, L19, L22])
+        # the stem reads 3 real channels out of the 8-channel padded input: pad its weights' Cin to 8 at pack time
+
+    # ------------------------------------------------------------------ accounting
+    def macs_per_image(self, H: int = 640, W: int = 640) -> int:
+        tot = 0
+        for _, f, m in self.flops_per_pixel:
+            pass
+        # exact count from conv op geometry
+        tot = 0
+        for op in self.ops:
+            a = op.args
+            if op.kind == "conv":
+                fo = self.out_factor(op)
+                npx = (H // fo) * (W // fo)
+                tot += npx * a["k"] * a["k"] * (a["c1"] if op.name != "model.0" else 3) * a["c2"]
+            elif op.kind == "dwconv":
+                f = a["src"].buf.f
+                tot += (H // f) * (W // f) * 9 * a["C"]
+            elif op.kind == "attn":
+                f = a["qkv"].buf.f
+                N = (H // f) * (W // f)
+                tot += N * N * a["nh"] * (a["kd"] + a["hd"]) + N * 9 * a["C"]
+        return tot
+
+    def out_factor(self, op: Op) -> int:
+        a = op.args
+        fin = a["src0"].buf.f // (2 if a["up0"] else 1)
+        if a["anchor_level"] >= 0:
+            return fin
+        return fin * a["s"]
+
+
+def _cls_shift(scale: str) -> float:
+    from .synth import CLS_BIAS_SHIFT
+    return CLS_BIAS_SHIFT[scale]
+
+
+def param_specs(scale: str = "n", task: str = "detect"):
+    g = GraphBuilder(scale, task)
+    return [(p.name, p.shape, p.kind, p.extra) for p in g.params]

@@ -1,0 +1,135 @@
+"""ctypes binding of `include/yolomi.h` (libyolomi.so, built in-tree for gfx950 by csrc/Makefile).
+
+There is no fallback: if the library or a GPU is missing, constructing a `Runtime` raises.
+"""
+from __future__ import annotations
+
+import ctypes as C
+import os
+from pathlib import Path
+
+LIB_PATH = Path(__file__).resolve().parent / "libyolomi.so"
+
+YM_ERRORS = {-1: "EINVAL", -2: "EBLOB", -3: "EHIP", -4: "ENOMEM", -5: "ESTATE"}
+
+
+class YMError(RuntimeError):
+    pass
+
+
+class ModelDesc(C.Structure):
+    _fields_ = [("max_batch", C.c_int), ("max_h", C.c_int), ("max_w", C.c_int), ("reserved", C.c_int * 5)]
+
+
+class InferArgs(C.Structure):
+    _fields_ = [("conf", C.c_float), ("max_wh", C.c_float), ("iou", C.c_double), ("max_det", C.c_int),
+                ("max_nms", C.c_int), ("agnostic", C.c_int), ("in_eps", C.c_float), ("has_classes", C.c_int),
+                ("classes", C.c_uint32 * 4), ("use_graph", C.c_int), ("reserved", C.c_int * 7)]
+
+
+_lib = None
+
+
+def load_library(path: os.PathLike = LIB_PATH):
+    """Load libyolomi.so once. torch must be imported first so the process shares torch's HIP runtime."""
+    global _lib
+    if _lib is not None:
+        return _lib
+    import torch  # noqa: F401  (binds libamdhip64 first; our .so then resolves to the same runtime)
+    if not Path(path).exists():
+        raise YMError(f"{path} not found: build it with `make -C yolo-infer_amd/csrc` "
+                      f"(or __graft_entry__.build()); there is no CPU fallback")
+    lib = C.CDLL(str(path))
+    P, I, F = C.c_void_p, C.c_int, C.POINTER(C.c_float)
+    sig = {
+        "ym_create": (I, [I, C.POINTER(ModelDesc), C.POINTER(P)]),
+        "ym_load_weights": (I, [P, P, C.c_size_t]),
+        "ym_infer": (I, [P, P, I, I, I, C.POINTER(InferArgs), P, P, P]),
+        "ym_profile": (I, [P, P, I, I, I, C.POINTER(InferArgs), P, P, P, F, I]),
+        "ym_num_ops": (I, [P]),
+        "ym_op_name": (C.c_char_p, [P, I]),
+        "ym_num_buffers": (I, [P]),
+        "ym_buffer_info": (I, [P, I, C.POINTER(P), C.POINTER(I), C.POINTER(I), C.POINTER(I), C.POINTER(I)]),
+        "ym_read_buffer": (I, [P, I, P, C.c_size_t]),
+        "ym_sync": (I, [P]),
+        "ym_last_error": (C.c_char_p, []),
+        "ym_destroy": (None, [P]),
+        "ym_version": (I, []),
+    }
+    for name, (res, args) in sig.items():
+        fn = getattr(lib, name)
+        fn.restype = res
+        fn.argtypes = args
+    _lib = lib
+    return lib
+
+
+EXPORTED = ("ym_create", "ym_load_weights", "ym_infer", "ym_profile", "ym_num_ops", "ym_op_name", "ym_num_buffers",
+            "ym_buffer_info", "ym_read_buffer", "ym_sync", "ym_last_error", "ym_destroy", "ym_version")
+
+
+def _check(rc: int):
+    if rc != 0:
+        msg = _lib.ym_last_error().decode(errors="replace")
+        raise YMError(f"yolomi {YM_ERRORS.get(rc, rc)}: {msg}")
+
+
+class Runtime:
+    """One ym_ctx on one device holding one packed model."""
+
+    def __init__(self, device_index: int, blob: bytes):
+        self.lib = load_library()
+        self.ctx = C.c_void_p()
+        desc = ModelDesc()
+        _check(self.lib.ym_create(device_index, C.byref(desc), C.byref(self.ctx)))
+        buf = C.create_string_buffer(blob, len(blob))
+        _check(self.lib.ym_load_weights(self.ctx, C.cast(buf, C.c_void_p), len(blob)))
+        self.n_ops = self.lib.ym_num_ops(self.ctx)
+        self.op_names = [self.lib.ym_op_name(self.ctx, i).decode() for i in range(self.n_ops)]
+
+    @staticmethod
+    def make_args(conf=0.25, iou=0.7, max_det=300, max_nms=30000, agnostic=False, max_wh=7680.0, in_eps=1.1920929e-07,
+                  classes=None, use_graph=True) -> InferArgs:
+        a = InferArgs()
+        a.conf, a.iou, a.max_det, a.max_nms = float(conf), float(iou), int(max_det), int(max_nms)
+        a.agnostic, a.max_wh, a.in_eps, a.use_graph = int(bool(agnostic)), float(max_wh), float(in_eps), int(use_graph)
+        if classes is not None:
+            a.has_classes = 1
+            for c in classes:
+                c = int(c)
+                if not 0 <= c < 128:
+                    raise ValueError(f"class id {c} out of range [0, 128)")
+                a.classes[c >> 5] |= 1 << (c & 31)
+        return a
+
+    def infer(self, x_ptr: int, B: int, H: int, W: int, args: InferArgs, dets_ptr: int, counts_ptr: int, stream: int):
+        _check(self.lib.ym_infer(self.ctx, C.c_void_p(x_ptr), B, H, W, C.byref(args), C.c_void_p(dets_ptr),
+                                 C.c_void_p(counts_ptr), C.c_void_p(stream)))
+
+    def profile(self, x_ptr, B, H, W, args, dets_ptr, counts_ptr, stream):
+        ms = (C.c_float * self.n_ops)()
+        _check(self.lib.ym_profile(self.ctx, C.c_void_p(x_ptr), B, H, W, C.byref(args), C.c_void_p(dets_ptr),
+                                   C.c_void_p(counts_ptr), C.c_void_p(stream), ms, self.n_ops))
+        return list(ms)
+
+    def buffer_info(self, buf: int):
+        p, c, h, w, e = C.c_void_p(), C.c_int(), C.c_int(), C.c_int(), C.c_int()
+        _check(self.lib.ym_buffer_info(self.ctx, buf, C.byref(p), C.byref(c), C.byref(h), C.byref(w), C.byref(e)))
+        return p.value, c.value, h.value, w.value, e.value
+
+    def read_buffer(self, buf: int, dst_ptr: int, nbytes: int):
+        _check(self.lib.ym_read_buffer(self.ctx, buf, C.c_void_p(dst_ptr), nbytes))
+
+    def sync(self):
+        _check(self.lib.ym_sync(self.ctx))
+
+    def close(self):
+        if self.ctx:
+            self.lib.ym_destroy(self.ctx)
+            self.ctx = C.c_void_p()
+
+    def __del__(self):
+        try:
+            self.close()
+        except Exception:
+            pass

@@ -1,0 +1,156 @@
+"""Model blob packer: Ultralytics-style state dict + YOLO11 plan → one binary blob for `ym_load_weights`.
+
+Replaces what Ultralytics' AutoBackend(fuse=True) does on first predict: Conv+BN folding
+(`fuse_conv_and_bn`, restated bit-for-bit in fp32: W' = (γ/√(eps+σ²))·W, b' = β − γ·μ/√(σ²+eps)), then — the MI355X
+part — packing every conv as a K-contiguous GEMM B operand [N][Kpad] with K ordered (ky, kx, c) to match the NHWC
+implicit-GEMM loader (`csrc/ym_conv.hip`), the stem's Cin padded 3→8, ConvTranspose2d(2,2) re-laid out as a 1x1
+GEMM with N = 4·C (pixel-shuffle epilogue), depthwise weights as [9][C] fp32.
+
+Blob layout (int32 little-endian; parsed by `csrc/ym_runtime.cpp:ym_load_weights`):
+  header[32] | buffers[nbuf][8] | ops[nop][32] | names[nop][48 bytes] | pad to 256 | weights
+"""
+from __future__ import annotations
+
+import struct
+from typing import Dict, List
+
+import numpy as np
+
+from .arch import REG_MAX, STRIDES, GraphBuilder
+
+MAGIC = 0x4C504D59
+VERSION = 1
+OP_IDS = {"input": 1, "conv": 2, "dwconv": 3, "sppf": 4, "attn": 5, "decode": 6, "nms": 7}
+DTYPES = {"f16": 0, "f32": 1}
+BK = 32
+
+
+def fuse_conv_bn(w: np.ndarray, gamma, beta, mean, var, eps=1e-3):
+    """ultralytics.utils.torch_utils.fuse_conv_and_bn in fp32 (bit-identical to the torch CPU path)."""
+    f = np.float32
+    w = w.astype(f)
+    scale = gamma.astype(f) / np.sqrt(f(eps) + var.astype(f))
+    wf = (scale.reshape(-1, *([1] * (w.ndim - 1))) * w).astype(f)
+    bf = (beta.astype(f) - (gamma.astype(f) * mean.astype(f)) / np.sqrt(var.astype(f) + f(eps))).astype(f)
+    return wf, bf
+
+
+class _WeightArena:
+    def __init__(self):
+        self.chunks: List[bytes] = []
+        self.size = 0
+
+    def add(self, arr: np.ndarray) -> int:
+        off = self.size
+        b = np.ascontiguousarray(arr).tobytes()
+        pad = (-len(b)) % 256
+        self.chunks.append(b + b"\0" * pad)
+        self.size += len(b) + pad
+        return off
+
+    def bytes(self) -> bytes:
+        return b"".join(self.chunks)
+
+
+def _conv_weights(a: dict, sd: Dict[str, np.ndarray]):
+    key = a["wkey"]
+    if a.get("convT"):
+        wt = sd[key + ".weight"].astype(np.float32)  # (in, out, 2, 2)
+        cin, cout = wt.shape[0], wt.shape[1]
+        # GEMM column n = (dy*2 + dx)*cout + o  ←  wt[c, o, dy, dx]
+        wg = np.transpose(wt, (2, 3, 1, 0)).reshape(4 * cout, cin)
+        bg = np.tile(sd[key + ".bias"].astype(np.float32), 4)
+        return wg[:, None, None, :], bg  # (N, 1, 1, cin)
+    if a["bn"]:
+        w, b = fuse_conv_bn(sd[key + ".conv.weight"], sd[key + ".bn.weight"], sd[key + ".bn.bias"],
+                            sd[key + ".bn.running_mean"], sd[key + ".bn.running_var"])
+    else:
+        w, b = sd[key + ".weight"].astype(np.float32), sd[key + ".bias"].astype(np.float32)
+    return np.transpose(w, (0, 2, 3, 1)), b  # (cout, k, k, cin) = NHWC-K order
+
+
+def _dw_weights(key: str, sd):
+    w, b = fuse_conv_bn(sd[key + ".conv.weight"], sd[key + ".bn.weight"], sd[key + ".bn.bias"],
+                        sd[key + ".bn.running_mean"], sd[key + ".bn.running_var"])
+    C = w.shape[0]
+    return np.ascontiguousarray(w.reshape(C, 9).T).astype(np.float32), b  # [9][C]
+
+
+def pack_model(scale: str, task: str, sd: Dict[str, np.ndarray], dtype: str = "f16") -> bytes:
+    g = GraphBuilder(scale, task)
+    return pack_graph(g, sd, dtype)
+
+
+def pack_graph(g: GraphBuilder, sd: Dict[str, np.ndarray], dtype: str = "f16") -> bytes:
+    if dtype not in DTYPES:
+        raise ValueError(f"dtype {dtype!r} not in {list(DTYPES)}")
+    np_dt = np.float16 if dtype == "f16" else np.float32
+    arena = _WeightArena()
+    op_recs: List[List[int]] = []
+    names: List[bytes] = []
+    for op in g.ops:
+        a = op.args
+        r = [0] * 32
+        r[0] = OP_IDS[op.kind]
+        if op.kind == "conv":
+            w, b = _conv_weights(a, sd)  # (N, k, k, cin)
+            src0 = a["src0"]
+            C0 = src0.C
+            if src0.buf is g.input:  # stem: RGB padded to 8 channels
+                pad = 8 - C0
+                w = np.concatenate([w, np.zeros(w.shape[:3] + (pad,), np.float32)], axis=3)
+                C0 = 8
+            N = w.shape[0]
+            K = w.shape[1] * w.shape[2] * w.shape[3]
+            Kpad = (K + BK - 1) // BK * BK
+            wp = np.zeros((N, Kpad), np.float32)
+            wp[:, :K] = w.reshape(N, K)
+            src1 = a["src1"]
+            C1 = src1.C if src1 is not None else 0
+            dst, res = a["dst"], a["res"]
+            r[1:6] = [a["k"], a["s"], C0 + C1, N, int(bool(a["act"]))]
+            r[6:10] = [src0.buf.id, src0.coff, C0, int(bool(a["up0"]))]
+            r[10:13] = [src1.buf.id, src1.coff, C1] if src1 is not None else [-1, 0, 0]
+            r[13:17] = [dst.buf.id, dst.coff, a["anchor_level"], int(bool(a["shuffle2x2"]))]
+            r[17:19] = [res.buf.id, res.coff] if res is not None else [-1, 0]
+            r[19] = arena.add(wp.astype(np_dt))
+            r[20] = arena.add(b.astype(np.float32))
+            r[21] = Kpad
+        elif op.kind == "dwconv":
+            w9, b = _dw_weights(a["wkey"], sd)
+            r[3], r[5] = a["C"], int(bool(a["act"]))
+            r[6], r[7] = a["src"].buf.id, a["src"].coff
+            r[13], r[14] = a["dst"].buf.id, a["dst"].coff
+            r[19], r[20] = arena.add(w9), arena.add(b)
+        elif op.kind == "sppf":
+            r[3] = a["C"]
+            r[7] = a["src"].coff
+            r[13] = a["dst"].id
+        elif op.kind == "attn":
+            w9, b = _dw_weights(a["wkey"], sd)
+            r[3], r[4], r[5], r[9] = a["C"], a["nh"], a["kd"], a["hd"]
+            r[6], r[7] = a["qkv"].buf.id, a["qkv"].coff
+            r[13], r[14] = a["dst"].buf.id, a["dst"].coff
+            r[19], r[20] = arena.add(w9), arena.add(b)
+            r[21] = struct.unpack("<i", struct.pack("<f", float(np.float32(a["kd"] ** -0.5))))[0]
+        op_recs.append(r)
+        nm = op.name.encode()[:47]
+        names.append(nm + b"\0" * (48 - len(nm)))
+
+    wbytes = arena.bytes()
+    hdr = [0] * 32
+    hdr[0], hdr[1], hdr[2] = MAGIC, VERSION, DTYPES[dtype]
+    hdr[3] = 1 if g.task == "segment" else 0
+    hdr[4], hdr[5], hdr[6], hdr[7] = g.nc, g.nm, REG_MAX, len(STRIDES)
+    hdr[8:11] = list(STRIDES)
+    hdr[11], hdr[12] = len(g.buffers), len(g.ops)
+    hdr[13], hdr[14] = len(wbytes) & 0xFFFFFFFF, len(wbytes) >> 32
+    hdr[15], hdr[16] = g.input.id, g.anchor_buf.id
+    hdr[17] = g.proto_buf.id if g.task == "segment" else -1
+    hdr[18] = g.no
+    head = struct.pack("<32i", *hdr)
+    bufs = b"".join(struct.pack("<8i", b.C, b.f, int(b.f32), 0, 0, 0, 0, 0) for b in g.buffers)
+    ops = b"".join(struct.pack("<32i", *rr) for rr in op_recs)
+    meta = head + bufs + ops + b"".join(names)
+    meta += b"\0" * ((-len(meta)) % 256)
+    return meta + wbytes
