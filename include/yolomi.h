@@ -72,6 +72,15 @@ int ym_infer(ym_ctx* ctx, const float* d_input, int B, int H, int W, const ym_in
 int ym_profile(ym_ctx* ctx, const float* d_input, int B, int H, int W, const ym_infer_args* args, float* d_dets,
                int* d_counts, void* stream, float* op_ms, int n_ops);
 
+/* On-device autotuning of the conv tile configuration, per op, for input shape (B, H, W): every candidate is timed
+ * as `reps` graph-captured back-to-back launches on this GPU (after one real forward so the buffers hold real
+ * activations); the fastest is kept for this shape.  Synchronous.  ym_get_op_cfg / ym_set_op_cfg export / import
+ * the per-op choices (n_ops ints, -1 = built-in heuristic) so a tuned plan can be pinned. */
+int ym_tune(ym_ctx* ctx, const float* d_input, int B, int H, int W, const ym_infer_args* args, float* d_dets,
+            int* d_counts, void* stream, int reps);
+int ym_get_op_cfg(ym_ctx* ctx, int* cfg, int n_ops);
+int ym_set_op_cfg(ym_ctx* ctx, int B, int H, int W, const int* cfg, int n_ops);
+
 /* Introspection for tests / bisecting: op count & names, and the device view of plan buffer `buf` as produced by
  * the last ym_infer/ym_profile (NHWC; elem_bytes 2 = fp16, 4 = fp32; for the anchor buffer H=1, W=A). */
 int ym_num_ops(ym_ctx* ctx);

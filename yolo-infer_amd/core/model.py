@@ -90,7 +90,11 @@ class YOLO11Model:
     HIP_TASKS = ("detect", "segment")
 
     def __init__(self, model_path: Optional[Union[str, Path]] = None, task: str = "detect", size: str = "n",
-                 device: Optional[str] = None, verbose: bool = True, dtype: str = "f16", seed: int = 0):
+                 device: Optional[str] = None, verbose: bool = True, dtype: str = "f16", seed: int = 0,
+                 weights_blob: Optional[bytes] = None):
+        """Extra keyword arguments over the reference: `dtype` ('f16' storage + fp32 accumulate, or 'f32' = exact
+        parity mode), `seed` of the synthetic weights used when no `model_path` is given, and `weights_blob` = an
+        already packed model (e.g. received over an RCCL broadcast from rank 0)."""
         self.task = task
         self.size = size
         self.device = device or self._get_default_device()
@@ -98,6 +102,7 @@ class YOLO11Model:
         self.model_path = model_path
         self.dtype = dtype
         self.seed = seed
+        self._blob = weights_blob
         self.optimization_history: List[Dict[str, Any]] = []
         self._validate_inputs()
         self.model = self._load_model()
@@ -123,11 +128,13 @@ class YOLO11Model:
             dev = torch.device("cuda", torch.cuda.current_device())
         self._dev = dev
         try:
-            if self.model_path:
+            if self._blob is not None:
+                sd = {}
+            elif self.model_path:
                 sd = _load_state_dict(Path(self.model_path))
             else:  # the reference fetches yolo11{size}.pt by name; offline we synthesise weights of that graph
                 sd = synth_weights(self.size, self.task, self.seed)
-            engine = Engine(self.size, self.task, sd, dev, self.dtype)
+            engine = Engine(self.size, self.task, sd, dev, self.dtype, blob=self._blob)
         except Exception as e:
             logger.error(f"Failed to load model: {e}")
             raise

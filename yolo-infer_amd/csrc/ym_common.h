@@ -36,6 +36,13 @@ template <> struct Vec8<float> {
   static __device__ __forceinline__ type zero() { return type{0, 0, 0, 0, 0, 0, 0, 0}; }
 };
 
+// order-preserving float <-> int map (atomicMax on floats of either sign)
+__device__ __forceinline__ int f2ord(float f) {
+  const int i = __float_as_int(f);
+  return i >= 0 ? i : i ^ 0x7FFFFFFF;
+}
+__device__ __forceinline__ float ord2f(int i) { return __int_as_float(i >= 0 ? i : i ^ 0x7FFFFFFF); }
+
 __device__ __forceinline__ float ym_silu(float x) { return x / (1.0f + expf(-x)); }
 __device__ __forceinline__ float ym_sigmoid(float x) { return 1.0f / (1.0f + expf(-x)); }
 
@@ -49,6 +56,8 @@ struct ConvArgs {
   void* dst; int d_ctot, d_coff, d_P, d_pixoff, d_W;            // output view (d_W: dst row width in pixels)
   const void* res; int r_ctot, r_coff, r_P;                     // optional residual view (same geometry as dst)
   int Hin, Win, Ho, Wo, k, s, pad, Cin8, Kc, N, Kpad, act, shuffle, npr, M, tiles_n;
+  // stem only: read the caller's NCHW fp32 input directly, applying LoadTensor's /255 rule on load
+  const float* nchw; const float* ctl; float eps;
 };
 
 struct DwArgs {
@@ -61,6 +70,7 @@ struct DwArgs {
 struct PoolArgs {
   void* buf; int ctot, coff, P;  // y0 at coff, writes y1,y2,y3 at coff+C, +2C, +3C
   int C, H, W, B;
+  int sep;                       // separable (row-max images in LDS) vs direct 2-D windows
 };
 
 struct AttnArgs {
@@ -100,10 +110,12 @@ struct PrepArgs {
 
 // ------------------------------------------------------------------------------------------------------------
 // Host-side launchers (defined in the .hip translation units).
-hipError_t ym_launch_conv(int dtype, int out_f32, const ConvArgs& a, hipStream_t st);
+hipError_t ym_launch_conv(int dtype, int out_f32, const ConvArgs& a, int cfg, hipStream_t st);  // cfg < 0: heuristic
+int ym_conv_num_cfgs();
 hipError_t ym_launch_dwconv(int dtype, const DwArgs& a, hipStream_t st);
 hipError_t ym_launch_sppf(int dtype, const PoolArgs& a, hipStream_t st);
 hipError_t ym_launch_attn(int dtype, const AttnArgs& a, hipStream_t st);
 hipError_t ym_launch_prep(int dtype, const PrepArgs& a, int* counts, int B, hipStream_t st);
 hipError_t ym_launch_decode(const DecodeArgs& a, hipStream_t st);
 hipError_t ym_launch_nms(const NmsArgs& a, hipStream_t st);
+hipError_t ym_launch_stem(int dtype, const ConvArgs& a, hipStream_t st);

@@ -3,241 +3,631 @@
 // Replaces the ATen conv2d + BN + SiLU + cat/upsample/add launches that Ultralytics' DetectionModel issues per
 // `Conv` module under `YOLO11Model.predict` (/root/reference/core/model.py:133).
 //
-// GEMM view: M = B·Ho·Wo output pixels, N = Cout, K = k·k·Cin ordered (ky, kx, c) so that every 8-element K chunk
-// is 8 consecutive channels of ONE input pixel = one 16-byte NHWC load (f16).  No im2col buffer: the A tile is
-// gathered straight from the producer's NHWC buffer(s):
-//   * two A sources split along K (concat fusion: channels [0, C0) from src0, [C0, C0+C1) from src1);
-//   * src0 may be read at (y>>1, x>>1) (nearest 2x Upsample fused into the consumer's loader);
-//   * channel-offset views (C2f chunk/split, SPPF/C3k2 concat slices) are just (ctot, coff) pairs.
-// Epilogue: + bias (BN folded at pack time), SiLU, + residual (Bottleneck / PSA shortcut), store into a channel
-// slice of the destination buffer, optionally fp32 into the anchor-major Detect buffer, or 2x2 pixel-shuffled
-// (ConvTranspose2d(k=2,s=2) of the Segment Proto).
+// GEMM orientation (transposed on purpose): D[n][m] = Σ_k W[n][k] · X[k][m] with
+//   n = output channel (MFMA rows, A operand = packed weights [N][Kpad]),
+//   m = output pixel   (MFMA cols, B operand = implicit im2col gathered straight from NHWC),
+//   k = (ky, kx, c)    so every 8-element K chunk is 8 consecutive channels of ONE input pixel: one 16-byte load.
+// With v_mfma_f32_32x32x16_f16 each lane then ends up holding 4 consecutive output channels of one pixel
+// (rows (reg&3) + 8(reg>>2) + 4(lane>>5), col lane&31), so the epilogue writes 8-byte NHWC vectors without an LDS
+// transpose.
 //
-// Tiles: BM×BN output tile per 256-thread workgroup (4 waves as 2×2), BK = 32; A/B staged global → registers →
-// LDS with the next K-step's global loads in flight during the current step's MFMAs.
-//   f16 plans: v_mfma_f32_16x16x32_f16 (fp32 accumulate)
-//   f32 plans: v_mfma_f32_16x16x4_f32  (exact-f32 MFMA: the parity mode)
+// Structure (MI355X-specific choices):
+//  * operands go global → VGPRs directly in MFMA fragment layout (A: W[n][8 k] 16 B, B: pixel's 8 channels 16 B),
+//    double-buffered in registers: no LDS and no barrier in the main loop; latency is hidden by the next step's loads
+//    in flight plus 4-8 waves per SIMD;
+//  * intra-workgroup split-K: WK waves share one output tile and take interleaved K steps, then reduce their fp32
+//    partial tiles once through LDS — this puts 4-8x more waves on the small-M deep layers (20x20, 40x40 maps);
+//  * 1x1/stride-1 convs (half the launches) use a division-free gather: pixel row base + channel, with the two-source
+//    concat (C3k2/C2PSA cv1/cv2 inputs) and the nearest-2x upsample (FPN) folded into the row base;
+//  * epilogue: + bias (BN folded at pack time), SiLU, + residual (Bottleneck / PSA shortcut), store into a channel
+//    slice of the destination buffer (zero-copy concat), fp32 into the anchor-major Detect buffer, or 2x2
+//    pixel-shuffled (Segment Proto ConvTranspose2d(2,2)).
+// f16 plans: v_mfma_f32_32x32x16_f16 (fp32 accumulate). f32 plans (parity mode): v_mfma_f32_32x32x2_f32 (exact f32).
+#include <stdlib.h>
+
 #include "ym_common.h"
+
+typedef float f32x16 __attribute__((ext_vector_type(16)));
 
 namespace {
 
-constexpr int BK = 32;
-constexpr int NT = 256;
-
-template <typename T> struct LdsPad { static constexpr int v = 8; };
-template <> struct LdsPad<float> { static constexpr int v = 1; };
+template <typename T> struct Frag;  // one lane's 8 consecutive K values of an MFMA operand
+template <> struct Frag<f16> { typedef f16x8 type; };
+template <> struct Frag<float> { typedef f32x8 type; };
 
 template <typename T>
-__device__ __forceinline__ typename Vec8<T>::type gather_a(const ConvArgs& a, int b, int iy0, int ix0, bool ok,
-                                                           int tap, int cb) {
-  if (!ok) return Vec8<T>::zero();
-  int ky = 0, kx = tap;
-  if (a.k != 1) { ky = tap / a.k; kx = tap - ky * a.k; } else { kx = 0; }
-  const int iy = iy0 + ky, ix = ix0 + kx;
-  if ((unsigned)iy >= (unsigned)a.Hin || (unsigned)ix >= (unsigned)a.Win) return Vec8<T>::zero();
-  const int c = cb * 8;
-  const T* p;
-  if (c < a.C0) {
-    const int sy = a.up0 ? (iy >> 1) : iy;
-    const int sx = a.up0 ? (ix >> 1) : ix;
-    p = static_cast<const T*>(a.src0) + ((size_t)(b * a.s0_P + sy * a.s0_W + sx) * a.s0_ctot + a.s0_coff + c);
-  } else {
-    p = static_cast<const T*>(a.src1) +
-        ((size_t)(b * a.s1_P + iy * a.Win + ix) * a.s1_ctot + a.s1_coff + (c - a.C0));
-  }
-  return Vec8<T>::load(p);
-}
+__device__ __forceinline__ typename Frag<T>::type load8(const T* p) { return Vec8<T>::load(p); }
 
 template <typename T>
-__device__ __forceinline__ void mma_step(const T* As, const T* Bs, int ldk, int lane, int arow, int bcol,
-                                         f32x4& acc);
+__device__ __forceinline__ void mma(const typename Frag<T>::type& a, const typename Frag<T>::type& b, f32x16& acc);
 
-// f16: one 16x16x32 MFMA per (i, j) per K-step. Lane l holds A[row l&15][k 8(l>>4)..+8), B[k ..][col l&15].
 template <>
-__device__ __forceinline__ void mma_step<f16>(const f16* As, const f16* Bs, int ldk, int lane, int arow, int bcol,
-                                              f32x4& acc) {
-  const f16x8 av = *reinterpret_cast<const f16x8*>(As + (arow + (lane & 15)) * ldk + 8 * (lane >> 4));
-  const f16x8 bv = *reinterpret_cast<const f16x8*>(Bs + (bcol + (lane & 15)) * ldk + 8 * (lane >> 4));
-  acc = __builtin_amdgcn_mfma_f32_16x16x32_f16(av, bv, acc, 0, 0, 0);
+__device__ __forceinline__ void mma<f16>(const f16x8& a, const f16x8& b, f32x16& acc) {
+  acc = __builtin_amdgcn_mfma_f32_32x32x16_f16(a, b, acc, 0, 0, 0);
 }
 
-// f32: eight exact-f32 16x16x4 MFMAs per K-step. Lane l holds A[row l&15][k l>>4], B[k l>>4][col l&15].
+// exact-f32: lane half h holds k = 8h..8h+7; MFMA s multiplies the pair {s, 8+s} (same k map on both operands)
 template <>
-__device__ __forceinline__ void mma_step<float>(const float* As, const float* Bs, int ldk, int lane, int arow,
-                                                int bcol, f32x4& acc) {
+__device__ __forceinline__ void mma<float>(const f32x8& a, const f32x8& b, f32x16& acc) {
 #pragma unroll
-  for (int kk = 0; kk < BK; kk += 4) {
-    const float av = As[(arow + (lane & 15)) * ldk + kk + (lane >> 4)];
-    const float bv = Bs[(bcol + (lane & 15)) * ldk + kk + (lane >> 4)];
-    acc = __builtin_amdgcn_mfma_f32_16x16x4f32(av, bv, acc, 0, 0, 0);
+  for (int s = 0; s < 8; ++s) acc = __builtin_amdgcn_mfma_f32_32x32x2f32(a[s], b[s], acc, 0, 0, 0);
+}
+
+template <typename OutT> struct Out4;
+template <> struct Out4<f16> {
+  static __device__ __forceinline__ void store(f16* p, const float* v) {
+    *reinterpret_cast<f16x4*>(p) = f16x4{(f16)v[0], (f16)v[1], (f16)v[2], (f16)v[3]};
+  }
+};
+template <> struct Out4<float> {
+  static __device__ __forceinline__ void store(float* p, const float* v) {
+    *reinterpret_cast<f32x4*>(p) = f32x4{v[0], v[1], v[2], v[3]};
+  }
+};
+
+template <typename T>
+__device__ __forceinline__ void load_res4(const T* p, float* v) {
+  if constexpr (sizeof(T) == 2) {
+    const f16x4 r = *reinterpret_cast<const f16x4*>(p);
+    v[0] += (float)r[0]; v[1] += (float)r[1]; v[2] += (float)r[2]; v[3] += (float)r[3];
+  } else {
+    const f32x4 r = *reinterpret_cast<const f32x4*>(p);
+    v[0] += r[0]; v[1] += r[1]; v[2] += r[2]; v[3] += r[3];
   }
 }
 
-template <typename OutT> __device__ __forceinline__ OutT cvt_out(float x);
-template <> __device__ __forceinline__ f16 cvt_out<f16>(float x) { return (f16)x; }
-template <> __device__ __forceinline__ float cvt_out<float>(float x) { return x; }
+// WTM: 32-pixel blocks per wave; WTN: 32-channel blocks per wave; WM x WN x WK waves per workgroup.
+// KIND 1: 1x1 stride-1 (two sources, optional up-sampled first source); KIND 3: 3x3 (one source, stride a.s);
+// KIND 0: the stem, a 3x3 whose source is the caller's NCHW fp32 batch (3 channels, /255 rule applied on load).
+// One K step = 64 (4 MFMAs per block pair): 4x fewer dependent memory round trips than a 16-deep step.
+constexpr int KSTEP = 64;
+constexpr int KS = KSTEP / 16;
 
-template <typename T, typename OutT, int BM, int BN>
-__global__ __launch_bounds__(NT) void conv_igemm_nhwc(const ConvArgs a) {
-  constexpr int LDK = BK + LdsPad<T>::v;
-  constexpr int NA = (BM * (BK / 8) + NT - 1) / NT;  // A chunks per thread
-  constexpr int NB = (BN * (BK / 8) + NT - 1) / NT;  // B chunks per thread
-  constexpr int TM = BM / 32, TN = BN / 32;           // 16x16 MFMA tiles per wave (2x2 waves)
-  typedef typename Vec8<T>::type V;
-
-  __shared__ T As[BM * LDK];
-  __shared__ T Bs[BN * LDK];
-
-  const int tid = threadIdx.x;
-  const int lane = tid & 63;
-  const int wid = tid >> 6;
-  const int wr = wid >> 1, wc = wid & 1;
-
+// XCD-aware tile map: workgroups are dealt round-robin over the 8 XCDs (bid % 8), so give every N tile of one pixel
+// tile the same bid % 8: the pixel rows they all read then sit in ONE XCD's L2.  The grid is padded to a multiple
+// of 8 pixel tiles; padding workgroups exit immediately.  (Placement only affects speed, never results.)
+__device__ __forceinline__ bool xcd_tile(const ConvArgs& a, int BM, int& tm, int& tn) {
   const int bid = blockIdx.x;
-  const int tn = bid % a.tiles_n;
-  const int tm = bid / a.tiles_n;
-  const int m0 = tm * BM, n0 = tn * BN;
+  const int rest = bid >> 3;
+  tn = rest % a.tiles_n;
+  tm = (rest / a.tiles_n) * 8 + (bid & 7);
+  return tm * BM < a.M;
+}
+
+template <typename T, typename OutT, int WTM, int WTN, int WM, int WN, int WK, int KIND>
+__global__ __launch_bounds__(WM * WN * WK * 64) void conv_igemm(const ConvArgs a) {
+  typedef typename Frag<T>::type F;
+  constexpr int BM = WM * WTM * 32, BN = WN * WTN * 32;
+  const int lane = threadIdx.x & 63;
+  const int wid = threadIdx.x >> 6;
+  const int wk = wid % WK;
+  const int wm = (wid / WK) % WM;
+  const int wn = wid / (WK * WM);
+  const int l32 = lane & 31, h = lane >> 5;
+  int tm, tn;
+  if (!xcd_tile(a, BM, tm, tn)) return;
+  const int pbase = tm * BM + wm * WTM * 32;
+  const int nbase = tn * BN + wn * WTN * 32;
   const int HWo = a.Ho * a.Wo;
 
-  // per-thread A rows: fixed for the whole K loop
-  int rb[NA], riy[NA], rix[NA];
-  bool rok[NA];
-  const int kc = tid & 3;  // this thread's 8-wide chunk inside a BK=32 step (same for every row it loads)
+  // ---- this lane's pixels (one per 32-pixel block)
+  int pb[WTM], py[WTM], px[WTM], iy0[WTM], ix0[WTM];
+  bool pv[WTM];
+  const T* row0[WTM];  // KIND 1: row base in src0 (up-sample mapped); KIND 3: image base in src0
+  const T* row1[WTM];  // KIND 1: row base in src1 (pre-offset by -C0)
 #pragma unroll
-  for (int i = 0; i < NA; ++i) {
-    const int r = (tid + i * NT) >> 2;
-    const int m = m0 + r;
-    rok[i] = (r < BM) && (m < a.M);
-    const int mm = rok[i] ? m : 0;
-    rb[i] = mm / HWo;
-    const int rem = mm - rb[i] * HWo;
-    const int oy = rem / a.Wo;
-    const int ox = rem - oy * a.Wo;
-    riy[i] = oy * a.s - a.pad;
-    rix[i] = ox * a.s - a.pad;
+  for (int i = 0; i < WTM; ++i) {
+    const int m = pbase + i * 32 + l32;
+    pv[i] = m < a.M;
+    const int mm = pv[i] ? m : 0;
+    pb[i] = mm / HWo;
+    const int rem = mm - pb[i] * HWo;
+    py[i] = rem / a.Wo;
+    px[i] = rem - py[i] * a.Wo;
+    if constexpr (KIND == 1) {
+      const int sy = a.up0 ? (py[i] >> 1) : py[i];
+      const int sx = a.up0 ? (px[i] >> 1) : px[i];
+      row0[i] = static_cast<const T*>(a.src0) +
+                ((size_t)(pb[i] * a.s0_P + sy * a.s0_W + sx) * a.s0_ctot + a.s0_coff);
+      row1[i] = a.src1 ? static_cast<const T*>(a.src1) +
+                             ((size_t)(pb[i] * a.s1_P + py[i] * a.Win + px[i]) * a.s1_ctot + a.s1_coff - a.C0)
+                       : row0[i];
+    } else {
+      row0[i] = KIND == 3 ? static_cast<const T*>(a.src0) + ((size_t)pb[i] * a.s0_P * a.s0_ctot + a.s0_coff)
+                          : nullptr;
+      row1[i] = nullptr;
+      iy0[i] = py[i] * a.s - 1;  // top-left input coordinate of the 3x3 window (pad 1)
+      ix0[i] = px[i] * a.s - 1;
+    }
+  }
+  const T* wrow[WTN];
+#pragma unroll
+  for (int j = 0; j < WTN; ++j) {
+    const int n = nbase + j * 32 + l32;
+    wrow[j] = static_cast<const T*>(a.w) + (size_t)(n < a.N ? n : 0) * a.Kpad;
   }
 
-  f32x4 acc[TM][TN];
-#pragma unroll
-  for (int i = 0; i < TM; ++i)
-#pragma unroll
-    for (int j = 0; j < TN; ++j) acc[i][j] = f32x4{0.f, 0.f, 0.f, 0.f};
+  // ---- K walk. Step g (this wave: g = wk, wk+WK, ...) covers chunks [g*2KS, (g+1)*2KS); lane half h loads
+  // chunks g*2KS + 2s + h, s < KS (chunk = 8 consecutive K = 8 channels of one tap).
+  const int nsteps = a.Kpad / KSTEP;
+  int g = wk;
+  int tap0 = 0, cb0 = 0;  // KIND 3: tap / channel-block of chunk g*2KS + h
+  if constexpr (KIND != 1) {
+    const int c = g * 2 * KS + h;
+    tap0 = c / a.Cin8;
+    cb0 = c - tap0 * a.Cin8;
+  }
 
-  const T* W = static_cast<const T*>(a.w);
-  V ra[NA], rbv[NB];
-  const int nk = a.Kpad / BK;
-
-  auto load_tiles = [&](int kt) {
-    const int kchunk = kt * (BK / 8) + kc;
-    const bool kok = kchunk < a.Kc;
-    const int tap = kok ? kchunk / a.Cin8 : 0;
-    const int cb = kchunk - tap * a.Cin8;
-#pragma unroll
-    for (int i = 0; i < NA; ++i) ra[i] = gather_a<T>(a, rb[i], riy[i], rix[i], rok[i] && kok, tap, cb);
-#pragma unroll
-    for (int i = 0; i < NB; ++i) {
-      const int c = tid + i * NT;
-      const int n = n0 + (c >> 2);
-      if ((c >> 2) < BN && n < a.N)
-        rbv[i] = Vec8<T>::load(W + (size_t)n * a.Kpad + kt * BK + (c & 3) * 8);
-      else
-        rbv[i] = Vec8<T>::zero();
+  bool div255 = false;
+  if constexpr (KIND == 0) div255 = ord2f(*reinterpret_cast<const int*>(a.ctl)) > 1.0f + a.eps;
+  auto gather = [&](int i, int s) -> F {
+    const int chunk = g * 2 * KS + 2 * s + h;
+    if (!pv[i] || chunk >= a.Kc) return Vec8<T>::zero();
+    if constexpr (KIND == 1) {
+      const int c = chunk * 8;
+      return load8<T>((c < a.C0 ? row0[i] : row1[i]) + c);
+    } else if constexpr (KIND == 0) {  // Cin8 == 1: chunk = tap; channels 3..7 are zero padding
+      const int ky = chunk / 3, kx = chunk - (chunk / 3) * 3;
+      const int iy = iy0[i] + ky, ix = ix0[i] + kx;
+      if ((unsigned)iy >= (unsigned)a.Hin || (unsigned)ix >= (unsigned)a.Win) return Vec8<T>::zero();
+      const size_t HW = (size_t)a.Hin * a.Win;
+      const float* p = a.nchw + (size_t)pb[i] * 3 * HW + (size_t)iy * a.Win + ix;
+      float x0 = p[0], x1 = p[HW], x2 = p[2 * HW];
+      if (div255) { x0 = x0 / 255.0f; x1 = x1 / 255.0f; x2 = x2 / 255.0f; }
+      F v = Vec8<T>::zero();
+      v[0] = (T)x0; v[1] = (T)x1; v[2] = (T)x2;
+      return v;
+    } else {
+      int cb = cb0 + 2 * s, t = tap0;
+      while (cb >= a.Cin8) { cb -= a.Cin8; ++t; }
+      const int ky = t / 3, kx = t - (t / 3) * 3;
+      const int iy = iy0[i] + ky, ix = ix0[i] + kx;
+      if ((unsigned)iy >= (unsigned)a.Hin || (unsigned)ix >= (unsigned)a.Win) return Vec8<T>::zero();
+      return load8<T>(row0[i] + (size_t)(iy * a.Win + ix) * a.s0_ctot + cb * 8);
+    }
+  };
+  auto advance = [&]() {
+    g += WK;
+    if constexpr (KIND != 1) {
+      cb0 += 2 * KS * WK;
+      while (cb0 >= a.Cin8) { cb0 -= a.Cin8; ++tap0; }
     }
   };
 
-  load_tiles(0);
-  for (int kt = 0; kt < nk; ++kt) {
-    __syncthreads();
+  f32x16 acc[WTM][WTN];
 #pragma unroll
-    for (int i = 0; i < NA; ++i) {
-      const int r = (tid + i * NT) >> 2;
-      if (r < BM) {
-        T* dp = As + r * LDK + kc * 8;
-        if constexpr (sizeof(T) == 2) {
-          *reinterpret_cast<V*>(dp) = ra[i];
-        } else {
+  for (int i = 0; i < WTM; ++i)
 #pragma unroll
-          for (int e = 0; e < 8; ++e) dp[e] = ra[i][e];
-        }
+    for (int j = 0; j < WTN; ++j)
+#pragma unroll
+      for (int r = 0; r < 16; ++r) acc[i][j][r] = 0.f;
+
+  F fa0[KS][WTN], fb0[KS][WTM], fa1[KS][WTN], fb1[KS][WTM];
+  auto load_step = [&](F (*fa)[WTN], F (*fb)[WTM]) {
+#pragma unroll
+    for (int s = 0; s < KS; ++s) {
+#pragma unroll
+      for (int j = 0; j < WTN; ++j) fa[s][j] = load8<T>(wrow[j] + (size_t)(g * 2 * KS + 2 * s + h) * 8);
+#pragma unroll
+      for (int i = 0; i < WTM; ++i) fb[s][i] = gather(i, s);
+    }
+  };
+  auto compute = [&](F (*fa)[WTN], F (*fb)[WTM]) {
+#pragma unroll
+    for (int s = 0; s < KS; ++s)
+#pragma unroll
+      for (int i = 0; i < WTM; ++i)
+#pragma unroll
+        for (int j = 0; j < WTN; ++j) mma<T>(fa[s][j], fb[s][i], acc[i][j]);
+  };
+
+  // epilogue operands (bias, residual) are fetched during the last step's MFMAs
+  float bias[WTN][4][4];
+  float resv[WTM][WTN][4][4];
+  const T* res = static_cast<const T*>(a.res);
+  auto load_epi = [&]() {
+    if (wk != 0) return;
+#pragma unroll
+    for (int j = 0; j < WTN; ++j)
+#pragma unroll
+      for (int q = 0; q < 4; ++q) {
+        const int n = nbase + j * 32 + 8 * q + 4 * h;
+        const f32x4 b4 = n < a.N ? *reinterpret_cast<const f32x4*>(a.bias + n) : f32x4{0, 0, 0, 0};
+#pragma unroll
+        for (int e = 0; e < 4; ++e) bias[j][q][e] = b4[e];
+      }
+#pragma unroll
+    for (int i = 0; i < WTM; ++i)
+#pragma unroll
+      for (int j = 0; j < WTN; ++j)
+#pragma unroll
+        for (int q = 0; q < 4; ++q)
+#pragma unroll
+          for (int e = 0; e < 4; ++e) resv[i][j][q][e] = 0.f;
+    if (res) {
+#pragma unroll
+      for (int i = 0; i < WTM; ++i) {
+        if (!pv[i]) continue;
+        const size_t rb = (size_t)(pb[i] * a.r_P + py[i] * a.Wo + px[i]) * a.r_ctot + a.r_coff;
+#pragma unroll
+        for (int j = 0; j < WTN; ++j)
+#pragma unroll
+          for (int q = 0; q < 4; ++q) {
+            const int n = nbase + j * 32 + 8 * q + 4 * h;
+            if (n >= a.N) continue;
+            float v[4] = {0.f, 0.f, 0.f, 0.f};
+            load_res4<T>(res + rb + n, v);
+#pragma unroll
+            for (int e = 0; e < 4; ++e) resv[i][j][q][e] = v[e];
+          }
       }
     }
-#pragma unroll
-    for (int i = 0; i < NB; ++i) {
-      const int c = tid + i * NT;
-      if ((c >> 2) < BN) {
-        T* dp = Bs + (c >> 2) * LDK + (c & 3) * 8;
-        if constexpr (sizeof(T) == 2) {
-          *reinterpret_cast<V*>(dp) = rbv[i];
-        } else {
-#pragma unroll
-          for (int e = 0; e < 8; ++e) dp[e] = rbv[i][e];
-        }
-      }
-    }
-    __syncthreads();
-    if (kt + 1 < nk) load_tiles(kt + 1);
-#pragma unroll
-    for (int i = 0; i < TM; ++i)
-#pragma unroll
-      for (int j = 0; j < TN; ++j)
-        mma_step<T>(As, Bs, LDK, lane, wr * (BM / 2) + i * 16, wc * (BN / 2) + j * 16, acc[i][j]);
+  };
+
+  if (g < nsteps) load_step(fa0, fb0);
+  else load_epi();
+  while (g < nsteps) {
+    if (g + WK < nsteps) { advance(); load_step(fa1, fb1); } else { g += WK; load_epi(); }
+    compute(fa0, fb0);
+    if (g >= nsteps) break;
+    if (g + WK < nsteps) { advance(); load_step(fa0, fb0); } else { g += WK; load_epi(); }
+    compute(fa1, fb1);
   }
 
-  // epilogue: bias, SiLU, residual, (shuffled) store into the destination channel slice
+  // ---- split-K reduction through LDS (waves wk > 0 hand their partial tiles to wave wk == 0)
+  if constexpr (WK > 1) {
+    extern __shared__ float red[];  // [(WK-1)][WM*WN][WTM*WTN*16][64]
+    constexpr int PER = WTM * WTN * 16;
+    const int grp = wid / WK;
+    if (wk > 0) {
+      float* dst = red + ((size_t)((wk - 1) * (WM * WN) + grp) * PER) * 64 + lane;
+#pragma unroll
+      for (int i = 0; i < WTM; ++i)
+#pragma unroll
+        for (int j = 0; j < WTN; ++j)
+#pragma unroll
+          for (int r = 0; r < 16; ++r) dst[((i * WTN + j) * 16 + r) * 64] = acc[i][j][r];
+    }
+    __syncthreads();
+    if (wk > 0) return;
+#pragma unroll 1
+    for (int q = 1; q < WK; ++q) {
+      const float* src = red + ((size_t)((q - 1) * (WM * WN) + grp) * PER) * 64 + lane;
+#pragma unroll
+      for (int i = 0; i < WTM; ++i)
+#pragma unroll
+        for (int j = 0; j < WTN; ++j)
+#pragma unroll
+          for (int r = 0; r < 16; ++r) acc[i][j][r] += src[((i * WTN + j) * 16 + r) * 64];
+    }
+  }
+
+  // ---- epilogue: lane owns channels nbase + 32j + 8q + 4h + {0..3} of pixel pbase + 32i + l32
+  OutT* dst = static_cast<OutT*>(a.dst);
+#pragma unroll
+  for (int i = 0; i < WTM; ++i) {
+    if (!pv[i]) continue;
+    const int oy = py[i], ox = px[i];
+    const int pix = a.shuffle ? (2 * oy) * a.d_W + 2 * ox : oy * a.d_W + ox;
+    const size_t obase = (size_t)(pb[i] * a.d_P + a.d_pixoff + pix) * a.d_ctot + a.d_coff;
+#pragma unroll
+    for (int j = 0; j < WTN; ++j) {
+#pragma unroll
+      for (int q = 0; q < 4; ++q) {
+        const int n = nbase + j * 32 + 8 * q + 4 * h;
+        if (n >= a.N) continue;
+        float v[4];
+#pragma unroll
+        for (int e = 0; e < 4; ++e) {
+          const float x = acc[i][j][4 * q + e] + bias[j][q][e];
+          v[e] = (a.act ? ym_silu(x) : x) + resv[i][j][q][e];
+        }
+        if (a.shuffle) {
+          const int sub = n / a.npr;
+          const int ch = n - sub * a.npr;
+          Out4<OutT>::store(dst + obase + (size_t)((sub >> 1) * a.d_W + (sub & 1)) * a.d_ctot + ch, v);
+        } else {
+          Out4<OutT>::store(dst + obase + n, v);
+        }
+      }
+    }
+  }
+}
+
+struct Cfg {
+  int wtm, wtn, wm, wn, wk;
+};
+
+template <typename T, typename OutT, int WTM, int WTN, int WM, int WN, int WK>
+hipError_t launch_cfg(ConvArgs a, int kind, hipStream_t st) {
+  constexpr int BM = WM * WTM * 32, BN = WN * WTN * 32, NT = WM * WN * WK * 64;
+  const int tiles_m8 = ((a.M + BM - 1) / BM + 7) / 8 * 8;
+  a.tiles_n = (a.N + BN - 1) / BN;
+  const size_t lds = WK > 1 ? (size_t)(WK - 1) * WM * WN * WTM * WTN * 16 * 64 * sizeof(float) : 0;
+  const dim3 grid(tiles_m8 * a.tiles_n);
+  if (kind == 1)
+    hipLaunchKernelGGL((conv_igemm<T, OutT, WTM, WTN, WM, WN, WK, 1>), grid, dim3(NT), lds, st, a);
+  else
+    hipLaunchKernelGGL((conv_igemm<T, OutT, WTM, WTN, WM, WN, WK, 3>), grid, dim3(NT), lds, st, a);
+  return hipGetLastError();
+}
+
+// ---------------------------------------------------------------------------------------------------------------
+// LDS-staged variant for the MFMA-dense layers (large K): one BM x BN tile per 256-thread workgroup (2x2 waves),
+// 64-deep K stages double-buffered in LDS.  Every operand byte is loaded from global ONCE per workgroup with
+// coalesced 16-byte row loads (8 lanes cover a 128-byte row), stored XOR-swizzled (chunk c of row r at c ^ (r&7))
+// so the MFMA fragment reads (ds_read_b128, 32 rows at one K offset) do not pile onto one bank group; the next
+// stage's global loads are in flight while the current stage's MFMAs run; one barrier per stage.
+template <typename T, typename OutT, int BM, int BN, int KIND>
+__global__ __launch_bounds__(256) void conv_lds(const ConvArgs a) {
+  constexpr int BK = 64;
+  constexpr int RB = BM * 8 / 256;  // pixel-row chunks per thread per stage
+  constexpr int RA = BN * 8 / 256;  // weight-row chunks per thread per stage
+  constexpr int TM = BM / 64, TN = BN / 64;  // 32x32 blocks per wave (2x2 waves)
+  typedef typename Vec8<T>::type V;
+  __shared__ __attribute__((aligned(16))) T sA[2][BN * BK];
+  __shared__ __attribute__((aligned(16))) T sB[2][BM * BK];
+  int tm, tn;
+  if (!xcd_tile(a, BM, tm, tn)) return;
+  const int tid = threadIdx.x;
+  const int lane = tid & 63, wid = tid >> 6;
+  const int wm = wid & 1, wn = wid >> 1;
+  const int l32 = lane & 31, h = lane >> 5;
+  const int HWo = a.Ho * a.Wo;
+  const int kc = tid & 7;  // this thread's chunk inside every 64-deep stage
+  // pixel rows this thread stages
+  const T* prow0[RB];
+  const T* prow1[RB];
+  int piy[RB], pix0[RB];
+  bool pok[RB];
+#pragma unroll
+  for (int i = 0; i < RB; ++i) {
+    const int r = (tid >> 3) + 32 * i;
+    const int m = tm * BM + r;
+    pok[i] = m < a.M;
+    const int mm = pok[i] ? m : 0;
+    const int b = mm / HWo, rem = mm - (mm / HWo) * HWo;
+    const int oy = rem / a.Wo, ox = rem - (rem / a.Wo) * a.Wo;
+    if constexpr (KIND == 1) {
+      const int sy = a.up0 ? (oy >> 1) : oy, sx = a.up0 ? (ox >> 1) : ox;
+      prow0[i] = static_cast<const T*>(a.src0) + ((size_t)(b * a.s0_P + sy * a.s0_W + sx) * a.s0_ctot + a.s0_coff);
+      prow1[i] = a.src1 ? static_cast<const T*>(a.src1) +
+                              ((size_t)(b * a.s1_P + oy * a.Win + ox) * a.s1_ctot + a.s1_coff - a.C0)
+                        : prow0[i];
+      piy[i] = pix0[i] = 0;
+    } else {
+      prow0[i] = static_cast<const T*>(a.src0) + ((size_t)b * a.s0_P * a.s0_ctot + a.s0_coff);
+      prow1[i] = nullptr;
+      piy[i] = oy * a.s - 1;
+      pix0[i] = ox * a.s - 1;
+    }
+  }
+  const T* wrow[RA];
+#pragma unroll
+  for (int i = 0; i < RA; ++i) {
+    const int n = tn * BN + (tid >> 3) + 32 * i;
+    wrow[i] = static_cast<const T*>(a.w) + (size_t)(n < a.N ? n : 0) * a.Kpad;
+  }
+  int tap = 0, cb = kc;  // KIND 3: tap / channel block of chunk kt*8 + kc
+  if constexpr (KIND == 3) {
+    tap = kc / a.Cin8;
+    cb = kc - tap * a.Cin8;
+  }
+  V ra[RB], rw[RA];
+  int kt = 0;
+  auto load = [&]() {
+    const int chunk = kt * 8 + kc;
+#pragma unroll
+    for (int i = 0; i < RA; ++i) rw[i] = Vec8<T>::load(wrow[i] + (size_t)chunk * 8);
+#pragma unroll
+    for (int i = 0; i < RB; ++i) {
+      V v = Vec8<T>::zero();
+      if (pok[i] && chunk < a.Kc) {
+        if constexpr (KIND == 1) {
+          const int c = chunk * 8;
+          v = Vec8<T>::load((c < a.C0 ? prow0[i] : prow1[i]) + c);
+        } else {
+          const int ky = tap / 3, kx = tap - (tap / 3) * 3;
+          const int iy = piy[i] + ky, ix = pix0[i] + kx;
+          if ((unsigned)iy < (unsigned)a.Hin && (unsigned)ix < (unsigned)a.Win)
+            v = Vec8<T>::load(prow0[i] + (size_t)(iy * a.Win + ix) * a.s0_ctot + cb * 8);
+        }
+      }
+      ra[i] = v;
+    }
+    if constexpr (KIND == 3) {  // advance this thread's chunk by one stage (8 chunks)
+      cb += 8;
+      while (cb >= a.Cin8) { cb -= a.Cin8; ++tap; }
+    }
+  };
+  auto store = [&](int buf) {
+#pragma unroll
+    for (int i = 0; i < RA; ++i) {
+      const int r = (tid >> 3) + 32 * i;
+      *reinterpret_cast<V*>(&sA[buf][r * BK + ((kc ^ (r & 7)) * 8)]) = rw[i];
+    }
+#pragma unroll
+    for (int i = 0; i < RB; ++i) {
+      const int r = (tid >> 3) + 32 * i;
+      *reinterpret_cast<V*>(&sB[buf][r * BK + ((kc ^ (r & 7)) * 8)]) = ra[i];
+    }
+  };
+  f32x16 acc[TM][TN];
+#pragma unroll
+  for (int i = 0; i < TM; ++i)
+#pragma unroll
+    for (int j = 0; j < TN; ++j)
+#pragma unroll
+      for (int r = 0; r < 16; ++r) acc[i][j][r] = 0.f;
+  const int nk = a.Kpad / BK;
+  load();
+  store(0);
+  __syncthreads();
+  for (kt = 0; kt < nk;) {
+    const int cur = kt & 1;
+    ++kt;
+    if (kt < nk) load();  // stage kt+1's global loads fly under this stage's MFMAs
+#pragma unroll
+    for (int s = 0; s < 4; ++s) {
+      const int cc = 2 * s + h;
+      typename Frag<T>::type fa[TN], fb[TM];
+#pragma unroll
+      for (int j = 0; j < TN; ++j) {
+        const int r = wn * (BN / 2) + j * 32 + l32;
+        fa[j] = *reinterpret_cast<const V*>(&sA[cur][r * BK + ((cc ^ (r & 7)) * 8)]);
+      }
+#pragma unroll
+      for (int i = 0; i < TM; ++i) {
+        const int r = wm * (BM / 2) + i * 32 + l32;
+        fb[i] = *reinterpret_cast<const V*>(&sB[cur][r * BK + ((cc ^ (r & 7)) * 8)]);
+      }
+#pragma unroll
+      for (int i = 0; i < TM; ++i)
+#pragma unroll
+        for (int j = 0; j < TN; ++j) mma<T>(fa[j], fb[i], acc[i][j]);
+    }
+    if (kt < nk) store(cur ^ 1);
+    __syncthreads();
+  }
+  // epilogue (same register layout as conv_igemm): lane owns channels n..n+3 of one pixel per (i, j, q)
   OutT* dst = static_cast<OutT*>(a.dst);
   const T* res = static_cast<const T*>(a.res);
 #pragma unroll
   for (int i = 0; i < TM; ++i) {
+    const int m = tm * BM + wm * (BM / 2) + i * 32 + l32;
+    if (m >= a.M) continue;
+    const int b = m / HWo, rem = m - (m / HWo) * HWo;
+    const int oy = rem / a.Wo, ox = rem - (rem / a.Wo) * a.Wo;
+    const int pix = a.shuffle ? (2 * oy) * a.d_W + 2 * ox : oy * a.d_W + ox;
+    const size_t obase = (size_t)(b * a.d_P + a.d_pixoff + pix) * a.d_ctot + a.d_coff;
+    const size_t rbase = res ? (size_t)(b * a.r_P + pix) * a.r_ctot + a.r_coff : 0;
 #pragma unroll
-    for (int v = 0; v < 4; ++v) {
-      const int row = m0 + wr * (BM / 2) + i * 16 + (lane >> 4) * 4 + v;
-      if (row >= a.M) continue;
-      const int b = row / HWo;
-      const int rem = row - b * HWo;
-      const int oy = rem / a.Wo;
-      const int ox = rem - oy * a.Wo;
+    for (int j = 0; j < TN; ++j) {
 #pragma unroll
-      for (int j = 0; j < TN; ++j) {
-        const int col = n0 + wc * (BN / 2) + j * 16 + (lane & 15);
-        if (col >= a.N) continue;
-        float x = acc[i][j][v] + a.bias[col];
-        if (a.act) x = ym_silu(x);
-        int pix, ch;
-        if (a.shuffle) {
-          const int sub = col / a.npr;
-          ch = col - sub * a.npr;
-          pix = (2 * oy + (sub >> 1)) * a.d_W + 2 * ox + (sub & 1);
-        } else {
-          ch = col;
-          pix = oy * a.d_W + ox;
+      for (int q = 0; q < 4; ++q) {
+        const int n = tn * BN + wn * (BN / 2) + j * 32 + 8 * q + 4 * h;
+        if (n >= a.N) continue;
+        const f32x4 b4 = *reinterpret_cast<const f32x4*>(a.bias + n);
+        float v[4];
+#pragma unroll
+        for (int e = 0; e < 4; ++e) {
+          const float x = acc[i][j][4 * q + e] + b4[e];
+          v[e] = a.act ? ym_silu(x) : x;
         }
-        if (res) x += (float)res[(size_t)(b * a.r_P + pix) * a.r_ctot + a.r_coff + ch];
-        dst[(size_t)(b * a.d_P + a.d_pixoff + pix) * a.d_ctot + a.d_coff + ch] = cvt_out<OutT>(x);
+        if (a.shuffle) {
+          const int sub = n / a.npr;
+          const int ch = n - sub * a.npr;
+          Out4<OutT>::store(dst + obase + (size_t)((sub >> 1) * a.d_W + (sub & 1)) * a.d_ctot + ch, v);
+        } else {
+          if (res) load_res4<T>(res + rbase + n, v);
+          Out4<OutT>::store(dst + obase + n, v);
+        }
       }
     }
   }
 }
 
 template <typename T, typename OutT, int BM, int BN>
-hipError_t launch(ConvArgs a, hipStream_t st) {
-  const int tiles_m = (a.M + BM - 1) / BM;
+hipError_t launch_lds(ConvArgs a, int kind, hipStream_t st) {
+  const int tiles_m8 = ((a.M + BM - 1) / BM + 7) / 8 * 8;
   a.tiles_n = (a.N + BN - 1) / BN;
-  hipLaunchKernelGGL((conv_igemm_nhwc<T, OutT, BM, BN>), dim3(tiles_m * a.tiles_n), dim3(NT), 0, st, a);
+  const dim3 grid(tiles_m8 * a.tiles_n);
+  if (kind == 1) hipLaunchKernelGGL((conv_lds<T, OutT, BM, BN, 1>), grid, dim3(256), 0, st, a);
+  else hipLaunchKernelGGL((conv_lds<T, OutT, BM, BN, 3>), grid, dim3(256), 0, st, a);
   return hipGetLastError();
 }
 
+// LDS-variant tile configurations (f16 plans only): (id, BM, BN)
+#define YM_LDS_CFGS(X) \
+  X(12, 128, 128)      \
+  X(13, 128, 64)       \
+  X(14, 64, 128)       \
+  X(15, 64, 64)        \
+  X(16, 256, 64)
+
+// The instantiated tile configurations: (id, WTM, WTN, WM, WN, WK).
+#define YM_CONV_CFGS(X) \
+  X(0, 2, 2, 2, 2, 1)   \
+  X(1, 2, 2, 4, 1, 1)   \
+  X(2, 2, 1, 4, 1, 1)   \
+  X(3, 1, 2, 1, 1, 4)   \
+  X(4, 1, 2, 1, 2, 4)   \
+  X(5, 1, 2, 4, 1, 1)   \
+  X(6, 2, 2, 1, 2, 2)   \
+  X(7, 1, 1, 1, 1, 8)   \
+  X(8, 1, 2, 2, 1, 2)   \
+  X(9, 1, 1, 4, 1, 1)   \
+  X(10, 1, 2, 2, 2, 1)  \
+  X(11, 1, 1, 1, 1, 4)
+
+constexpr int kNumCfg = 12;
+constexpr Cfg kCfgs[kNumCfg] = {
+#define YM_X(id, a, b, c, d, e) {a, b, c, d, e},
+    YM_CONV_CFGS(YM_X)
+#undef YM_X
+};
+
+constexpr int kNumAllCfg = 17;
+
 template <typename T, typename OutT>
-hipError_t pick(const ConvArgs& a, hipStream_t st) {
-  // tile choice: wide N tiles for wide layers, 128-pixel tiles when there are enough of them to fill 256 CUs
-  const long tiles128 = (long)((a.M + 127) / 128) * ((a.N + 63) / 64);
-  if (a.N <= 32) return launch<T, OutT, 128, 32>(a, st);
-  if (tiles128 >= 512) return launch<T, OutT, 128, 64>(a, st);
-  return launch<T, OutT, 64, 64>(a, st);
+hipError_t launch_id(int id, const ConvArgs& a, int kind, hipStream_t st) {
+  switch (id) {
+#define YM_X(cid, A, B, C, D, E) \
+  case cid: return launch_cfg<T, OutT, A, B, C, D, E>(a, kind, st);
+    YM_CONV_CFGS(YM_X)
+#undef YM_X
+  }
+  if constexpr (sizeof(T) == 2) {
+    switch (id) {
+#define YM_X(cid, BM_, BN_) \
+  case cid: return launch_lds<T, OutT, BM_, BN_>(a, kind, st);
+      YM_LDS_CFGS(YM_X)
+#undef YM_X
+    }
+  }
+  return hipErrorInvalidValue;
+}
+
+// Default tile choice when no autotuned choice is given: fill the 256 CUs before making tiles big.
+int choose_cfg(const ConvArgs& a) {
+  const char* env = getenv("YM_CONV_CFG");
+  if (env && *env) {
+    const int id = atoi(env);
+    if (id >= 0 && id < kNumCfg) return id;
+  }
+  const long M = a.M, N = a.N;
+  const int steps = a.Kpad / KSTEP;
+  auto waves = [&](int id) {
+    const Cfg& c = kCfgs[id];
+    const long BM = c.wm * c.wtm * 32, BN = c.wn * c.wtn * 32;
+    return ((M + BM - 1) / BM) * ((N + BN - 1) / BN) * c.wm * c.wn * c.wk;
+  };
+  if (N <= 32) return waves(2) >= 2048 ? 2 : (steps >= 4 ? 7 : 9);
+  if (N <= 64) {
+    if (waves(1) >= 2048) return 1;
+    if (waves(5) >= 2048) return 5;
+    return steps >= 4 ? 3 : 8;
+  }
+  if (waves(0) >= 2048) return 0;
+  if (waves(10) >= 2048) return 10;
+  return steps >= 4 ? 4 : 6;
 }
 
 }  // namespace
 
-hipError_t ym_launch_conv(int dtype, int out_f32, const ConvArgs& a, hipStream_t st) {
-  if (dtype == YM_DT_F16) return out_f32 ? pick<f16, float>(a, st) : pick<f16, f16>(a, st);
-  return pick<float, float>(a, st);
+int ym_conv_num_cfgs() { return kNumAllCfg; }
+
+hipError_t ym_launch_conv(int dtype, int out_f32, const ConvArgs& a, int cfg, hipStream_t st) {
+  int kind;
+  if (a.nchw) kind = (a.k == 3 && a.Cin8 == 1) ? 0 : -1;
+  else if (a.k == 1 && a.s == 1) kind = 1;
+  else if (a.k == 3 && !a.src1 && !a.up0) kind = 3;
+  else kind = -1;
+  if (kind < 0) return hipErrorInvalidValue;
+  // (concat/upsample sources only feed 1x1 convs; YOLO11 has k in {1, 3})
+  if (a.Kpad % KSTEP) return hipErrorInvalidValue;
+  int id = (cfg >= 0 && cfg < kNumAllCfg) ? cfg : choose_cfg(a);
+  if (id >= kNumCfg && dtype != YM_DT_F16) id = choose_cfg(a);  // LDS variants are instantiated for f16 only
+  if (dtype == YM_DT_F16) return out_f32 ? launch_id<f16, float>(id, a, kind, st) : launch_id<f16, f16>(id, a, kind, st);
+  return launch_id<float, float>(id, a, kind, st);
 }

@@ -1,21 +1,16 @@
 // Bandwidth-/latency-bound kernels of the YOLO11 inference path on gfx950:
-//   input prep (LoadTensor /255 rule + NCHW fp32 → NHWC), depthwise 3x3 (Detect cv3 DWConv), fused SPPF max-pool
-//   pyramid, C2PSA attention (+ fused positional depthwise conv), anchor-free DFL decode, class-offset greedy NMS.
+//   input statistics (LoadTensor /255 rule), depthwise 3x3 (Detect cv3 DWConv), fused SPPF max-pool pyramid, C2PSA
+//   attention (+ fused positional depthwise conv), anchor-free DFL decode, class-offset greedy NMS.
 // Each replaces an upstream Ultralytics/ATen/torchvision op reached from `YOLO11Model.predict`
 // (/root/reference/core/model.py:133) — SURVEY §2.2 and §8a rows a2, a8, a9, a11-a14.
 #include "ym_common.h"
 
 namespace {
 
-// ------------------------------------------------------------------------------------------------- input prep
+// ------------------------------------------------------------------------------------------------- input stats
 // LoadTensor._single_check: `if im.max() > 1 + finfo(dtype).eps: im = im.float() / 255` over the WHOLE batch.
 // ctl[0] holds max as an order-preserving int; ctl is reset by the init kernel at the start of every forward.
-__device__ __forceinline__ int f2ord(float f) {
-  int i = __float_as_int(f);
-  return i >= 0 ? i : i ^ 0x7FFFFFFF;
-}
-__device__ __forceinline__ float ord2f(int i) { return __int_as_float(i >= 0 ? i : i ^ 0x7FFFFFFF); }
-
+// The division itself happens in the stem conv's loader (csrc/ym_conv.hip KIND 0), which reads the NCHW batch.
 __global__ void init_ctl(float* ctl, int* counts, int B) {
   const int t = threadIdx.x;
   if (t == 0) reinterpret_cast<int*>(ctl)[0] = f2ord(-INFINITY);
@@ -43,27 +38,14 @@ __global__ __launch_bounds__(256) void max_reduce(const float* __restrict__ x, l
   }
 }
 
-template <typename T>
-__global__ __launch_bounds__(256) void prep_nhwc(const PrepArgs a) {
-  const long HW = (long)a.H * a.W;
-  const long i = blockIdx.x * (long)blockDim.x + threadIdx.x;
-  if (i >= (long)a.B * HW) return;
-  const long b = i / HW, p = i - b * HW;
-  const float mx = ord2f(reinterpret_cast<const int*>(a.ctl)[0]);
-  const bool div = mx > 1.0f + a.eps;
-  typename Vec8<T>::type v = Vec8<T>::zero();
-  for (int c = 0; c < a.C; ++c) {
-    float x = a.in[(b * a.C + c) * HW + p];
-    if (div) x = x / 255.0f;
-    v[c] = (T)x;
-  }
-  Vec8<T>::store(static_cast<T*>(a.out) + i * 8, v);
-}
-
 // ------------------------------------------------------------------------------------------------- depthwise 3x3
-// DWConv(c, c, 3) = Conv(g=c): 3x3, stride 1, pad 1, BN folded, SiLU.  One thread = 8 channels of one pixel.
+// DWConv(c, c, 3) = Conv(g=c): 3x3, stride 1, pad 1, BN folded, SiLU.  One thread = 8 channels of one pixel;
+// the workgroup's [9][C] weights and bias are staged once in LDS.
 template <typename T>
 __global__ __launch_bounds__(256) void dwconv3x3(const DwArgs a) {
+  extern __shared__ float wl[];  // [9*C] weights, then [C] bias
+  for (int i = threadIdx.x; i < 10 * a.C; i += 256) wl[i] = i < 9 * a.C ? a.w[i] : a.bias[i - 9 * a.C];
+  __syncthreads();
   const int C8 = a.C >> 3;
   const long idx = blockIdx.x * (long)blockDim.x + threadIdx.x;
   const long total = (long)a.B * a.H * a.W * C8;
@@ -77,7 +59,7 @@ __global__ __launch_bounds__(256) void dwconv3x3(const DwArgs a) {
   const int c0 = cg * 8;
   float acc[8];
 #pragma unroll
-  for (int e = 0; e < 8; ++e) acc[e] = a.bias[c0 + e];
+  for (int e = 0; e < 8; ++e) acc[e] = wl[9 * a.C + c0 + e];
   const T* src = static_cast<const T*>(a.src);
 #pragma unroll
   for (int ky = 0; ky < 3; ++ky) {
@@ -89,7 +71,7 @@ __global__ __launch_bounds__(256) void dwconv3x3(const DwArgs a) {
       if ((unsigned)ix >= (unsigned)a.W) continue;
       const typename Vec8<T>::type v =
           Vec8<T>::load(src + (size_t)(b * a.s_P + iy * a.W + ix) * a.s_ctot + a.s_coff + c0);
-      const float* wr = a.w + (ky * 3 + kx) * a.C + c0;
+      const float* wr = wl + (ky * 3 + kx) * a.C + c0;
 #pragma unroll
       for (int e = 0; e < 8; ++e) acc[e] = fmaf((float)v[e], wr[e], acc[e]);
     }
@@ -101,66 +83,91 @@ __global__ __launch_bounds__(256) void dwconv3x3(const DwArgs a) {
 }
 
 // ------------------------------------------------------------------------------------------------- SPPF pools
-// y1 = max5(y0), y2 = max5(y1) = max9(y0), y3 = max13(y0): stride 1, -inf padding, all three in one pass.
+// y1 = max5(y0), y2 = max5(y1) = max9(y0), y3 = max13(y0) (stride 1, -inf padding: the cascade is exactly the
+// wider window).  Separable: row maxima of radius 2/4/6 in one pass over the 13-wide row window, then column
+// maxima.  One workgroup = one image x 8 channels; pixels move as 16-byte vectors and stay in LDS in the storage
+// type (max is exact in any precision).
 template <typename T>
 __global__ __launch_bounds__(256) void sppf_pool(const PoolArgs a) {
-  const int C8 = a.C >> 3;
-  const long idx = blockIdx.x * (long)blockDim.x + threadIdx.x;
-  const long total = (long)a.B * a.H * a.W * C8;
-  if (idx >= total) return;
-  const int cg = idx % C8;
-  const long pix = idx / C8;
+  typedef typename Vec8<T>::type V;
+  extern __shared__ __attribute__((aligned(16))) unsigned char smraw[];
+  V* in = reinterpret_cast<V*>(smraw);  // [HW]
   const int HW = a.H * a.W;
-  const int b = pix / HW;
-  const int p = pix - (long)b * HW;
-  const int y = p / a.W, x = p - (p / a.W) * a.W;
-  const int c0 = cg * 8;
+  V* hr = in + HW;                      // [3][HW] row maxima, radius 2, 4, 6
+  const int ng = a.C / 8;
+  const int b = blockIdx.x / ng;
+  const int c0 = (blockIdx.x % ng) * 8;
   T* buf = static_cast<T*>(a.buf);
-  float m5[8], m9[8], m13[8];
+  for (int p = threadIdx.x; p < HW; p += 256)
+    in[p] = Vec8<T>::load(buf + (size_t)(b * a.P + p) * a.ctot + a.coff + c0);
+  __syncthreads();
+  if (!a.sep) {  // LDS holds only the input image (large maps in f32): direct 2-D windows
+    for (int it = threadIdx.x; it < 3 * HW; it += 256) {
+      const int j = it / HW, p = it - (it / HW) * HW;
+      const int r = 2 * (j + 1);
+      const int y = p / a.W, x = p - (p / a.W) * a.W;
+      V m = in[p];
+      for (int yy = y - r < 0 ? 0 : y - r; yy <= y + r && yy < a.H; ++yy)
+        for (int xx = x - r < 0 ? 0 : x - r; xx <= x + r && xx < a.W; ++xx) {
+          const V v = in[yy * a.W + xx];
 #pragma unroll
-  for (int e = 0; e < 8; ++e) m5[e] = m9[e] = m13[e] = -INFINITY;
-  for (int dy = -6; dy <= 6; ++dy) {
-    const int iy = y + dy;
-    if ((unsigned)iy >= (unsigned)a.H) continue;
-    const int ady = dy < 0 ? -dy : dy;
+          for (int e = 0; e < 8; ++e) m[e] = v[e] > m[e] ? v[e] : m[e];
+        }
+      Vec8<T>::store(buf + (size_t)(b * a.P + p) * a.ctot + a.coff + (j + 1) * a.C + c0, m);
+    }
+    return;
+  }
+  for (int p = threadIdx.x; p < HW; p += 256) {
+    const int y = p / a.W, x = p - (p / a.W) * a.W;
+    V m2 = in[p], m4 = m2, m6 = m2;
     for (int dx = -6; dx <= 6; ++dx) {
-      const int ix = x + dx;
-      if ((unsigned)ix >= (unsigned)a.W) continue;
-      const int adx = dx < 0 ? -dx : dx;
-      const int r = ady > adx ? ady : adx;
-      const typename Vec8<T>::type v =
-          Vec8<T>::load(buf + (size_t)(b * a.P + iy * a.W + ix) * a.ctot + a.coff + c0);
+      const int xx = x + dx;
+      if (dx == 0 || (unsigned)xx >= (unsigned)a.W) continue;
+      const V v = in[y * a.W + xx];
+      const int ad = dx < 0 ? -dx : dx;
 #pragma unroll
       for (int e = 0; e < 8; ++e) {
-        const float f = (float)v[e];
-        m13[e] = fmaxf(m13[e], f);
-        if (r <= 4) m9[e] = fmaxf(m9[e], f);
-        if (r <= 2) m5[e] = fmaxf(m5[e], f);
+        m6[e] = v[e] > m6[e] ? v[e] : m6[e];
+        if (ad <= 4) m4[e] = v[e] > m4[e] ? v[e] : m4[e];
+        if (ad <= 2) m2[e] = v[e] > m2[e] ? v[e] : m2[e];
       }
     }
+    hr[p] = m2;
+    hr[HW + p] = m4;
+    hr[2 * HW + p] = m6;
   }
-  typename Vec8<T>::type o5, o9, o13;
+  __syncthreads();
+  for (int it = threadIdx.x; it < 3 * HW; it += 256) {
+    const int j = it / HW, p = it - (it / HW) * HW;
+    const int r = 2 * (j + 1);
+    const int y = p / a.W, x = p - (p / a.W) * a.W;
+    const V* h = hr + (size_t)j * HW;
+    V m = h[p];
+    for (int dy = -r; dy <= r; ++dy) {
+      const int yy = y + dy;
+      if (dy == 0 || (unsigned)yy >= (unsigned)a.H) continue;
+      const V v = h[yy * a.W + x];
 #pragma unroll
-  for (int e = 0; e < 8; ++e) { o5[e] = (T)m5[e]; o9[e] = (T)m9[e]; o13[e] = (T)m13[e]; }
-  T* base = buf + (size_t)(b * a.P + p) * a.ctot + a.coff + c0;
-  Vec8<T>::store(base + a.C, o5);
-  Vec8<T>::store(base + 2 * a.C, o9);
-  Vec8<T>::store(base + 3 * a.C, o13);
+      for (int e = 0; e < 8; ++e) m[e] = v[e] > m[e] ? v[e] : m[e];
+    }
+    Vec8<T>::store(buf + (size_t)(b * a.P + p) * a.ctot + a.coff + (j + 1) * a.C + c0, m);
+  }
 }
 
 // ------------------------------------------------------------------------------------------------- attention
-// C2PSA Attention: per (image, head): softmax((qᵀk)·kd^-½) over N = H·W tokens, o = v·Aᵀ, plus pe(v) (depthwise
-// 3x3 + folded BN, no act) — the `(v @ attn.T).view(B,C,H,W) + self.pe(v)` of the upstream module.
-// One workgroup = 64 queries of one (b, head); keys streamed in chunks of 64 with an online softmax (fp32).
-constexpr int AQ = 64, AK = 64, AKD = 32, AHD = 64;
+// C2PSA Attention, one workgroup = (image, head, QB queries):
+//   1. S = (Q·Kᵀ)·kd^-½ for all N keys into LDS (each thread holds one key row in registers, Q is broadcast);
+//   2. row softmax in LDS (max-subtracted exp, divide by the sum — as torch.softmax);
+//   3. O = P·V: thread = (head dim d, group of QB/4 queries), V rows read coalesced (128 B per key);
+//   4. + pe(v): depthwise 3x3 + folded BN on v (the `+ self.pe(v.reshape(B,C,H,W))` term), store.
+constexpr int AKD = 32, AHD = 64;
 
-template <typename T>
+template <typename T, int QB>
 __global__ __launch_bounds__(256) void attn_psa(const AttnArgs a) {
-  __shared__ float Qs[AQ][AKD + 1];
-  __shared__ float Ks[AK][AKD + 1];
-  __shared__ float Vs[AK][AHD + 1];
-  __shared__ float Ps[AQ][AK + 1];
-  const int nqb = (a.N + AQ - 1) / AQ;
+  extern __shared__ float S[];  // [QB][N], then Q [QB][AKD]
+  const int N = a.N;
+  float* Qs = S + (size_t)QB * N;
+  const int nqb = (N + QB - 1) / QB;
   const int qb = blockIdx.x % nqb;
   const int bh = blockIdx.x / nqb;
   const int h = bh % a.nh;
@@ -170,79 +177,90 @@ __global__ __launch_bounds__(256) void attn_psa(const AttnArgs a) {
   const T* qkv = static_cast<const T*>(a.qkv);
   const size_t img = (size_t)b * a.q_P;
   const int hq = a.q_coff + h * per;
-
-  for (int i = tid; i < AQ * AKD; i += 256) {
+  for (int i = tid; i < QB * AKD; i += 256) {
     const int r = i / AKD, c = i % AKD;
-    const int n = qb * AQ + r;
-    Qs[r][c] = (n < a.N && c < a.kd) ? (float)qkv[(img + n) * a.q_ctot + hq + c] : 0.f;
+    const int n = qb * QB + r;
+    Qs[i] = (n < N && c < a.kd) ? (float)qkv[(img + n) * a.q_ctot + hq + c] : 0.f;
   }
-  const int qr = tid >> 2;    // query row owned (4 threads per row)
-  const int sub = tid & 3;    // key quarter for scores, dim quarter for the output
-  const int d0 = sub * (AHD / 4);
-  float mrow = -INFINITY, lrow = 0.f;
-  float o[AHD / 4];
+  __syncthreads();
+  // 1. scores
+  for (int key = tid; key < N; key += 256) {
+    float k[AKD];
+    const T* kp = qkv + (img + key) * a.q_ctot + hq + a.kd;
 #pragma unroll
-  for (int e = 0; e < AHD / 4; ++e) o[e] = 0.f;
-
-  for (int k0 = 0; k0 < a.N; k0 += AK) {
-    __syncthreads();
-    for (int i = tid; i < AK * AKD; i += 256) {
-      const int r = i / AKD, c = i % AKD;
-      const int n = k0 + r;
-      Ks[r][c] = (n < a.N && c < a.kd) ? (float)qkv[(img + n) * a.q_ctot + hq + a.kd + c] : 0.f;
+    for (int c8 = 0; c8 < AKD / 8; ++c8) {
+      const typename Vec8<T>::type v = Vec8<T>::load(kp + c8 * 8);
+#pragma unroll
+      for (int e = 0; e < 8; ++e) k[c8 * 8 + e] = (c8 * 8 + e < a.kd) ? (float)v[e] : 0.f;
     }
-    for (int i = tid; i < AK * AHD; i += 256) {
-      const int r = i / AHD, c = i % AHD;
-      const int n = k0 + r;
-      Vs[r][c] = (n < a.N && c < a.hd) ? (float)qkv[(img + n) * a.q_ctot + hq + 2 * a.kd + c] : 0.f;
-    }
-    __syncthreads();
-    float s[AK / 4];
-    float cmax = -INFINITY;
+#pragma unroll 4
+    for (int q = 0; q < QB; ++q) {
+      float s = 0.f;
 #pragma unroll
-    for (int j = 0; j < AK / 4; ++j) {
-      const int kj = sub * (AK / 4) + j;
-      float acc = 0.f;
-#pragma unroll
-      for (int c = 0; c < AKD; ++c) acc = fmaf(Qs[qr][c], Ks[kj][c], acc);
-      acc *= a.scale;
-      if (k0 + kj >= a.N) acc = -INFINITY;
-      s[j] = acc;
-      cmax = fmaxf(cmax, acc);
-    }
-    cmax = fmaxf(cmax, __shfl_xor(cmax, 1));
-    cmax = fmaxf(cmax, __shfl_xor(cmax, 2));
-    const float mnew = fmaxf(mrow, cmax);
-    const float alpha = expf(mrow - mnew);
-    float psum = 0.f;
-#pragma unroll
-    for (int j = 0; j < AK / 4; ++j) {
-      const float pj = expf(s[j] - mnew);
-      psum += pj;
-      Ps[qr][sub * (AK / 4) + j] = pj;
-    }
-    psum += __shfl_xor(psum, 1);
-    psum += __shfl_xor(psum, 2);
-    lrow = lrow * alpha + psum;
-    mrow = mnew;
-    __syncthreads();
-#pragma unroll
-    for (int e = 0; e < AHD / 4; ++e) o[e] *= alpha;
-    for (int kj = 0; kj < AK; ++kj) {
-      const float pj = Ps[qr][kj];
-#pragma unroll
-      for (int e = 0; e < AHD / 4; ++e) o[e] = fmaf(pj, Vs[kj][d0 + e], o[e]);
+      for (int c = 0; c < AKD; ++c) s = fmaf(Qs[q * AKD + c], k[c], s);
+      S[q * N + key] = s * a.scale;
     }
   }
-  const int n = qb * AQ + qr;
-  if (n >= a.N) return;
-  const int y = n / a.W, x = n - (n / a.W) * a.W;
+  __syncthreads();
+  // 2. softmax: 256/QB threads per row
+  {
+    constexpr int TPR = 256 / QB;
+    const int q = tid / TPR, sub = tid % TPR;
+    float* row = S + (size_t)q * N;
+    float m = -INFINITY;
+    for (int j = sub; j < N; j += TPR) m = fmaxf(m, row[j]);
+#pragma unroll
+    for (int o = TPR / 2; o > 0; o >>= 1) m = fmaxf(m, __shfl_xor(m, o));
+    float sum = 0.f;
+    for (int j = sub; j < N; j += TPR) {
+      const float e = expf(row[j] - m);
+      row[j] = e;
+      sum += e;
+    }
+#pragma unroll
+    for (int o = TPR / 2; o > 0; o >>= 1) sum += __shfl_xor(sum, o);
+    for (int j = sub; j < N; j += TPR) row[j] = row[j] / sum;
+  }
+  __syncthreads();
+  // 3. O = P·V
+  constexpr int QPG = QB / 4;
+  const int d = tid & 63, qg = tid >> 6;
+  float o[QPG];
+#pragma unroll
+  for (int i = 0; i < QPG; ++i) o[i] = 0.f;
+  const T* vp = qkv + img * a.q_ctot + hq + 2 * a.kd + d;
+  float* Vs = Qs + QB * AKD;  // [64 keys][AHD] chunk of V, staged with 16-byte loads
+  for (int k0 = 0; k0 < N; k0 += 64) {
+    __syncthreads();
+    {
+      const int kk = tid >> 2, part = tid & 3;  // 64 keys x 4 quarters of 16 dims
+      const int key = k0 + kk;
+#pragma unroll
+      for (int h8 = 0; h8 < 2; ++h8) {
+        const int d0 = part * 16 + h8 * 8;
+        typename Vec8<T>::type v = Vec8<T>::zero();
+        if (key < N && d0 < a.hd) v = Vec8<T>::load(qkv + (img + key) * a.q_ctot + hq + 2 * a.kd + d0);
+#pragma unroll
+        for (int e = 0; e < 8; ++e) Vs[kk * AHD + d0 + e] = (float)v[e];
+      }
+    }
+    __syncthreads();
+    const int kn = N - k0 < 64 ? N - k0 : 64;
+    for (int kj = 0; kj < kn; ++kj) {
+      const float v = Vs[kj * AHD + d];
+#pragma unroll
+      for (int i = 0; i < QPG; ++i) o[i] = fmaf(S[(qg + 4 * i) * N + k0 + kj], v, o[i]);
+    }
+  }
+  // 4. + pe(v), store
+  if (d >= a.hd) return;
+  const int ch = h * a.hd + d;
   T* dst = static_cast<T*>(a.dst);
-  const float inv = 1.0f / lrow;
-  for (int e = 0; e < AHD / 4; ++e) {
-    const int d = d0 + e;
-    if (d >= a.hd) break;
-    const int ch = h * a.hd + d;
+#pragma unroll
+  for (int i = 0; i < QPG; ++i) {
+    const int n = qb * QB + qg + 4 * i;
+    if (n >= N) continue;
+    const int y = n / a.W, x = n - (n / a.W) * a.W;
     float pe = a.pe_b[ch];
     for (int ky = 0; ky < 3; ++ky) {
       const int iy = y + ky - 1;
@@ -250,58 +268,80 @@ __global__ __launch_bounds__(256) void attn_psa(const AttnArgs a) {
       for (int kx = 0; kx < 3; ++kx) {
         const int ix = x + kx - 1;
         if ((unsigned)ix >= (unsigned)a.W) continue;
-        pe = fmaf((float)qkv[(img + iy * a.W + ix) * a.q_ctot + hq + 2 * a.kd + d], a.pe_w[(ky * 3 + kx) * a.C + ch],
-                  pe);
+        pe = fmaf((float)vp[(size_t)(iy * a.W + ix) * a.q_ctot], a.pe_w[(ky * 3 + kx) * a.C + ch], pe);
       }
     }
-    dst[((size_t)b * a.d_P + n) * a.d_ctot + a.d_coff + ch] = (T)(o[e] * inv + pe);
+    dst[((size_t)b * a.d_P + n) * a.d_ctot + a.d_coff + ch] = (T)(o[i] + pe);
   }
 }
 
 // ------------------------------------------------------------------------------------------------- decode
-// Detect._inference + the candidate stage of non_max_suppression, one thread per anchor:
-//   DFL softmax over reg_max bins per side → ltrb distances → dist2bbox(xywh) · stride → xywh2xyxy;
+// Detect._inference + the candidate stage of non_max_suppression; 4 lanes per anchor (lane s: DFL side s and a
+// quarter of the classes):
+//   DFL softmax over reg_max bins → ltrb distances → dist2bbox(xywh) · stride → xywh2xyxy;
 //   sigmoid class scores → (max, first argmax); candidate iff max > conf (and class in the filter).
 // Candidates are appended to a per-image key list: key = score bits << 32 | ~anchor, so a descending sort gives
 // score-descending order with ties broken by ascending anchor index (torchvision's stable sort).
 __global__ __launch_bounds__(256) void decode_anchors(const DecodeArgs a) {
-  const long idx = blockIdx.x * (long)blockDim.x + threadIdx.x;
-  if (idx >= (long)a.B * a.A) return;
+  // the workgroup's 64 anchor rows are contiguous: stage them in LDS with coalesced 16-byte loads
+  extern __shared__ float rows[];  // [64][no_tot]
+  const long total = (long)a.B * a.A;
+  const long a0 = blockIdx.x * 64L;
+  const int nrow = total - a0 < 64 ? (int)(total - a0) : 64;
+  {
+    const f32x4* src = reinterpret_cast<const f32x4*>(a.anchors + a0 * a.no_tot);
+    f32x4* dst = reinterpret_cast<f32x4*>(rows);
+    const int n4 = nrow * a.no_tot / 4;
+    for (int i = threadIdx.x; i < n4; i += 256) dst[i] = src[i];
+  }
+  __syncthreads();
+  const long gidx = a0 + (threadIdx.x >> 2);
+  const int sub = threadIdx.x & 3;
+  const bool valid = gidx < total;
+  const long idx = valid ? gidx : 0;
   const int b = idx / a.A;
   const int ai = idx - (long)b * a.A;
-  const float* row = a.anchors + idx * a.no_tot;
+  const float* row = rows + (valid ? (threadIdx.x >> 2) : 0) * a.no_tot;
+  float dist;
+  {
+    const float* r = row + sub * a.reg_max;
+    float mx = -INFINITY;
+    for (int i = 0; i < a.reg_max; ++i) mx = fmaxf(mx, r[i]);
+    float den = 0.f, num = 0.f;
+    for (int i = 0; i < a.reg_max; ++i) den += expf(r[i] - mx);
+    for (int i = 0; i < a.reg_max; ++i) num = fmaf(expf(r[i] - mx) / den, (float)i, num);
+    dist = num;
+  }
+  const int q = (a.nc + 3) / 4;
+  const float* cl = row + 4 * a.reg_max;
+  float best = -INFINITY;
+  int bi = 0x7FFFFFFF;
+  for (int c = sub * q; c < a.nc && c < (sub + 1) * q; ++c) {
+    const float sc = ym_sigmoid(cl[c]);
+    if (sc > best) { best = sc; bi = c; }
+  }
+#pragma unroll
+  for (int o = 1; o < 4; o <<= 1) {
+    const float ob = __shfl_xor(best, o);
+    const int oi = __shfl_xor(bi, o);
+    if (ob > best || (ob == best && oi < bi)) { best = ob; bi = oi; }
+  }
+  const int base = threadIdx.x & 60;
+  const float d0 = __shfl(dist, base), d1 = __shfl(dist, base + 1), d2 = __shfl(dist, base + 2),
+              d3 = __shfl(dist, base + 3);
+  if (sub != 0 || !valid) return;
   int l = 0;
   while (l + 1 < a.nl && ai >= a.lvl_off[l + 1]) ++l;
   const int p = ai - a.lvl_off[l];
   const float ax = (float)(p % a.lvl_W[l]) + 0.5f;
   const float ay = (float)(p / a.lvl_W[l]) + 0.5f;
   const float st = a.lvl_stride[l];
-  float dist[4];
-  for (int s = 0; s < 4; ++s) {
-    const float* r = row + s * a.reg_max;
-    float mx = -INFINITY;
-    for (int i = 0; i < a.reg_max; ++i) mx = fmaxf(mx, r[i]);
-    float den = 0.f, num = 0.f;
-    for (int i = 0; i < a.reg_max; ++i) {
-      const float e = expf(r[i] - mx);
-      den += e;
-    }
-    for (int i = 0; i < a.reg_max; ++i) num = fmaf(expf(r[i] - mx) / den, (float)i, num);
-    dist[s] = num;
-  }
-  const float x1 = ax - dist[0], y1 = ay - dist[1];
-  const float x2 = ax + dist[2], y2 = ay + dist[3];
+  const float x1 = ax - d0, y1 = ay - d1;
+  const float x2 = ax + d2, y2 = ay + d3;
   const float cx = (x1 + x2) / 2.0f * st, cy = (y1 + y2) / 2.0f * st;
   const float w = (x2 - x1) * st, hh = (y2 - y1) * st;
   const float hw = w / 2.0f, hh2 = hh / 2.0f;
   a.boxes[idx] = make_float4(cx - hw, cy - hh2, cx + hw, cy + hh2);
-  const float* cl = row + 4 * a.reg_max;
-  float best = -INFINITY;
-  int bi = 0;
-  for (int c = 0; c < a.nc; ++c) {
-    const float sc = ym_sigmoid(cl[c]);
-    if (sc > best) { best = sc; bi = c; }
-  }
   a.scores[idx] = best;
   a.cls[idx] = bi;
   bool cand = best > a.conf;
@@ -314,11 +354,13 @@ __global__ __launch_bounds__(256) void decode_anchors(const DecodeArgs a) {
 }
 
 // ------------------------------------------------------------------------------------------------- NMS
-// Per image, one 1024-thread workgroup: bitonic sort of the candidate keys (LDS when they fit), then greedy
-// suppression exactly as torchvision's CPU nms: boxes offset by cls·max_wh (0 if agnostic), areas and IoU in fp32
-// on the offset boxes, suppress iff IoU > iou (compared in double), keep ≤ max_det, clip to the image.
+// Per image, one 1024-thread workgroup: bitonic sort of the candidate keys, then greedy suppression exactly as
+// torchvision's CPU nms: boxes offset by cls·max_wh (0 if agnostic), areas and IoU in fp32 on the offset boxes,
+// suppress iff IoU > iou (compared in double), keep <= max_det, clip to the image.  Up to NMS_LDS candidates
+// everything (keys, boxes, areas, flags) lives in LDS, so the serial scan costs LDS latency per candidate;
+// larger candidate sets fall back to the same algorithm on global scratch.
 constexpr int NMS_T = 1024;
-constexpr int NMS_LDS_KEYS = 8192;
+constexpr int NMS_LDS = 4096;
 
 __device__ void bitonic_sort_desc(unsigned long long* k, int n2, int tid) {
   for (int size = 2; size <= n2; size <<= 1) {
@@ -335,77 +377,135 @@ __device__ void bitonic_sort_desc(unsigned long long* k, int n2, int tid) {
   }
 }
 
-__global__ __launch_bounds__(NMS_T) void nms_image(const NmsArgs a) {
-  __shared__ unsigned long long sk[NMS_LDS_KEYS];
+__device__ __forceinline__ bool iou_gt(const float4 bi, float ai_area, const float4 bj, float aj_area, double thr) {
+  const float xx1 = fmaxf(bi.x, bj.x), yy1 = fmaxf(bi.y, bj.y);
+  const float xx2 = fminf(bi.z, bj.z), yy2 = fminf(bi.w, bj.w);
+  const float w = fmaxf(0.0f, __fsub_rn(xx2, xx1));
+  const float h = fmaxf(0.0f, __fsub_rn(yy2, yy1));
+  const float inter = __fmul_rn(w, h);
+  const float ovr = __fdiv_rn(inter, __fsub_rn(__fadd_rn(ai_area, aj_area), inter));
+  return (double)ovr > thr;
+}
 
+__global__ __launch_bounds__(NMS_T) void nms_image(const NmsArgs a) {
+  __shared__ unsigned long long sk[NMS_LDS];
+  __shared__ float4 sbx[NMS_LDS];
+  __shared__ float sar[NMS_LDS];
+  __shared__ unsigned char ssup[NMS_LDS];
   const int b = blockIdx.x;
   const int tid = threadIdx.x;
   int n = a.counts[b];
   if (n > a.A) n = a.A;
   unsigned long long* gk = a.keys + (size_t)b * a.kstride;
-  int n2 = 1;
-  while (n2 < n) n2 <<= 1;
-  const bool in_lds = n2 <= NMS_LDS_KEYS;
-  unsigned long long* k = in_lds ? sk : gk;
-  if (in_lds) {
-    for (int i = tid; i < n2; i += NMS_T) sk[i] = i < n ? gk[i] : 0ull;
-  } else {
-    // the key list of each image has a power-of-two stride >= A (runtime), so padding up to n2 is in bounds
-    for (int i = n + tid; i < n2; i += NMS_T) gk[i] = 0ull;
-  }
-  __syncthreads();
-  if (n > 1) bitonic_sort_desc(k, n2, tid);
-  if (n > a.max_nms) n = a.max_nms;
-
-  // sorted, class-offset boxes and areas
-  float4* sb = a.sboxes + (size_t)b * a.A;
-  float* sa = a.sareas + (size_t)b * a.A;
-  unsigned char* sup = a.sup + (size_t)b * a.A;
   const size_t ib = (size_t)b * a.A;
-  for (int i = tid; i < n; i += NMS_T) {
-    const unsigned ai = 0xFFFFFFFFu - (unsigned)(k[i] & 0xFFFFFFFFull);
-    const float4 bx = a.boxes[ib + ai];
-    const float off = a.agnostic ? 0.0f : (float)a.cls[ib + ai] * a.max_wh;
-    const float4 o = make_float4(bx.x + off, bx.y + off, bx.z + off, bx.w + off);
-    sb[i] = o;
-    sa[i] = __fmul_rn(__fsub_rn(o.z, o.x), __fsub_rn(o.w, o.y));
-    sup[i] = 0;
-  }
-
-  __syncthreads();
-
   const int rowlen = 6 + a.nm;
   float* out = a.dets + (size_t)b * a.max_det * rowlen;
-  int kept = 0;
-  for (int i = 0; i < n && kept < a.max_det; ++i) {
-    if (sup[i]) continue;  // written before the last barrier; uniform across the workgroup
-    const float4 bi = sb[i];
-    const float ai_area = sa[i];
-    if (tid == 0) {
-      const unsigned ai = 0xFFFFFFFFu - (unsigned)(k[i] & 0xFFFFFFFFull);
-      const float4 bx = a.boxes[ib + ai];
-      float* r = out + (size_t)kept * rowlen;
-      r[0] = fminf(fmaxf(bx.x, 0.f), a.img_w);
-      r[1] = fminf(fmaxf(bx.y, 0.f), a.img_h);
-      r[2] = fminf(fmaxf(bx.z, 0.f), a.img_w);
-      r[3] = fminf(fmaxf(bx.w, 0.f), a.img_h);
+  if (n <= 64) {
+    // common case at predict thresholds: one wave, everything in registers, no barriers.
+    // lane i holds candidate i; bitonic sort by key across lanes, then the greedy scan with shuffles.
+    if (tid >= 64) return;
+    const int lane = tid;
+    unsigned long long key = lane < n ? gk[lane] : 0ull;
+#pragma unroll
+    for (int size = 2; size <= 64; size <<= 1) {
+#pragma unroll
+      for (int stride = size >> 1; stride > 0; stride >>= 1) {
+        const unsigned long long other = __shfl_xor(key, stride);
+        const bool desc = (lane & size) == 0 || size == 64;
+        const bool lower = (lane & stride) == 0;
+        const bool keep_max = lower == desc;
+        key = keep_max ? (key > other ? key : other) : (key < other ? key : other);
+      }
+    }
+    const int ne = n < a.max_nms ? n : a.max_nms;
+    const unsigned ai = 0xFFFFFFFFu - (unsigned)(key & 0xFFFFFFFFull);
+    float4 bx = make_float4(0.f, 0.f, 0.f, 0.f);
+    float ar = 0.f;
+    if (lane < ne) {
+      const float4 v = a.boxes[ib + ai];
+      const float off = a.agnostic ? 0.0f : (float)a.cls[ib + ai] * a.max_wh;
+      bx = make_float4(v.x + off, v.y + off, v.z + off, v.w + off);
+      ar = __fmul_rn(__fsub_rn(bx.z, bx.x), __fsub_rn(bx.w, bx.y));
+    }
+    int sup = lane >= ne;
+    int keep = 0, kept = 0;
+    for (int i = 0; i < ne && kept < a.max_det; ++i) {
+      if (__shfl(sup, i)) continue;
+      ++kept;
+      if (lane == i) keep = 1;
+      const float4 bi = make_float4(__shfl(bx.x, i), __shfl(bx.y, i), __shfl(bx.z, i), __shfl(bx.w, i));
+      const float ai_area = __shfl(ar, i);
+      if (lane > i && !sup && iou_gt(bi, ai_area, bx, ar, a.iou)) sup = 1;
+    }
+    const unsigned long long km = __ballot(keep);
+    if (keep) {
+      const int pos = __popcll(km & ((1ull << lane) - 1ull));
+      const float4 v = a.boxes[ib + ai];
+      float* r = out + (size_t)pos * rowlen;
+      r[0] = fminf(fmaxf(v.x, 0.f), a.img_w);
+      r[1] = fminf(fmaxf(v.y, 0.f), a.img_h);
+      r[2] = fminf(fmaxf(v.z, 0.f), a.img_w);
+      r[3] = fminf(fmaxf(v.w, 0.f), a.img_h);
       r[4] = a.scores[ib + ai];
       r[5] = (float)a.cls[ib + ai];
       for (int m = 0; m < a.nm; ++m) r[6 + m] = a.anchors[(ib + ai) * a.no_tot + a.mask_off + m];
     }
+    if (lane == 0) a.out_counts[b] = kept;
+    return;
+  }
+  int n2 = 1;
+  while (n2 < n) n2 <<= 1;
+  const bool lds = n2 <= NMS_LDS;
+  unsigned long long* k = lds ? sk : gk;
+  if (lds) {
+    for (int i = tid; i < n2; i += NMS_T) sk[i] = i < n ? gk[i] : 0ull;
+  } else {
+    for (int i = n + tid; i < n2; i += NMS_T) gk[i] = 0ull;  // keys have a power-of-two stride >= A
+  }
+  __syncthreads();
+  if (n > 1) bitonic_sort_desc(k, n2, tid);
+  if (n > a.max_nms) n = a.max_nms;
+  float4* bx = lds ? sbx : a.sboxes + (size_t)b * a.A;
+  float* ar = lds ? sar : a.sareas + (size_t)b * a.A;
+  unsigned char* sup = lds ? ssup : a.sup + (size_t)b * a.A;
+  for (int i = tid; i < n; i += NMS_T) {
+    const unsigned ai = 0xFFFFFFFFu - (unsigned)(k[i] & 0xFFFFFFFFull);
+    const float4 v = a.boxes[ib + ai];
+    const float off = a.agnostic ? 0.0f : (float)a.cls[ib + ai] * a.max_wh;
+    const float4 o = make_float4(v.x + off, v.y + off, v.z + off, v.w + off);
+    bx[i] = o;
+    ar[i] = __fmul_rn(__fsub_rn(o.z, o.x), __fsub_rn(o.w, o.y));
+    sup[i] = 0;
+  }
+  __syncthreads();
+  // greedy scan: only LDS traffic inside the loop (a global store here would make every barrier drain vmcnt);
+  // the kept sorted positions are recorded and written out in parallel afterwards
+  __shared__ int keep_pos[1024];
+  const int cap = a.max_det < 1024 ? a.max_det : 1024;
+  int kept = 0;
+  for (int i = 0; i < n && kept < cap; ++i) {
+    if (sup[i]) continue;  // written before the last barrier; uniform across the workgroup
+    const float4 bi = bx[i];
+    const float ai_area = ar[i];
+    if (tid == 0) keep_pos[kept] = i;
     ++kept;
-    for (int j = i + 1 + tid; j < n; j += NMS_T) {
-      if (sup[j]) continue;
-      const float4 bj = sb[j];
-      const float xx1 = fmaxf(bi.x, bj.x), yy1 = fmaxf(bi.y, bj.y);
-      const float xx2 = fminf(bi.z, bj.z), yy2 = fminf(bi.w, bj.w);
-      const float w = fmaxf(0.0f, __fsub_rn(xx2, xx1));
-      const float h = fmaxf(0.0f, __fsub_rn(yy2, yy1));
-      const float inter = __fmul_rn(w, h);
-      const float ovr = __fdiv_rn(inter, __fsub_rn(__fadd_rn(ai_area, sa[j]), inter));
-      if ((double)ovr > a.iou) sup[j] = 1;
-    }
+    for (int j = i + 1 + tid; j < n; j += NMS_T)
+      if (!sup[j] && iou_gt(bi, ai_area, bx[j], ar[j], a.iou)) sup[j] = 1;
     __syncthreads();
+  }
+  __syncthreads();
+  for (int q = tid; q < kept; q += NMS_T) {
+    const int i = keep_pos[q];
+    const unsigned ai = 0xFFFFFFFFu - (unsigned)(k[i] & 0xFFFFFFFFull);
+    const float4 v = a.boxes[ib + ai];
+    float* r = out + (size_t)q * rowlen;
+    r[0] = fminf(fmaxf(v.x, 0.f), a.img_w);
+    r[1] = fminf(fmaxf(v.y, 0.f), a.img_h);
+    r[2] = fminf(fmaxf(v.z, 0.f), a.img_w);
+    r[3] = fminf(fmaxf(v.w, 0.f), a.img_h);
+    r[4] = a.scores[ib + ai];
+    r[5] = (float)a.cls[ib + ai];
+    for (int m = 0; m < a.nm; ++m) r[6 + m] = a.anchors[(ib + ai) * a.no_tot + a.mask_off + m];
   }
   if (tid == 0) a.out_counts[b] = kept;
 }
@@ -414,48 +514,69 @@ __global__ __launch_bounds__(NMS_T) void nms_image(const NmsArgs a) {
 
 // ------------------------------------------------------------------------------------------------- launchers
 hipError_t ym_launch_prep(int dtype, const PrepArgs& a, int* counts, int B, hipStream_t st) {
+  (void)dtype;
   hipLaunchKernelGGL(init_ctl, dim3(1), dim3(64), 0, st, a.ctl, counts, B);
+  // one atomic per block: a few hundred same-address atomics, not thousands (one word takes ~90 per us)
   const long n = (long)a.B * a.C * a.H * a.W;
   long blocks = (n / 4 + 255) / 256;
-  if (blocks > 2048) blocks = 2048;
+  if (blocks > 512) blocks = 512;
   if (blocks < 1) blocks = 1;
   hipLaunchKernelGGL(max_reduce, dim3(blocks), dim3(256), 0, st, a.in, n, a.ctl);
-  const long np = (long)a.B * a.H * a.W;
-  if (dtype == YM_DT_F16)
-    hipLaunchKernelGGL(prep_nhwc<f16>, dim3((np + 255) / 256), dim3(256), 0, st, a);
-  else
-    hipLaunchKernelGGL(prep_nhwc<float>, dim3((np + 255) / 256), dim3(256), 0, st, a);
   return hipGetLastError();
 }
 
 hipError_t ym_launch_dwconv(int dtype, const DwArgs& a, hipStream_t st) {
   const long total = (long)a.B * a.H * a.W * (a.C / 8);
   const dim3 g((total + 255) / 256);
-  if (dtype == YM_DT_F16) hipLaunchKernelGGL(dwconv3x3<f16>, g, dim3(256), 0, st, a);
-  else hipLaunchKernelGGL(dwconv3x3<float>, g, dim3(256), 0, st, a);
+  const size_t lds = (size_t)10 * a.C * sizeof(float);
+  if (dtype == YM_DT_F16) hipLaunchKernelGGL(dwconv3x3<f16>, g, dim3(256), lds, st, a);
+  else hipLaunchKernelGGL(dwconv3x3<float>, g, dim3(256), lds, st, a);
   return hipGetLastError();
 }
 
 hipError_t ym_launch_sppf(int dtype, const PoolArgs& a, hipStream_t st) {
-  const long total = (long)a.B * a.H * a.W * (a.C / 8);
-  const dim3 g((total + 255) / 256);
-  if (dtype == YM_DT_F16) hipLaunchKernelGGL(sppf_pool<f16>, g, dim3(256), 0, st, a);
-  else hipLaunchKernelGGL(sppf_pool<float>, g, dim3(256), 0, st, a);
+  const size_t HW = (size_t)a.H * a.W;
+  const size_t img = HW * 8 * (dtype == YM_DT_F16 ? 2 : 4);
+  PoolArgs b = a;
+  b.sep = 4 * img <= 128 * 1024;  // input + 3 row-max images, 8 channels
+  const size_t lds = b.sep ? 4 * img : img;
+  if (a.C % 8 || lds > 160 * 1024) return hipErrorInvalidValue;
+  const dim3 g(a.B * (a.C / 8));
+  if (dtype == YM_DT_F16) hipLaunchKernelGGL(sppf_pool<f16>, g, dim3(256), lds, st, b);
+  else hipLaunchKernelGGL(sppf_pool<float>, g, dim3(256), lds, st, b);
+  return hipGetLastError();
+}
+
+template <typename T>
+hipError_t launch_attn_t(const AttnArgs& a, hipStream_t st) {
+  const size_t budget = 150 * 1024;
+  auto lds = [&](int qb) { return ((size_t)qb * a.N + (size_t)qb * AKD + 64 * AHD) * sizeof(float); };
+  // fewer queries per workgroup = more workgroups: with one wave per SIMD nothing hides this kernel's latencies
+  auto wgs = [&](int qb) { return (long)a.B * a.nh * ((a.N + qb - 1) / qb); };
+  if (lds(32) <= budget && wgs(32) >= 512) {
+    hipLaunchKernelGGL((attn_psa<T, 32>), dim3(a.B * a.nh * ((a.N + 31) / 32)), dim3(256), lds(32), st, a);
+  } else if (lds(16) <= budget && (wgs(16) >= 512 || lds(8) > budget)) {
+    hipLaunchKernelGGL((attn_psa<T, 16>), dim3(a.B * a.nh * ((a.N + 15) / 16)), dim3(256), lds(16), st, a);
+  } else if (lds(8) <= budget) {
+    hipLaunchKernelGGL((attn_psa<T, 8>), dim3(a.B * a.nh * ((a.N + 7) / 8)), dim3(256), lds(8), st, a);
+  } else if (lds(4) <= budget) {
+    hipLaunchKernelGGL((attn_psa<T, 4>), dim3(a.B * a.nh * ((a.N + 3) / 4)), dim3(256), lds(4), st, a);
+  } else {
+    return hipErrorInvalidValue;  // N > ~9,600 tokens (input > 3136 px): not supported
+  }
   return hipGetLastError();
 }
 
 hipError_t ym_launch_attn(int dtype, const AttnArgs& a, hipStream_t st) {
   if (a.kd > AKD || a.hd > AHD) return hipErrorInvalidValue;
-  const int nqb = (a.N + AQ - 1) / AQ;
-  const dim3 g(a.B * a.nh * nqb);
-  if (dtype == YM_DT_F16) hipLaunchKernelGGL(attn_psa<f16>, g, dim3(256), 0, st, a);
-  else hipLaunchKernelGGL(attn_psa<float>, g, dim3(256), 0, st, a);
-  return hipGetLastError();
+  return dtype == YM_DT_F16 ? launch_attn_t<f16>(a, st) : launch_attn_t<float>(a, st);
 }
 
 hipError_t ym_launch_decode(const DecodeArgs& a, hipStream_t st) {
   const long total = (long)a.B * a.A;
-  hipLaunchKernelGGL(decode_anchors, dim3((total + 255) / 256), dim3(256), 0, st, a);
+  if (a.no_tot % 4) return hipErrorInvalidValue;
+  hipLaunchKernelGGL(decode_anchors, dim3((total + 63) / 64), dim3(256), (size_t)64 * a.no_tot * sizeof(float), st,
+                     a);
   return hipGetLastError();
 }
 

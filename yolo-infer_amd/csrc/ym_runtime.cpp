@@ -90,6 +90,13 @@ struct ym_ctx {
   hipStream_t cap_stream = nullptr;
   std::vector<GraphEntry> graphs;
   std::vector<hipEvent_t> prof_events;
+  // per-op conv tile configuration for the current workspace shape (-1 = heuristic); set by ym_tune / ym_set_op_cfg
+  std::vector<int> cfg;
+  int tB = 0, tH = 0, tW = 0;
+  int op_cfg(long i, int B) const {
+    if (B != tB || cH != tH || cW != tW) return -1;
+    return (i >= 0 && i < (long)cfg.size()) ? cfg[i] : -1;
+  }
 
   ~ym_ctx() {
     (void)hipSetDevice(device);
@@ -144,6 +151,7 @@ int ensure_workspace(ym_ctx* c, int B, int H, int W) {
   c->buf_off.assign(c->bufs.size(), 0);
   for (size_t b = 0; b < c->bufs.size(); ++b) {
     c->buf_off[b] = off;
+    if ((int)b == c->input_buf) continue;  // the stem conv reads the caller's NCHW fp32 batch directly
     off = align_up(off + (size_t)nB * c->buf_P((int)b) * c->bufs[b].C * c->elem((int)b), 256);
   }
   const size_t BA = (size_t)nB * c->A;
@@ -167,28 +175,20 @@ int ensure_workspace(ym_ctx* c, int B, int H, int W) {
   return YM_OK;
 }
 
-int launch_op(ym_ctx* c, const Op& op, int B, const float* d_in, const ym_infer_args* args, float* d_dets,
-              int* d_counts, hipStream_t st) {
-  const int32_t* r = op.r;
-  const int dt = c->dtype;
-  hipError_t e = hipSuccess;
-  switch (r[0]) {
-    case OP_INPUT: {
-      PrepArgs a{};
-      a.in = d_in;
-      a.out = c->bptr(c->input_buf);
-      a.ctl = reinterpret_cast<float*>(c->d_arena + c->off_ctl);
-      a.B = B; a.C = 3; a.H = c->cH; a.W = c->cW;
-      a.eps = args->in_eps;
-      e = ym_launch_prep(dt, a, reinterpret_cast<int*>(c->d_arena + c->off_counts), B, st);
-      break;
-    }
-    case OP_CONV: {
-      ConvArgs a{};
+// Kernel arguments of a conv op for batch B at the current workspace shape.
+int conv_args(ym_ctx* c, const Op& op, int B, const float* d_in, float in_eps, ConvArgs& a, int& out_f32) {
+      const int32_t* r = op.r;
+      a = ConvArgs{};
       const int k = r[1], s = r[2], cin = r[3], cout = r[4];
       const int b0 = r[6], b1 = r[10], bd = r[13], br = r[17];
       const int up0 = r[9];
       a.src0 = c->bptr(b0); a.s0_ctot = c->bufs[b0].C; a.s0_coff = r[7]; a.C0 = r[8];
+      if (b0 == c->input_buf) {  // stem: NCHW fp32 source, LoadTensor /255 decided on device from ctl[0]
+        a.src0 = nullptr;
+        a.nchw = d_in;
+        a.ctl = reinterpret_cast<const float*>(c->d_arena + c->off_ctl);
+        a.eps = in_eps;
+      }
       a.s0_W = c->buf_Wd(b0); a.s0_P = c->buf_P(b0); a.up0 = up0;
       a.Hin = c->buf_H(b0) * (up0 ? 2 : 1);
       a.Win = c->buf_Wd(b0) * (up0 ? 2 : 1);
@@ -226,7 +226,32 @@ int launch_op(ym_ctx* c, const Op& op, int B, const float* d_in, const ym_infer_
       }
       if (br >= 0) { a.res = c->bptr(br); a.r_ctot = c->bufs[br].C; a.r_coff = r[18]; a.r_P = c->buf_P(br); }
       a.M = B * a.Ho * a.Wo;
-      e = ym_launch_conv(dt, c->bufs[bd].f32 && dt == YM_DT_F16, a, st);
+      out_f32 = c->bufs[bd].f32 && c->dtype == YM_DT_F16;
+      return YM_OK;
+}
+
+int launch_op(ym_ctx* c, const Op& op, int B, const float* d_in, const ym_infer_args* args, float* d_dets,
+              int* d_counts, hipStream_t st) {
+  const int32_t* r = op.r;
+  const int dt = c->dtype;
+  hipError_t e = hipSuccess;
+  switch (r[0]) {
+    case OP_INPUT: {
+      PrepArgs a{};
+      a.in = d_in;
+      a.out = c->bptr(c->input_buf);
+      a.ctl = reinterpret_cast<float*>(c->d_arena + c->off_ctl);
+      a.B = B; a.C = 3; a.H = c->cH; a.W = c->cW;
+      a.eps = args->in_eps;
+      e = ym_launch_prep(dt, a, reinterpret_cast<int*>(c->d_arena + c->off_counts), B, st);
+      break;
+    }
+    case OP_CONV: {
+      ConvArgs a{};
+      int out_f32 = 0;
+      const int rc = conv_args(c, op, B, d_in, args->in_eps, a, out_f32);
+      if (rc) return rc;
+      e = a.nchw ? ym_launch_stem(dt, a, st) : ym_launch_conv(dt, out_f32, a, c->op_cfg(&op - c->ops.data(), B), st);
       break;
     }
     case OP_DW: {
@@ -317,6 +342,7 @@ int check_call(ym_ctx* c, const float* d_in, int B, int H, int W, const ym_infer
   if (B < 1 || H < 32 || W < 32 || H % 32 || W % 32)
     return fail(YM_EINVAL, "input shape (%d,3,%d,%d): H and W must be positive multiples of 32", B, H, W);
   if (args->max_det < 1 || args->max_nms < 1) return fail(YM_EINVAL, "max_det/max_nms must be >= 1");
+  if (args->max_det > 1024) return fail(YM_EINVAL, "max_det %d > 1024 is not supported", args->max_det);
   return YM_OK;
 }
 
@@ -453,6 +479,82 @@ int ym_profile(ym_ctx* c, const float* d_in, int B, int H, int W, const ym_infer
   HIPCK(hipEventSynchronize(c->prof_events[ne - 1]));
   for (size_t i = 0; i < c->ops.size(); ++i)
     HIPCK(hipEventElapsedTime(&op_ms[i], c->prof_events[i], c->prof_events[i + 1]));
+  return YM_OK;
+}
+
+int ym_tune(ym_ctx* c, const float* d_in, int B, int H, int W, const ym_infer_args* args, float* d_dets,
+            int* d_counts, void* stream, int reps) {
+  int rc = check_call(c, d_in, B, H, W, args, d_dets, d_counts);
+  if (rc) return rc;
+  HIPCK(hipSetDevice(c->device));
+  hipStream_t st = static_cast<hipStream_t>(stream);
+  if ((rc = ensure_workspace(c, B, H, W))) return rc;
+  if (reps < 1) reps = 8;
+  // one real forward first so every buffer a candidate reads holds this model's activations
+  c->tB = c->tH = c->tW = 0;
+  for (const Op& op : c->ops)
+    if ((rc = launch_op(c, op, B, d_in, args, d_dets, d_counts, st))) return rc;
+  HIPCK(hipStreamSynchronize(st));
+  std::vector<int> best(c->ops.size(), -1);
+  hipEvent_t e0, e1;
+  HIPCK(hipEventCreate(&e0));
+  HIPCK(hipEventCreate(&e1));
+  const int ncfg = ym_conv_num_cfgs();
+  for (size_t i = 0; i < c->ops.size(); ++i) {
+    const Op& op = c->ops[i];
+    if (op.r[0] != OP_CONV) continue;
+    ConvArgs a;
+    int out_f32 = 0;
+    if ((rc = conv_args(c, op, B, d_in, args->in_eps, a, out_f32))) return rc;
+    if (a.nchw) continue;  // the stem has its own kernel (csrc/ym_stem.hip)
+    float bt = 1e30f;
+    for (int cf = 0; cf < ncfg; ++cf) {
+      // time `reps` back-to-back launches of this candidate as one graph: device-bound even for tiny kernels
+      hipGraph_t g = nullptr;
+      hipGraphExec_t ge = nullptr;
+      HIPCK(hipStreamBeginCapture(c->cap_stream, hipStreamCaptureModeRelaxed));
+      hipError_t le = hipSuccess;
+      for (int r = 0; r < reps && le == hipSuccess; ++r) le = ym_launch_conv(c->dtype, out_f32, a, cf, c->cap_stream);
+      HIPCK(hipStreamEndCapture(c->cap_stream, &g));
+      if (le != hipSuccess) {
+        (void)hipGraphDestroy(g);
+        continue;
+      }
+      HIPCK(hipGraphInstantiate(&ge, g, nullptr, nullptr, 0));
+      HIPCK(hipGraphLaunch(ge, st));
+      HIPCK(hipEventRecord(e0, st));
+      HIPCK(hipGraphLaunch(ge, st));
+      HIPCK(hipGraphLaunch(ge, st));
+      HIPCK(hipEventRecord(e1, st));
+      HIPCK(hipEventSynchronize(e1));
+      float ms = 0.f;
+      HIPCK(hipEventElapsedTime(&ms, e0, e1));
+      (void)hipGraphExecDestroy(ge);
+      (void)hipGraphDestroy(g);
+      if (ms < bt) { bt = ms; best[i] = cf; }
+    }
+  }
+  (void)hipEventDestroy(e0);
+  (void)hipEventDestroy(e1);
+  c->clear_graphs();
+  c->cfg = best;
+  c->tB = B; c->tH = H; c->tW = W;
+  return YM_OK;
+}
+
+int ym_get_op_cfg(ym_ctx* c, int* cfg, int n) {
+  if (!c || !cfg || n < (int)c->ops.size()) return fail(YM_EINVAL, "cfg array must hold %zu entries", c ? c->ops.size() : 0);
+  for (size_t i = 0; i < c->ops.size(); ++i) cfg[i] = c->op_cfg((long)i, c->tB);
+  return YM_OK;
+}
+
+int ym_set_op_cfg(ym_ctx* c, int B, int H, int W, const int* cfg, int n) {
+  if (!c || !cfg || n != (int)c->ops.size()) return fail(YM_EINVAL, "cfg array must hold %zu entries", c ? c->ops.size() : 0);
+  for (int i = 0; i < n; ++i)
+    if (cfg[i] >= ym_conv_num_cfgs()) return fail(YM_EINVAL, "cfg[%d] = %d out of range", i, cfg[i]);
+  c->cfg.assign(cfg, cfg + n);
+  c->tB = B; c->tH = H; c->tW = W;
+  c->clear_graphs();
   return YM_OK;
 }
 

@@ -312,10 +312,52 @@ class GraphBuilder:
         # the stem reads 3 real channels out of the 8-channel padded input: pad its weights' Cin to 8 at pack time
 
     # ------------------------------------------------------------------ accounting
+    def op_costs(self, B: int, H: int, W: int, act_bytes: int = 2):
+        """Per op (aligned with self.ops): (algorithmic FLOPs, algorithmic HBM bytes) for one forward of B images.
+        FLOPs = 2·MACs (stem counted at its real Cin=3); bytes = each input element read once + weights +
+        outputs written once (+ residual read), at the storage dtype."""
+        out = []
+        for op in self.ops:
+            a = op.args
+            fl, by = 0, 0
+            if op.kind == "conv":
+                fo = self.out_factor(op)
+                npx = B * (H // fo) * (W // fo)
+                cin = 3 if op.name == "model.0" else a["c1"]
+                fl = 2 * npx * a["k"] * a["k"] * cin * a["c2"]
+                f0 = a["src0"].buf.f
+                by += B * (H // f0) * (W // f0) * a["src0"].C * act_bytes
+                if a["src1"] is not None:
+                    f1 = a["src1"].buf.f
+                    by += B * (H // f1) * (W // f1) * a["src1"].C * act_bytes
+                by += a["k"] * a["k"] * cin * a["c2"] * act_bytes + a["c2"] * 4
+                ob = 4 if a["dst"].buf.f32 else act_bytes
+                by += npx * a["c2"] * ob
+                if a["res"] is not None:
+                    by += npx * a["c2"] * act_bytes
+            elif op.kind == "dwconv":
+                f = a["src"].buf.f
+                npx = B * (H // f) * (W // f)
+                fl = 2 * npx * 9 * a["C"]
+                by = 2 * npx * a["C"] * act_bytes
+            elif op.kind == "sppf":
+                f = a["dst"].f
+                npx = B * (H // f) * (W // f)
+                by = 4 * npx * a["C"] * act_bytes
+            elif op.kind == "attn":
+                f = a["qkv"].buf.f
+                N = (H // f) * (W // f)
+                fl = 2 * B * (N * N * a["nh"] * (a["kd"] + a["hd"]) + N * 9 * a["C"])
+                by = B * N * (a["qkv"].C + a["C"]) * act_bytes
+            elif op.kind == "input":
+                by = B * H * W * (3 * 4 * 2 + 8 * act_bytes)
+            elif op.kind == "decode":
+                A = sum((H // s) * (W // s) for s in STRIDES)
+                by = B * A * (a["anchor"].C * 4 + 24)
+            out.append((fl, by))
+        return out
+
     def macs_per_image(self, H: int = 640, W: int = 640) -> int:
-        tot = 0
-        for _, f, m in self.flops_per_pixel:
-            pass
         # exact count from conv op geometry
         tot = 0
         for op in self.ops:

@@ -5,6 +5,7 @@ of the forward runs in libyolomi's gfx950 kernels.
 """
 from __future__ import annotations
 
+import os
 from typing import Dict, Optional, Sequence
 
 import numpy as np
@@ -27,6 +28,9 @@ class Engine:
         self.rt = Runtime(device.index if device.index is not None else torch.cuda.current_device(), self.blob)
         self.nm = self.graph.nm
         self._out: Dict[int, tuple] = {}
+        # per-shape on-device autotuning of the conv tiles (ym_tune) on the first call of each (B, H, W)
+        self.autotune = os.environ.get("YM_AUTOTUNE", "1") != "0"
+        self._tuned = set()
 
     def outputs(self, B: int, max_det: int):
         key = (B, max_det)
@@ -46,6 +50,9 @@ class Engine:
         args = Runtime.make_args(conf, iou, max_det, max_nms, agnostic, max_wh, in_eps, classes, use_graph)
         dets, counts = self.outputs(B, max_det)
         stream = torch.cuda.current_stream(self.device).cuda_stream
+        if self.autotune and (B, H, W) not in self._tuned:
+            self.rt.tune(x.data_ptr(), B, H, W, args, dets.data_ptr(), counts.data_ptr(), stream)
+            self._tuned.add((B, H, W))
         self.rt.infer(x.data_ptr(), B, H, W, args, dets.data_ptr(), counts.data_ptr(), stream)
         return dets, counts
 

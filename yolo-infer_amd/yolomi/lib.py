@@ -46,6 +46,9 @@ def load_library(path: os.PathLike = LIB_PATH):
         "ym_load_weights": (I, [P, P, C.c_size_t]),
         "ym_infer": (I, [P, P, I, I, I, C.POINTER(InferArgs), P, P, P]),
         "ym_profile": (I, [P, P, I, I, I, C.POINTER(InferArgs), P, P, P, F, I]),
+        "ym_tune": (I, [P, P, I, I, I, C.POINTER(InferArgs), P, P, P, I]),
+        "ym_get_op_cfg": (I, [P, C.POINTER(I), I]),
+        "ym_set_op_cfg": (I, [P, I, I, I, C.POINTER(I), I]),
         "ym_num_ops": (I, [P]),
         "ym_op_name": (C.c_char_p, [P, I]),
         "ym_num_buffers": (I, [P]),
@@ -64,7 +67,8 @@ def load_library(path: os.PathLike = LIB_PATH):
     return lib
 
 
-EXPORTED = ("ym_create", "ym_load_weights", "ym_infer", "ym_profile", "ym_num_ops", "ym_op_name", "ym_num_buffers",
+EXPORTED = ("ym_create", "ym_load_weights", "ym_infer", "ym_profile", "ym_tune", "ym_get_op_cfg", "ym_set_op_cfg",
+            "ym_num_ops", "ym_op_name", "ym_num_buffers",
             "ym_buffer_info", "ym_read_buffer", "ym_sync", "ym_last_error", "ym_destroy", "ym_version")
 
 
@@ -111,6 +115,19 @@ class Runtime:
         _check(self.lib.ym_profile(self.ctx, C.c_void_p(x_ptr), B, H, W, C.byref(args), C.c_void_p(dets_ptr),
                                    C.c_void_p(counts_ptr), C.c_void_p(stream), ms, self.n_ops))
         return list(ms)
+
+    def tune(self, x_ptr, B, H, W, args, dets_ptr, counts_ptr, stream, reps=8):
+        _check(self.lib.ym_tune(self.ctx, C.c_void_p(x_ptr), B, H, W, C.byref(args), C.c_void_p(dets_ptr),
+                                C.c_void_p(counts_ptr), C.c_void_p(stream), reps))
+
+    def get_op_cfg(self):
+        arr = (C.c_int * self.n_ops)()
+        _check(self.lib.ym_get_op_cfg(self.ctx, arr, self.n_ops))
+        return list(arr)
+
+    def set_op_cfg(self, B, H, W, cfg):
+        arr = (C.c_int * self.n_ops)(*cfg)
+        _check(self.lib.ym_set_op_cfg(self.ctx, B, H, W, arr, self.n_ops))
 
     def buffer_info(self, buf: int):
         p, c, h, w, e = C.c_void_p(), C.c_int(), C.c_int(), C.c_int(), C.c_int()

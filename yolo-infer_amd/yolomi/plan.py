@@ -22,7 +22,7 @@ MAGIC = 0x4C504D59
 VERSION = 1
 OP_IDS = {"input": 1, "conv": 2, "dwconv": 3, "sppf": 4, "attn": 5, "decode": 6, "nms": 7}
 DTYPES = {"f16": 0, "f32": 1}
-BK = 32
+BK = 64  # conv K is padded to the kernel K step (csrc/ym_conv.hip KSTEP)
 
 
 def fuse_conv_bn(w: np.ndarray, gamma, beta, mean, var, eps=1e-3):
