@@ -1,0 +1,107 @@
+"""Generate the committed golden fixtures from the CPU oracle.
+
+    python tests/golden/make_golden.py
+
+Parity with Ultralytics itself is UNPINNED (the reference ships no fixtures/tests and Ultralytics is not installable
+offline); these vectors pin the oracle + the portable synthetic weights so the GPU path and future rounds are checked
+against fixed numbers.  Inputs are regenerated from seeds (splitmix64, bit-portable); outputs are stored.
+
+Fixtures (tests/golden/*.json):
+  weights_<scale>.json  : per-tensor sum / abs-sum of the synthetic state dict (seed 0) + fused conv checksums
+  det_n_uniform.json    : yolo11n, 2 x U[0,1) 640x640 (seeds 1001, 1002), conf 0.25 iou 0.7: per-image (n,6) dets,
+                          per-layer output checksums and sampled values (L2, L9, L16, L22, head)
+  det_n_randn.json      : yolo11n, 1 x N(0,1) 640x640 (seed 2001) → LoadTensor /255 rule, conf 0.25
+  det_n_320_lowconf.json: yolo11n, 1 x U[0,1) 320x320 (seed 3001), conf 0.05 (many candidates)
+  det_s_uniform.json    : yolo11s, 1 x U[0,1) 640x640 (seed 4001)
+"""
+from __future__ import annotations
+
+import json
+import os
+import sys
+
+import numpy as np
+import torch
+
+ROOT = os.path.dirname(os.path.dirname(os.path.dirname(os.path.abspath(__file__))))
+sys.path.insert(0, os.path.join(ROOT, "yolo-infer_amd"))
+sys.path.insert(0, ROOT)
+
+from oracle.predict import OracleModel  # noqa: E402
+from yolomi.plan import fuse_conv_bn  # noqa: E402
+from yolomi.synth import normal, synth_weights, uniform  # noqa: E402
+
+HERE = os.path.dirname(os.path.abspath(__file__))
+LAYERS = (2, 9, 16, 22)
+
+
+def make_input(kind: str, seeds, S: int) -> torch.Tensor:
+    xs = []
+    for s in seeds:
+        n = 3 * S * S
+        v = uniform(s, n) if kind == "uniform" else normal(s, n)
+        xs.append(v.astype(np.float32).reshape(3, S, S))
+    return torch.from_numpy(np.stack(xs))
+
+
+def layer_stats(t: torch.Tensor):
+    t = t.double()
+    flat = t.reshape(-1)
+    idx = np.linspace(0, flat.numel() - 1, 16).astype(np.int64)
+    return {"shape": list(t.shape), "sum": float(t.sum()), "abs_sum": float(t.abs().sum()),
+            "samples_idx": idx.tolist(), "samples": flat[idx].tolist()}
+
+
+def det_fixture(scale, kind, seeds, S, conf=0.25, iou=0.7):
+    sd = synth_weights(scale, "detect", 0)
+    om = OracleModel(scale, "detect", sd)
+    x = make_input(kind, seeds, S)
+    im, y, ex = om.raw(x, keep=LAYERS)
+    B = x.shape[0]
+    no = 144
+    head = torch.cat([f.view(B, no, -1) for f in ex["feats"]], 2).transpose(1, 2)
+    dets = om.predict(x, conf=conf, iou=iou)
+    return {
+        "scale": scale, "task": "detect", "weights_seed": 0, "input": {"kind": kind, "seeds": list(seeds), "size": S},
+        "conf": conf, "iou": iou, "max_det": 300,
+        "layers": {f"L{i}": layer_stats(ex["saved"][i].permute(0, 2, 3, 1)) for i in LAYERS},
+        "head": layer_stats(head),
+        "dets": [d["boxes"].tolist() for d in dets],
+    }
+
+
+def weight_fixture(scale):
+    sd = synth_weights(scale, "detect", 0)
+    out = {"scale": scale, "seed": 0, "tensors": {}}
+    for k in sorted(sd):
+        v = sd[k].astype(np.float64)
+        out["tensors"][k] = [float(v.sum()), float(np.abs(v).sum())]
+    fused = {}
+    for k in sorted(sd):
+        p = k[: -len(".conv.weight")]
+        if k.endswith(".conv.weight") and p + ".bn.weight" in sd:
+            w, b = fuse_conv_bn(sd[k], sd[p + ".bn.weight"], sd[p + ".bn.bias"], sd[p + ".bn.running_mean"],
+                                sd[p + ".bn.running_var"])
+            fused[p] = [float(w.astype(np.float64).sum()), float(b.astype(np.float64).sum())]
+    out["fused"] = fused
+    return out
+
+
+def main():
+    torch.set_num_threads(min(8, os.cpu_count() or 1))
+    for scale in ("n", "s"):
+        json.dump(weight_fixture(scale), open(os.path.join(HERE, f"weights_{scale}.json"), "w"), indent=0)
+    fx = {
+        "det_n_uniform": ("n", "uniform", (1001, 1002), 640, 0.25),
+        "det_n_randn": ("n", "randn", (2001,), 640, 0.25),
+        "det_n_320_lowconf": ("n", "uniform", (3001,), 320, 0.05),
+        "det_s_uniform": ("s", "uniform", (4001,), 640, 0.25),
+    }
+    for name, (scale, kind, seeds, S, conf) in fx.items():
+        d = det_fixture(scale, kind, seeds, S, conf)
+        json.dump(d, open(os.path.join(HERE, f"{name}.json"), "w"))
+        print(name, [len(x) for x in d["dets"]])
+
+
+if __name__ == "__main__":
+    main()

@@ -60,13 +60,27 @@ def _exempt(d: np.ndarray, same: np.ndarray, conf: float, iou_thr: float, conf_m
 
 
 def match_image(ref: np.ndarray, got: np.ndarray, conf: float, iou_thr: float, tol_xy: float, tol_score: float,
-                conf_margin: float = 2e-3, iou_margin: float = 2e-2, rep: MatchReport = None) -> MatchReport:
+                conf_margin: float = 2e-3, iou_margin: float = 2e-2, rep: MatchReport = None,
+                max_det: int = 300) -> MatchReport:
+    """When a list is truncated at max_det, detections scoring within conf_margin of the last kept score are
+    exempt too (which of several near-equal candidates make the cut is an ulp-level decision)."""
     rep = rep or MatchReport()
     ref = ref[np.argsort(-ref[:, 4], kind="stable")] if len(ref) else ref.reshape(0, 6)
     got = got[np.argsort(-got[:, 4], kind="stable")] if len(got) else got.reshape(0, 6)
+    cut = -np.inf
+    for d in (ref, got):
+        if len(d) >= max_det:
+            cut = max(cut, float(d[:, 4].min()))
     used = np.zeros(len(got), bool)
     ious = iou_matrix(ref[:, :4], got[:, :4])
-    ex_ref = _exempt(ref, ref, conf, iou_thr, conf_margin, iou_margin) if len(ref) else np.zeros(0, bool)
+
+    def exempt(d, same):
+        if not len(d):
+            return np.zeros(0, bool)
+        ex = _exempt(d, same, conf, iou_thr, conf_margin, iou_margin)
+        return ex | (d[:, 4] <= cut + conf_margin)
+
+    ex_ref = exempt(ref, ref)
     for i in range(len(ref)):
         cand = np.where((~used) & (got[:, 5] == ref[i, 5]) & (ious[i] >= 0.99))[0] if len(got) else []
         ok = False
@@ -88,7 +102,7 @@ def match_image(ref: np.ndarray, got: np.ndarray, conf: float, iou_thr: float, t
                 rep.failures.append(f"ref det {ref[i].tolist()} unmatched")
     rest = got[~used]
     if len(rest):
-        ex_b = _exempt(rest, got, conf, iou_thr, conf_margin, iou_margin)
+        ex_b = exempt(rest, got)
         rep.exempt += int(ex_b.sum())
         rep.unmatched_build += int((~ex_b).sum())
         for r in rest[~ex_b]:

@@ -1,0 +1,68 @@
+"""Multi-rank plumbing on CPU with gloo (world_size 2): the init-time model-blob broadcast is byte-exact on every
+rank and batch shards tile the global batch.  On MI355X the same code runs over RCCL (backend 'nccl')."""
+import os
+import socket
+
+import pytest
+import torch
+import torch.distributed as dist
+import torch.multiprocessing as mp
+
+from yolomi.dist import broadcast_blob, digest, shard
+
+
+def _free_port():
+    s = socket.socket()
+    s.bind(("127.0.0.1", 0))
+    p = s.getsockname()[1]
+    s.close()
+    return p
+
+
+def _worker(rank, world, port, q):
+    os.environ.update(MASTER_ADDR="127.0.0.1", MASTER_PORT=str(port))
+    dist.init_process_group("gloo", rank=rank, world_size=world)
+    try:
+        blob = None
+        if rank == 0:
+            from yolomi.plan import pack_model
+            from yolomi.synth import synth_weights
+            blob = pack_model("n", "detect", synth_weights("n", "detect", 0), "f16")
+        got = broadcast_blob(blob, torch.device("cpu"))
+        h = torch.tensor(list(bytes.fromhex(digest(got))), dtype=torch.uint8)
+        hs = [torch.zeros_like(h) for _ in range(world)]
+        dist.all_gather(hs, h)
+        q.put((rank, len(got), all(torch.equal(hs[0], x) for x in hs), shard(8 * world, rank, world)))
+    finally:
+        dist.destroy_process_group()
+
+
+@pytest.mark.timeout(300)
+def test_blob_broadcast_and_shards_gloo_world2():
+    world = 2
+    ctx = mp.get_context("spawn")
+    q = ctx.Queue()
+    procs = [ctx.Process(target=_worker, args=(r, world, _free_port() if r < 0 else PORT, q)) for r in range(world)]
+    for p in procs:
+        p.start()
+    res = [q.get(timeout=240) for _ in range(world)]
+    for p in procs:
+        p.join(60)
+        assert p.exitcode == 0
+    res.sort()
+    assert res[0][1] == res[1][1] > 1_000_000
+    assert all(r[2] for r in res)
+    assert [r[3] for r in res] == [(0, 8), (8, 16)]
+
+
+PORT = _free_port()
+
+
+def test_shard_ranges():
+    for gb, w in ((8, 1), (16, 2), (17, 4), (3, 8)):
+        spans = [shard(gb, r, w) for r in range(w)]
+        assert spans[0][0] == 0 and spans[-1][1] == gb
+        assert all(a[1] == b[0] for a, b in zip(spans, spans[1:]))
+        assert max(e - s for s, e in spans) - min(e - s for s, e in spans) <= 1
+    with pytest.raises(ValueError):
+        shard(8, 2, 2)

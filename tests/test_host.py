@@ -1,0 +1,166 @@
+"""CPU tests of the host side: synthetic weights, packer, blob, C-ABI exports, facade contract, metrics, matching.
+(No compute calls: there is no GPU in this container.)"""
+import json
+import os
+import re
+import struct
+
+import numpy as np
+import pytest
+import torch
+
+from tests.matching import MatchReport, match_image
+from yolomi.arch import GraphBuilder, param_specs
+from yolomi.metrics import evaluate
+from yolomi.plan import MAGIC, fuse_conv_bn, pack_model
+from yolomi.synth import splitmix64, synth_weights, uniform
+
+ROOT = os.path.dirname(os.path.dirname(os.path.abspath(__file__)))
+GOLD = os.path.join(ROOT, "tests", "golden")
+
+
+def test_splitmix64_known_answer():
+    # first outputs of splitmix64 from seed 0 (published reference sequence)
+    assert [hex(int(v)) for v in splitmix64(0, 3)] == ["0xe220a8397b1dcdaf", "0x6e789e6aa1b965f4",
+                                                        "0x6c45d188009454f"]
+    u = uniform(7, 1000)
+    assert u.min() >= 0 and u.max() < 1 and abs(u.mean() - 0.5) < 0.05
+
+
+@pytest.mark.parametrize("scale", ["n", "s"])
+def test_synth_weights_match_golden(scale):
+    g = json.load(open(os.path.join(GOLD, f"weights_{scale}.json")))
+    sd = synth_weights(scale, "detect", 0)
+    assert set(sd) == set(g["tensors"])
+    for k, (s, a) in g["tensors"].items():
+        v = sd[k].astype(np.float64)
+        assert v.sum() == pytest.approx(s, rel=1e-12, abs=1e-12), k
+        assert np.abs(v).sum() == pytest.approx(a, rel=1e-12, abs=1e-12), k
+
+
+def test_fused_weights_match_oracle_to_one_ulp():
+    """The packer's fp32 BN fold (exact elementwise scale·W) equals the oracle's torch fuse_conv_and_bn (diag(scale)
+    @ W through the CPU BLAS, which rounds a few channels differently) to ~1e-6 relative."""
+    from oracle.yolo11 import build
+    sd = synth_weights("n", "detect", 0)
+    m = build("n", "detect", sd, fuse=True)
+    mods = dict(m.named_modules())
+    for p in ("model.0", "model.2.m.0.cv2", "model.10.m.0.attn.pe", "model.23.cv3.1.0.0"):
+        w, b = fuse_conv_bn(sd[p + ".conv.weight"], sd[p + ".bn.weight"], sd[p + ".bn.bias"],
+                            sd[p + ".bn.running_mean"], sd[p + ".bn.running_var"])
+        ref_w, ref_b = mods[p].conv.weight.numpy(), mods[p].conv.bias.numpy()
+        np.testing.assert_allclose(w, ref_w, rtol=2e-6, atol=1e-9, err_msg=p)
+        np.testing.assert_allclose(b, ref_b, rtol=2e-6, atol=1e-9, err_msg=p)
+
+
+@pytest.mark.parametrize("scale,task,dtype", [("n", "detect", "f16"), ("s", "segment", "f32")])
+def test_blob_layout(scale, task, dtype):
+    sd = synth_weights(scale, task, 0)
+    blob = pack_model(scale, task, sd, dtype)
+    h = struct.unpack("<32i", blob[:128])
+    g = GraphBuilder(scale, task)
+    assert h[0] == MAGIC and h[1] == 1 and h[2] == (0 if dtype == "f16" else 1)
+    assert h[3] == (1 if task == "segment" else 0) and h[4] == 80 and h[5] == g.nm and h[6] == 16
+    assert h[8:11] == (8, 16, 32) and h[11] == len(g.buffers) and h[12] == len(g.ops)
+    meta = 128 + 32 * h[11] + 128 * h[12] + 48 * h[12]
+    wb = h[13] | (h[14] << 32)
+    assert len(blob) == (meta + 255) // 256 * 256 + wb
+    # every conv record: Cin multiple of 8, K padded to the 64-deep kernel step, offsets inside the weight region
+    for i in range(h[12]):
+        r = struct.unpack("<32i", blob[128 + 32 * h[11] + 128 * i: 128 + 32 * h[11] + 128 * (i + 1)])
+        if r[0] == 2:
+            assert r[3] % 8 == 0 and r[21] % 64 == 0 and r[21] >= r[1] * r[1] * r[3]
+            assert 0 <= r[19] < wb and 0 <= r[20] < wb
+
+
+def test_capi_exports_every_declared_symbol():
+    import ctypes
+    import yolomi.lib as L
+    hdr = open(os.path.join(ROOT, "include", "yolomi.h")).read()
+    declared = set(re.findall(r"^\s*(?:int|void|const char\*)\s+(ym_\w+)\s*\(", hdr, re.M))
+    assert len(declared) >= 15
+    lib = ctypes.CDLL(str(L.LIB_PATH))
+    for name in declared:
+        assert hasattr(lib, name), name
+    assert set(L.EXPORTED) == declared
+    assert lib.ym_version() == 1
+
+
+def test_facade_contract_without_gpu():
+    from core.model import YOLO11Model
+    with pytest.raises(ValueError):
+        YOLO11Model(task="bogus", device="cuda")
+    with pytest.raises(ValueError):
+        YOLO11Model(size="q", device="cuda")
+    with pytest.raises(NotImplementedError):
+        YOLO11Model(task="classify", device="cuda")
+    with pytest.raises(RuntimeError, match="no HIP path"):
+        YOLO11Model(device="cpu")  # no silent CPU fallback
+    assert set(YOLO11Model.SUPPORTED_TASKS) == {"detect", "segment", "classify", "pose", "obb"}
+
+
+def test_param_count_matches_ultralytics_cards():
+    # fused parameter counts (conv weights + biases) — SURVEY §0 table
+    for scale, expect in (("n", 2_616_232), ("s", 9_443_744)):
+        sd = synth_weights(scale, "detect", 0)
+        n = 0
+        for k, v in sd.items():
+            if k.endswith(".conv.weight") and "dfl" not in k:  # conv + its folded BN bias
+                n += v.size + v.shape[0]
+            elif k.endswith(".weight") and ".bn." not in k and ".conv." not in k:  # plain Conv2d heads
+                n += v.size
+            elif k.endswith(".bias") and ".bn." not in k:
+                n += v.size
+        assert n == expect
+
+
+def test_metrics_map():
+    gt = [np.array([[10, 10, 50, 50, 1, 3], [100, 100, 150, 180, 1, 5]], np.float64)]
+    # perfect predictions score 0.995 under the 101-point interpolation + trapezoid rule (the Ultralytics value)
+    assert evaluate([gt[0].copy()], gt)["map"] == pytest.approx(0.995)
+    shifted = gt[0].copy()
+    shifted[1, :4] += 20  # IoU of the second box drops to ~0.4: below every threshold
+    m = evaluate([shifted], gt)
+    assert 0.4 < m["map"] < 0.6 and m["map50"] == pytest.approx(0.4975)
+    assert evaluate([np.zeros((0, 6))], gt)["map"] == 0.0
+
+
+def test_matching_protocol():
+    ref = np.array([[0, 0, 10, 10, 0.9, 1], [20, 20, 40, 40, 0.2505, 2]], np.float32)
+    got = np.array([[0, 0, 10, 10.0005, 0.9002, 1]], np.float32)
+    rep = match_image(ref, got, 0.25, 0.7, 1e-3, 1e-3, rep=MatchReport())
+    assert rep.matched == 1 and rep.exempt == 1 and rep.ok  # 0.2505 is within 2e-3 of conf
+    bad = np.array([[0, 0, 10, 10, 0.9, 2]], np.float32)  # wrong class
+    assert not match_image(ref[:1], bad, 0.25, 0.7, 1e-3, 1e-3, rep=MatchReport()).ok
+
+
+def test_validator_benchmark_schema(tmp_path):
+    from core.validator import YOLO11Validator
+
+    class FakeModel:
+        def get_model_info(self):
+            return {"task": "detect", "size": "n"}
+
+        def benchmark(self, data_source, num_runs=100, warmup_runs=10):
+            return {"avg_inference_time": 0.002, "min_inference_time": 0.001, "max_inference_time": 0.003,
+                    "fps": 500.0}
+
+    v = YOLO11Validator(FakeModel(), device="cpu", output_dir=tmp_path)
+    r = v.benchmark_speed(None, num_runs=2, warmup_runs=1, batch_sizes=[1, 8], image_sizes=[320, 640])
+    assert set(r) == {"device", "model_info", "configurations", "summary"}
+    assert len(r["configurations"]) == 4
+    c = r["configurations"][1]
+    assert set(c) == {"avg_inference_time", "min_inference_time", "max_inference_time", "fps", "batch_size",
+                      "image_size", "images_per_second"}
+    assert c["images_per_second"] == 8 * 500.0
+    assert set(r["summary"]) == {"best_fps", "avg_fps", "best_latency", "avg_latency", "best_throughput",
+                                 "total_configurations_tested", "best_configuration"}
+    assert (tmp_path / "benchmark_results.json").exists() and (tmp_path / "benchmark_summary.txt").exists()
+
+
+def test_op_costs_cover_all_flops():
+    g = GraphBuilder("n", "detect")
+    costs = g.op_costs(8, 640, 640)
+    conv_flops = sum(c[0] for c, op in zip(costs, g.ops) if op.kind in ("conv", "dwconv", "attn"))
+    assert conv_flops == pytest.approx(8 * 2 * g.macs_per_image(640, 640), rel=1e-9)
+    assert len(param_specs("n")) == 499
