@@ -40,15 +40,35 @@ def synthetic_batch(B, S, seed, device):
     return torch.from_numpy(x).to(device)
 
 
-def conv_roofline(model, x, dtype, reps=5):
-    """Live per-op device times (HIP events around every launch on the launch stream, eager) → conv aggregate."""
+def pmc_traffic(workload):
+    """HBM-side bytes per forward of the conv family from the newest committed PMC summary of this workload
+    (profiles/<round>_pmc.json, produced by tools/rocprof_summary.py from separate rocprofv3 --pmc passes)."""
+    import glob
+    best = None
+    for p in sorted(glob.glob(os.path.join(ROOT, "profiles", "*_pmc.json"))):
+        try:
+            j = json.load(open(p))
+        except (OSError, ValueError):
+            continue
+        if j.get("workload") == workload and "conv" in j.get("families", {}):
+            best = (p, j)
+    if best is None:
+        return None, None
+    return best[1]["families"]["conv"]["bytes_corrected"], os.path.relpath(best[0], ROOT)
+
+
+def conv_roofline(model, x, dtype, workload, reps=20):
+    """Live per-op device times on the launch stream → conv-family roofline.
+
+    Each conv launch of the forward is captured as a HIP graph of `reps` back-to-back launches on the real
+    activation buffers and bracketed by one HIP event pair (ym_profile_replay): per-launch device time without the
+    per-op marker packets an eager event pair would add.  `achieved` = Σ algorithmic FLOPs of the forward's conv
+    launches ÷ Σ their per-launch times (per-unit figures: DESIGN.md §4)."""
     eng = model.model.engine
     B, _, H, W = x.shape
     costs = eng.graph.op_costs(B, H, W, 2 if dtype == "f16" else 4)
-    times = np.zeros(len(eng.graph.ops))
-    for _ in range(reps):
-        times += np.array(eng.profile(x))
-    times /= reps
+    times = np.array(eng.profile_replay(x, reps=reps))
+    eng.run(x)  # restore the buffers the replay clobbered
     kinds = [op.kind for op in eng.graph.ops]
     conv = [i for i, k in enumerate(kinds) if k == "conv"]
     t_conv = float(times[conv].sum()) * 1e-3
@@ -56,19 +76,24 @@ def conv_roofline(model, x, dtype, reps=5):
     by = float(sum(costs[i][1] for i in conv))
     per_kind = {}
     for k, t in zip(kinds, times):
-        per_kind[k] = per_kind.get(k, 0.0) + float(t)
+        if t >= 0:
+            per_kind[k] = per_kind.get(k, 0.0) + float(t)
     top = sorted(((float(times[i]), eng.graph.ops[i].name, costs[i][0] / max(times[i] * 1e-3, 1e-12) / 1e12)
                   for i in conv), reverse=True)[:8]
     ach = fl / t_conv / 1e12
+    traffic, tsrc = pmc_traffic(workload)
     return {
         "bound": "mfma", "achieved": round(ach, 2), "peak": PEAK_TFLOPS[dtype], "unit": "TFLOP/s",
-        "frac": round(ach / PEAK_TFLOPS[dtype], 4), "traffic": None,
-        "kernel": "conv_igemm_nhwc (all %d conv launches of one forward, aggregated)" % len(conv),
+        "frac": round(ach / PEAK_TFLOPS[dtype], 4), "traffic": traffic,
+        "traffic_note": (f"HBM-side bytes per forward of all conv launches (PMC FETCH_SIZE x2 + WRITE_SIZE, {tsrc}); "
+                         f"algorithmic bytes per forward {int(by)}") if traffic else "no PMC summary for this workload",
+        "kernel": "conv implicit GEMM (conv_igemm/conv_lds): all %d conv launches of one forward, aggregated"
+                  % len(conv),
+        "timing": f"HIP events around a graph of {reps} back-to-back launches per op, on the launch stream",
         "launches": len(conv), "avg_launch_us": round(t_conv / len(conv) * 1e6, 2),
-        "flops_per_forward": fl, "hbm_algorithmic_GBps": round(by / t_conv / 1e9, 1),
-        "hbm_frac": round(by / t_conv / 1e9 / PEAK_HBM_GBS, 4),
-        "forward_ms_eager_sum": round(float(times.sum()), 4),
-        "ms_by_kind": {k: round(v, 4) for k, v in per_kind.items()},
+        "flops_per_forward": fl, "bytes_per_forward_algorithmic": by,
+        "hbm_algorithmic_GBps": round(by / t_conv / 1e9, 1), "hbm_frac": round(by / t_conv / 1e9 / PEAK_HBM_GBS, 4),
+        "ms_by_kind_replay": {k: round(v, 4) for k, v in per_kind.items()},
         "top_convs": [{"op": n, "ms": round(t, 4), "tflops": round(tf, 1)} for t, n, tf in top],
     }
 
@@ -190,8 +215,9 @@ def main():
         "device_images_per_s": round(dev_ips * world, 2),
         "init_s": round(init_s, 3),
     }
+    out["config"]["conv_tiles"] = model.model.engine.tune_source.get((B, a.size, a.size), "heuristic")
     if rank == 0 and not a.no_roofline:
-        out["roofline"] = conv_roofline(model, x, a.dtype)
+        out["roofline"] = conv_roofline(model, x, a.dtype, out["config"]["workload"])
     if rank == 0 and world == 1 and not a.no_cpu:
         gdets = [r.boxes.data.cpu().numpy() for r in res]
         base, acc = cpu_baseline(a.model, a.task, gdets, x, a.cpu_seconds)

@@ -72,13 +72,21 @@ int ym_infer(ym_ctx* ctx, const float* d_input, int B, int H, int W, const ym_in
 int ym_profile(ym_ctx* ctx, const float* d_input, int B, int H, int W, const ym_infer_args* args, float* d_dets,
                int* d_counts, void* stream, float* op_ms, int n_ops);
 
+/* Per-op device time without per-op markers: after one real forward, every conv / depthwise / SPPF / attention op
+ * is captured as a graph of `reps` back-to-back launches on the real buffers and timed with one HIP event pair;
+ * op_ms[i] = that time / reps (launch gaps included, as in the forward graph).  Ops that are not idempotent
+ * (input statistics, decode, NMS) get -1.  Synchronous; leaves the activation buffers in an unspecified state. */
+int ym_profile_replay(ym_ctx* ctx, const float* d_input, int B, int H, int W, const ym_infer_args* args,
+                      float* d_dets, int* d_counts, void* stream, int reps, float* op_ms, int n_ops);
+
 /* On-device autotuning of the conv tile configuration, per op, for input shape (B, H, W): every candidate is timed
  * as `reps` graph-captured back-to-back launches on this GPU (after one real forward so the buffers hold real
- * activations); the fastest is kept for this shape.  Synchronous.  ym_get_op_cfg / ym_set_op_cfg export / import
- * the per-op choices (n_ops ints, -1 = built-in heuristic) so a tuned plan can be pinned. */
+ * activations); the fastest is kept for this shape (one table per (B, H, W)).  Synchronous.  ym_get_op_cfg /
+ * ym_set_op_cfg export / import the per-op choices for a shape (n_ops ints, -1 = built-in heuristic) so a tuned plan
+ * can be cached and pinned; ym_get_op_cfg returns 1 (and all -1) when the shape has no table. */
 int ym_tune(ym_ctx* ctx, const float* d_input, int B, int H, int W, const ym_infer_args* args, float* d_dets,
             int* d_counts, void* stream, int reps);
-int ym_get_op_cfg(ym_ctx* ctx, int* cfg, int n_ops);
+int ym_get_op_cfg(ym_ctx* ctx, int B, int H, int W, int* cfg, int n_ops);
 int ym_set_op_cfg(ym_ctx* ctx, int B, int H, int W, const int* cfg, int n_ops);
 
 /* Introspection for tests / bisecting: op count & names, and the device view of plan buffer `buf` as produced by

@@ -1,0 +1,44 @@
+#!/usr/bin/env python3
+"""Eager forwards of the bench workload for rocprofv3 PMC passes (one counter group per run, no trace domains).
+
+    rocprofv3 --pmc FETCH_SIZE -d gpurun_out/pmc_fetch -o run --output-format csv -- python3 tools/pmc_forward.py
+
+Uses the same tuned conv tables as bench.py (YM_TUNE_DIR / yolomi/tuned), so the dispatch sequence of the last
+`--reps` forwards is exactly one bench forward each; tools/rocprof_summary.py splits them at the init_ctl kernel.
+"""
+import argparse
+import os
+import sys
+
+ROOT = os.path.dirname(os.path.dirname(os.path.abspath(__file__)))
+sys.path.insert(0, os.path.join(ROOT, "yolo-infer_amd"))
+sys.path.insert(0, ROOT)
+
+import torch  # noqa: E402
+
+
+def main():
+    ap = argparse.ArgumentParser()
+    ap.add_argument("--model", default="n")
+    ap.add_argument("--task", default="detect")
+    ap.add_argument("--batch", type=int, default=8)
+    ap.add_argument("--size", type=int, default=640)
+    ap.add_argument("--dtype", default="f16")
+    ap.add_argument("--reps", type=int, default=3)
+    a = ap.parse_args()
+    from bench import synthetic_batch
+    from core.model import YOLO11Model
+    m = YOLO11Model(task=a.task, size=a.model, device="cuda:0", dtype=a.dtype)
+    x = synthetic_batch(a.batch, a.size, 1000, torch.device("cuda", 0))
+    eng = m.model.engine
+    eng.run(x, use_graph=False)  # table lookup (or tuning) happens here
+    torch.cuda.synchronize()
+    for _ in range(a.reps):
+        eng.run(x, use_graph=False)
+    torch.cuda.synchronize()
+    print(f"pmc_forward: {a.reps} eager forwards of yolo11{a.model} B={a.batch} {a.size}^2 {a.dtype}; tune source "
+          f"{eng.tune_source}")
+
+
+if __name__ == "__main__":
+    main()

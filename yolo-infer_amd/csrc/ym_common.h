@@ -119,3 +119,4 @@ hipError_t ym_launch_prep(int dtype, const PrepArgs& a, int* counts, int B, hipS
 hipError_t ym_launch_decode(const DecodeArgs& a, hipStream_t st);
 hipError_t ym_launch_nms(const NmsArgs& a, hipStream_t st);
 hipError_t ym_launch_stem(int dtype, const ConvArgs& a, hipStream_t st);
+hipError_t ym_launch_spin(int usec, hipStream_t st);  // profiling: park the stream for usec (wall clock)

@@ -510,9 +510,25 @@ __global__ __launch_bounds__(NMS_T) void nms_image(const NmsArgs a) {
   if (tid == 0) a.out_counts[b] = kept;
 }
 
+// ------------------------------------------------------------------------------------------------- profiling aid
+// One wave parks for `ticks` of the constant 100 MHz wall clock.  ym_profile queues it ahead of the per-op event
+// pairs so the host enqueues the whole forward while the GPU waits: the events then time device work only, not host
+// launch latency.  Always terminates (bounded by the clock, not by memory state).
+__global__ void spin_wait(long long ticks) {
+  const long long t0 = wall_clock64();
+  while (wall_clock64() - t0 < ticks) __builtin_amdgcn_s_sleep(127);
+}
+
 }  // namespace
 
 // ------------------------------------------------------------------------------------------------- launchers
+hipError_t ym_launch_spin(int usec, hipStream_t st) {
+  if (usec < 0) usec = 0;
+  if (usec > 200000) usec = 200000;
+  hipLaunchKernelGGL(spin_wait, dim3(1), dim3(64), 0, st, (long long)usec * 100);
+  return hipGetLastError();
+}
+
 hipError_t ym_launch_prep(int dtype, const PrepArgs& a, int* counts, int B, hipStream_t st) {
   (void)dtype;
   hipLaunchKernelGGL(init_ctl, dim3(1), dim3(64), 0, st, a.ctl, counts, B);

@@ -90,12 +90,29 @@ struct ym_ctx {
   hipStream_t cap_stream = nullptr;
   std::vector<GraphEntry> graphs;
   std::vector<hipEvent_t> prof_events;
-  // per-op conv tile configuration for the current workspace shape (-1 = heuristic); set by ym_tune / ym_set_op_cfg
-  std::vector<int> cfg;
-  int tB = 0, tH = 0, tW = 0;
-  int op_cfg(long i, int B) const {
-    if (B != tB || cH != tH || cW != tW) return -1;
-    return (i >= 0 && i < (long)cfg.size()) ? cfg[i] : -1;
+  // per-shape, per-op conv tile configuration (-1 = heuristic); set by ym_tune / ym_set_op_cfg
+  struct ShapeCfg {
+    int B, H, W;
+    std::vector<int> cfg;
+  };
+  std::vector<ShapeCfg> cfgs;
+  const std::vector<int>* find_cfg(int B, int H, int W) const {
+    for (const auto& e : cfgs)
+      if (e.B == B && e.H == H && e.W == W) return &e.cfg;
+    return nullptr;
+  }
+  void put_cfg(int B, int H, int W, std::vector<int> v) {
+    for (auto& e : cfgs)
+      if (e.B == B && e.H == H && e.W == W) { e.cfg = std::move(v); return; }
+    cfgs.push_back({B, H, W, std::move(v)});
+  }
+  void drop_cfg(int B, int H, int W) {
+    for (size_t i = 0; i < cfgs.size(); ++i)
+      if (cfgs[i].B == B && cfgs[i].H == H && cfgs[i].W == W) { cfgs.erase(cfgs.begin() + i); return; }
+  }
+  int op_cfg(long i, int B) const {  // for the current workspace height/width
+    const std::vector<int>* v = find_cfg(B, cH, cW);
+    return (v && i >= 0 && i < (long)v->size()) ? (*v)[i] : -1;
   }
 
   ~ym_ctx() {
@@ -471,6 +488,9 @@ int ym_profile(ym_ctx* c, const float* d_in, int B, int H, int W, const ym_infer
     HIPCK(hipEventCreate(&e));
     c->prof_events.push_back(e);
   }
+  // park the stream first so the host has queued every op + event before the GPU reaches them: the event pairs
+  // then bracket device execution only (an eager host launch takes longer than most of these kernels)
+  HIPCK(ym_launch_spin(20 * (int)c->ops.size() + 2000, st));
   HIPCK(hipEventRecord(c->prof_events[0], st));
   for (size_t i = 0; i < c->ops.size(); ++i) {
     if ((rc = launch_op(c, c->ops[i], B, d_in, args, d_dets, d_counts, st))) return rc;
@@ -479,6 +499,54 @@ int ym_profile(ym_ctx* c, const float* d_in, int B, int H, int W, const ym_infer
   HIPCK(hipEventSynchronize(c->prof_events[ne - 1]));
   for (size_t i = 0; i < c->ops.size(); ++i)
     HIPCK(hipEventElapsedTime(&op_ms[i], c->prof_events[i], c->prof_events[i + 1]));
+  return YM_OK;
+}
+
+int ym_profile_replay(ym_ctx* c, const float* d_in, int B, int H, int W, const ym_infer_args* args, float* d_dets,
+                      int* d_counts, void* stream, int reps, float* op_ms, int n_ops) {
+  int rc = check_call(c, d_in, B, H, W, args, d_dets, d_counts);
+  if (rc) return rc;
+  if (!op_ms || n_ops < (int)c->ops.size()) return fail(YM_EINVAL, "op_ms must hold %zu entries", c->ops.size());
+  if (reps < 1) reps = 20;
+  HIPCK(hipSetDevice(c->device));
+  hipStream_t st = static_cast<hipStream_t>(stream);
+  if ((rc = ensure_workspace(c, B, H, W))) return rc;
+  // one real forward so every buffer holds this input's activations (and the /255 flag is set)
+  for (const Op& op : c->ops)
+    if ((rc = launch_op(c, op, B, d_in, args, d_dets, d_counts, st))) return rc;
+  hipEvent_t e0, e1;
+  HIPCK(hipEventCreate(&e0));
+  HIPCK(hipEventCreate(&e1));
+  for (size_t i = 0; i < c->ops.size(); ++i) {
+    const Op& op = c->ops[i];
+    const int k = op.r[0];
+    op_ms[i] = -1.f;
+    // input (resets counters), decode (appends candidates) and NMS (consumes them) are not idempotent: skipped
+    if (k != OP_CONV && k != OP_DW && k != OP_SPPF && k != OP_ATTN) continue;
+    hipGraph_t g = nullptr;
+    hipGraphExec_t ge = nullptr;
+    HIPCK(hipStreamBeginCapture(c->cap_stream, hipStreamCaptureModeRelaxed));
+    int lrc = YM_OK;
+    for (int r = 0; r < reps && lrc == YM_OK; ++r) lrc = launch_op(c, op, B, d_in, args, d_dets, d_counts, c->cap_stream);
+    HIPCK(hipStreamEndCapture(c->cap_stream, &g));
+    if (lrc != YM_OK) {
+      (void)hipGraphDestroy(g);
+      return lrc;
+    }
+    HIPCK(hipGraphInstantiate(&ge, g, nullptr, nullptr, 0));
+    HIPCK(hipGraphLaunch(ge, st));  // warm
+    HIPCK(hipEventRecord(e0, st));
+    HIPCK(hipGraphLaunch(ge, st));
+    HIPCK(hipEventRecord(e1, st));
+    HIPCK(hipEventSynchronize(e1));
+    float ms = 0.f;
+    HIPCK(hipEventElapsedTime(&ms, e0, e1));
+    op_ms[i] = ms / reps;
+    (void)hipGraphExecDestroy(ge);
+    (void)hipGraphDestroy(g);
+  }
+  (void)hipEventDestroy(e0);
+  (void)hipEventDestroy(e1);
   return YM_OK;
 }
 
@@ -491,7 +559,7 @@ int ym_tune(ym_ctx* c, const float* d_in, int B, int H, int W, const ym_infer_ar
   if ((rc = ensure_workspace(c, B, H, W))) return rc;
   if (reps < 1) reps = 8;
   // one real forward first so every buffer a candidate reads holds this model's activations
-  c->tB = c->tH = c->tW = 0;
+  c->drop_cfg(B, H, W);
   for (const Op& op : c->ops)
     if ((rc = launch_op(c, op, B, d_in, args, d_dets, d_counts, st))) return rc;
   HIPCK(hipStreamSynchronize(st));
@@ -537,23 +605,22 @@ int ym_tune(ym_ctx* c, const float* d_in, int B, int H, int W, const ym_infer_ar
   (void)hipEventDestroy(e0);
   (void)hipEventDestroy(e1);
   c->clear_graphs();
-  c->cfg = best;
-  c->tB = B; c->tH = H; c->tW = W;
+  c->put_cfg(B, H, W, best);
   return YM_OK;
 }
 
-int ym_get_op_cfg(ym_ctx* c, int* cfg, int n) {
+int ym_get_op_cfg(ym_ctx* c, int B, int H, int W, int* cfg, int n) {
   if (!c || !cfg || n < (int)c->ops.size()) return fail(YM_EINVAL, "cfg array must hold %zu entries", c ? c->ops.size() : 0);
-  for (size_t i = 0; i < c->ops.size(); ++i) cfg[i] = c->op_cfg((long)i, c->tB);
-  return YM_OK;
+  const std::vector<int>* v = c->find_cfg(B, H, W);
+  for (size_t i = 0; i < c->ops.size(); ++i) cfg[i] = (v && i < v->size()) ? (*v)[i] : -1;
+  return v ? YM_OK : 1;
 }
 
 int ym_set_op_cfg(ym_ctx* c, int B, int H, int W, const int* cfg, int n) {
   if (!c || !cfg || n != (int)c->ops.size()) return fail(YM_EINVAL, "cfg array must hold %zu entries", c ? c->ops.size() : 0);
   for (int i = 0; i < n; ++i)
     if (cfg[i] >= ym_conv_num_cfgs()) return fail(YM_EINVAL, "cfg[%d] = %d out of range", i, cfg[i]);
-  c->cfg.assign(cfg, cfg + n);
-  c->tB = B; c->tH = H; c->tW = W;
+  c->put_cfg(B, H, W, std::vector<int>(cfg, cfg + n));
   c->clear_graphs();
   return YM_OK;
 }

@@ -5,6 +5,7 @@ of the forward runs in libyolomi's gfx950 kernels.
 """
 from __future__ import annotations
 
+import json
 import os
 from typing import Dict, Optional, Sequence
 
@@ -14,6 +15,14 @@ import torch
 from .arch import GraphBuilder
 from .lib import Runtime
 from .plan import pack_graph
+
+# Bump when the meaning of a conv config index (csrc/ym_conv.hip kCfgs) changes: stale tables are then ignored.
+TUNE_VERSION = 2
+TUNED_DIR = os.path.join(os.path.dirname(os.path.abspath(__file__)), "tuned")  # committed tables
+
+
+def tune_cache_dir() -> str:
+    return os.environ.get("YM_TUNE_DIR", os.path.join(os.path.expanduser("~"), ".cache", "yolomi", "tune"))
 
 
 class Engine:
@@ -28,9 +37,49 @@ class Engine:
         self.rt = Runtime(device.index if device.index is not None else torch.cuda.current_device(), self.blob)
         self.nm = self.graph.nm
         self._out: Dict[int, tuple] = {}
-        # per-shape on-device autotuning of the conv tiles (ym_tune) on the first call of each (B, H, W)
+        # Per-shape conv tile tables: on the first call of each (B, H, W) a table is taken from the writable tune
+        # cache or the committed `tuned/` directory; failing both, ym_tune measures one on this GPU (and caches it).
         self.autotune = os.environ.get("YM_AUTOTUNE", "1") != "0"
         self._tuned = set()
+        self.tune_source: Dict[tuple, str] = {}
+
+    def _table_name(self, B, H, W):
+        return f"{self.scale}-{self.task}-{self.dtype}-b{B}-{H}x{W}.json"
+
+    def _load_table(self, B, H, W):
+        name = self._table_name(B, H, W)
+        for tag, d in (("cache", tune_cache_dir()), ("committed", TUNED_DIR)):
+            p = os.path.join(d, name)
+            try:
+                t = json.load(open(p))
+            except (OSError, ValueError):
+                continue
+            if t.get("version") == TUNE_VERSION and len(t.get("cfg", [])) == self.rt.n_ops:
+                self.rt.set_op_cfg(B, H, W, t["cfg"])
+                return f"{tag} table {name}"
+        return None
+
+    def _save_table(self, B, H, W):
+        cfg = self.rt.get_op_cfg(B, H, W)
+        if cfg is None:
+            return
+        d = tune_cache_dir()
+        try:
+            os.makedirs(d, exist_ok=True)
+            with open(os.path.join(d, self._table_name(B, H, W)), "w") as f:
+                json.dump({"version": TUNE_VERSION, "device": torch.cuda.get_device_properties(self.device).gcnArchName,
+                           "ops": [op.name for op in self.graph.ops], "cfg": cfg}, f)
+        except OSError:
+            pass  # a read-only home: the table lives for this process only
+
+    def _prepare_shape(self, x, B, H, W, args, dets, counts, stream):
+        src = None if os.environ.get("YM_TUNE_TABLES", "1") == "0" else self._load_table(B, H, W)
+        if src is None and self.autotune:
+            self.rt.tune(x.data_ptr(), B, H, W, args, dets.data_ptr(), counts.data_ptr(), stream)
+            self._save_table(B, H, W)
+            src = "ym_tune"
+        self.tune_source[(B, H, W)] = src or "heuristic"
+        self._tuned.add((B, H, W))
 
     def outputs(self, B: int, max_det: int):
         key = (B, max_det)
@@ -50,9 +99,8 @@ class Engine:
         args = Runtime.make_args(conf, iou, max_det, max_nms, agnostic, max_wh, in_eps, classes, use_graph)
         dets, counts = self.outputs(B, max_det)
         stream = torch.cuda.current_stream(self.device).cuda_stream
-        if self.autotune and (B, H, W) not in self._tuned:
-            self.rt.tune(x.data_ptr(), B, H, W, args, dets.data_ptr(), counts.data_ptr(), stream)
-            self._tuned.add((B, H, W))
+        if (B, H, W) not in self._tuned:
+            self._prepare_shape(x, B, H, W, args, dets, counts, stream)
         self.rt.infer(x.data_ptr(), B, H, W, args, dets.data_ptr(), counts.data_ptr(), stream)
         return dets, counts
 
@@ -61,7 +109,19 @@ class Engine:
         args = Runtime.make_args(use_graph=False, **kw)
         dets, counts = self.outputs(B, args.max_det)
         stream = torch.cuda.current_stream(self.device).cuda_stream
+        if (B, H, W) not in self._tuned:
+            self._prepare_shape(x, B, H, W, args, dets, counts, stream)
         return self.rt.profile(x.data_ptr(), B, H, W, args, dets.data_ptr(), counts.data_ptr(), stream)
+
+    def profile_replay(self, x: torch.Tensor, reps=20, **kw):
+        """Per-op device ms from graph-captured back-to-back launches (-1 for input/decode/NMS); clobbers buffers."""
+        B, _, H, W = x.shape
+        args = Runtime.make_args(use_graph=False, **kw)
+        dets, counts = self.outputs(B, args.max_det)
+        stream = torch.cuda.current_stream(self.device).cuda_stream
+        if (B, H, W) not in self._tuned:
+            self._prepare_shape(x, B, H, W, args, dets, counts, stream)
+        return self.rt.profile_replay(x.data_ptr(), B, H, W, args, dets.data_ptr(), counts.data_ptr(), stream, reps)
 
     def read_buffer(self, buf_id: int, B: int) -> torch.Tensor:
         """NHWC contents of plan buffer `buf_id` for the first B images (after run/profile), as a CPU float32 tensor."""

@@ -46,8 +46,9 @@ def load_library(path: os.PathLike = LIB_PATH):
         "ym_load_weights": (I, [P, P, C.c_size_t]),
         "ym_infer": (I, [P, P, I, I, I, C.POINTER(InferArgs), P, P, P]),
         "ym_profile": (I, [P, P, I, I, I, C.POINTER(InferArgs), P, P, P, F, I]),
+        "ym_profile_replay": (I, [P, P, I, I, I, C.POINTER(InferArgs), P, P, P, I, F, I]),
         "ym_tune": (I, [P, P, I, I, I, C.POINTER(InferArgs), P, P, P, I]),
-        "ym_get_op_cfg": (I, [P, C.POINTER(I), I]),
+        "ym_get_op_cfg": (I, [P, I, I, I, C.POINTER(I), I]),
         "ym_set_op_cfg": (I, [P, I, I, I, C.POINTER(I), I]),
         "ym_num_ops": (I, [P]),
         "ym_op_name": (C.c_char_p, [P, I]),
@@ -67,7 +68,7 @@ def load_library(path: os.PathLike = LIB_PATH):
     return lib
 
 
-EXPORTED = ("ym_create", "ym_load_weights", "ym_infer", "ym_profile", "ym_tune", "ym_get_op_cfg", "ym_set_op_cfg",
+EXPORTED = ("ym_create", "ym_load_weights", "ym_infer", "ym_profile", "ym_profile_replay", "ym_tune", "ym_get_op_cfg", "ym_set_op_cfg",
             "ym_num_ops", "ym_op_name", "ym_num_buffers",
             "ym_buffer_info", "ym_read_buffer", "ym_sync", "ym_last_error", "ym_destroy", "ym_version")
 
@@ -116,13 +117,23 @@ class Runtime:
                                    C.c_void_p(counts_ptr), C.c_void_p(stream), ms, self.n_ops))
         return list(ms)
 
+    def profile_replay(self, x_ptr, B, H, W, args, dets_ptr, counts_ptr, stream, reps=20):
+        ms = (C.c_float * self.n_ops)()
+        _check(self.lib.ym_profile_replay(self.ctx, C.c_void_p(x_ptr), B, H, W, C.byref(args), C.c_void_p(dets_ptr),
+                                          C.c_void_p(counts_ptr), C.c_void_p(stream), reps, ms, self.n_ops))
+        return list(ms)
+
     def tune(self, x_ptr, B, H, W, args, dets_ptr, counts_ptr, stream, reps=8):
         _check(self.lib.ym_tune(self.ctx, C.c_void_p(x_ptr), B, H, W, C.byref(args), C.c_void_p(dets_ptr),
                                 C.c_void_p(counts_ptr), C.c_void_p(stream), reps))
 
-    def get_op_cfg(self):
+    def get_op_cfg(self, B, H, W):
+        """Per-op conv configs of shape (B, H, W), or None when the shape has no tuned/pinned table."""
         arr = (C.c_int * self.n_ops)()
-        _check(self.lib.ym_get_op_cfg(self.ctx, arr, self.n_ops))
+        rc = self.lib.ym_get_op_cfg(self.ctx, B, H, W, arr, self.n_ops)
+        if rc == 1:
+            return None
+        _check(rc)
         return list(arr)
 
     def set_op_cfg(self, B, H, W, cfg):

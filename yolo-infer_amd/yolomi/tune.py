@@ -57,7 +57,7 @@ def main(argv=None):
     dets, counts = eng.outputs(B, 300)
     st = torch.cuda.current_stream().cuda_stream
     eng.rt.tune(x.data_ptr(), B, S, S, args, dets.data_ptr(), counts.data_ptr(), st)
-    cfg = eng.rt.get_op_cfg()
+    cfg = eng.rt.get_op_cfg(B, S, S)
     t = np.zeros(len(eng.graph.ops))
     for _ in range(a.reps):
         t += np.array(eng.profile(x))
