@@ -215,3 +215,58 @@ def test_results_contract_and_benchmark():
     assert set(b) == {"avg_inference_time", "min_inference_time", "max_inference_time", "fps"}
     info = m.get_model_info()
     assert info["total_parameters"] > 2_000_000 and info["task"] == "detect"
+
+
+# ------------------------------------------------------------------------------------------------ LDS-DMA conv configs
+DMA_FIRST = 17  # csrc/ym_conv.hip: ids >= 17 are the LDS-DMA / split-K kernels of csrc/ym_conv_dma.hip
+
+
+def _force_cfg(eng, x, cfg):
+    """Run once (tables), then pin `cfg` on every conv op for x's shape (inapplicable ops fall back)."""
+    eng.run(x, use_graph=False)
+    B, _, H, W = x.shape
+    eng.rt.set_op_cfg(B, H, W, [cfg if op.kind == "conv" else -1 for op in eng.graph.ops])
+
+
+@pytest.mark.parametrize("cfg", list(range(DMA_FIRST, DMA_FIRST + 12)))
+def test_dma_conv_configs_match_oracle(cfg):
+    """Every conv of yolo11n (1x1 two-source/upsampled, 3x3 s1/s2, residual, fp32 Detect rows) on one DMA config."""
+    m = model("n", "f16")
+    eng = m.model.engine
+    x = make_input("uniform", (11, 12), 640)
+    _, y, ex = oracle().raw(x, keep=(2, 4, 6, 8, 9, 10, 13, 16, 19, 22))
+    xd = x.to(DEV)
+    try:
+        _force_cfg(eng, xd, cfg)
+        eng.run(xd, use_graph=False)
+        for b in eng.graph.buffers:
+            if b.name.startswith("L") and b.name[1:].isdigit() and int(b.name[1:]) in ex["saved"]:
+                ref = ex["saved"][int(b.name[1:])].permute(0, 2, 3, 1)
+                got = eng.read_buffer(b.id, 2)
+                rel = (got - ref).abs().max().item() / ref.abs().max().item()
+                assert rel < 1e-2, (cfg, b.name, rel)
+        no = eng.graph.no
+        ref_h = torch.cat([f.view(2, no, -1) for f in ex["feats"]], 2).transpose(1, 2)
+        got_h = eng.read_buffer(eng.graph.anchor_buf.id, 2).reshape(2, -1, eng.graph.anchor_buf.C)[..., :no]
+        assert (got_h - ref_h).abs().max().item() / ref_h.abs().max().item() < 1e-2
+        # graph replay of the same pinned plan is deterministic (split-K reduction order is fixed per tile)
+        d1, c1 = eng.run(xd, use_graph=True)
+        d1, c1 = d1.clone(), c1.clone()
+        d2, c2 = eng.run(xd, use_graph=True)
+        assert torch.equal(c1, c2) and torch.equal(d1, d2)
+    finally:
+        eng._tuned.discard((2, 640, 640))  # the next run reloads the tuned table
+
+
+def test_dma_split_configs_on_segment_head():
+    """yolo11n-seg f16 with a split-K DMA config everywhere: Proto (ConvTranspose2d as a pixel-shuffled GEMM)."""
+    x = make_input("uniform", (81,), 640)
+    _, y, ex = oracle("n", "segment").raw(x)
+    eng = model("n", "f16", "segment").model.engine
+    xd = x.to(DEV)
+    for cfg in (DMA_FIRST + 2, DMA_FIRST + 5):
+        _force_cfg(eng, xd, cfg)
+        eng.run(xd, use_graph=False)
+        proto = eng.read_buffer(eng.graph.proto_buf.id, 1)
+        ref_p = ex["proto"].permute(0, 2, 3, 1)
+        assert (proto - ref_p).abs().max().item() / ref_p.abs().max().item() < 1e-2, cfg

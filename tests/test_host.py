@@ -164,3 +164,13 @@ def test_op_costs_cover_all_flops():
     conv_flops = sum(c[0] for c, op in zip(costs, g.ops) if op.kind in ("conv", "dwconv", "attn"))
     assert conv_flops == pytest.approx(8 * 2 * g.macs_per_image(640, 640), rel=1e-9)
     assert len(param_specs("n")) == 499
+
+
+@pytest.mark.skipif(not os.path.exists("/opt/rocm/bin/hipcc"), reason="needs hipcc")
+def test_dma_kernels_issue_exactly_the_counted_loads():
+    """The LDS-DMA conv kernels' counted vmcnt waits assume 3·(BM/32 + BN/32) DMA instructions per kernel."""
+    import subprocess
+    import sys
+    r = subprocess.run([sys.executable, os.path.join(ROOT, "tools", "check_dma_asm.py")], capture_output=True,
+                       text=True, timeout=300)
+    assert r.returncode == 0, r.stdout[-2000:] + r.stderr[-2000:]

@@ -58,6 +58,10 @@ struct ConvArgs {
   int Hin, Win, Ho, Wo, k, s, pad, Cin8, Kc, N, Kpad, act, shuffle, npr, M, tiles_n;
   // stem only: read the caller's NCHW fp32 input directly, applying LoadTensor's /255 rule on load
   const float* nchw; const float* ctl; float eps;
+  // LDS-DMA kernels (csrc/ym_conv_dma.hip): operand extents (elements) and the split-K slab/counter workspace
+  long s0_elems, s1_elems;
+  float* slab; long slab_cap;  // bytes
+  int* cnt; int cnt_cap;       // per-tile arrival counters, zero between launches
 };
 
 struct DwArgs {
@@ -104,13 +108,15 @@ struct NmsArgs {
 struct PrepArgs {
   const float* in; void* out;  // NCHW fp32 → NHWC act dtype, 8 channels (3 real + 5 zero)
   float* ctl;                  // ctl[0] = running max (ordered-int encoded) of the input
+  int* cnt; int cnt_len;       // split-K arrival counters, zeroed at the start of every forward
   int B, C, H, W;
   float eps;                   // LoadTensor rule: /255 when max > 1 + eps
 };
 
 // ------------------------------------------------------------------------------------------------------------
 // Host-side launchers (defined in the .hip translation units).
-hipError_t ym_launch_conv(int dtype, int out_f32, const ConvArgs& a, int cfg, hipStream_t st);  // cfg < 0: heuristic
+// cfg < 0: heuristic; strict: an inapplicable cfg is an error (else the heuristic runs)
+hipError_t ym_launch_conv(int dtype, int out_f32, const ConvArgs& a, int cfg, hipStream_t st, bool strict = false);
 int ym_conv_num_cfgs();
 hipError_t ym_launch_dwconv(int dtype, const DwArgs& a, hipStream_t st);
 hipError_t ym_launch_sppf(int dtype, const PoolArgs& a, hipStream_t st);
@@ -120,3 +126,5 @@ hipError_t ym_launch_decode(const DecodeArgs& a, hipStream_t st);
 hipError_t ym_launch_nms(const NmsArgs& a, hipStream_t st);
 hipError_t ym_launch_stem(int dtype, const ConvArgs& a, hipStream_t st);
 hipError_t ym_launch_spin(int usec, hipStream_t st);  // profiling: park the stream for usec (wall clock)
+hipError_t ym_launch_conv_dma(int out_f32, const ConvArgs& a, int i, hipStream_t st);  // f16 plans only
+int ym_conv_dma_num_cfgs();

@@ -615,9 +615,10 @@ int choose_cfg(const ConvArgs& a) {
 
 }  // namespace
 
-int ym_conv_num_cfgs() { return kNumAllCfg; }
+// ids [0, 17): first-generation kernels above; [17, 17 + ym_conv_dma_num_cfgs()): LDS-DMA / split-K kernels
+int ym_conv_num_cfgs() { return kNumAllCfg + ym_conv_dma_num_cfgs(); }
 
-hipError_t ym_launch_conv(int dtype, int out_f32, const ConvArgs& a, int cfg, hipStream_t st) {
+hipError_t ym_launch_conv(int dtype, int out_f32, const ConvArgs& a, int cfg, hipStream_t st, bool strict) {
   int kind;
   if (a.nchw) kind = (a.k == 3 && a.Cin8 == 1) ? 0 : -1;
   else if (a.k == 1 && a.s == 1) kind = 1;
@@ -626,6 +627,14 @@ hipError_t ym_launch_conv(int dtype, int out_f32, const ConvArgs& a, int cfg, hi
   if (kind < 0) return hipErrorInvalidValue;
   // (concat/upsample sources only feed 1x1 convs; YOLO11 has k in {1, 3})
   if (a.Kpad % KSTEP) return hipErrorInvalidValue;
+  if (cfg >= kNumAllCfg) {
+    // a DMA config that does not apply to this op (checked before anything is launched): the tuner skips the
+    // candidate (strict); a pinned table falls back to the heuristic
+    const hipError_t e = dtype == YM_DT_F16 ? ym_launch_conv_dma(out_f32, a, cfg - kNumAllCfg, st)
+                                            : hipErrorInvalidValue;
+    if (e != hipErrorInvalidValue || strict) return e;
+    cfg = -1;
+  }
   int id = (cfg >= 0 && cfg < kNumAllCfg) ? cfg : choose_cfg(a);
   if (id >= kNumCfg && dtype != YM_DT_F16) id = choose_cfg(a);  // LDS variants are instantiated for f16 only
   if (dtype == YM_DT_F16) return out_f32 ? launch_id<f16, float>(id, a, kind, st) : launch_id<f16, f16>(id, a, kind, st);

@@ -11,10 +11,11 @@ namespace {
 // LoadTensor._single_check: `if im.max() > 1 + finfo(dtype).eps: im = im.float() / 255` over the WHOLE batch.
 // ctl[0] holds max as an order-preserving int; ctl is reset by the init kernel at the start of every forward.
 // The division itself happens in the stem conv's loader (csrc/ym_conv.hip KIND 0), which reads the NCHW batch.
-__global__ void init_ctl(float* ctl, int* counts, int B) {
+__global__ void init_ctl(float* ctl, int* counts, int B, int* cnt, int cnt_len) {
   const int t = threadIdx.x;
   if (t == 0) reinterpret_cast<int*>(ctl)[0] = f2ord(-INFINITY);
   for (int b = t; b < B; b += blockDim.x) counts[b] = 0;
+  for (int i = t; i < cnt_len; i += blockDim.x) cnt[i] = 0;  // split-K tile counters (csrc/ym_conv_dma.hip)
 }
 
 __global__ __launch_bounds__(256) void max_reduce(const float* __restrict__ x, long n, float* ctl) {
@@ -531,7 +532,7 @@ hipError_t ym_launch_spin(int usec, hipStream_t st) {
 
 hipError_t ym_launch_prep(int dtype, const PrepArgs& a, int* counts, int B, hipStream_t st) {
   (void)dtype;
-  hipLaunchKernelGGL(init_ctl, dim3(1), dim3(64), 0, st, a.ctl, counts, B);
+  hipLaunchKernelGGL(init_ctl, dim3(1), dim3(256), 0, st, a.ctl, counts, B, a.cnt, a.cnt_len);
   // one atomic per block: a few hundred same-address atomics, not thousands (one word takes ~90 per us)
   const long n = (long)a.B * a.C * a.H * a.W;
   long blocks = (n / 4 + 255) / 256;

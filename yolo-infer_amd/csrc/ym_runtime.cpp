@@ -5,6 +5,7 @@
 // (input /255 rule → 80+ fused conv launches → attention → decode → NMS), so the Python host issues one call.
 #include <hip/hip_runtime.h>
 
+#include <algorithm>
 #include <cstdarg>
 #include <cstdio>
 #include <cstring>
@@ -36,6 +37,7 @@ int fail(int code, const char* fmt, ...) {
 
 constexpr int32_t kMagic = 0x4C504D59;  // 'YMPL'
 constexpr int kHdr = 32, kBufRec = 8, kOpRec = 32, kNameLen = 48;
+constexpr int kSplitCounters = 16384;  // split-K tiles per conv launch (csrc/ym_conv_dma.hip)
 
 enum OpKind { OP_INPUT = 1, OP_CONV = 2, OP_DW = 3, OP_SPPF = 4, OP_ATTN = 5, OP_DECODE = 6, OP_NMS = 7 };
 
@@ -84,7 +86,7 @@ struct ym_ctx {
   size_t arena_bytes = 0;
   std::vector<size_t> buf_off;
   size_t off_boxes = 0, off_scores = 0, off_cls = 0, off_keys = 0, off_counts = 0, off_ctl = 0, off_sboxes = 0,
-         off_sareas = 0, off_sup = 0;
+         off_sareas = 0, off_sup = 0, off_slab = 0, off_cnt = 0, slab_bytes = 0;
   int A = 0, kstride = 0;
   int lvl_W[4] = {0}, lvl_off[4] = {0};
   hipStream_t cap_stream = nullptr;
@@ -181,6 +183,10 @@ int ensure_workspace(ym_ctx* c, int B, int H, int W) {
   c->off_sboxes = off; off = align_up(off + BA * 16, 256);
   c->off_sareas = off; off = align_up(off + BA * 4, 256);
   c->off_sup = off;    off = align_up(off + BA, 256);
+  // split-K workspace of the LDS-DMA conv kernels: fp32 partial tiles + per-tile arrival counters
+  c->slab_bytes = std::max<size_t>(32u << 20, (size_t)nB << 22);
+  c->off_slab = off;   off = align_up(off + c->slab_bytes, 256);
+  c->off_cnt = off;    off = align_up(off + (size_t)kSplitCounters * 4, 256);
   c->arena_bytes = off;
   hipError_t e = hipMalloc(&c->d_arena, off);
   if (e != hipSuccess) {
@@ -244,6 +250,12 @@ int conv_args(ym_ctx* c, const Op& op, int B, const float* d_in, float in_eps, C
       if (br >= 0) { a.res = c->bptr(br); a.r_ctot = c->bufs[br].C; a.r_coff = r[18]; a.r_P = c->buf_P(br); }
       a.M = B * a.Ho * a.Wo;
       out_f32 = c->bufs[bd].f32 && c->dtype == YM_DT_F16;
+      a.s0_elems = (b0 == c->input_buf) ? 0 : (long)c->cB * c->buf_P(b0) * c->bufs[b0].C;
+      a.s1_elems = b1 >= 0 ? (long)c->cB * c->buf_P(b1) * c->bufs[b1].C : 0;
+      a.slab = reinterpret_cast<float*>(c->d_arena + c->off_slab);
+      a.slab_cap = (long)c->slab_bytes;
+      a.cnt = reinterpret_cast<int*>(c->d_arena + c->off_cnt);
+      a.cnt_cap = kSplitCounters;
       return YM_OK;
 }
 
@@ -260,6 +272,8 @@ int launch_op(ym_ctx* c, const Op& op, int B, const float* d_in, const ym_infer_
       a.ctl = reinterpret_cast<float*>(c->d_arena + c->off_ctl);
       a.B = B; a.C = 3; a.H = c->cH; a.W = c->cW;
       a.eps = args->in_eps;
+      a.cnt = reinterpret_cast<int*>(c->d_arena + c->off_cnt);
+      a.cnt_len = kSplitCounters;
       e = ym_launch_prep(dt, a, reinterpret_cast<int*>(c->d_arena + c->off_counts), B, st);
       break;
     }
@@ -582,7 +596,7 @@ int ym_tune(ym_ctx* c, const float* d_in, int B, int H, int W, const ym_infer_ar
       hipGraphExec_t ge = nullptr;
       HIPCK(hipStreamBeginCapture(c->cap_stream, hipStreamCaptureModeRelaxed));
       hipError_t le = hipSuccess;
-      for (int r = 0; r < reps && le == hipSuccess; ++r) le = ym_launch_conv(c->dtype, out_f32, a, cf, c->cap_stream);
+      for (int r = 0; r < reps && le == hipSuccess; ++r) le = ym_launch_conv(c->dtype, out_f32, a, cf, c->cap_stream, true);
       HIPCK(hipStreamEndCapture(c->cap_stream, &g));
       if (le != hipSuccess) {
         (void)hipGraphDestroy(g);
