@@ -22,7 +22,7 @@ import sys
 
 ROOT = os.path.dirname(os.path.dirname(os.path.abspath(__file__)))
 PROF = os.path.join(ROOT, "profiles")
-CONV = re.compile(r"conv_igemm|conv_lds")
+CONV = re.compile(r"conv_igemm|conv_lds|conv_dma")
 STEM = re.compile(r"stem_conv3x3s2")
 
 

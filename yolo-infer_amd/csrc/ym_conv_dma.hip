@@ -102,7 +102,9 @@ __global__ __launch_bounds__(256) void conv_dma(const ConvArgs a) {
     if constexpr (KIND == 1) {
       const int sy = a.up0 ? (oy >> 1) : oy, sx = a.up0 ? (ox >> 1) : ox;
       pbase0[gi] = ok ? (b * a.s0_P + sy * a.s0_W + sx) * a.s0_ctot + a.s0_coff : -1;
-      pbase1[gi] = ok && a.src1 ? (b * a.s1_P + oy * a.Win + ox) * a.s1_ctot + a.s1_coff - a.C0 : -1;
+      // (row bases stay >= 0 for valid rows: -1 marks an M-tail row, so the -C0 of the second source's channel
+      // index is applied per stage, not folded in here)
+      pbase1[gi] = ok && a.src1 ? (b * a.s1_P + oy * a.Win + ox) * a.s1_ctot + a.s1_coff : -1;
       piy[gi] = pix[gi] = 0;
     } else {
       pbase0[gi] = ok ? b * a.s0_P : -1;  // image pixel base
@@ -139,7 +141,7 @@ __global__ __launch_bounds__(256) void conv_dma(const ConvArgs a) {
 #pragma unroll
       for (int gi = 0; gi < GB; ++gi) {
         const int pb = second ? pbase1[gi] : pbase0[gi];
-        const unsigned off = pb >= 0 ? (unsigned)(pb + chunk * 8) * 2u : OOB;
+        const unsigned off = pb >= 0 ? (unsigned)(pb + chunk * 8 - (second ? a.C0 : 0)) * 2u : OOB;
         dma16(second ? rs1 : rs0, sbase + (wid + 4 * gi) * 1024, off);
       }
     } else {
@@ -231,9 +233,16 @@ __global__ __launch_bounds__(256) void conv_dma(const ConvArgs a) {
     }
     __syncthreads();
     if (!*flag) return;
+    // sum every slab (this workgroup's own included) in split order, so the result does not depend on which split
+    // arrived last: bitwise-reproducible launches
+#pragma unroll
+    for (int i = 0; i < TM; ++i)
+#pragma unroll
+      for (int j = 0; j < TN; ++j)
+#pragma unroll
+        for (int r = 0; r < 16; ++r) acc[i][j][r] = 0.f;
 #pragma unroll 1
     for (int s2 = 0; s2 < SPLIT; ++s2) {
-      if (s2 == sp) continue;
       const float* o = a.slab + (size_t)(tile * SPLIT + s2) * (256 * NREG);
 #pragma unroll
       for (int i = 0; i < TM; ++i)
