@@ -66,9 +66,11 @@ def conv_roofline(model, x, dtype, workload, reps=20):
     launches ÷ Σ their per-launch times (per-unit figures: DESIGN.md §4)."""
     eng = model.model.engine
     B, _, H, W = x.shape
-    costs = eng.graph.op_costs(B, H, W, 2 if dtype == "f16" else 4)
+    Bl = eng.lane_batch(B)  # every kernel of a lane sees Bl images: time and count one lane's launches
+    x = x[:Bl]
+    costs = eng.graph.op_costs(Bl, H, W, 2 if dtype == "f16" else 4)
     times = np.array(eng.profile_replay(x, reps=reps))
-    eng.run(x)  # restore the buffers the replay clobbered
+    eng.run(x, lanes=1)  # restore the buffers the replay clobbered
     kinds = [op.kind for op in eng.graph.ops]
     conv = [i for i, k in enumerate(kinds) if k == "conv"]
     t_conv = float(times[conv].sum()) * 1e-3
@@ -87,8 +89,8 @@ def conv_roofline(model, x, dtype, workload, reps=20):
         "frac": round(ach / PEAK_TFLOPS[dtype], 4), "traffic": traffic,
         "traffic_note": (f"HBM-side bytes per forward of all conv launches (PMC FETCH_SIZE x2 + WRITE_SIZE, {tsrc}); "
                          f"algorithmic bytes per forward {int(by)}") if traffic else "no PMC summary for this workload",
-        "kernel": "conv implicit GEMM (conv_igemm/conv_lds): all %d conv launches of one forward, aggregated"
-                  % len(conv),
+        "kernel": "conv implicit GEMM (conv_igemm/conv_lds/conv_dma): all %d conv launches of one lane's forward "
+                  "(%d images), aggregated" % (len(conv), Bl),
         "timing": f"HIP events around a graph of {reps} back-to-back launches per op, on the launch stream",
         "launches": len(conv), "avg_launch_us": round(t_conv / len(conv) * 1e6, 2),
         "flops_per_forward": fl, "bytes_per_forward_algorithmic": by,
@@ -143,6 +145,8 @@ def main():
     ap.add_argument("--cpu-seconds", type=float, default=15.0)
     ap.add_argument("--no-cpu", action="store_true")
     ap.add_argument("--no-roofline", action="store_true")
+    ap.add_argument("--lanes", type=int, default=int(os.environ.get("YM_LANES", "1")),
+                    help="concurrent image slices per forward graph (yolomi lanes)")
     a = ap.parse_args()
 
     world = int(os.environ.get("WORLD_SIZE", "1"))
@@ -173,6 +177,7 @@ def main():
         dist.broadcast(buf, 0)
         blob = bytes(buf.cpu().numpy())
     model = YOLO11Model(task=a.task, size=a.model, device=f"cuda:{local}", dtype=a.dtype, weights_blob=blob)
+    model.model.engine.lanes = a.lanes
     init_s = time.perf_counter() - t_init
 
     B = a.batch
@@ -215,7 +220,9 @@ def main():
         "device_images_per_s": round(dev_ips * world, 2),
         "init_s": round(init_s, 3),
     }
-    out["config"]["conv_tiles"] = model.model.engine.tune_source.get((B, a.size, a.size), "heuristic")
+    Bl = model.model.engine.lane_batch(B)
+    out["config"]["lanes"] = -(-B // Bl)
+    out["config"]["conv_tiles"] = model.model.engine.tune_source.get((Bl, a.size, a.size), "heuristic")
     if rank == 0 and not a.no_roofline:
         out["roofline"] = conv_roofline(model, x, a.dtype, out["config"]["workload"])
     if rank == 0 and world == 1 and not a.no_cpu:

@@ -51,7 +51,9 @@ typedef struct {
   int has_classes;
   uint32_t classes[4]; /* bit c set = keep class c (c < 128) */
   int use_graph;       /* 1: capture/replay a HIP graph per (shape, pointers, args); 0: eager launches */
-  int reserved[7];
+  int lanes;           /* 1..4 image slices run as concurrent graph branches (0 = 1); conv tile tables are looked
+                          up at the slice batch ceil(B / lanes) */
+  int reserved[6];
 } ym_infer_args;
 
 /* Replaces `YOLO(model_path)` construction (core/model.py:100-116): create a context on `device`. */

@@ -228,7 +228,7 @@ def _force_cfg(eng, x, cfg):
     eng.rt.set_op_cfg(B, H, W, [cfg if op.kind == "conv" else -1 for op in eng.graph.ops])
 
 
-@pytest.mark.parametrize("cfg", list(range(DMA_FIRST, DMA_FIRST + 12)))
+@pytest.mark.parametrize("cfg", list(range(DMA_FIRST, DMA_FIRST + 18)))
 def test_dma_conv_configs_match_oracle(cfg):
     """Every conv of yolo11n (1x1 two-source/upsampled, 3x3 s1/s2, residual, fp32 Detect rows) on one DMA config."""
     m = model("n", "f16")
@@ -270,3 +270,35 @@ def test_dma_split_configs_on_segment_head():
         proto = eng.read_buffer(eng.graph.proto_buf.id, 1)
         ref_p = ex["proto"].permute(0, 2, 3, 1)
         assert (proto - ref_p).abs().max().item() / ref_p.abs().max().item() < 1e-2, cfg
+
+
+# ------------------------------------------------------------------------------------------------ lanes
+@pytest.mark.parametrize("B,lanes", [(8, 2), (8, 4), (3, 2), (1, 4), (5, 3)])
+def test_lanes_match_single_lane(B, lanes):
+    """Concurrent image slices (parallel graph branches) give the single-lane detections: same NMS input per image,
+    the /255 decision still over the whole batch (slices see different kernel batches, hence the f32 tolerance)."""
+    eng = model("n", "f32").model.engine
+    x = make_input("uniform", tuple(range(101, 101 + B)), 320).to(DEV)
+    d1, c1 = eng.run(x, conf=0.1, lanes=1)
+    d1, c1 = d1.clone(), c1.clone()
+    for use_graph in (True, False):
+        d2, c2 = eng.run(x, conf=0.1, lanes=lanes, use_graph=use_graph)
+        for i in range(B):
+            rep = match_image(d1[i, :int(c1[i])].cpu().numpy(), d2[i, :int(c2[i])].cpu().numpy(), 0.1, 0.7, 1e-3, 1e-3,
+                              rep=MatchReport())
+            assert rep.ok and rep.matched >= int(c1[i]) - rep.exempt, (i, rep)
+
+
+def test_lanes_keep_batch_wide_255_rule():
+    """One image in [0, 255] makes the whole batch divide by 255 (LoadTensor), even when it sits in another lane."""
+    eng = model("n", "f32").model.engine
+    x = make_input("uniform", (111, 112, 113, 114), 320).to(DEV)
+    x255 = x.clone()
+    x255[3] *= 255.0
+    d1, c1 = eng.run(x255 / 255.0, conf=0.1, lanes=1)
+    d1, c1 = d1.clone(), c1.clone()
+    d2, c2 = eng.run(x255, conf=0.1, lanes=2)
+    for i in range(4):
+        rep = match_image(d1[i, :int(c1[i])].cpu().numpy(), d2[i, :int(c2[i])].cpu().numpy(), 0.1, 0.7, 1e-3, 1e-3,
+                          rep=MatchReport())
+        assert rep.ok, (i, rep)

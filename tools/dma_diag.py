@@ -14,7 +14,7 @@ sys.path.insert(0, ROOT)
 
 import torch  # noqa: E402
 
-DMA_FIRST, NDMA = 17, 12
+DMA_FIRST, NDMA = 17, 18
 
 
 def main():

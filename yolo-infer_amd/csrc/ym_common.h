@@ -44,6 +44,24 @@ __device__ __forceinline__ int f2ord(float f) {
 __device__ __forceinline__ float ord2f(int i) { return __int_as_float(i >= 0 ? i : i ^ 0x7FFFFFFF); }
 
 __device__ __forceinline__ float ym_silu(float x) { return x / (1.0f + expf(-x)); }
+// SiLU from the hardware exp2 / reciprocal (each ~1 ulp): for epilogues whose outputs are rounded to fp16 anyway
+__device__ __forceinline__ float ym_silu_fast(float x) {
+  return x * __builtin_amdgcn_rcpf(1.0f + __builtin_amdgcn_exp2f(-1.4426950408889634f * x));
+}
+
+// Division by a runtime constant d >= 1 for 0 <= n < 2^31: n / d == (n * m) >> p with p = 31 + ceil(log2 d),
+// m = ceil(2^p / d) < 2^32 (the rounding error m*d - 2^p < d <= 2^(p-31) keeps the floor exact).
+struct FDiv {
+  unsigned m;
+  int p;
+};
+inline FDiv ym_fdiv(int d) {
+  int s = 0;
+  while ((1LL << s) < d) ++s;
+  const int p = 31 + s;
+  return FDiv{(unsigned)(((1ULL << p) + (unsigned long long)d - 1) / (unsigned long long)d), p};
+}
+__device__ __forceinline__ int ym_div(int n, FDiv f) { return (int)(((unsigned long long)(unsigned)n * f.m) >> f.p); }
 __device__ __forceinline__ float ym_sigmoid(float x) { return 1.0f / (1.0f + expf(-x)); }
 
 // ------------------------------------------------------------------------------------------------------------
@@ -60,6 +78,7 @@ struct ConvArgs {
   const float* nchw; const float* ctl; float eps;
   // LDS-DMA kernels (csrc/ym_conv_dma.hip): operand extents (elements) and the split-K slab/counter workspace
   long s0_elems, s1_elems;
+  FDiv fd_hw, fd_w;            // division by Ho*Wo and by Wo
   float* slab; long slab_cap;  // bytes
   int* cnt; int cnt_cap;       // per-tile arrival counters, zero between launches
 };

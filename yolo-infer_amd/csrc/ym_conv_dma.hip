@@ -4,8 +4,8 @@
 // the columns, k = (ky, kx, c) so an 8-element K chunk is 8 channels of one input pixel), built for the two regimes
 // that cost the first-generation kernels most on YOLO11 shapes:
 //  * operands stream global → LDS with `buffer_load_dwordx4 … lds` (LDS-DMA: no VGPR staging, no ds_write pass)
-//    into a 3-deep ring of 64-deep K stages, one raw barrier per stage and a counted `s_waitcnt vmcnt`, so two
-//    stages of loads are always in flight behind the MFMAs.  The implicit-im2col gather is per lane (each lane
+//    into a 4-deep ring of 64-deep K stages, one raw barrier per stage and a counted `s_waitcnt vmcnt`, so three
+//    stages of loads are in flight behind the MFMAs (a stage's load latency, not its MFMAs, sets the pace here).  The implicit-im2col gather is per lane (each lane
 //    computes its own pixel/tap byte offset); 3x3 zero padding, K tails and M/N tails are out-of-range buffer offsets,
 //    which the DMA turns into zeros in LDS — no branches in the load path;
 //  * LDS image: row = one pixel (or one weight row) × 64 K = 128 B; chunk c of row r sits at slot c ^ ((r >> 1) & 7),
@@ -13,19 +13,34 @@
 //    the swizzle is applied on the SOURCE side (the DMA destination is lane-linear);
 //  * small-M deep layers (20x20 / 40x40 maps: a few hundred pixels per image, K up to 4608) are bound by the serial
 //    chain of K stages, not by MFMA or HBM: SPLIT workgroups share one output tile, each takes a contiguous K range,
-//    writes its fp32 partial tile (a "slab"), and the last to arrive at the tile's counter (agent-scope release /
-//    acquire, cdna_hip_programming.md §5 "In-launch split-K reduction") sums the slabs and runs the epilogue.
+//    writes its fp32 partial tile (a "slab") with write-through (sc1) stores, and the last to arrive at the tile's
+//    counter sums the slabs (sc1 loads) and runs the epilogue — the sc1 hand-off of cdna_hip_programming.md §6
+//    Guideline 16: no release fence, whose L2 write-back (the previous layers' dirty activations) cost ~2 µs per
+//    workgroup, and no L1 invalidate.
 // Epilogue as in ym_conv.hip: + folded-BN bias, SiLU, + residual, channel-slice store (zero-copy concat), fp32
 // anchor-major Detect rows, 2x2 pixel shuffle (Proto ConvTranspose2d).
 #include "ym_common.h"
 
 typedef float f32x16 __attribute__((ext_vector_type(16)));
 typedef __attribute__((address_space(3))) void lds_void_t;
+typedef unsigned u32x4 __attribute__((ext_vector_type(4)));
+
+#ifdef YM_DMA_STAMPS  // tools/dma_probe.hip: cycle stamps of workgroup 0, wave 0 (never built into the library)
+__device__ unsigned long long* ym_dma_stamps;
+#define YM_STAMP(i)                                                                          \
+  do {                                                                                       \
+    if (blockIdx.x == 0 && threadIdx.x == 0) ym_dma_stamps[(i)] = __builtin_readcyclecounter(); \
+  } while (0)
+#else
+#define YM_STAMP(i) \
+  do {              \
+  } while (0)
+#endif
 
 namespace {
 
 constexpr int DK = 64;                    // K per stage
-constexpr int NSTAGE = 3;                 // LDS ring depth
+constexpr int NSTAGE = 4;                 // LDS ring depth (three stages of loads in flight)
 constexpr unsigned OOB = 0x80000000u;     // byte offset past num_records: the DMA deposits zeros
 
 template <int N>
@@ -52,18 +67,32 @@ template <> struct Store4<float> {
   }
 };
 
-// 256 threads = 2x2 waves; a wave owns (BM/2) pixels x (BN/2) channels = TM x TN blocks of 32x32.
-template <typename OutT, int BM, int BN, int KIND, int SPLIT>
-__global__ __launch_bounds__(256) void conv_dma(const ConvArgs a) {
+// A workgroup = KG groups of 2x2 waves (256·KG threads).  Every wave group covers the whole BM x BN tile — a wave
+// owns (BM/2) pixels x (BN/2) channels = TM x TN blocks of 32x32 — and takes 4/KG of each stage's four 16-deep k
+// sub-steps; the groups' partial tiles are summed once through LDS after the K loop.  KG = 2 puts two waves on every
+// SIMD, so one wave's LDS reads, barrier and DMA issue overlap the other's MFMAs (the small-M layers are latency-bound
+// with one wave per SIMD: tools/dma_probe.hip).
+// KIND 1: 1x1 stride 1 (two sources, upsampled first source); KIND 3: 3x3, any Cin (per-lane tap walk);
+// KIND 4: 3x3 with Cin % 64 == 0 — every 64-deep stage is ONE tap, so the tap, its pixel offset and the channel
+// block are wave-uniform scalars and a DMA address is one add onto a per-row base, validity one bit of a 9-bit
+// per-row tap mask.
+template <typename OutT, int BM, int BN, int KIND, int SPLIT, int KG>
+__global__ __launch_bounds__(256 * KG) void conv_dma(const ConvArgs a) {
+  constexpr int NW = 4 * KG;
   constexpr int TM = BM / 64, TN = BN / 64;
-  constexpr int GB = BM / 32, GA = BN / 32;  // DMA wave-instructions per stage per wave (8 rows of 128 B each)
+  static_assert((BM / 8) % NW == 0 && (BN / 8) % NW == 0, "DMA groups must divide over the waves");
+  constexpr int GB = BM / 8 / NW, GA = BN / 8 / NW;  // DMA wave-instructions per stage per wave (8 rows x 128 B)
   constexpr int NL = GA + GB;
-  constexpr int SB = (BM + BN) * 128;        // bytes per stage
+  constexpr int SB = (BM + BN) * 128;                // bytes per stage
   constexpr int NREG = TM * TN * 16;
+  constexpr int SPW = 4 / KG;                        // 16-deep k sub-steps per wave per stage
+  constexpr int NACC = TM * TN == 1 && SPW >= 2 ? 2 : 1;  // one 32x32 block per wave: alternate two accumulators
   __shared__ __attribute__((aligned(16))) char smem[NSTAGE * SB + 16];
 
+  YM_STAMP(0);
   const int tid = threadIdx.x, lane = tid & 63, wid = tid >> 6;
-  const int wm = wid & 1, wn = wid >> 1;
+  const int kg = wid >> 2, wq = wid & 3;
+  const int wm = wq & 1, wn = wq >> 1;
   const int l32 = lane & 31, h = lane >> 5;
   // tile map: every N tile and every K split of pixel tile tm share bid % 8 = one XCD (its L2 holds the pixels and
   // the split's slabs); padding workgroups (tm beyond M) exit before touching a counter
@@ -74,11 +103,46 @@ __global__ __launch_bounds__(256) void conv_dma(const ConvArgs a) {
   const int tn = rest % a.tiles_n;
   const int tm = (rest / a.tiles_n) * 8 + (bid & 7);
   if (tm * BM >= a.M) return;
-  const int HWo = a.Ho * a.Wo;
+
+  // ---- epilogue operands first (bias, residual; wave group 0 runs the epilogue): their latency hides behind the
+  // K loop.  They are older than every DMA, so the counted vmcnt waits below stay exact (loads retire in order).
+  int ep_m[TM];
+  size_t ep_obase[TM];
+  f32x4 bias4[TN][4];
+  f16x4 res4[TM][TN][4];
+  const f16* res = static_cast<const f16*>(a.res);
+  if (kg == 0) {
+#pragma unroll
+    for (int j = 0; j < TN; ++j)
+#pragma unroll
+      for (int q = 0; q < 4; ++q) {
+        const int n = tn * BN + wn * (BN / 2) + 32 * j + 8 * q + 4 * h;
+        bias4[j][q] = n < a.N ? *reinterpret_cast<const f32x4*>(a.bias + n) : f32x4{0.f, 0.f, 0.f, 0.f};
+      }
+#pragma unroll
+    for (int i = 0; i < TM; ++i) {
+      const int m = tm * BM + wm * (BM / 2) + 32 * i + l32;
+      ep_m[i] = m;
+      const int mm = m < a.M ? m : 0;
+      const int b = ym_div(mm, a.fd_hw), rem = mm - b * (a.Ho * a.Wo);
+      const int oy = ym_div(rem, a.fd_w), ox = rem - oy * a.Wo;
+      const int pix = a.shuffle ? (2 * oy) * a.d_W + 2 * ox : oy * a.d_W + ox;
+      ep_obase[i] = (size_t)(b * a.d_P + a.d_pixoff + pix) * a.d_ctot + a.d_coff;
+      const size_t rbase = res ? (size_t)(b * a.r_P + oy * a.Wo + ox) * a.r_ctot + a.r_coff : 0;
+#pragma unroll
+      for (int j = 0; j < TN; ++j)
+#pragma unroll
+        for (int q = 0; q < 4; ++q) {
+          const int n = tn * BN + wn * (BN / 2) + 32 * j + 8 * q + 4 * h;
+          res4[i][j][q] = (res && m < a.M && n < a.N) ? *reinterpret_cast<const f16x4*>(res + rbase + n)
+                                                       : f16x4{0, 0, 0, 0};
+        }
+    }
+  }
 
   // ---- DMA lanes: instruction-row rr = lane >> 3, LDS slot lane & 7, so this lane fetches chunk c of its row with
-  // c = slot ^ ((row >> 1) & 7); rows of wave wid's groups are (wid + 4 gi) * 8 + rr, hence (row >> 1) & 7 =
-  // ((wid & 1) << 2) | (rr >> 1) for every group of this wave: one chunk index per lane.
+  // c = slot ^ ((row >> 1) & 7); rows of wave wid's groups are (wid + NW gi) * 8 + rr, hence (row >> 1) & 7 =
+  // ((wid & 1) << 2) | (rr >> 1) for every group of this wave (NW even): one chunk index per lane.
   const int rr = lane >> 3;
   const int c = (lane & 7) ^ (((wid & 1) << 2) | (rr >> 1));
   // exact extents: a K-tail chunk past the end of a buffer reads zeros, inside it a finite activation (times a
@@ -92,13 +156,15 @@ __global__ __launch_bounds__(256) void conv_dma(const ConvArgs a) {
                                                                       (int)((long)a.N * a.Kpad * 2), 0x00020000);
   // pixel rows of this lane's B groups
   int pbase0[GB], pbase1[GB], piy[GB], pix[GB];
+  unsigned tmask[GB];  // KIND 4: bit t = tap t of the 3x3 window lies inside the image (0 for an M-tail row)
 #pragma unroll
   for (int gi = 0; gi < GB; ++gi) {
-    const int m = tm * BM + (wid + 4 * gi) * 8 + rr;
+    const int m = tm * BM + (wid + NW * gi) * 8 + rr;
     const bool ok = m < a.M;
     const int mm = ok ? m : 0;
-    const int b = mm / HWo, rem = mm - (mm / HWo) * HWo;
-    const int oy = rem / a.Wo, ox = rem - (rem / a.Wo) * a.Wo;
+    const int b = ym_div(mm, a.fd_hw), rem = mm - b * (a.Ho * a.Wo);
+    const int oy = ym_div(rem, a.fd_w), ox = rem - oy * a.Wo;
+    tmask[gi] = 0;
     if constexpr (KIND == 1) {
       const int sy = a.up0 ? (oy >> 1) : oy, sx = a.up0 ? (ox >> 1) : ox;
       pbase0[gi] = ok ? (b * a.s0_P + sy * a.s0_W + sx) * a.s0_ctot + a.s0_coff : -1;
@@ -106,29 +172,49 @@ __global__ __launch_bounds__(256) void conv_dma(const ConvArgs a) {
       // index is applied per stage, not folded in here)
       pbase1[gi] = ok && a.src1 ? (b * a.s1_P + oy * a.Win + ox) * a.s1_ctot + a.s1_coff : -1;
       piy[gi] = pix[gi] = 0;
-    } else {
+    } else if constexpr (KIND == 3) {
       pbase0[gi] = ok ? b * a.s0_P : -1;  // image pixel base
       pbase1[gi] = 0;
       piy[gi] = oy * a.s - 1;
       pix[gi] = ox * a.s - 1;
+    } else {
+      const int iy0 = oy * a.s - 1, ix0 = ox * a.s - 1;
+      // element offset of this lane's chunk at the window's top-left pixel (may be negative: only in-image taps
+      // are ever added to it)
+      pbase0[gi] = (b * a.s0_P + iy0 * a.Win + ix0) * a.s0_ctot + a.s0_coff + c * 8;
+      pbase1[gi] = 0;
+      piy[gi] = pix[gi] = 0;
+      unsigned mk = 0;
+#pragma unroll
+      for (int t = 0; t < 9; ++t) {
+        const int iy = iy0 + t / 3, ix = ix0 + t % 3;
+        mk |= ((unsigned)iy < (unsigned)a.Hin && (unsigned)ix < (unsigned)a.Win) ? (1u << t) : 0u;
+      }
+      tmask[gi] = ok ? mk : 0u;
     }
   }
   int wbase[GA];
 #pragma unroll
   for (int gi = 0; gi < GA; ++gi) {
-    const int n = tn * BN + (wid + 4 * gi) * 8 + rr;
+    const int n = tn * BN + (wid + NW * gi) * 8 + rr;
     wbase[gi] = n < a.N ? n * a.Kpad + c * 8 : -1;
   }
 
   const int nst = a.Kpad / DK;
   const int k_lo = (nst * sp) / SPLIT, k_hi = (nst * (sp + 1)) / SPLIT;
   const int nk = k_hi - k_lo;
-  // KIND 3: tap / channel block of this lane's chunk at stage k_lo (chunk index k*8 + c)
-  int tap = 0, cb = 0;
+  // KIND 3: tap / channel block of this lane's chunk at stage k_lo (chunk index k*8 + c);
+  // KIND 4: the stage's tap (ky, kx) and channel block cb (wave-uniform)
+  int tap = 0, cb = 0, ky = 0, kx = 0;
   if constexpr (KIND == 3) {
     const int idx = k_lo * 8 + c;
     tap = idx / a.Cin8;
     cb = idx - tap * a.Cin8;
+  } else if constexpr (KIND == 4) {
+    tap = (k_lo * 8) / a.Cin8;
+    cb = k_lo * 8 - tap * a.Cin8;
+    ky = tap / 3;
+    kx = tap - ky * 3;
   }
   int kcur = k_lo;  // stage whose loads are issued next
 
@@ -142,108 +228,141 @@ __global__ __launch_bounds__(256) void conv_dma(const ConvArgs a) {
       for (int gi = 0; gi < GB; ++gi) {
         const int pb = second ? pbase1[gi] : pbase0[gi];
         const unsigned off = pb >= 0 ? (unsigned)(pb + chunk * 8 - (second ? a.C0 : 0)) * 2u : OOB;
-        dma16(second ? rs1 : rs0, sbase + (wid + 4 * gi) * 1024, off);
+        dma16(second ? rs1 : rs0, sbase + (wid + NW * gi) * 1024, off);
       }
-    } else {
-      const int ky = tap / 3, kx = tap - (tap / 3) * 3;
+    } else if constexpr (KIND == 3) {
+      const int ty = tap / 3, tx = tap - (tap / 3) * 3;
 #pragma unroll
       for (int gi = 0; gi < GB; ++gi) {
-        const int iy = piy[gi] + ky, ix = pix[gi] + kx;
+        const int iy = piy[gi] + ty, ix = pix[gi] + tx;
         const bool ok = pbase0[gi] >= 0 && (unsigned)iy < (unsigned)a.Hin && (unsigned)ix < (unsigned)a.Win;
         const unsigned off =
             ok ? (unsigned)((pbase0[gi] + iy * a.Win + ix) * a.s0_ctot + a.s0_coff + cb * 8) * 2u : OOB;
-        dma16(rs0, sbase + (wid + 4 * gi) * 1024, off);
+        dma16(rs0, sbase + (wid + NW * gi) * 1024, off);
       }
       cb += 8;
       while (cb >= a.Cin8) { cb -= a.Cin8; ++tap; }
+    } else {
+      const int S = (ky * a.Win + kx) * a.s0_ctot + cb * 8;  // uniform
+#pragma unroll
+      for (int gi = 0; gi < GB; ++gi) {
+        const unsigned off = (tmask[gi] >> tap) & 1u ? (unsigned)(pbase0[gi] + S) * 2u : OOB;
+        dma16(rs0, sbase + (wid + NW * gi) * 1024, off);
+      }
+      cb += 8;
+      if (cb == a.Cin8) {
+        cb = 0;
+        ++tap;
+        if (++kx == 3) { kx = 0; ++ky; }
+      }
     }
     // A: weights
 #pragma unroll
     for (int gi = 0; gi < GA; ++gi) {
       const unsigned off = wbase[gi] >= 0 ? (unsigned)(wbase[gi] + kcur * DK) * 2u : OOB;
-      dma16(rw, sbase + BM * 128 + (wid + 4 * gi) * 1024, off);
+      dma16(rw, sbase + BM * 128 + (wid + NW * gi) * 1024, off);
     }
     ++kcur;
   };
 
-  f32x16 acc[TM][TN];
+  f32x16 acc[NACC][TM][TN];
 #pragma unroll
-  for (int i = 0; i < TM; ++i)
+  for (int u = 0; u < NACC; ++u)
 #pragma unroll
-    for (int j = 0; j < TN; ++j)
+    for (int i = 0; i < TM; ++i)
 #pragma unroll
-      for (int r = 0; r < 16; ++r) acc[i][j][r] = 0.f;
+      for (int j = 0; j < TN; ++j)
+#pragma unroll
+        for (int r = 0; r < 16; ++r) acc[u][i][j][r] = 0.f;
 
   const int key = (l32 >> 1) & 7;
+  // this wave's k sub-steps of the stage: fragment reads first, then the MFMAs (one LDS latency per stage)
   auto compute = [&](int slot) {
     const char* sb = smem + slot * SB;
     const char* sa = sb + BM * 128;
+    f16x8 fb[SPW][TM], fa[SPW][TN];
 #pragma unroll
-    for (int s = 0; s < 4; ++s) {
+    for (int u = 0; u < SPW; ++u) {
+      const int s = kg * SPW + u;
       const int off = ((((2 * s + h) ^ key)) << 4) + l32 * 128;
-      f16x8 fb[TM], fa[TN];
 #pragma unroll
-      for (int i = 0; i < TM; ++i) fb[i] = *reinterpret_cast<const f16x8*>(sb + (wm * (BM / 2) + 32 * i) * 128 + off);
+      for (int i = 0; i < TM; ++i) fb[u][i] = *reinterpret_cast<const f16x8*>(sb + (wm * (BM / 2) + 32 * i) * 128 + off);
 #pragma unroll
-      for (int j = 0; j < TN; ++j) fa[j] = *reinterpret_cast<const f16x8*>(sa + (wn * (BN / 2) + 32 * j) * 128 + off);
+      for (int j = 0; j < TN; ++j) fa[u][j] = *reinterpret_cast<const f16x8*>(sa + (wn * (BN / 2) + 32 * j) * 128 + off);
+    }
+#pragma unroll
+    for (int u = 0; u < SPW; ++u)
 #pragma unroll
       for (int i = 0; i < TM; ++i)
 #pragma unroll
-        for (int j = 0; j < TN; ++j) acc[i][j] = __builtin_amdgcn_mfma_f32_32x32x16_f16(fa[j], fb[i], acc[i][j], 0, 0, 0);
-    }
+        for (int j = 0; j < TN; ++j)
+          acc[u % NACC][i][j] = __builtin_amdgcn_mfma_f32_32x32x16_f16(fa[u][j], fb[u][i], acc[u % NACC][i][j], 0, 0, 0);
   };
 
+  static_assert(NSTAGE == 4, "the waits below assume three stages in flight");
   if (nk > 0) issue(0);
   if (nk > 1) issue(1);
+  if (nk > 2) issue(2);
+  YM_STAMP(1);
   for (int it = 0; it < nk; ++it) {
-    if (it + 1 < nk) wait_vm<NL>(); else wait_vm<0>();
+    // stage it is complete when at most the stages issued after it are outstanding (loads retire in order)
+    if (it + 2 < nk) wait_vm<2 * NL>();
+    else if (it + 1 < nk) wait_vm<NL>();
+    else wait_vm<0>();
+    YM_STAMP(8 + 4 * (it & 63));
     raw_barrier();  // stage it is in LDS for every wave; every wave is done reading stage it-1's slot
-    if (it + 2 < nk) issue((it + 2) % NSTAGE);
+    YM_STAMP(9 + 4 * (it & 63));
+    if (it + 3 < nk) issue((it + 3) % NSTAGE);
+    YM_STAMP(10 + 4 * (it & 63));
     compute(it % NSTAGE);
+    YM_STAMP(11 + 4 * (it & 63));
   }
-
-  // ---- split-K: publish the partial tile, the last arriver reduces
-  if constexpr (SPLIT > 1) {
-    const int tile = tm * a.tiles_n + tn;
-    float* slab = a.slab + (size_t)(tile * SPLIT + sp) * (256 * NREG);
+  YM_STAMP(2);
+  if constexpr (NACC == 2) {
 #pragma unroll
     for (int i = 0; i < TM; ++i)
 #pragma unroll
-      for (int j = 0; j < TN; ++j)
+      for (int j = 0; j < TN; ++j) acc[0][i][j] += acc[1][i][j];
+  }
+  // ---- wave groups 1..KG-1 hand their partial tiles to group 0 through the (now idle) stage ring
+  if constexpr (KG > 1) {
+    static_assert(NSTAGE * SB >= (KG - 1) * 4 * NREG * 64 * 4, "reduction area exceeds the ring");
+    float* red = reinterpret_cast<float*>(smem);  // [(kg-1)][wq][NREG][64]
+    __syncthreads();                              // every wave is past its last ds_read of the ring
+    if (kg > 0) {
+      float* d = red + ((size_t)((kg - 1) * 4 + wq) * NREG) * 64 + lane;
 #pragma unroll
-        for (int q = 0; q < 4; ++q) {
-          const int qq = (i * TN + j) * 4 + q;
-          *reinterpret_cast<f32x4*>(slab + ((size_t)qq * 256 + tid) * 4) =
-              f32x4{acc[i][j][4 * q], acc[i][j][4 * q + 1], acc[i][j][4 * q + 2], acc[i][j][4 * q + 3]};
-        }
-    asm volatile("s_waitcnt vmcnt(0)" ::: "memory");
-    __syncthreads();
-    int* flag = reinterpret_cast<int*>(smem + NSTAGE * SB);
-    if (tid == 0) {
-      __builtin_amdgcn_fence(__ATOMIC_RELEASE, "agent");
-      asm volatile("s_waitcnt vmcnt(0)" ::: "memory");
-      const int t = __hip_atomic_fetch_add(a.cnt + tile, 1, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
-      const int last = t == SPLIT - 1;
-      if (last) {
-        __hip_atomic_store(a.cnt + tile, 0, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
-        __builtin_amdgcn_fence(__ATOMIC_ACQUIRE, "agent");
-        asm volatile("s_waitcnt vmcnt(0)" ::: "memory");
-      }
-      *flag = last;
+      for (int i = 0; i < TM; ++i)
+#pragma unroll
+        for (int j = 0; j < TN; ++j)
+#pragma unroll
+          for (int r = 0; r < 16; ++r) d[((i * TN + j) * 16 + r) * 64] = acc[0][i][j][r];
     }
     __syncthreads();
-    if (!*flag) return;
-    // sum every slab (this workgroup's own included) in split order, so the result does not depend on which split
-    // arrived last: bitwise-reproducible launches
+    if (kg == 0) {
 #pragma unroll
-    for (int i = 0; i < TM; ++i)
+      for (int g = 1; g < KG; ++g) {
+        const float* q = red + ((size_t)((g - 1) * 4 + wq) * NREG) * 64 + lane;
 #pragma unroll
-      for (int j = 0; j < TN; ++j)
+        for (int i = 0; i < TM; ++i)
 #pragma unroll
-        for (int r = 0; r < 16; ++r) acc[i][j][r] = 0.f;
-#pragma unroll 1
-    for (int s2 = 0; s2 < SPLIT; ++s2) {
-      const float* o = a.slab + (size_t)(tile * SPLIT + s2) * (256 * NREG);
+          for (int j = 0; j < TN; ++j)
+#pragma unroll
+            for (int r = 0; r < 16; ++r) acc[0][i][j][r] += q[((i * TN + j) * 16 + r) * 64];
+      }
+    }
+  }
+
+  // ---- split-K: publish the partial tile write-through, the last arriver reduces (wave group 0 only holds the
+  // tile; every thread still takes part in the workgroup barriers)
+  if constexpr (SPLIT > 1) {
+    const int tile = tm * a.tiles_n + tn;
+    const __amdgpu_buffer_rsrc_t rsl =
+        __builtin_amdgcn_make_buffer_rsrc(a.slab, 0, (int)(a.slab_cap < 0x7FFFFFF0L ? a.slab_cap : 0x7FFFFFF0L),
+                                          0x00020000);
+    constexpr int SC1 = 16;  // cache-policy aux bit: sc1 (write-through stores / L1-bypassing loads)
+    const unsigned mine = (unsigned)(tile * SPLIT + sp) * (256u * NREG * 4u);
+    if (kg == 0) {
 #pragma unroll
       for (int i = 0; i < TM; ++i)
 #pragma unroll
@@ -251,62 +370,97 @@ __global__ __launch_bounds__(256) void conv_dma(const ConvArgs a) {
 #pragma unroll
           for (int q = 0; q < 4; ++q) {
             const int qq = (i * TN + j) * 4 + q;
-            const f32x4 v = *reinterpret_cast<const f32x4*>(o + ((size_t)qq * 256 + tid) * 4);
-#pragma unroll
-            for (int e = 0; e < 4; ++e) acc[i][j][4 * q + e] += v[e];
+            const f32x4 v{acc[0][i][j][4 * q], acc[0][i][j][4 * q + 1], acc[0][i][j][4 * q + 2],
+                          acc[0][i][j][4 * q + 3]};
+            __builtin_amdgcn_raw_buffer_store_b128(__builtin_bit_cast(u32x4, v), rsl,
+                                                   mine + (qq * 256u + tid) * 16u, 0, SC1);
           }
+      asm volatile("s_waitcnt vmcnt(0)" ::: "memory");  // every storing wave drains its sc1 stores
     }
+    __syncthreads();
+    int* flag = reinterpret_cast<int*>(smem + NSTAGE * SB);
+    if (tid == 0) {
+      const int t = __hip_atomic_fetch_add(a.cnt + tile, 1, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
+      const int last = t == SPLIT - 1;
+      if (last) __hip_atomic_store(a.cnt + tile, 0, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
+      *flag = last;
+    }
+    __syncthreads();
+    if (!*flag || kg != 0) return;
+    __builtin_amdgcn_fence(__ATOMIC_ACQUIRE, "wavefront");  // no instruction: keeps the sc1 loads below the ticket
+    // sum every slab (this workgroup's own included) in split order — bitwise-reproducible whichever split arrived
+    // last; all slabs' loads are issued together (one memory latency, not SPLIT)
+    f32x4 part[SPLIT][TM * TN * 4];
+#pragma unroll
+    for (int s2 = 0; s2 < SPLIT; ++s2) {
+      const unsigned o = (unsigned)(tile * SPLIT + s2) * (256u * NREG * 4u);
+#pragma unroll
+      for (int qq = 0; qq < TM * TN * 4; ++qq)
+        part[s2][qq] = __builtin_bit_cast(f32x4, __builtin_amdgcn_raw_buffer_load_b128(rsl, o + (qq * 256u + tid) * 16u,
+                                                                                       0, SC1));
+    }
+#pragma unroll
+    for (int i = 0; i < TM; ++i)
+#pragma unroll
+      for (int j = 0; j < TN; ++j)
+#pragma unroll
+        for (int q = 0; q < 4; ++q) {
+          const int qq = (i * TN + j) * 4 + q;
+          f32x4 v = part[0][qq];
+#pragma unroll
+          for (int s2 = 1; s2 < SPLIT; ++s2) v += part[s2][qq];
+#pragma unroll
+          for (int e = 0; e < 4; ++e) acc[0][i][j][4 * q + e] = v[e];
+        }
   }
+  if (kg != 0) return;
 
   // ---- epilogue: lane owns channels nb + 32j + 8q + 4h + {0..3} of pixel pbm + 32i + l32
   OutT* dst = static_cast<OutT*>(a.dst);
-  const f16* res = static_cast<const f16*>(a.res);
 #pragma unroll
   for (int i = 0; i < TM; ++i) {
-    const int m = tm * BM + wm * (BM / 2) + 32 * i + l32;
-    if (m >= a.M) continue;
-    const int b = m / HWo, rem = m - (m / HWo) * HWo;
-    const int oy = rem / a.Wo, ox = rem - (rem / a.Wo) * a.Wo;
-    const int pix = a.shuffle ? (2 * oy) * a.d_W + 2 * ox : oy * a.d_W + ox;
-    const size_t obase = (size_t)(b * a.d_P + a.d_pixoff + pix) * a.d_ctot + a.d_coff;
-    const size_t rbase = res ? (size_t)(b * a.r_P + oy * a.Wo + ox) * a.r_ctot + a.r_coff : 0;
+    if (ep_m[i] >= a.M) continue;
 #pragma unroll
     for (int j = 0; j < TN; ++j)
 #pragma unroll
       for (int q = 0; q < 4; ++q) {
         const int n = tn * BN + wn * (BN / 2) + 32 * j + 8 * q + 4 * h;
         if (n >= a.N) continue;
-        const f32x4 b4 = *reinterpret_cast<const f32x4*>(a.bias + n);
         float v[4];
 #pragma unroll
         for (int e = 0; e < 4; ++e) {
-          const float x = acc[i][j][4 * q + e] + b4[e];
-          v[e] = a.act ? ym_silu(x) : x;
-        }
-        if (res) {
-          const f16x4 r4 = *reinterpret_cast<const f16x4*>(res + rbase + n);
-#pragma unroll
-          for (int e = 0; e < 4; ++e) v[e] += (float)r4[e];
+          const float x = acc[0][i][j][4 * q + e] + bias4[j][q][e];
+          v[e] = (a.act ? ym_silu_fast(x) : x) + (float)res4[i][j][q][e];
         }
         if (a.shuffle) {
           const int sub = n / a.npr;
           const int ch = n - sub * a.npr;
-          Store4<OutT>::st(dst + obase + (size_t)((sub >> 1) * a.d_W + (sub & 1)) * a.d_ctot + ch, v);
+          Store4<OutT>::st(dst + ep_obase[i] + (size_t)((sub >> 1) * a.d_W + (sub & 1)) * a.d_ctot + ch, v);
         } else {
-          Store4<OutT>::st(dst + obase + n, v);
+          Store4<OutT>::st(dst + ep_obase[i] + n, v);
         }
       }
   }
+  YM_STAMP(3);
 }
 
 struct DmaCfg {
-  int bm, bn, split;
+  int bm, bn, split, kg;
 };
-constexpr DmaCfg kDma[] = {{64, 64, 1}, {64, 64, 2}, {64, 64, 4}, {64, 64, 8}, {128, 64, 1}, {128, 64, 2},
-                           {128, 64, 4}, {64, 128, 1}, {64, 128, 2}, {64, 128, 4}, {128, 128, 1}, {128, 128, 2}};
+// (ids 17 + i in the conv config space of csrc/ym_conv.hip)
+#define YM_DMA_CFGS(X)                                                                                   \
+  X(0, 64, 64, 1, 1) X(1, 64, 64, 2, 1) X(2, 64, 64, 4, 1) X(3, 64, 64, 8, 1) X(4, 128, 64, 1, 1)     \
+  X(5, 128, 64, 2, 1) X(6, 128, 64, 4, 1) X(7, 64, 128, 1, 1) X(8, 64, 128, 2, 1) X(9, 64, 128, 4, 1) \
+  X(10, 128, 128, 1, 1) X(11, 128, 128, 2, 1) X(12, 64, 64, 1, 2) X(13, 64, 64, 2, 2)                  \
+  X(14, 64, 64, 4, 2) X(15, 128, 64, 1, 2) X(16, 64, 128, 1, 2) X(17, 128, 128, 1, 2)
+constexpr DmaCfg kDma[] = {
+#define YM_X(id, bm, bn, sp, kg) {bm, bn, sp, kg},
+    YM_DMA_CFGS(YM_X)
+#undef YM_X
+};
 constexpr int kNumDma = sizeof(kDma) / sizeof(kDma[0]);
 
-template <typename OutT, int BM, int BN, int SPLIT>
+template <typename OutT, int BM, int BN, int SPLIT, int KG>
 hipError_t launch_dma(ConvArgs a, int kind, hipStream_t st) {
   const int tiles_m8 = ((a.M + BM - 1) / BM + 7) / 8 * 8;
   a.tiles_n = (a.N + BN - 1) / BN;
@@ -315,29 +469,27 @@ hipError_t launch_dma(ConvArgs a, int kind, hipStream_t st) {
     if (tiles > a.cnt_cap || tiles * SPLIT * BM * BN * 4 > a.slab_cap) return hipErrorInvalidValue;
     if (a.Kpad / DK < SPLIT) return hipErrorInvalidValue;
   }
-  const dim3 grid(tiles_m8 * a.tiles_n * SPLIT);
-  if (kind == 1)
-    hipLaunchKernelGGL((conv_dma<OutT, BM, BN, 1, SPLIT>), grid, dim3(256), 0, st, a);
-  else
-    hipLaunchKernelGGL((conv_dma<OutT, BM, BN, 3, SPLIT>), grid, dim3(256), 0, st, a);
+  const dim3 grid(tiles_m8 * a.tiles_n * SPLIT), block(256 * KG);
+  if (kind == 1) {
+    hipLaunchKernelGGL((conv_dma<OutT, BM, BN, 1, SPLIT, KG>), grid, block, 0, st, a);
+  } else if constexpr (sizeof(OutT) == 2) {  // fp32 outputs exist only for the Detect head's 1x1 convs
+    if (kind == 4)
+      hipLaunchKernelGGL((conv_dma<OutT, BM, BN, 4, SPLIT, KG>), grid, block, 0, st, a);
+    else
+      hipLaunchKernelGGL((conv_dma<OutT, BM, BN, 3, SPLIT, KG>), grid, block, 0, st, a);
+  } else {
+    return hipErrorInvalidValue;
+  }
   return hipGetLastError();
 }
 
 template <typename OutT>
 hipError_t dispatch(const ConvArgs& a, int kind, int i, hipStream_t st) {
   switch (i) {
-    case 0: return launch_dma<OutT, 64, 64, 1>(a, kind, st);
-    case 1: return launch_dma<OutT, 64, 64, 2>(a, kind, st);
-    case 2: return launch_dma<OutT, 64, 64, 4>(a, kind, st);
-    case 3: return launch_dma<OutT, 64, 64, 8>(a, kind, st);
-    case 4: return launch_dma<OutT, 128, 64, 1>(a, kind, st);
-    case 5: return launch_dma<OutT, 128, 64, 2>(a, kind, st);
-    case 6: return launch_dma<OutT, 128, 64, 4>(a, kind, st);
-    case 7: return launch_dma<OutT, 64, 128, 1>(a, kind, st);
-    case 8: return launch_dma<OutT, 64, 128, 2>(a, kind, st);
-    case 9: return launch_dma<OutT, 64, 128, 4>(a, kind, st);
-    case 10: return launch_dma<OutT, 128, 128, 1>(a, kind, st);
-    case 11: return launch_dma<OutT, 128, 128, 2>(a, kind, st);
+#define YM_X(id, bm, bn, sp, kg) \
+  case id: return launch_dma<OutT, bm, bn, sp, kg>(a, kind, st);
+    YM_DMA_CFGS(YM_X)
+#undef YM_X
   }
   return hipErrorInvalidValue;
 }
@@ -352,7 +504,7 @@ hipError_t ym_launch_conv_dma(int out_f32, const ConvArgs& a, int i, hipStream_t
   if (i < 0 || i >= kNumDma) return hipErrorInvalidValue;
   int kind;
   if (a.k == 1 && a.s == 1) kind = 1;
-  else if (a.k == 3) kind = 3;
+  else if (a.k == 3) kind = a.Cin8 % 8 == 0 ? 4 : 3;
   else return hipErrorInvalidValue;
   if (a.Kpad % DK || !a.src0 || a.nchw) return hipErrorInvalidValue;
   if (kind == 1 && a.src1 && a.C0 % DK) return hipErrorInvalidValue;

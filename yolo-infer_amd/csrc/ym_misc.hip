@@ -40,13 +40,12 @@ __global__ __launch_bounds__(256) void max_reduce(const float* __restrict__ x, l
 }
 
 // ------------------------------------------------------------------------------------------------- depthwise 3x3
-// DWConv(c, c, 3) = Conv(g=c): 3x3, stride 1, pad 1, BN folded, SiLU.  One thread = 8 channels of one pixel;
-// the workgroup's [9][C] weights and bias are staged once in LDS.
+// DWConv(c, c, 3) = Conv(g=c): 3x3, stride 1, pad 1, BN folded, SiLU.  One thread = 8 channels of one pixel.
+// Every load a thread needs (9 taps x 16 B of activations, 9 x 2 float4 of weights + 2 of bias, the weights L1/L2-
+// resident) is independent and issued up front: one memory latency per thread, no LDS staging loop (a strided
+// staging loop of 10·C floats was ~10 dependent global round trips for C = 512).
 template <typename T>
 __global__ __launch_bounds__(256) void dwconv3x3(const DwArgs a) {
-  extern __shared__ float wl[];  // [9*C] weights, then [C] bias
-  for (int i = threadIdx.x; i < 10 * a.C; i += 256) wl[i] = i < 9 * a.C ? a.w[i] : a.bias[i - 9 * a.C];
-  __syncthreads();
   const int C8 = a.C >> 3;
   const long idx = blockIdx.x * (long)blockDim.x + threadIdx.x;
   const long total = (long)a.B * a.H * a.W * C8;
@@ -58,25 +57,27 @@ __global__ __launch_bounds__(256) void dwconv3x3(const DwArgs a) {
   const int p = pix - (long)b * HW;
   const int y = p / a.W, x = p - (p / a.W) * a.W;
   const int c0 = cg * 8;
-  float acc[8];
-#pragma unroll
-  for (int e = 0; e < 8; ++e) acc[e] = wl[9 * a.C + c0 + e];
   const T* src = static_cast<const T*>(a.src);
+  typename Vec8<T>::type v[9];
 #pragma unroll
-  for (int ky = 0; ky < 3; ++ky) {
-    const int iy = y + ky - 1;
-    if ((unsigned)iy >= (unsigned)a.H) continue;
-#pragma unroll
-    for (int kx = 0; kx < 3; ++kx) {
-      const int ix = x + kx - 1;
-      if ((unsigned)ix >= (unsigned)a.W) continue;
-      const typename Vec8<T>::type v =
-          Vec8<T>::load(src + (size_t)(b * a.s_P + iy * a.W + ix) * a.s_ctot + a.s_coff + c0);
-      const float* wr = wl + (ky * 3 + kx) * a.C + c0;
-#pragma unroll
-      for (int e = 0; e < 8; ++e) acc[e] = fmaf((float)v[e], wr[e], acc[e]);
-    }
+  for (int t = 0; t < 9; ++t) {
+    const int iy = y + t / 3 - 1, ix = x + t % 3 - 1;
+    v[t] = ((unsigned)iy < (unsigned)a.H && (unsigned)ix < (unsigned)a.W)
+               ? Vec8<T>::load(src + (size_t)(b * a.s_P + iy * a.W + ix) * a.s_ctot + a.s_coff + c0)
+               : Vec8<T>::zero();
   }
+  f32x4 w[9][2];
+#pragma unroll
+  for (int t = 0; t < 9; ++t) {
+    w[t][0] = *reinterpret_cast<const f32x4*>(a.w + t * a.C + c0);
+    w[t][1] = *reinterpret_cast<const f32x4*>(a.w + t * a.C + c0 + 4);
+  }
+  const f32x4 b0 = *reinterpret_cast<const f32x4*>(a.bias + c0), b1 = *reinterpret_cast<const f32x4*>(a.bias + c0 + 4);
+  float acc[8] = {b0[0], b0[1], b0[2], b0[3], b1[0], b1[1], b1[2], b1[3]};
+#pragma unroll
+  for (int t = 0; t < 9; ++t)
+#pragma unroll
+    for (int e = 0; e < 8; ++e) acc[e] = fmaf((float)v[t][e], w[t][e >> 2][e & 3], acc[e]);
   typename Vec8<T>::type o;
 #pragma unroll
   for (int e = 0; e < 8; ++e) o[e] = (T)(a.act ? ym_silu(acc[e]) : acc[e]);
@@ -545,9 +546,9 @@ hipError_t ym_launch_prep(int dtype, const PrepArgs& a, int* counts, int B, hipS
 hipError_t ym_launch_dwconv(int dtype, const DwArgs& a, hipStream_t st) {
   const long total = (long)a.B * a.H * a.W * (a.C / 8);
   const dim3 g((total + 255) / 256);
-  const size_t lds = (size_t)10 * a.C * sizeof(float);
-  if (dtype == YM_DT_F16) hipLaunchKernelGGL(dwconv3x3<f16>, g, dim3(256), lds, st, a);
-  else hipLaunchKernelGGL(dwconv3x3<float>, g, dim3(256), lds, st, a);
+  if (a.C % 8) return hipErrorInvalidValue;
+  if (dtype == YM_DT_F16) hipLaunchKernelGGL(dwconv3x3<f16>, g, dim3(256), 0, st, a);
+  else hipLaunchKernelGGL(dwconv3x3<float>, g, dim3(256), 0, st, a);
   return hipGetLastError();
 }
 

@@ -38,6 +38,7 @@ int fail(int code, const char* fmt, ...) {
 constexpr int32_t kMagic = 0x4C504D59;  // 'YMPL'
 constexpr int kHdr = 32, kBufRec = 8, kOpRec = 32, kNameLen = 48;
 constexpr int kSplitCounters = 16384;  // split-K tiles per conv launch (csrc/ym_conv_dma.hip)
+constexpr int kMaxLanes = 4;           // concurrent batch slices in one forward graph (<= GPU_MAX_HW_QUEUES)
 
 enum OpKind { OP_INPUT = 1, OP_CONV = 2, OP_DW = 3, OP_SPPF = 4, OP_ATTN = 5, OP_DECODE = 6, OP_NMS = 7 };
 
@@ -90,6 +91,11 @@ struct ym_ctx {
   int A = 0, kstride = 0;
   int lvl_W[4] = {0}, lvl_off[4] = {0};
   hipStream_t cap_stream = nullptr;
+  // lanes: the batch is cut into image slices whose op chains are captured as parallel branches of one graph, so
+  // the fixed per-launch latency of one slice's small kernels overlaps the other slices' work
+  hipStream_t lane_streams[kMaxLanes] = {};
+  hipEvent_t fork_ev = nullptr, join_ev[kMaxLanes] = {};
+  int lane = 0, lane_img0 = 0;  // lane / first image of the ops being launched
   std::vector<GraphEntry> graphs;
   std::vector<hipEvent_t> prof_events;
   // per-shape, per-op conv tile configuration (-1 = heuristic); set by ym_tune / ym_set_op_cfg
@@ -124,6 +130,11 @@ struct ym_ctx {
     if (d_arena) (void)hipFree(d_arena);
     if (d_weights) (void)hipFree(d_weights);
     if (cap_stream) (void)hipStreamDestroy(cap_stream);
+    for (int l = 0; l < kMaxLanes; ++l) {
+      if (lane_streams[l]) (void)hipStreamDestroy(lane_streams[l]);
+      if (join_ev[l]) (void)hipEventDestroy(join_ev[l]);
+    }
+    if (fork_ev) (void)hipEventDestroy(fork_ev);
   }
   void clear_graphs() {
     for (auto& g : graphs) {
@@ -140,7 +151,13 @@ struct ym_ctx {
   int buf_H(int b) const { return bufs[b].f == 0 ? 1 : cH / bufs[b].f; }
   int buf_Wd(int b) const { return bufs[b].f == 0 ? A : cW / bufs[b].f; }
   int elem(int b) const { return (bufs[b].f32 || dtype == YM_DT_F32) ? 4 : 2; }
-  void* bptr(int b) const { return d_arena + buf_off[b]; }
+  // buffer b of the current lane: its image slice of the whole-batch buffer (all buffers are image-major)
+  void* bptr(int b) const {
+    return d_arena + buf_off[b] + (size_t)lane_img0 * buf_P(b) * bufs[b].C * elem(b);
+  }
+  template <typename T> T* scratch(size_t off, size_t per_image_bytes) const {
+    return reinterpret_cast<T*>(d_arena + off + (size_t)lane_img0 * per_image_bytes);
+  }
 };
 
 namespace {
@@ -184,9 +201,9 @@ int ensure_workspace(ym_ctx* c, int B, int H, int W) {
   c->off_sareas = off; off = align_up(off + BA * 4, 256);
   c->off_sup = off;    off = align_up(off + BA, 256);
   // split-K workspace of the LDS-DMA conv kernels: fp32 partial tiles + per-tile arrival counters
-  c->slab_bytes = std::max<size_t>(32u << 20, (size_t)nB << 22);
-  c->off_slab = off;   off = align_up(off + c->slab_bytes, 256);
-  c->off_cnt = off;    off = align_up(off + (size_t)kSplitCounters * 4, 256);
+  c->slab_bytes = std::min<size_t>(std::max<size_t>(32u << 20, (size_t)nB << 22), 1u << 30);
+  c->off_slab = off;   off = align_up(off + kMaxLanes * c->slab_bytes, 256);  // one slab region per lane
+  c->off_cnt = off;    off = align_up(off + (size_t)kMaxLanes * kSplitCounters * 4, 256);
   c->arena_bytes = off;
   hipError_t e = hipMalloc(&c->d_arena, off);
   if (e != hipSuccess) {
@@ -249,12 +266,14 @@ int conv_args(ym_ctx* c, const Op& op, int B, const float* d_in, float in_eps, C
       }
       if (br >= 0) { a.res = c->bptr(br); a.r_ctot = c->bufs[br].C; a.r_coff = r[18]; a.r_P = c->buf_P(br); }
       a.M = B * a.Ho * a.Wo;
+      a.fd_hw = ym_fdiv(a.Ho * a.Wo);
+      a.fd_w = ym_fdiv(a.Wo);
       out_f32 = c->bufs[bd].f32 && c->dtype == YM_DT_F16;
       a.s0_elems = (b0 == c->input_buf) ? 0 : (long)c->cB * c->buf_P(b0) * c->bufs[b0].C;
       a.s1_elems = b1 >= 0 ? (long)c->cB * c->buf_P(b1) * c->bufs[b1].C : 0;
-      a.slab = reinterpret_cast<float*>(c->d_arena + c->off_slab);
+      a.slab = reinterpret_cast<float*>(c->d_arena + c->off_slab + (size_t)c->lane * c->slab_bytes);
       a.slab_cap = (long)c->slab_bytes;
-      a.cnt = reinterpret_cast<int*>(c->d_arena + c->off_cnt);
+      a.cnt = reinterpret_cast<int*>(c->d_arena + c->off_cnt) + (size_t)c->lane * kSplitCounters;
       a.cnt_cap = kSplitCounters;
       return YM_OK;
 }
@@ -273,7 +292,7 @@ int launch_op(ym_ctx* c, const Op& op, int B, const float* d_in, const ym_infer_
       a.B = B; a.C = 3; a.H = c->cH; a.W = c->cW;
       a.eps = args->in_eps;
       a.cnt = reinterpret_cast<int*>(c->d_arena + c->off_cnt);
-      a.cnt_len = kSplitCounters;
+      a.cnt_len = kMaxLanes * kSplitCounters;
       e = ym_launch_prep(dt, a, reinterpret_cast<int*>(c->d_arena + c->off_counts), B, st);
       break;
     }
@@ -321,11 +340,11 @@ int launch_op(ym_ctx* c, const Op& op, int B, const float* d_in, const ym_infer_
       DecodeArgs a{};
       a.anchors = reinterpret_cast<const float*>(c->bptr(c->anchor_buf));
       a.no_tot = c->bufs[c->anchor_buf].C;
-      a.boxes = reinterpret_cast<float4*>(c->d_arena + c->off_boxes);
-      a.scores = reinterpret_cast<float*>(c->d_arena + c->off_scores);
-      a.cls = reinterpret_cast<int*>(c->d_arena + c->off_cls);
-      a.keys = reinterpret_cast<unsigned long long*>(c->d_arena + c->off_keys);
-      a.counts = reinterpret_cast<int*>(c->d_arena + c->off_counts);
+      a.boxes = c->scratch<float4>(c->off_boxes, (size_t)c->A * 16);
+      a.scores = c->scratch<float>(c->off_scores, (size_t)c->A * 4);
+      a.cls = c->scratch<int>(c->off_cls, (size_t)c->A * 4);
+      a.keys = c->scratch<unsigned long long>(c->off_keys, (size_t)c->kstride * 8);
+      a.counts = c->scratch<int>(c->off_counts, 4);
       a.A = c->A; a.kstride = c->kstride; a.nc = c->nc; a.reg_max = c->reg_max; a.B = B; a.nl = c->nl;
       for (int l = 0; l < c->nl; ++l) {
         a.lvl_W[l] = c->lvl_W[l]; a.lvl_off[l] = c->lvl_off[l]; a.lvl_stride[l] = (float)c->strides[l];
@@ -341,14 +360,14 @@ int launch_op(ym_ctx* c, const Op& op, int B, const float* d_in, const ym_infer_
       a.anchors = reinterpret_cast<const float*>(c->bptr(c->anchor_buf));
       a.no_tot = c->bufs[c->anchor_buf].C;
       a.mask_off = c->no;
-      a.boxes = reinterpret_cast<const float4*>(c->d_arena + c->off_boxes);
-      a.scores = reinterpret_cast<const float*>(c->d_arena + c->off_scores);
-      a.cls = reinterpret_cast<const int*>(c->d_arena + c->off_cls);
-      a.keys = reinterpret_cast<unsigned long long*>(c->d_arena + c->off_keys);
-      a.counts = reinterpret_cast<const int*>(c->d_arena + c->off_counts);
-      a.sboxes = reinterpret_cast<float4*>(c->d_arena + c->off_sboxes);
-      a.sareas = reinterpret_cast<float*>(c->d_arena + c->off_sareas);
-      a.sup = reinterpret_cast<unsigned char*>(c->d_arena + c->off_sup);
+      a.boxes = c->scratch<const float4>(c->off_boxes, (size_t)c->A * 16);
+      a.scores = c->scratch<const float>(c->off_scores, (size_t)c->A * 4);
+      a.cls = c->scratch<const int>(c->off_cls, (size_t)c->A * 4);
+      a.keys = c->scratch<unsigned long long>(c->off_keys, (size_t)c->kstride * 8);
+      a.counts = c->scratch<const int>(c->off_counts, 4);
+      a.sboxes = c->scratch<float4>(c->off_sboxes, (size_t)c->A * 16);
+      a.sareas = c->scratch<float>(c->off_sareas, (size_t)c->A * 4);
+      a.sup = c->scratch<unsigned char>(c->off_sup, (size_t)c->A);
       a.dets = d_dets;
       a.out_counts = d_counts;
       a.A = c->A; a.kstride = c->kstride; a.nm = c->nm; a.max_det = args->max_det; a.max_nms = args->max_nms;
@@ -395,9 +414,12 @@ int ym_create(int device, const ym_model_desc* desc, ym_ctx** out) {
   c->device = device;
   if (desc) c->desc = *desc;
   hipError_t e = hipStreamCreateWithFlags(&c->cap_stream, hipStreamNonBlocking);
+  for (int l = 1; l < kMaxLanes && e == hipSuccess; ++l) e = hipStreamCreateWithFlags(&c->lane_streams[l], hipStreamNonBlocking);
+  if (e == hipSuccess) e = hipEventCreateWithFlags(&c->fork_ev, hipEventDisableTiming);
+  for (int l = 1; l < kMaxLanes && e == hipSuccess; ++l) e = hipEventCreateWithFlags(&c->join_ev[l], hipEventDisableTiming);
   if (e != hipSuccess) {
     delete c;
-    return fail(YM_EHIP, "hipStreamCreate: %s", hipGetErrorString(e));
+    return fail(YM_EHIP, "hipStreamCreate/hipEventCreate: %s", hipGetErrorString(e));
   }
   *out = c;
   return YM_OK;
@@ -443,6 +465,51 @@ int ym_load_weights(ym_ctx* c, const void* blob, size_t bytes) {
   return YM_OK;
 }
 
+// Lane split of a B-image batch: L = clamp(args->lanes, 1, kMaxLanes) slices of ceil(B / L) images (0 = 1 lane).
+static void lane_split(const ym_infer_args* args, int B, int& L, int& Bl) {
+  L = args->lanes < 1 ? 1 : (args->lanes > kMaxLanes ? kMaxLanes : args->lanes);
+  if (L > B) L = B;
+  Bl = (B + L - 1) / L;
+  L = (B + Bl - 1) / Bl;
+}
+
+// Launch one forward: the input statistics over the WHOLE batch (LoadTensor's /255 rule is a batch-wide max), then
+// every other op per lane on its image slice.  With fork/join events the lanes are parallel graph branches when
+// `st` is capturing; eagerly (no capture) they run on the lane streams concurrently as well.
+static int launch_forward(ym_ctx* c, const float* d_in, int B, const ym_infer_args* args, float* d_dets,
+                          int* d_counts, hipStream_t st) {
+  int L, Bl, rc;
+  lane_split(args, B, L, Bl);
+  c->lane = 0;
+  c->lane_img0 = 0;
+  size_t o = 0;
+  for (o = 0; o < c->ops.size() && c->ops[o].r[0] == OP_INPUT; ++o)
+    if ((rc = launch_op(c, c->ops[o], B, d_in, args, d_dets, d_counts, st))) return rc;
+  if (L > 1) HIPCK(hipEventRecord(c->fork_ev, st));
+  const size_t in_img = (size_t)3 * c->cH * c->cW, det_img = (size_t)args->max_det * (6 + c->nm);
+  for (int l = 0; l < L; ++l) {
+    hipStream_t ls = l == 0 ? st : c->lane_streams[l];
+    if (l > 0) HIPCK(hipStreamWaitEvent(ls, c->fork_ev, 0));
+    c->lane = l;
+    c->lane_img0 = l * Bl;
+    const int nb = B - l * Bl < Bl ? B - l * Bl : Bl;
+    for (size_t i = o; i < c->ops.size(); ++i) {
+      rc = launch_op(c, c->ops[i], nb, d_in + c->lane_img0 * in_img, args, d_dets + c->lane_img0 * det_img,
+                     d_counts + c->lane_img0, ls);
+      if (rc) {
+        c->lane = c->lane_img0 = 0;
+        return rc;
+      }
+    }
+    if (l > 0) {
+      HIPCK(hipEventRecord(c->join_ev[l], ls));
+      HIPCK(hipStreamWaitEvent(st, c->join_ev[l], 0));
+    }
+  }
+  c->lane = c->lane_img0 = 0;
+  return YM_OK;
+}
+
 int ym_infer(ym_ctx* c, const float* d_in, int B, int H, int W, const ym_infer_args* args, float* d_dets,
              int* d_counts, void* stream) {
   int rc = check_call(c, d_in, B, H, W, args, d_dets, d_counts);
@@ -451,11 +518,7 @@ int ym_infer(ym_ctx* c, const float* d_in, int B, int H, int W, const ym_infer_a
   hipStream_t st = static_cast<hipStream_t>(stream);
   rc = ensure_workspace(c, B, H, W);
   if (rc) return rc;
-  if (!args->use_graph) {
-    for (const Op& op : c->ops)
-      if ((rc = launch_op(c, op, B, d_in, args, d_dets, d_counts, st))) return rc;
-    return YM_OK;
-  }
+  if (!args->use_graph) return launch_forward(c, d_in, B, args, d_dets, d_counts, st);
   GraphKey key;
   memset(&key, 0, sizeof(key));
   key.B = B; key.H = H; key.W = W; key.in = d_in; key.dets = d_dets; key.counts = d_counts; key.args = *args;
@@ -469,15 +532,13 @@ int ym_infer(ym_ctx* c, const float* d_in, int B, int H, int W, const ym_infer_a
     (void)hipGraphDestroy(c->graphs.front().graph);
     c->graphs.erase(c->graphs.begin());
   }
-  // capture on the private stream (ordered after the caller's stream), replay on the caller's stream
+  // capture on the private stream (lane streams join through the fork event), replay on the caller's stream
   HIPCK(hipStreamBeginCapture(c->cap_stream, hipStreamCaptureModeRelaxed));
-  for (const Op& op : c->ops) {
-    if ((rc = launch_op(c, op, B, d_in, args, d_dets, d_counts, c->cap_stream))) {
-      hipGraph_t g = nullptr;
-      (void)hipStreamEndCapture(c->cap_stream, &g);
-      if (g) (void)hipGraphDestroy(g);
-      return rc;
-    }
+  if ((rc = launch_forward(c, d_in, B, args, d_dets, d_counts, c->cap_stream))) {
+    hipGraph_t g = nullptr;
+    (void)hipStreamEndCapture(c->cap_stream, &g);
+    if (g) (void)hipGraphDestroy(g);
+    return rc;
   }
   GraphEntry ge;
   ge.key = key;

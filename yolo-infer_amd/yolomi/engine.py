@@ -17,7 +17,7 @@ from .lib import Runtime
 from .plan import pack_graph
 
 # Bump when the meaning of a conv config index (csrc/ym_conv.hip kCfgs) changes: stale tables are then ignored.
-TUNE_VERSION = 3
+TUNE_VERSION = 4
 TUNED_DIR = os.path.join(os.path.dirname(os.path.abspath(__file__)), "tuned")  # committed tables
 
 
@@ -40,6 +40,9 @@ class Engine:
         # Per-shape conv tile tables: on the first call of each (B, H, W) a table is taken from the writable tune
         # cache or the committed `tuned/` directory; failing both, ym_tune measures one on this GPU (and caches it).
         self.autotune = os.environ.get("YM_AUTOTUNE", "1") != "0"
+        # Lanes: the batch runs as up to 4 concurrent image slices (parallel branches of one graph); conv tables are
+        # per slice batch.  Default from YM_LANES (1).
+        self.lanes = int(os.environ.get("YM_LANES", "1"))
         self._tuned = set()
         self.tune_source: Dict[tuple, str] = {}
 
@@ -89,18 +92,25 @@ class Engine:
             self._out[key] = (dets, counts)
         return self._out[key]
 
+    def lane_batch(self, B: int, lanes: Optional[int] = None) -> int:
+        """Images per lane (the batch every kernel sees) for a B-image call: ceil(B / clamp(lanes, 1, 4, B))."""
+        L = max(1, min(self.lanes if lanes is None else lanes, 4, B))
+        return -(-B // L)
+
     def run(self, x: torch.Tensor, conf=0.25, iou=0.7, max_det=300, classes: Optional[Sequence[int]] = None,
-            agnostic=False, in_eps=None, use_graph=True, max_nms=30000, max_wh=7680.0):
+            agnostic=False, in_eps=None, use_graph=True, max_nms=30000, max_wh=7680.0, lanes=None):
         """x: (B,3,H,W) float32 contiguous on this device. Returns the engine-owned (dets, counts) tensors."""
         assert x.is_cuda and x.dtype == torch.float32 and x.is_contiguous() and x.dim() == 4 and x.shape[1] == 3
         B, _, H, W = x.shape
         if in_eps is None:
             in_eps = torch.finfo(torch.float32).eps
-        args = Runtime.make_args(conf, iou, max_det, max_nms, agnostic, max_wh, in_eps, classes, use_graph)
+        lanes = self.lanes if lanes is None else lanes
+        args = Runtime.make_args(conf, iou, max_det, max_nms, agnostic, max_wh, in_eps, classes, use_graph, lanes)
         dets, counts = self.outputs(B, max_det)
         stream = torch.cuda.current_stream(self.device).cuda_stream
-        if (B, H, W) not in self._tuned:
-            self._prepare_shape(x, B, H, W, args, dets, counts, stream)
+        Bl = self.lane_batch(B, lanes)
+        if (Bl, H, W) not in self._tuned:
+            self._prepare_shape(x[:Bl], Bl, H, W, args, dets, counts, stream)
         self.rt.infer(x.data_ptr(), B, H, W, args, dets.data_ptr(), counts.data_ptr(), stream)
         return dets, counts
 

@@ -24,7 +24,8 @@ class ModelDesc(C.Structure):
 class InferArgs(C.Structure):
     _fields_ = [("conf", C.c_float), ("max_wh", C.c_float), ("iou", C.c_double), ("max_det", C.c_int),
                 ("max_nms", C.c_int), ("agnostic", C.c_int), ("in_eps", C.c_float), ("has_classes", C.c_int),
-                ("classes", C.c_uint32 * 4), ("use_graph", C.c_int), ("reserved", C.c_int * 7)]
+                ("classes", C.c_uint32 * 4), ("use_graph", C.c_int), ("lanes", C.c_int),
+                ("reserved", C.c_int * 6)]
 
 
 _lib = None
@@ -94,10 +95,11 @@ class Runtime:
 
     @staticmethod
     def make_args(conf=0.25, iou=0.7, max_det=300, max_nms=30000, agnostic=False, max_wh=7680.0, in_eps=1.1920929e-07,
-                  classes=None, use_graph=True) -> InferArgs:
+                  classes=None, use_graph=True, lanes=1) -> InferArgs:
         a = InferArgs()
         a.conf, a.iou, a.max_det, a.max_nms = float(conf), float(iou), int(max_det), int(max_nms)
         a.agnostic, a.max_wh, a.in_eps, a.use_graph = int(bool(agnostic)), float(max_wh), float(in_eps), int(use_graph)
+        a.lanes = int(lanes)
         if classes is not None:
             a.has_classes = 1
             for c in classes:
