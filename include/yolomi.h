@@ -102,6 +102,14 @@ int ym_buffer_info(ym_ctx* ctx, int buf, void** ptr, int* C, int* H, int* W, int
  * pointer); synchronous. */
 int ym_read_buffer(ym_ctx* ctx, int buf, void* dst, size_t bytes);
 
+/* Segment plans: instance masks of the detections of the last ym_infer (same B, H, W, stream order), i.e. Ultralytics
+ * `ops.process_mask(proto, coef, boxes, (H, W), upsample=True)` per image.  d_dets: the ym_infer output rows;
+ * d_offsets: B+1 device ints, offsets[b] = first mask of image b, offsets[B] = total (prefix of the kept counts);
+ * d_masks: total x H x W bytes (1 = inside the instance); d_nonempty: total ints, 1 when the mask has any pixel
+ * set (the predictor drops empty masks).  Asynchronous on `stream`. */
+int ym_masks(ym_ctx* ctx, const float* d_dets, int B, int max_det, const int* d_offsets, int total, int H, int W,
+             unsigned char* d_masks, int* d_nonempty, void* stream);
+
 int ym_sync(ym_ctx* ctx);
 const char* ym_last_error(void);
 void ym_destroy(ym_ctx* ctx);

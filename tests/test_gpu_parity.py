@@ -302,3 +302,41 @@ def test_lanes_keep_batch_wide_255_rule():
         rep = match_image(d1[i, :int(c1[i])].cpu().numpy(), d2[i, :int(c2[i])].cpu().numpy(), 0.1, 0.7, 1e-3, 1e-3,
                           rep=MatchReport())
         assert rep.ok, (i, rep)
+
+
+# ------------------------------------------------------------------------------------------------ segment masks
+def _box_iou(a, b):
+    lt = torch.maximum(a[:, None, :2], b[None, :, :2])
+    rb = torch.minimum(a[:, None, 2:4], b[None, :, 2:4])
+    inter = (rb - lt).clamp(min=0).prod(-1)
+    area = lambda t: (t[:, 2] - t[:, 0]) * (t[:, 3] - t[:, 1])
+    return inter / (area(a)[:, None] + area(b)[None] - inter)
+
+
+@pytest.mark.parametrize("dtype,agree,min_frac", [("f32", 0.999, 1.0), ("f16", 0.99, 0.9)])
+def test_segment_masks_match_oracle(dtype, agree, min_frac):
+    """process_mask(upsample=True) on the GPU vs the oracle (>= 99.9 % pixel agreement on matched
+    detections in parity mode); empty masks are dropped on both sides."""
+    x = make_input("uniform", (81, 82), 640)
+    ref = oracle("n", "segment").predict(x, conf=0.25)
+    res = model("n", dtype, "segment").predict(x.to(DEV), conf=0.25)
+    total = matched = 0
+    for r, g in zip(ref, res):
+        rb, gb = r["boxes"], g.boxes.data.cpu()
+        assert g.masks is not None and tuple(g.masks.data.shape) == (len(gb), 640, 640)
+        assert g.masks.data.dtype == torch.bool and bool(g.masks.data.flatten(1).any(1).all())
+        total += len(rb)
+        if not len(rb) or not len(gb):
+            continue
+        iou = _box_iou(rb[:, :4], gb[:, :4])
+        iou[rb[:, 5][:, None] != gb[:, 5][None, :]] = 0
+        used = set()
+        for i in torch.argsort(rb[:, 4], descending=True).tolist():
+            j = int(torch.argmax(iou[i]))
+            if iou[i, j] < 0.99 or j in used:
+                continue
+            used.add(j)
+            matched += 1
+            a = (r["masks"][i] == g.masks.data[j].cpu()).float().mean().item()
+            assert a >= agree, (i, j, a)
+    assert total > 0 and matched >= min_frac * total - 1, (matched, total)

@@ -177,11 +177,25 @@ class YOLO11Model:
                                in_eps=eps)
         B = im.shape[0]
         out = dets[:B].clone()
-        n = counts[:B].tolist()  # the one device→host sync of a predict call
+        n = counts[:B].tolist()  # the device→host sync of a predict call
+        names = self.model.names
+        if self.task != "segment":
+            dt = (time.perf_counter() - t0) * 1e3
+            speed = {"preprocess": 0.0, "inference": dt, "postprocess": 0.0}
+            return [Results(im[b], names, out[b, : n[b], :6], path=f"image{b}.jpg", speed=speed) for b in range(B)]
+        # Segment: process_mask(upsample=True) on the GPU, then the predictor keeps only non-empty masks
+        H, W = im.shape[2:]
+        masks, nonempty, offs = eng.masks(out, n, H, W)
+        keep = nonempty.tolist()
         dt = (time.perf_counter() - t0) * 1e3
         speed = {"preprocess": 0.0, "inference": dt, "postprocess": 0.0}
-        names = self.model.names
-        return [Results(im[b], names, out[b, : n[b], :6], path=f"image{b}.jpg", speed=speed) for b in range(B)]
+        res = []
+        for b in range(B):
+            idx = [i for i in range(n[b]) if keep[offs[b] + i]]
+            sel = torch.tensor(idx, dtype=torch.long, device=out.device)
+            res.append(Results(im[b], names, out[b].index_select(0, sel)[:, :6], path=f"image{b}.jpg", speed=speed,
+                               masks=masks[offs[b]:offs[b + 1]].index_select(0, sel).bool()))
+        return res
 
     def __call__(self, source, **kwargs):
         return self.predict(source, **kwargs)

@@ -132,6 +132,15 @@ struct PrepArgs {
   float eps;                   // LoadTensor rule: /255 when max > 1 + eps
 };
 
+struct MaskArgs {
+  const float* proto; int MH, MW, nm;   // (B, MH, MW, nm) fp32 NHWC prototypes of the last forward
+  const float* dets; int max_det, no;   // (B, max_det, no) rows [x1 y1 x2 y2 conf cls coef_0..coef_nm-1]
+  const int* offsets; int B, total;     // offsets[b] = first mask row of image b (prefix of kept counts)
+  float* lowres;                        // (total, MH, MW) cropped prototype-space masks
+  unsigned char* masks; int H, W;       // (total, H, W) 0/1 masks at input resolution
+  int* nonempty;                        // (total) 1 when any pixel of the mask is set
+};
+
 // ------------------------------------------------------------------------------------------------------------
 // Host-side launchers (defined in the .hip translation units).
 // cfg < 0: heuristic; strict: an inapplicable cfg is an error (else the heuristic runs)
@@ -147,3 +156,4 @@ hipError_t ym_launch_stem(int dtype, const ConvArgs& a, hipStream_t st);
 hipError_t ym_launch_spin(int usec, hipStream_t st);  // profiling: park the stream for usec (wall clock)
 hipError_t ym_launch_conv_dma(int out_f32, const ConvArgs& a, int i, hipStream_t st);  // f16 plans only
 int ym_conv_dma_num_cfgs();
+hipError_t ym_launch_masks(const MaskArgs& a, hipStream_t st);  // Segment: process_mask(upsample=True)

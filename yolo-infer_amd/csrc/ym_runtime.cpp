@@ -76,7 +76,9 @@ struct ym_ctx {
   // plan
   int dtype = YM_DT_F16, task = 0, nc = 80, nm = 0, reg_max = 16, nl = 3;
   int strides[4] = {8, 16, 32, 0};
-  int input_buf = -1, anchor_buf = -1, no = 0;
+  int input_buf = -1, anchor_buf = -1, proto_buf = -1, no = 0;
+  float* d_lowres = nullptr;  // Segment mask assembly scratch (ym_masks)
+  size_t lowres_bytes = 0;
   std::vector<BufDesc> bufs;
   std::vector<Op> ops;
   char* d_weights = nullptr;
@@ -129,6 +131,7 @@ struct ym_ctx {
     for (auto e : prof_events) (void)hipEventDestroy(e);
     if (d_arena) (void)hipFree(d_arena);
     if (d_weights) (void)hipFree(d_weights);
+    if (d_lowres) (void)hipFree(d_lowres);
     if (cap_stream) (void)hipStreamDestroy(cap_stream);
     for (int l = 0; l < kMaxLanes; ++l) {
       if (lane_streams[l]) (void)hipStreamDestroy(lane_streams[l]);
@@ -440,7 +443,8 @@ int ym_load_weights(ym_ctx* c, const void* blob, size_t bytes) {
   c->task = h[3]; c->nc = h[4]; c->nm = h[5]; c->reg_max = h[6]; c->nl = h[7];
   if (c->nl < 1 || c->nl > 4) return fail(YM_EBLOB, "bad level count");
   for (int l = 0; l < c->nl; ++l) c->strides[l] = h[8 + l];
-  c->input_buf = h[15]; c->anchor_buf = h[16]; c->no = h[18];
+  c->input_buf = h[15]; c->anchor_buf = h[16]; c->proto_buf = h[17]; c->no = h[18];
+  if (c->task == 1 && (c->proto_buf < 0 || c->proto_buf >= nbuf)) return fail(YM_EBLOB, "segment plan without proto buffer");
   const int32_t* bp = h + kHdr;
   c->bufs.resize(nbuf);
   for (int i = 0; i < nbuf; ++i) c->bufs[i] = BufDesc{bp[i * kBufRec], bp[i * kBufRec + 1], bp[i * kBufRec + 2]};
@@ -728,6 +732,39 @@ int ym_read_buffer(ym_ctx* c, int b, void* dst, size_t bytes) {
   HIPCK(hipSetDevice(c->device));
   HIPCK(hipDeviceSynchronize());
   HIPCK(hipMemcpy(dst, c->bptr(b), bytes, hipMemcpyDefault));
+  return YM_OK;
+}
+
+int ym_masks(ym_ctx* c, const float* d_dets, int B, int max_det, const int* d_offsets, int total, int H, int W,
+             unsigned char* d_masks, int* d_nonempty, void* stream) {
+  if (!c) return fail(YM_EINVAL, "null context");
+  if (c->task != 1 || c->proto_buf < 0) return fail(YM_ESTATE, "ym_masks needs a segment plan");
+  if (!c->d_arena || B > c->cB || H != c->cH || W != c->cW)
+    return fail(YM_ESTATE, "ym_masks must follow ym_infer of the same (B, H, W) (workspace %dx%dx%d)", c->cB, c->cH,
+                c->cW);
+  if (total < 0 || max_det < 1 || (total > 0 && (!d_dets || !d_offsets || !d_masks || !d_nonempty)))
+    return fail(YM_EINVAL, "bad ym_masks arguments");
+  if (total == 0) return YM_OK;
+  HIPCK(hipSetDevice(c->device));
+  const int MH = c->buf_H(c->proto_buf), MW = c->buf_Wd(c->proto_buf);
+  const size_t need = (size_t)total * MH * MW * sizeof(float);
+  if (need > c->lowres_bytes) {
+    if (c->d_lowres) HIPCK(hipFree(c->d_lowres));
+    c->d_lowres = nullptr;
+    hipError_t e = hipMalloc(&c->d_lowres, need);
+    if (e != hipSuccess) return fail(YM_ENOMEM, "mask scratch hipMalloc(%zu): %s", need, hipGetErrorString(e));
+    c->lowres_bytes = need;
+  }
+  MaskArgs a{};
+  a.proto = reinterpret_cast<const float*>(c->bptr(c->proto_buf));
+  a.MH = MH; a.MW = MW; a.nm = c->nm;
+  a.dets = d_dets; a.max_det = max_det; a.no = 6 + c->nm;
+  a.offsets = d_offsets; a.B = B; a.total = total;
+  a.lowres = c->d_lowres;
+  a.masks = d_masks; a.H = H; a.W = W;
+  a.nonempty = d_nonempty;
+  const hipError_t e = ym_launch_masks(a, static_cast<hipStream_t>(stream));
+  if (e != hipSuccess) return fail(YM_EHIP, "mask kernels: %s", hipGetErrorString(e));
   return YM_OK;
 }
 

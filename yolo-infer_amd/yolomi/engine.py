@@ -133,6 +133,23 @@ class Engine:
             self._prepare_shape(x, B, H, W, args, dets, counts, stream)
         return self.rt.profile_replay(x.data_ptr(), B, H, W, args, dets.data_ptr(), counts.data_ptr(), stream, reps)
 
+    def masks(self, dets: torch.Tensor, counts: Sequence[int], H: int, W: int):
+        """Segment plans: instance masks of the last run()'s detections (process_mask, upsample=True).  Returns the
+        (total, H, W) uint8 masks, the (total,) int32 non-empty flags and the per-image row offsets (host list)."""
+        B = len(counts)
+        offs = [0]
+        for n in counts:
+            offs.append(offs[-1] + int(n))
+        total = offs[-1]
+        masks = torch.empty((total, H, W), dtype=torch.uint8, device=self.device)
+        nonempty = torch.zeros((total,), dtype=torch.int32, device=self.device)
+        if total:
+            off_t = torch.tensor(offs, dtype=torch.int32).to(self.device, non_blocking=True)
+            stream = torch.cuda.current_stream(self.device).cuda_stream
+            self.rt.masks(dets.data_ptr(), B, dets.shape[1], off_t.data_ptr(), total, H, W, masks.data_ptr(),
+                          nonempty.data_ptr(), stream)
+        return masks, nonempty, offs
+
     def read_buffer(self, buf_id: int, B: int) -> torch.Tensor:
         """NHWC contents of plan buffer `buf_id` for the first B images (after run/profile), as a CPU float32 tensor."""
         _, C, H, W, eb = self.rt.buffer_info(buf_id)
