@@ -30,7 +30,8 @@ import torch  # noqa: E402
 import torch.distributed as dist  # noqa: E402
 
 METRIC = "images/sec @640×640 (1/2/4/8 MI355X) + mAP50-95 vs CPU ref"
-PEAK_TFLOPS = {"f16": 2500.0, "f32": 157.3}  # dense MFMA peaks (MI355X_MICROARCH.md)
+PEAK_TFLOPS = {"f16": 2500.0, "f32": 157.3, "i8": 5000.0}  # dense MFMA peaks (MI355X_MICROARCH.md; i8 = TOP/s)
+ACT_BYTES = {"f16": 2, "f32": 4, "i8": 1}
 PEAK_HBM_GBS = 8000.0
 
 
@@ -68,7 +69,7 @@ def conv_roofline(model, x, dtype, workload, reps=20):
     B, _, H, W = x.shape
     Bl = eng.lane_batch(B)  # every kernel of a lane sees Bl images: time and count one lane's launches
     x = x[:Bl]
-    costs = eng.graph.op_costs(Bl, H, W, 2 if dtype == "f16" else 4)
+    costs = eng.graph.op_costs(Bl, H, W, ACT_BYTES[dtype])
     times = np.array(eng.profile_replay(x, reps=reps))
     eng.run(x, lanes=1)  # restore the buffers the replay clobbered
     kinds = [op.kind for op in eng.graph.ops]
@@ -89,8 +90,9 @@ def conv_roofline(model, x, dtype, workload, reps=20):
         "frac": round(ach / PEAK_TFLOPS[dtype], 4), "traffic": traffic,
         "traffic_note": (f"HBM-side bytes per forward of all conv launches (PMC FETCH_SIZE x2 + WRITE_SIZE, {tsrc}); "
                          f"algorithmic bytes per forward {int(by)}") if traffic else "no PMC summary for this workload",
-        "kernel": "conv implicit GEMM (conv_igemm/conv_lds/conv_dma): all %d conv launches of one lane's forward "
-                  "(%d images), aggregated" % (len(conv), Bl),
+        "kernel": "conv implicit GEMM (%s): all %d conv launches of one lane's forward (%d images), aggregated%s"
+                  % ("conv_i8, v_mfma_i32_32x32x32_i8" if dtype == "i8" else "conv_igemm/conv_lds/conv_dma", len(conv),
+                     Bl, "; int8 ops counted as FLOPs" if dtype == "i8" else ""),
         "timing": f"HIP events around a graph of {reps} back-to-back launches per op, on the launch stream",
         "launches": len(conv), "avg_launch_us": round(t_conv / len(conv) * 1e6, 2),
         "flops_per_forward": fl, "bytes_per_forward_algorithmic": by,
@@ -100,14 +102,19 @@ def conv_roofline(model, x, dtype, workload, reps=20):
     }
 
 
-def cpu_baseline(scale, task, x_gpu_dets, xs, seconds):
-    """Oracle (torch CPU fp32, fused) timed on this host; also mAP of the GPU dets against oracle dets."""
+def cpu_baseline(scale, task, x_gpu_dets, xs, seconds, qparams=None):
+    """Oracle (torch CPU fp32, fused; or the int8 oracle of oracle/quant.py for an int8 run) timed on this host; also
+    mAP of the GPU dets against the oracle's dets (and, for int8, against the float oracle's: the quantisation loss)."""
     from oracle.predict import OracleModel
     from yolomi.metrics import evaluate
     from yolomi.synth import synth_weights
     nthreads = int(os.environ.get("OMP_NUM_THREADS", 0)) or len(os.sched_getaffinity(0))
     torch.set_num_threads(nthreads)
-    om = OracleModel(scale, task, synth_weights(scale, task, 0))
+    if qparams is not None:
+        from oracle.quant import Int8OracleModel
+        om = Int8OracleModel(scale, task, synth_weights(scale, task, 0), qparams)
+    else:
+        om = OracleModel(scale, task, synth_weights(scale, task, 0))
     x1 = xs[:1].cpu()
     om.predict(x1)  # warm-up
     n, t0 = 0, time.perf_counter()
@@ -123,12 +130,18 @@ def cpu_baseline(scale, task, x_gpu_dets, xs, seconds):
                         "unknown")
     except OSError:
         cpu_name = "unknown"
+    what = "int8 oracle (oracle/quant.py: integer convs as exact float64 convs)" if qparams else "oracle"
     base = {"value": round(n / dt, 3), "unit": "images/s", "cores": nthreads, "kind": "port",
-            "sample": f"oracle predict yolo11{scale} B=1 640x640 U[0,1): {n} images in {dt:.1f}s on {cpu_name} "
+            "sample": f"{what} predict yolo11{scale} B=1 640x640 U[0,1): {n} images in {dt:.1f}s on {cpu_name} "
                       f"(os.cpu_count={os.cpu_count()})"}
     acc = {"map50_95": round(m["map"], 4), "map50": round(m["map50"], 4), "images": len(gts),
-           "gt": "oracle (CPU fp32) detections as pseudo ground truth",
+           "gt": ("int8 oracle (CPU) detections, same qparams, as pseudo ground truth" if qparams else
+                  "oracle (CPU fp32) detections as pseudo ground truth"),
            "dets_gpu": int(sum(len(d) for d in x_gpu_dets)), "dets_oracle": int(sum(len(g) for g in gts))}
+    if qparams is not None:  # quantisation loss: int8 GPU detections vs the float oracle's
+        fl = OracleModel(scale, task, synth_weights(scale, task, 0)).predict(xs.cpu())
+        mf = evaluate(x_gpu_dets, [r["boxes"].numpy() for r in fl])
+        acc["vs_fp32_oracle"] = {"map50_95": round(mf["map"], 4), "map50": round(mf["map50"], 4)}
     return base, acc
 
 
@@ -141,7 +154,9 @@ def main():
     ap.add_argument("--task", default="detect")
     ap.add_argument("--batch", type=int, default=8, help="images per GPU per step")
     ap.add_argument("--size", type=int, default=640)
-    ap.add_argument("--dtype", default="f16", choices=["f16", "f32"])
+    ap.add_argument("--dtype", default="f16", choices=["f16", "f32", "i8"])
+    ap.add_argument("--backend", default="qnnpack", choices=["qnnpack", "fbgemm"], help="i8: PTQ qconfig")
+    ap.add_argument("--calib-batches", type=int, default=4, help="i8: calibration batches (B images each)")
     ap.add_argument("--cpu-seconds", type=float, default=15.0)
     ap.add_argument("--no-cpu", action="store_true")
     ap.add_argument("--no-roofline", action="store_true")
@@ -163,10 +178,19 @@ def main():
     from yolomi.plan import pack_model
     from yolomi.synth import synth_weights
 
-    # weights: packed once on rank 0, broadcast over RCCL as one uint8 blob
+    # weights: packed once on rank 0, broadcast over RCCL as one uint8 blob.  i8: rank 0 first runs the PTQ
+    # calibration (exact-f32 plan + torch.ao observers, yolomi.quant) on synthetic batches disjoint from the timed one
     t_init = time.perf_counter()
+    qp = None
+    if rank == 0 and a.dtype == "i8":
+        from yolomi.engine import Engine
+        from yolomi.quant import calibrate
+        ce = Engine(a.model, a.task, synth_weights(a.model, a.task, 0), dev, "f32")
+        qp = calibrate(ce, [synthetic_batch(a.batch, a.size, 500 + i, dev) for i in range(a.calib_batches)],
+                       a.backend)
+        del ce
     if rank == 0:
-        blob = pack_model(a.model, a.task, synth_weights(a.model, a.task, 0), a.dtype)
+        blob = pack_model(a.model, a.task, synth_weights(a.model, a.task, 0), a.dtype, qp)
         nbytes = torch.tensor([len(blob)], dtype=torch.int64, device=dev)
     else:
         blob, nbytes = None, torch.zeros(1, dtype=torch.int64, device=dev)
@@ -227,7 +251,7 @@ def main():
         out["roofline"] = conv_roofline(model, x, a.dtype, out["config"]["workload"])
     if rank == 0 and world == 1 and not a.no_cpu:
         gdets = [r.boxes.data.cpu().numpy() for r in res]
-        base, acc = cpu_baseline(a.model, a.task, gdets, x, a.cpu_seconds)
+        base, acc = cpu_baseline(a.model, a.task, gdets, x, a.cpu_seconds, qp)
         out["cpu_baseline"] = base
         out["accuracy"] = acc
     if rank == 0:

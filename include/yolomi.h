@@ -62,6 +62,9 @@ int ym_create(int device, const ym_model_desc* desc, ym_ctx** out);
 /* Load a model blob (plan + BN-folded packed weights, produced by yolomi.plan.pack_model) from host memory.
  * Replaces AutoBackend(fuse=True) weight preparation.  Copies to device; the host blob may be freed after. */
 int ym_load_weights(ym_ctx* ctx, const void* blob, size_t bytes);
+/* (blob dtypes: f16 and f32 plans, and int8 PTQ plans packed with calibrated quantisation parameters by
+ *  yolomi.plan.pack_graph(..., dtype="i8", qparams=...) — the runtime of PostTrainingQuantizer.optimize,
+ *  /root/reference/optimization/quantization/quantizers.py:48-91.) */
 
 /* Replaces `YOLO11Model.predict(tensor)` (core/model.py:118-133) for tensor sources: asynchronous on `stream`
  * (a hipStream_t, NULL = default).  d_input: B×3×H×W fp32 NCHW device tensor (H, W multiples of 32).
@@ -69,6 +72,14 @@ int ym_load_weights(ym_ctx* ctx, const void* blob, size_t bytes);
  * d_counts: B int32 kept counts.  d_dets / d_counts must be device pointers. */
 int ym_infer(ym_ctx* ctx, const float* d_input, int B, int H, int W, const ym_infer_args* args, float* d_dets,
              int* d_counts, void* stream);
+
+/* PTQ calibration support (f32 plans only): one eager forward in which op i also writes its pre-activation output
+ * to d_raw[i] (device pointer or NULL; fp32 row-major (pixels, channels): conv / depthwise ops their conv output, the
+ * attention op its positional depthwise conv pe(v), ConvTranspose2d its (pixels, 4·C) GEMM output).  Feeds the
+ * conv-output observers of the reference's PostTrainingQuantizer (optimization/quantization/quantizers.py:146-177).
+ * Asynchronous on `stream`. */
+int ym_calibrate(ym_ctx* ctx, const float* d_input, int B, int H, int W, const ym_infer_args* args, float* d_dets,
+                 int* d_counts, float* const* d_raw, int n_ops, void* stream);
 
 /* Eager run with a HIP event pair around every op: op_ms[i] = device time of op i (n_ops entries). */
 int ym_profile(ym_ctx* ctx, const float* d_input, int B, int H, int W, const ym_infer_args* args, float* d_dets,

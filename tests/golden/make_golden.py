@@ -13,6 +13,10 @@ Fixtures (tests/golden/*.json):
   det_n_randn.json      : yolo11n, 1 x N(0,1) 640x640 (seed 2001) → LoadTensor /255 rule, conf 0.25
   det_n_320_lowconf.json: yolo11n, 1 x U[0,1) 320x320 (seed 3001), conf 0.05 (many candidates)
   det_s_uniform.json    : yolo11s, 1 x U[0,1) 640x640 (seed 4001)
+  det_n_i8_qnnpack.json : yolo11n PTQ int8 (oracle/quant.py, qnnpack qconfig): calibrated on 2 x U[0,1) 640x640
+                          (seeds 5001, 5002); the qparams + int8-oracle detections of 2 other images (5101, 5102)
+  det_n_i8_fbgemm_320.json: same with the fbgemm qconfig (per-channel weights, reduce_range), 320x320 (5201 / 5301)
+    python tests/golden/make_golden.py i8      # regenerates only the int8 fixtures
 """
 from __future__ import annotations
 
@@ -27,6 +31,7 @@ ROOT = os.path.dirname(os.path.dirname(os.path.dirname(os.path.abspath(__file__)
 sys.path.insert(0, os.path.join(ROOT, "yolo-infer_amd"))
 sys.path.insert(0, ROOT)
 
+from oracle import quant as Q  # noqa: E402
 from oracle.predict import OracleModel  # noqa: E402
 from yolomi.plan import fuse_conv_bn  # noqa: E402
 from yolomi.synth import normal, synth_weights, uniform  # noqa: E402
@@ -87,6 +92,40 @@ def weight_fixture(scale):
     return out
 
 
+def det_i8_fixture(scale, backend, calib_seeds, seeds, S, conf=0.25, iou=0.7):
+    sd = synth_weights(scale, "detect", 0)
+    net = Q.build_folded(scale, "detect", sd)
+    qp = Q.calibrate(net, [make_input("uniform", calib_seeds, S)], backend)
+    m = Q.Int8OracleModel(scale, "detect", sd, qp)
+    x = make_input("uniform", seeds, S)
+    im, y, ex = m.raw(x)
+    B = x.shape[0]
+    head = torch.cat([f.reshape(B, 144, -1) for f in ex["feats"]], 2).transpose(1, 2)
+    dets = m.predict(x, conf=conf, iou=iou)
+    return {
+        "scale": scale, "task": "detect", "weights_seed": 0, "backend": backend,
+        "calibration": {"kind": "uniform", "seeds": list(calib_seeds), "size": S},
+        "input": {"kind": "uniform", "seeds": list(seeds), "size": S}, "conf": conf, "iou": iou, "max_det": 300,
+        "qparams": Q.qparams_to_json(qp),
+        "layers": {f"L{i}": layer_stats(ex["stored"][i].q.permute(0, 2, 3, 1)) for i in LAYERS},
+        "head": layer_stats(head),
+        "dets": [d["boxes"].tolist() for d in dets],
+    }
+
+
+I8_FIXTURES = {
+    "det_n_i8_qnnpack": ("n", "qnnpack", (5001, 5002), (5101, 5102), 640),
+    "det_n_i8_fbgemm_320": ("n", "fbgemm", (5201,), (5301,), 320),
+}
+
+
+def main_i8():
+    for name, (scale, backend, cs, seeds, S) in I8_FIXTURES.items():
+        d = det_i8_fixture(scale, backend, cs, seeds, S)
+        json.dump(d, open(os.path.join(HERE, f"{name}.json"), "w"))
+        print(name, [len(x) for x in d["dets"]])
+
+
 def main():
     torch.set_num_threads(min(8, os.cpu_count() or 1))
     for scale in ("n", "s"):
@@ -104,4 +143,9 @@ def main():
 
 
 if __name__ == "__main__":
-    main()
+    if len(sys.argv) > 1 and sys.argv[1] == "i8":
+        torch.set_num_threads(min(8, os.cpu_count() or 1))
+        main_i8()
+    else:
+        main()
+        main_i8()

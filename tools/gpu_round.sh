@@ -11,8 +11,12 @@ fatal() { local rc=$1; [ "$rc" -eq 124 ] || [ "$rc" -eq 137 ] || [ "$rc" -eq 134
 for s in "${steps[@]}"; do
   echo "[gpu_round] step $s $(date +%T)"
   case $s in
-    tests) timeout -k 10 900 python -m pytest tests -m gpu -q -x -p no:cacheprovider > gpurun_out/gt.log 2>&1; rc=$?
+    tests) timeout -k 10 900 python -u -m pytest tests -m gpu -q -p no:cacheprovider --timeout 300 --timeout-method thread > gpurun_out/gt.log 2>&1; rc=$?
            tail -15 gpurun_out/gt.log ;;
+    qtests) timeout -k 10 600 python -u -m pytest tests/test_gpu_quant.py -v -p no:cacheprovider --timeout 240 --timeout-method thread > gpurun_out/qt.log 2>&1; rc=$?
+           tail -25 gpurun_out/qt.log ;;
+    bench_i8) timeout -k 10 500 python bench.py --dtype i8 > gpurun_out/bench_i8.json 2> gpurun_out/bench_i8.err; rc=$?
+           cat gpurun_out/bench_i8.json; tail -3 gpurun_out/bench_i8.err ;;
     bench) timeout -k 10 400 python bench.py > gpurun_out/bench.json 2> gpurun_out/bench.err; rc=$?
            cat gpurun_out/bench.json ;;
     bench_s) timeout -k 10 400 python bench.py --model s > gpurun_out/bench_s.json 2> gpurun_out/bench_s.err; rc=$?
@@ -31,4 +35,6 @@ for s in "${steps[@]}"; do
   esac
   echo "[gpu_round] step $s rc=$rc $(date +%T)"
   if fatal $rc; then echo "[gpu_round] fatal rc=$rc in $s: stopping"; exit $rc; fi
+  if [ "$rc" -ne 0 ]; then any_fail=$rc; fi
 done
+exit ${any_fail:-0}

@@ -40,6 +40,7 @@ class _ModelHandle:
     (speed_benchmark.py:323), `.parameters()` / `.model.parameters()` (model.py:240), `.names`."""
 
     def __init__(self, state_dict: Dict[str, np.ndarray], engine: Engine, names: Dict[int, str]):
+        self._sd = state_dict
         self._params = {k: torch.from_numpy(np.asarray(v)) for k, v in state_dict.items()
                         if not k.endswith("num_batches_tracked")}
         for p in self._params.values():
@@ -57,6 +58,12 @@ class _ModelHandle:
 
     def state_dict(self):
         return dict(self._params)
+
+    def state_dict_numpy(self) -> Dict[str, np.ndarray]:
+        """The Ultralytics-key weights this model was packed from (what a quantizer re-packs)."""
+        if not self._sd:
+            raise ValueError("this model was built from a packed blob only; its weights are not on the host")
+        return self._sd
 
 
 def _load_state_dict(path: Path) -> Dict[str, np.ndarray]:
@@ -91,10 +98,13 @@ class YOLO11Model:
 
     def __init__(self, model_path: Optional[Union[str, Path]] = None, task: str = "detect", size: str = "n",
                  device: Optional[str] = None, verbose: bool = True, dtype: str = "f16", seed: int = 0,
-                 weights_blob: Optional[bytes] = None):
-        """Extra keyword arguments over the reference: `dtype` ('f16' storage + fp32 accumulate, or 'f32' = exact
-        parity mode), `seed` of the synthetic weights used when no `model_path` is given, and `weights_blob` = an
-        already packed model (e.g. received over an RCCL broadcast from rank 0)."""
+                 weights_blob: Optional[bytes] = None, qparams: Optional[Dict] = None,
+                 state_dict: Optional[Dict[str, np.ndarray]] = None):
+        """Extra keyword arguments over the reference: `dtype` ('f16' storage + fp32 accumulate, 'f32' = exact
+        parity mode, or 'i8' = the PTQ int8 plan, which needs calibrated `qparams`; see
+        optimization.quantization.PostTrainingQuantizer), `seed` of the synthetic weights used when no `model_path`
+        is given, `weights_blob` = an already packed model (e.g. received over an RCCL broadcast from rank 0), and
+        `state_dict` = weights already in memory."""
         self.task = task
         self.size = size
         self.device = device or self._get_default_device()
@@ -103,6 +113,8 @@ class YOLO11Model:
         self.dtype = dtype
         self.seed = seed
         self._blob = weights_blob
+        self._qparams = qparams
+        self._sd = state_dict
         self.optimization_history: List[Dict[str, Any]] = []
         self._validate_inputs()
         self.model = self._load_model()
@@ -129,12 +141,14 @@ class YOLO11Model:
         self._dev = dev
         try:
             if self._blob is not None:
-                sd = {}
+                sd = self._sd or {}
+            elif self._sd is not None:
+                sd = self._sd
             elif self.model_path:
                 sd = _load_state_dict(Path(self.model_path))
             else:  # the reference fetches yolo11{size}.pt by name; offline we synthesise weights of that graph
                 sd = synth_weights(self.size, self.task, self.seed)
-            engine = Engine(self.size, self.task, sd, dev, self.dtype, blob=self._blob)
+            engine = Engine(self.size, self.task, sd, dev, self.dtype, blob=self._blob, qparams=self._qparams)
         except Exception as e:
             logger.error(f"Failed to load model: {e}")
             raise

@@ -11,8 +11,11 @@ typedef float f32x8 __attribute__((ext_vector_type(8)));
 
 #define YM_WAVE 64
 
-// Activation storage precision of a plan: f16 (MFMA 16x16x32 f16) or f32 (exact-f32 MFMA 16x16x4, parity mode).
-enum { YM_DT_F16 = 0, YM_DT_F32 = 1 };
+// Activation storage precision of a plan: f16 (MFMA 32x32x16 f16), f32 (exact-f32 MFMA 32x32x2, parity mode) or
+// i8 (PTQ int8: activations stored as q - 128 in int8, weights int8, MFMA 32x32x32 i8 with int32 accumulation).
+enum { YM_DT_F16 = 0, YM_DT_F32 = 1, YM_DT_I8 = 2 };
+
+typedef signed char i8;
 
 // 8 consecutive channels of one pixel: the unit of every NHWC load in this runtime (16 B in f16, 32 B in f32).
 template <typename T> struct Vec8;
@@ -33,6 +36,13 @@ template <> struct Vec8<float> {
     *reinterpret_cast<f32x4*>(p) = f32x4{v[0], v[1], v[2], v[3]};
     *reinterpret_cast<f32x4*>(p + 4) = f32x4{v[4], v[5], v[6], v[7]};
   }
+  static __device__ __forceinline__ type zero() { return type{0, 0, 0, 0, 0, 0, 0, 0}; }
+};
+
+template <> struct Vec8<i8> {  // int8 plans (8 bytes)
+  typedef i8 type __attribute__((ext_vector_type(8)));
+  static __device__ __forceinline__ type load(const i8* p) { return *reinterpret_cast<const type*>(p); }
+  static __device__ __forceinline__ void store(i8* p, type v) { *reinterpret_cast<type*>(p) = v; }
   static __device__ __forceinline__ type zero() { return type{0, 0, 0, 0, 0, 0, 0, 0}; }
 };
 
@@ -65,6 +75,26 @@ __device__ __forceinline__ int ym_div(int n, FDiv f) { return (int)(((unsigned l
 __device__ __forceinline__ float ym_sigmoid(float x) { return 1.0f / (1.0f + expf(-x)); }
 
 // ------------------------------------------------------------------------------------------------------------
+// int8 (PTQ) quantisation record of one op, stored in the weight blob (yolomi/plan.py `_qrec`; semantics:
+// oracle/quant.py).  A quantized conv: acc = Σ (q_x - z_x)·q_w (int32, exact; the int8 storage holds q - 128, the
+// difference is folded into a per-channel int32 bias), y = float(acc)·sasw[n] + bias[n] (two fp32 roundings),
+// q_c = clamp(rint(y·inv_sc) + zc, qlo, qhi); then by mode
+//   0: v = post[q_c] (+ residual (q_r - z_r)·s_r), stored as clamp(rint(v·inv_so) + zo, qlo, qhi) - 128,
+//   1: stored as q_c - 128 (the tensor keeps the conv's own output quantisation: Attention.qkv, Proto.upsample),
+//   2: v written as fp32 (terminal head outputs).
+struct QRec {
+  float inv_sc; int zc;  // conv output requantisation (1 / s_out, zero point)
+  int qlo, qhi;          // [0, 255], or [0, 127] with reduce_range
+  int mode;
+  float inv_so; int zo;  // stored tensor (mode 0)
+  float s_r; int z_r;    // residual tensor
+  float s_in; int z_in;  // input tensor (dequantisation; 3x3 padding reads z_in)
+  float inv_s_in;        // stem: quantisation of the image
+  int pad[4];
+  float post[256];       // post[q] = act((q - zc)·s_out) (SiLU in float64, rounded to fp32) or the plain dequant
+};
+
+// ------------------------------------------------------------------------------------------------------------
 // Kernel argument blocks (plain structs passed by value).
 
 struct ConvArgs {
@@ -81,6 +111,9 @@ struct ConvArgs {
   FDiv fd_hw, fd_w;            // division by Ho*Wo and by Wo
   float* slab; long slab_cap;  // bytes
   int* cnt; int cnt_cap;       // per-tile arrival counters, zero between launches
+  // int8 plans: quantisation record, per-channel s_in·s_w and the int32 zero-point correction Σ_k (128 - z_in)·w
+  const QRec* q; const float* sasw; const int* biasi;
+  float* raw;                  // f32 calibration runs: pre-activation conv output, (M, N) row-major, or null
 };
 
 struct DwArgs {
@@ -88,6 +121,8 @@ struct DwArgs {
   void* dst; int d_ctot, d_coff, d_P;
   const float* w; const float* bias;  // w: [9][C] f32
   int C, H, W, act, B;
+  const i8* wq; const QRec* q; const float* sasw;  // int8 plans: w [9][C] int8
+  float* raw;                                      // f32 calibration runs: pre-activation output (B·H·W, C)
 };
 
 struct PoolArgs {
@@ -102,6 +137,15 @@ struct AttnArgs {
   const float* pe_w; const float* pe_b;  // [9][C], [C]
   int C, nh, kd, hd, H, W, N, B;
   float scale;
+  const i8* pe_wq; const QRec* q; const float* pe_sasw;  // int8 plans (q: pe output, qkv input, attn.x store)
+  float* raw;                                            // f32 calibration runs: pe(v) before the add, (B·N, C)
+};
+
+struct ReqArgs {  // int8 plans: dst slice = requantised (optionally 2x nearest up-sampled) src slice
+  const i8* src; int s_ctot, s_coff, s_P, s_W, up;
+  i8* dst; int d_ctot, d_coff, d_P, d_W;
+  int C, H, W, B;  // dst geometry
+  const QRec* q;   // s_in / z_in: source, inv_so / zo: destination
 };
 
 struct DecodeArgs {
@@ -157,3 +201,10 @@ hipError_t ym_launch_spin(int usec, hipStream_t st);  // profiling: park the str
 hipError_t ym_launch_conv_dma(int out_f32, const ConvArgs& a, int i, hipStream_t st);  // f16 plans only
 int ym_conv_dma_num_cfgs();
 hipError_t ym_launch_masks(const MaskArgs& a, hipStream_t st);  // Segment: process_mask(upsample=True)
+// int8 (PTQ) plans: csrc/ym_conv_i8.hip
+hipError_t ym_launch_conv_i8(const ConvArgs& a, int cfg, hipStream_t st, bool strict);
+int ym_conv_i8_num_cfgs();
+hipError_t ym_launch_stem_i8(const ConvArgs& a, hipStream_t st);
+hipError_t ym_launch_dwconv_i8(const DwArgs& a, hipStream_t st);
+hipError_t ym_launch_attn_i8(const AttnArgs& a, hipStream_t st);
+hipError_t ym_launch_requant(const ReqArgs& a, hipStream_t st);

@@ -321,6 +321,7 @@ __global__ __launch_bounds__(WM * WN * WK * 64) void conv_igemm(const ConvArgs a
         for (int e = 0; e < 4; ++e) {
           const float x = acc[i][j][4 * q + e] + bias[j][q][e];
           v[e] = (a.act ? ym_silu(x) : x) + resv[i][j][q][e];
+          if (a.raw) a.raw[(size_t)(pbase + i * 32 + l32) * a.N + n + e] = x;  // f32 calibration run
         }
         if (a.shuffle) {
           const int sub = n / a.npr;
@@ -625,6 +626,7 @@ hipError_t ym_launch_conv(int dtype, int out_f32, const ConvArgs& a, int cfg, hi
   else if (a.k == 3 && !a.src1 && !a.up0) kind = 3;
   else kind = -1;
   if (kind < 0) return hipErrorInvalidValue;
+  if (dtype == YM_DT_I8) return ym_launch_conv_i8(a, cfg, st, strict);  // csrc/ym_conv_i8.hip
   // (concat/upsample sources only feed 1x1 convs; YOLO11 has k in {1, 3})
   if (a.Kpad % KSTEP) return hipErrorInvalidValue;
   if (cfg >= kNumAllCfg) {

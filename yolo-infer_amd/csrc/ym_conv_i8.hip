@@ -1,0 +1,684 @@
+// int8 (PTQ) kernels for gfx950: the quantized runtime behind the reference's PostTrainingQuantizer
+// (/root/reference/optimization/quantization/quantizers.py:24-308; qconfig :124-131) — SURVEY §8a row a20, config 4.
+//
+// Numerics (pinned by oracle/quant.py, bit-exact apart from the float attention island):
+//   activations are stored as int8 b = q - 128 (q = quint8 value, per-tensor affine), weights int8 symmetric;
+//   a quantized conv accumulates Σ b·w with v_mfma_i32_32x32x32_i8 and adds the per-channel int32 correction
+//   Σ_k (128 - z_in)·w, which makes acc = Σ (q - z_in)·w exactly (3x3 padding taps read the byte z_in - 128, i.e.
+//   real zero); then y = float(acc)·(s_in·s_w) + bias, q_c = clamp(rint(y / s_out) + z_out), and the epilogue maps
+//   q_c through the op's 256-entry `post` table (SiLU or plain dequant of the requantised output), adds the residual
+//   ((q_r - z_r)·s_r), and quantizes into the stored tensor (or writes fp32 head rows).  All float steps use
+//   explicit __fmul_rn / __fadd_rn (no FMA contraction) so they round exactly as the oracle's torch fp32 ops.
+//
+// Kernels: conv_i8 (implicit GEMM over NHWC int8, same transposed orientation and tile structure as
+// csrc/ym_conv.hip: MFMA A = weights [N][Kpad], B = im2col gathered straight from NHWC, one 16-byte K chunk = 16
+// channels of one input pixel), stem_i8 (the image → int8 quantisation folded into the 3x3 s2 stem),
+// dwconv3x3_i8, attn_psa_i8 (float attention on dequantised q/k/v + int8 positional depthwise conv), requant (the
+// materialised concats of an int8 plan).
+#include <stdlib.h>
+
+#include "ym_common.h"
+
+typedef int i32x4 __attribute__((ext_vector_type(4)));
+typedef int i32x16 __attribute__((ext_vector_type(16)));
+typedef signed char i8x16 __attribute__((ext_vector_type(16)));
+
+namespace {
+
+constexpr int KSTEP = 64;        // K bytes per step: two 32-deep MFMAs per 32x32 block pair
+constexpr int KS = KSTEP / 32;
+
+__device__ __forceinline__ i8x16 ld16(const i8* p) { return *reinterpret_cast<const i8x16*>(p); }
+__device__ __forceinline__ int clampi(int v, int lo, int hi) { return v < lo ? lo : (v > hi ? hi : v); }
+
+// quantized::conv2d output requantisation
+__device__ __forceinline__ int requant_out(int acc, float sasw, float bias, const QRec* Q) {
+  const float y = __fadd_rn(__fmul_rn((float)acc, sasw), bias);
+  return clampi((int)rintf(__fmul_rn(y, Q->inv_sc)) + Q->zc, Q->qlo, Q->qhi);
+}
+// quantize a float into a stored tensor: returns the int8 storage value q - 128
+__device__ __forceinline__ int quant_store(float v, float inv, int z, int lo, int hi) {
+  return clampi((int)rintf(__fmul_rn(v, inv)) + z, lo, hi) - 128;
+}
+__device__ __forceinline__ float deq(int q, int z, float s) { return __fmul_rn((float)(q - z), s); }
+__device__ __forceinline__ int pack4(const int* v) {
+  return (v[0] & 0xFF) | ((v[1] & 0xFF) << 8) | ((v[2] & 0xFF) << 16) | ((unsigned)(v[3] & 0xFF) << 24);
+}
+
+__device__ __forceinline__ bool xcd_tile(const ConvArgs& a, int BM, int& tm, int& tn) {
+  const int bid = blockIdx.x;
+  const int rest = bid >> 3;
+  tn = rest % a.tiles_n;
+  tm = (rest / a.tiles_n) * 8 + (bid & 7);
+  return tm * BM < a.M;
+}
+
+// WTM x WTN 32x32 blocks per wave; WM x WN x WK waves (WK: intra-workgroup split-K, partial tiles summed through LDS
+// — integer sums, so the result does not depend on the split).  KIND 1: 1x1 stride 1; KIND 3: 3x3 (stride a.s).
+// a.Cin8 holds the number of 16-channel blocks per tap in int8 plans.
+template <int WTM, int WTN, int WM, int WN, int WK, int KIND>
+__global__ __launch_bounds__(WM * WN * WK * 64) void conv_i8(const ConvArgs a) {
+  constexpr int BM = WM * WTM * 32, BN = WN * WTN * 32, NT = WM * WN * WK * 64;
+  __shared__ float post[256];
+  const int lane = threadIdx.x & 63;
+  const int wid = threadIdx.x >> 6;
+  const int wk = wid % WK;
+  const int wm = (wid / WK) % WM;
+  const int wn = wid / (WK * WM);
+  const int l32 = lane & 31, h = lane >> 5;
+  int tm, tn;
+  if (!xcd_tile(a, BM, tm, tn)) return;
+  const QRec* Q = a.q;
+  for (int i = threadIdx.x; i < 256; i += NT) post[i] = Q->post[i];
+  __syncthreads();
+  const int pbase = tm * BM + wm * WTM * 32;
+  const int nbase = tn * BN + wn * WTN * 32;
+  const int HWo = a.Ho * a.Wo;
+
+  int pb[WTM], py[WTM], px[WTM], iy0[WTM], ix0[WTM];
+  bool pv[WTM];
+  const i8* row0[WTM];
+#pragma unroll
+  for (int i = 0; i < WTM; ++i) {
+    const int m = pbase + i * 32 + l32;
+    pv[i] = m < a.M;
+    const int mm = pv[i] ? m : 0;
+    pb[i] = mm / HWo;
+    const int rem = mm - pb[i] * HWo;
+    py[i] = rem / a.Wo;
+    px[i] = rem - py[i] * a.Wo;
+    if constexpr (KIND == 1) {
+      row0[i] = static_cast<const i8*>(a.src0) + ((size_t)(pb[i] * a.s0_P + py[i] * a.s0_W + px[i]) * a.s0_ctot + a.s0_coff);
+    } else {
+      row0[i] = static_cast<const i8*>(a.src0) + ((size_t)pb[i] * a.s0_P * a.s0_ctot + a.s0_coff);
+    }
+    iy0[i] = py[i] * a.s - 1;
+    ix0[i] = px[i] * a.s - 1;
+  }
+  const i8* wrow[WTN];
+#pragma unroll
+  for (int j = 0; j < WTN; ++j) {
+    const int n = nbase + j * 32 + l32;
+    wrow[j] = static_cast<const i8*>(a.w) + (size_t)(n < a.N ? n : 0) * a.Kpad;
+  }
+
+  const int nsteps = a.Kpad / KSTEP;
+  int g = wk;
+  int tap0 = 0, cb0 = 0;
+  if constexpr (KIND == 3) {
+    const int c = g * 2 * KS + h;
+    tap0 = c / a.Cin8;
+    cb0 = c - tap0 * a.Cin8;
+  }
+  const int fb = (Q->z_in - 128) & 0xFF;
+  const int f4 = fb | (fb << 8) | (fb << 16) | (fb << 24);
+  const i8x16 FILL = __builtin_bit_cast(i8x16, i32x4{f4, f4, f4, f4});
+  const i8x16 ZERO = __builtin_bit_cast(i8x16, i32x4{0, 0, 0, 0});
+  auto gather = [&](int i, int s) -> i8x16 {
+    const int chunk = g * 2 * KS + 2 * s + h;
+    if (!pv[i] || chunk >= a.Kc) return ZERO;
+    if constexpr (KIND == 1) {
+      return ld16(row0[i] + chunk * 16);
+    } else {
+      int cb = cb0 + 2 * s, t = tap0;
+      while (cb >= a.Cin8) { cb -= a.Cin8; ++t; }
+      const int ky = t / 3, kx = t - (t / 3) * 3;
+      const int iy = iy0[i] + ky, ix = ix0[i] + kx;
+      if ((unsigned)iy >= (unsigned)a.Hin || (unsigned)ix >= (unsigned)a.Win) return FILL;
+      return ld16(row0[i] + (size_t)(iy * a.Win + ix) * a.s0_ctot + cb * 16);
+    }
+  };
+  auto advance = [&]() {
+    g += WK;
+    if constexpr (KIND == 3) {
+      cb0 += 2 * KS * WK;
+      while (cb0 >= a.Cin8) { cb0 -= a.Cin8; ++tap0; }
+    }
+  };
+
+  i32x16 acc[WTM][WTN];
+#pragma unroll
+  for (int i = 0; i < WTM; ++i)
+#pragma unroll
+    for (int j = 0; j < WTN; ++j)
+#pragma unroll
+      for (int r = 0; r < 16; ++r) acc[i][j][r] = 0;
+
+  i8x16 fa0[KS][WTN], fb0[KS][WTM], fa1[KS][WTN], fb1[KS][WTM];
+  auto load_step = [&](i8x16 (*fa)[WTN], i8x16 (*fbv)[WTM]) {
+#pragma unroll
+    for (int s = 0; s < KS; ++s) {
+#pragma unroll
+      for (int j = 0; j < WTN; ++j) fa[s][j] = ld16(wrow[j] + (size_t)(g * 2 * KS + 2 * s + h) * 16);
+#pragma unroll
+      for (int i = 0; i < WTM; ++i) fbv[s][i] = gather(i, s);
+    }
+  };
+  auto compute = [&](i8x16 (*fa)[WTN], i8x16 (*fbv)[WTM]) {
+#pragma unroll
+    for (int s = 0; s < KS; ++s)
+#pragma unroll
+      for (int i = 0; i < WTM; ++i)
+#pragma unroll
+        for (int j = 0; j < WTN; ++j)
+          acc[i][j] = __builtin_amdgcn_mfma_i32_32x32x32_i8(fa[s][j], fbv[s][i], acc[i][j], 0, 0, 0);
+  };
+
+  if (g < nsteps) load_step(fa0, fb0);
+  while (g < nsteps) {
+    if (g + WK < nsteps) { advance(); load_step(fa1, fb1); } else { g += WK; }
+    compute(fa0, fb0);
+    if (g >= nsteps) break;
+    if (g + WK < nsteps) { advance(); load_step(fa0, fb0); } else { g += WK; }
+    compute(fa1, fb1);
+  }
+
+  if constexpr (WK > 1) {
+    extern __shared__ int red[];  // [(WK-1)][WM*WN][WTM*WTN*16][64]
+    constexpr int PER = WTM * WTN * 16;
+    const int grp = wid / WK;
+    if (wk > 0) {
+      int* dst = red + ((size_t)((wk - 1) * (WM * WN) + grp) * PER) * 64 + lane;
+#pragma unroll
+      for (int i = 0; i < WTM; ++i)
+#pragma unroll
+        for (int j = 0; j < WTN; ++j)
+#pragma unroll
+          for (int r = 0; r < 16; ++r) dst[((i * WTN + j) * 16 + r) * 64] = acc[i][j][r];
+    }
+    __syncthreads();
+    if (wk > 0) return;
+#pragma unroll 1
+    for (int q = 1; q < WK; ++q) {
+      const int* src = red + ((size_t)((q - 1) * (WM * WN) + grp) * PER) * 64 + lane;
+#pragma unroll
+      for (int i = 0; i < WTM; ++i)
+#pragma unroll
+        for (int j = 0; j < WTN; ++j)
+#pragma unroll
+          for (int r = 0; r < 16; ++r) acc[i][j][r] += src[((i * WTN + j) * 16 + r) * 64];
+    }
+  }
+
+  // ---- epilogue: lane owns channels nbase + 32j + 8q + 4h + {0..3} of pixel pbase + 32i + l32
+  const int mode = Q->mode;
+  const i8* res = static_cast<const i8*>(a.res);
+#pragma unroll
+  for (int i = 0; i < WTM; ++i) {
+    if (!pv[i]) continue;
+    const int oy = py[i], ox = px[i];
+    const int pix = a.shuffle ? (2 * oy) * a.d_W + 2 * ox : oy * a.d_W + ox;
+    const size_t obase = (size_t)(pb[i] * a.d_P + a.d_pixoff + pix) * a.d_ctot + a.d_coff;
+    const size_t rbase = res ? (size_t)(pb[i] * a.r_P + oy * a.Wo + ox) * a.r_ctot + a.r_coff : 0;
+#pragma unroll
+    for (int j = 0; j < WTN; ++j) {
+#pragma unroll
+      for (int q = 0; q < 4; ++q) {
+        const int n = nbase + j * 32 + 8 * q + 4 * h;
+        if (n >= a.N) continue;
+        const i32x4 bi = *reinterpret_cast<const i32x4*>(a.biasi + n);
+        const f32x4 sa = *reinterpret_cast<const f32x4*>(a.sasw + n);
+        const f32x4 bf = *reinterpret_cast<const f32x4*>(a.bias + n);
+        const int r4 = res ? *reinterpret_cast<const int*>(res + rbase + n) : 0;
+        int ov[4];
+        float fv[4];
+#pragma unroll
+        for (int e = 0; e < 4; ++e) {
+          const int qc = requant_out(acc[i][j][4 * q + e] + bi[e], sa[e], bf[e], Q);
+          if (mode == 1) {
+            ov[e] = qc - 128;
+            continue;
+          }
+          float v = post[qc];
+          if (res) v = __fadd_rn(v, deq(((r4 >> (8 * e)) & 0xFF) ^ 0x80, Q->z_r, Q->s_r));
+          fv[e] = v;
+          ov[e] = quant_store(v, Q->inv_so, Q->zo, Q->qlo, Q->qhi);
+        }
+        size_t off = obase + n;
+        if (a.shuffle) {
+          const int sub = n / a.npr;
+          const int ch = n - sub * a.npr;
+          off = obase + (size_t)((sub >> 1) * a.d_W + (sub & 1)) * a.d_ctot + ch;
+        }
+        if (mode == 2) *reinterpret_cast<f32x4*>(static_cast<float*>(a.dst) + off) = f32x4{fv[0], fv[1], fv[2], fv[3]};
+        else *reinterpret_cast<int*>(static_cast<i8*>(a.dst) + off) = pack4(ov);
+      }
+    }
+  }
+}
+
+template <int WTM, int WTN, int WM, int WN, int WK>
+hipError_t launch_cfg(ConvArgs a, int kind, hipStream_t st) {
+  constexpr int BM = WM * WTM * 32, BN = WN * WTN * 32, NT = WM * WN * WK * 64;
+  const int tiles_m8 = ((a.M + BM - 1) / BM + 7) / 8 * 8;
+  a.tiles_n = (a.N + BN - 1) / BN;
+  const size_t lds = WK > 1 ? (size_t)(WK - 1) * WM * WN * WTM * WTN * 16 * 64 * sizeof(int) : 0;
+  const dim3 grid(tiles_m8 * a.tiles_n);
+  if (kind == 1)
+    hipLaunchKernelGGL((conv_i8<WTM, WTN, WM, WN, WK, 1>), grid, dim3(NT), lds, st, a);
+  else
+    hipLaunchKernelGGL((conv_i8<WTM, WTN, WM, WN, WK, 3>), grid, dim3(NT), lds, st, a);
+  return hipGetLastError();
+}
+
+// (id, WTM, WTN, WM, WN, WK) — the same tile family as the f16/f32 conv_igemm configs
+#define YM_I8_CFGS(X) \
+  X(0, 2, 2, 2, 2, 1)  \
+  X(1, 2, 2, 4, 1, 1)  \
+  X(2, 2, 1, 4, 1, 1)  \
+  X(3, 1, 2, 1, 1, 4)  \
+  X(4, 1, 2, 1, 2, 4)  \
+  X(5, 1, 2, 4, 1, 1)  \
+  X(6, 2, 2, 1, 2, 2)  \
+  X(7, 1, 1, 1, 1, 8)  \
+  X(8, 1, 2, 2, 1, 2)  \
+  X(9, 1, 1, 4, 1, 1)  \
+  X(10, 1, 2, 2, 2, 1) \
+  X(11, 1, 1, 1, 1, 4)
+
+struct Cfg {
+  int wtm, wtn, wm, wn, wk;
+};
+constexpr Cfg kCfgs[] = {
+#define YM_X(id, a, b, c, d, e) {a, b, c, d, e},
+    YM_I8_CFGS(YM_X)
+#undef YM_X
+};
+constexpr int kNumCfg = sizeof(kCfgs) / sizeof(kCfgs[0]);
+
+hipError_t launch_id(int id, const ConvArgs& a, int kind, hipStream_t st) {
+  switch (id) {
+#define YM_X(cid, A, B, C, D, E) \
+  case cid: return launch_cfg<A, B, C, D, E>(a, kind, st);
+    YM_I8_CFGS(YM_X)
+#undef YM_X
+  }
+  return hipErrorInvalidValue;
+}
+
+int choose_cfg(const ConvArgs& a) {
+  const char* env = getenv("YM_CONV_CFG");
+  if (env && *env) {
+    const int id = atoi(env);
+    if (id >= 0 && id < kNumCfg) return id;
+  }
+  const long M = a.M, N = a.N;
+  const int steps = a.Kpad / KSTEP;
+  auto waves = [&](int id) {
+    const Cfg& c = kCfgs[id];
+    const long BM = c.wm * c.wtm * 32, BN = c.wn * c.wtn * 32;
+    return ((M + BM - 1) / BM) * ((N + BN - 1) / BN) * c.wm * c.wn * c.wk;
+  };
+  if (N <= 32) return waves(2) >= 2048 ? 2 : (steps >= 4 ? 7 : 9);
+  if (N <= 64) {
+    if (waves(1) >= 2048) return 1;
+    if (waves(5) >= 2048) return 5;
+    return steps >= 4 ? 3 : 8;
+  }
+  if (waves(0) >= 2048) return 0;
+  if (waves(10) >= 2048) return 10;
+  return steps >= 4 ? 4 : 6;
+}
+
+// ------------------------------------------------------------------------------------------------- stem
+// Conv(3, c, 3, 2) on the caller's NCHW fp32 batch: LoadTensor's /255 rule, then the image's int8 quantisation
+// (q = clamp(rint(x / s_in) + z_in)) folded into the LDS patch as q - z_in (0 for padding), integer MACs in fp32
+// (|partial sums| < 2^24: exact), the quantized-conv epilogue, 16 channels (16 bytes) per thread.
+constexpr int TH = 8;
+
+template <int G>
+__global__ __launch_bounds__(256) void stem_i8(const ConvArgs a) {
+  constexpr int TW = 32 / G;
+  constexpr int PH = 2 * TH + 1;
+  constexpr int PW4 = (2 * TW + 4 + 3) / 4 + 1;
+  constexpr int PW = PW4 * 4;
+  constexpr int N = 16 * G;
+  extern __shared__ float sm[];
+  float* patch = sm;                // [3][PH][PW]
+  float* wl = patch + 3 * PH * PW;  // [27][N]
+  float* post = wl + 27 * N;        // [256]
+  const QRec* Q = a.q;
+  const int tiles_x = (a.Wo + TW - 1) / TW, tiles_y = (a.Ho + TH - 1) / TH;
+  int bid = blockIdx.x;
+  const int tx = bid % tiles_x;
+  bid /= tiles_x;
+  const int ty = bid % tiles_y;
+  const int b = bid / tiles_y;
+  const int oy0 = ty * TH, ox0 = tx * TW;
+  const int iy0 = 2 * oy0 - 1, xs = 2 * ox0 - 4;
+  const bool div = ord2f(*reinterpret_cast<const int*>(a.ctl)) > 1.0f + a.eps;
+  const size_t HW = (size_t)a.Hin * a.Win;
+  const float* img = a.nchw + (size_t)b * 3 * HW;
+  const float inv = Q->inv_s_in;
+  const int zi = Q->z_in, lo = Q->qlo, hi = Q->qhi;
+  for (int i = threadIdx.x; i < 3 * PH * PW4; i += 256) {
+    const int c = i / (PH * PW4), r = i - c * (PH * PW4);
+    const int py = r / PW4, q = r - (r / PW4) * PW4;
+    const int iy = iy0 + py, ix = xs + 4 * q;
+    f32x4 v = {0.f, 0.f, 0.f, 0.f};
+    if ((unsigned)iy < (unsigned)a.Hin && (unsigned)ix < (unsigned)a.Win) {
+      v = *reinterpret_cast<const f32x4*>(img + c * HW + (size_t)iy * a.Win + ix);
+#pragma unroll
+      for (int e = 0; e < 4; ++e) {
+        float x = v[e];
+        if (div) x = x / 255.0f;
+        v[e] = (float)(clampi((int)rintf(__fmul_rn(x, inv)) + zi, lo, hi) - zi);
+      }
+    }
+    *reinterpret_cast<f32x4*>(patch + (c * PH + py) * PW + 4 * q) = v;
+  }
+  const i8* W = static_cast<const i8*>(a.w);
+  for (int i = threadIdx.x; i < 27 * N; i += 256) {
+    const int tap = i / N, n = i - (i / N) * N;
+    const int kk = tap / 3, c = tap - (tap / 3) * 3;
+    wl[i] = (float)W[(size_t)n * a.Kpad + kk * 8 + c];
+  }
+  for (int i = threadIdx.x; i < 256; i += 256) post[i] = Q->post[i];
+  __syncthreads();
+  const int t = threadIdx.x;
+  if (t >= TH * TW * G) return;
+  const int g = t % G, pix = t / G;
+  const int ly = pix / TW, lx = pix - (pix / TW) * TW;
+  const int oy = oy0 + ly, ox = ox0 + lx;
+  if (oy >= a.Ho || ox >= a.Wo) return;
+  float x[27];
+#pragma unroll
+  for (int ky = 0; ky < 3; ++ky)
+#pragma unroll
+    for (int kx = 0; kx < 3; ++kx)
+#pragma unroll
+      for (int c = 0; c < 3; ++c)
+        x[(ky * 3 + kx) * 3 + c] = patch[(c * PH + 2 * ly + ky) * PW + 2 * lx + kx + 3];
+  const int n0 = g * 16;
+  float acc[16];
+#pragma unroll
+  for (int e = 0; e < 16; ++e) acc[e] = 0.f;
+#pragma unroll
+  for (int k = 0; k < 27; ++k) {
+    const float* wr = wl + k * N + n0;
+#pragma unroll
+    for (int e = 0; e < 16; ++e) acc[e] = fmaf(x[k], wr[e], acc[e]);
+  }
+  int ov[16];
+#pragma unroll
+  for (int e = 0; e < 16; ++e) {
+    const int qc = requant_out((int)acc[e] + a.biasi[n0 + e], a.sasw[n0 + e], a.bias[n0 + e], Q);
+    ov[e] = quant_store(post[qc], Q->inv_so, Q->zo, lo, hi);
+  }
+  const i32x4 o{pack4(ov), pack4(ov + 4), pack4(ov + 8), pack4(ov + 12)};
+  i8* dst = static_cast<i8*>(a.dst) + (size_t)(b * a.d_P + oy * a.d_W + ox) * a.d_ctot + a.d_coff + n0;
+  *reinterpret_cast<i32x4*>(dst) = o;
+}
+
+template <int G>
+hipError_t launch_stem_g(const ConvArgs& a, hipStream_t st) {
+  constexpr int TW = 32 / G;
+  constexpr int PW = ((2 * TW + 4 + 3) / 4 + 1) * 4;
+  const int B = a.M / (a.Ho * a.Wo);
+  const dim3 grid(B * ((a.Ho + TH - 1) / TH) * ((a.Wo + TW - 1) / TW));
+  const size_t lds = ((size_t)3 * (2 * TH + 1) * PW + 27 * 16 * G + 256) * sizeof(float);
+  hipLaunchKernelGGL((stem_i8<G>), grid, dim3(256), lds, st, a);
+  return hipGetLastError();
+}
+
+// ------------------------------------------------------------------------------------------------- depthwise
+// DWConv 3x3 (Detect cv3): one thread = 8 channels of one pixel; acc = Σ over in-image taps (q - z_in)·w, then the
+// quantized-conv epilogue (mode 0).
+__global__ __launch_bounds__(256) void dwconv3x3_i8(const DwArgs a) {
+  __shared__ float post[256];
+  const QRec* Q = a.q;
+  post[threadIdx.x] = Q->post[threadIdx.x];
+  __syncthreads();
+  const int C8 = a.C >> 3;
+  const long idx = blockIdx.x * (long)blockDim.x + threadIdx.x;
+  const long total = (long)a.B * a.H * a.W * C8;
+  if (idx >= total) return;
+  const int cg = idx % C8;
+  const long pix = idx / C8;
+  const int HW = a.H * a.W;
+  const int b = pix / HW;
+  const int p = pix - (long)b * HW;
+  const int y = p / a.W, x = p - (p / a.W) * a.W;
+  const int c0 = cg * 8;
+  const i8* src = static_cast<const i8*>(a.src);
+  typedef Vec8<i8>::type V;
+  V v[9], w[9];
+  bool ok[9];
+#pragma unroll
+  for (int t = 0; t < 9; ++t) {
+    const int iy = y + t / 3 - 1, ix = x + t % 3 - 1;
+    ok[t] = (unsigned)iy < (unsigned)a.H && (unsigned)ix < (unsigned)a.W;
+    v[t] = ok[t] ? Vec8<i8>::load(src + (size_t)(b * a.s_P + iy * a.W + ix) * a.s_ctot + a.s_coff + c0)
+                 : Vec8<i8>::zero();
+    w[t] = Vec8<i8>::load(a.wq + t * a.C + c0);
+  }
+  const int zi = Q->z_in;
+  int acc[8];
+#pragma unroll
+  for (int e = 0; e < 8; ++e) acc[e] = 0;
+#pragma unroll
+  for (int t = 0; t < 9; ++t)
+    if (ok[t]) {
+#pragma unroll
+      for (int e = 0; e < 8; ++e) acc[e] += ((int)v[t][e] + 128 - zi) * (int)w[t][e];
+    }
+  V o;
+#pragma unroll
+  for (int e = 0; e < 8; ++e) {
+    const int qc = requant_out(acc[e], a.sasw[c0 + e], a.bias[c0 + e], Q);
+    o[e] = (i8)quant_store(post[qc], Q->inv_so, Q->zo, Q->qlo, Q->qhi);
+  }
+  Vec8<i8>::store(static_cast<i8*>(a.dst) + (size_t)(b * a.d_P + p) * a.d_ctot + a.d_coff + c0, o);
+}
+
+// ------------------------------------------------------------------------------------------------- attention
+// C2PSA Attention on the int8 qkv tensor (stored in the qkv conv's own output quantisation): q, k, v dequantised to
+// fp32, S = q·kᵀ·scale, fp32 softmax, O = P·V (as csrc/ym_misc.hip attn_psa), + pe(v) as a quantized depthwise conv
+// (int MACs on the stored v bytes, requantised, dequantised), then the sum is quantized into the attn.x tensor.
+constexpr int AKD = 32, AHD = 64;
+
+template <int QB>
+__global__ __launch_bounds__(256) void attn_psa_i8(const AttnArgs a) {
+  extern __shared__ float S[];  // [QB][N], then Q [QB][AKD], then V chunk [64][AHD]
+  __shared__ float post[256];
+  const QRec* Qr = a.q;
+  post[threadIdx.x] = Qr->post[threadIdx.x];
+  const int N = a.N;
+  float* Qs = S + (size_t)QB * N;
+  const int nqb = (N + QB - 1) / QB;
+  const int qb = blockIdx.x % nqb;
+  const int bh = blockIdx.x / nqb;
+  const int h = bh % a.nh;
+  const int b = bh / a.nh;
+  const int tid = threadIdx.x;
+  const int per = 2 * a.kd + a.hd;
+  const i8* qkv = static_cast<const i8*>(a.qkv);
+  const size_t img = (size_t)b * a.q_P;
+  const int hq = a.q_coff + h * per;
+  const float s_in = Qr->s_in;
+  const int z_in = Qr->z_in;
+  for (int i = tid; i < QB * AKD; i += 256) {
+    const int r = i / AKD, c = i % AKD;
+    const int n = qb * QB + r;
+    Qs[i] = (n < N && c < a.kd) ? deq((int)qkv[(img + n) * a.q_ctot + hq + c] + 128, z_in, s_in) : 0.f;
+  }
+  __syncthreads();
+  for (int key = tid; key < N; key += 256) {
+    float k[AKD];
+    const i8* kp = qkv + (img + key) * a.q_ctot + hq + a.kd;
+#pragma unroll
+    for (int c8 = 0; c8 < AKD / 8; ++c8) {
+      const Vec8<i8>::type v = Vec8<i8>::load(kp + c8 * 8);
+#pragma unroll
+      for (int e = 0; e < 8; ++e) k[c8 * 8 + e] = (c8 * 8 + e < a.kd) ? deq((int)v[e] + 128, z_in, s_in) : 0.f;
+    }
+#pragma unroll 4
+    for (int q = 0; q < QB; ++q) {
+      float s = 0.f;
+#pragma unroll
+      for (int c = 0; c < AKD; ++c) s = fmaf(Qs[q * AKD + c], k[c], s);
+      S[q * N + key] = s * a.scale;
+    }
+  }
+  __syncthreads();
+  {
+    constexpr int TPR = 256 / QB;
+    const int q = tid / TPR, sub = tid % TPR;
+    float* row = S + (size_t)q * N;
+    float m = -INFINITY;
+    for (int j = sub; j < N; j += TPR) m = fmaxf(m, row[j]);
+#pragma unroll
+    for (int o = TPR / 2; o > 0; o >>= 1) m = fmaxf(m, __shfl_xor(m, o));
+    float sum = 0.f;
+    for (int j = sub; j < N; j += TPR) {
+      const float e = expf(row[j] - m);
+      row[j] = e;
+      sum += e;
+    }
+#pragma unroll
+    for (int o = TPR / 2; o > 0; o >>= 1) sum += __shfl_xor(sum, o);
+    for (int j = sub; j < N; j += TPR) row[j] = row[j] / sum;
+  }
+  __syncthreads();
+  constexpr int QPG = QB / 4;
+  const int d = tid & 63, qg = tid >> 6;
+  float o[QPG];
+#pragma unroll
+  for (int i = 0; i < QPG; ++i) o[i] = 0.f;
+  float* Vs = Qs + QB * AKD;
+  for (int k0 = 0; k0 < N; k0 += 64) {
+    __syncthreads();
+    {
+      const int kk = tid >> 2, part = tid & 3;
+      const int key = k0 + kk;
+#pragma unroll
+      for (int h8 = 0; h8 < 2; ++h8) {
+        const int d0 = part * 16 + h8 * 8;
+        Vec8<i8>::type v = Vec8<i8>::zero();
+        const bool okv = key < N && d0 < a.hd;
+        if (okv) v = Vec8<i8>::load(qkv + (img + key) * a.q_ctot + hq + 2 * a.kd + d0);
+#pragma unroll
+        for (int e = 0; e < 8; ++e) Vs[kk * AHD + d0 + e] = okv ? deq((int)v[e] + 128, z_in, s_in) : 0.f;
+      }
+    }
+    __syncthreads();
+    const int kn = N - k0 < 64 ? N - k0 : 64;
+    for (int kj = 0; kj < kn; ++kj) {
+      const float v = Vs[kj * AHD + d];
+#pragma unroll
+      for (int i = 0; i < QPG; ++i) o[i] = fmaf(S[(qg + 4 * i) * N + k0 + kj], v, o[i]);
+    }
+  }
+  if (d >= a.hd) return;
+  const int ch = h * a.hd + d;
+  const i8* vp = qkv + img * a.q_ctot + hq + 2 * a.kd + d;
+  i8* dst = static_cast<i8*>(a.dst);
+  int wv[9];
+#pragma unroll
+  for (int t = 0; t < 9; ++t) wv[t] = (int)a.pe_wq[t * a.C + ch];
+  const float sa = a.pe_sasw[ch], pb = a.pe_b[ch];
+#pragma unroll
+  for (int i = 0; i < QPG; ++i) {
+    const int n = qb * QB + qg + 4 * i;
+    if (n >= N) continue;
+    const int y = n / a.W, x = n - (n / a.W) * a.W;
+    int acc = 0;
+    for (int ky = 0; ky < 3; ++ky) {
+      const int iy = y + ky - 1;
+      if ((unsigned)iy >= (unsigned)a.H) continue;
+      for (int kx = 0; kx < 3; ++kx) {
+        const int ix = x + kx - 1;
+        if ((unsigned)ix >= (unsigned)a.W) continue;
+        acc += ((int)vp[(size_t)(iy * a.W + ix) * a.q_ctot] + 128 - z_in) * wv[ky * 3 + kx];
+      }
+    }
+    const float pe = post[requant_out(acc, sa, pb, Qr)];
+    dst[((size_t)b * a.d_P + n) * a.d_ctot + a.d_coff + ch] =
+        (i8)quant_store(__fadd_rn(o[i], pe), Qr->inv_so, Qr->zo, Qr->qlo, Qr->qhi);
+  }
+}
+
+// ------------------------------------------------------------------------------------------------- requant
+// dst[p, coff + c] = quantize(dequantize(src[p' , c])) with p' = p or (y/2, x/2): 16 channels per thread.
+__global__ __launch_bounds__(256) void requant_copy(const ReqArgs a) {
+  const int C16 = a.C >> 4;
+  const long idx = blockIdx.x * (long)blockDim.x + threadIdx.x;
+  const long total = (long)a.B * a.H * a.W * C16;
+  if (idx >= total) return;
+  const int cg = idx % C16;
+  const long pix = idx / C16;
+  const int HW = a.H * a.W;
+  const int b = pix / HW;
+  const int p = pix - (long)b * HW;
+  const int y = p / a.W, x = p - (p / a.W) * a.W;
+  const int sy = a.up ? (y >> 1) : y, sx = a.up ? (x >> 1) : x;
+  const QRec* Q = a.q;
+  const i8x16 v = ld16(a.src + (size_t)(b * a.s_P + sy * a.s_W + sx) * a.s_ctot + a.s_coff + cg * 16);
+  int ov[16];
+#pragma unroll
+  for (int e = 0; e < 16; ++e)
+    ov[e] = quant_store(deq((int)v[e] + 128, Q->z_in, Q->s_in), Q->inv_so, Q->zo, Q->qlo, Q->qhi);
+  const i32x4 o{pack4(ov), pack4(ov + 4), pack4(ov + 8), pack4(ov + 12)};
+  *reinterpret_cast<i32x4*>(a.dst + (size_t)(b * a.d_P + p) * a.d_ctot + a.d_coff + cg * 16) = o;
+}
+
+}  // namespace
+
+int ym_conv_i8_num_cfgs() { return kNumCfg; }
+
+hipError_t ym_launch_conv_i8(const ConvArgs& a, int cfg, hipStream_t st, bool strict) {
+  int kind;
+  if (a.k == 1 && a.s == 1 && !a.src1 && !a.up0) kind = 1;
+  else if (a.k == 3 && !a.src1 && !a.up0) kind = 3;
+  else return hipErrorInvalidValue;
+  if (a.Kpad % KSTEP || !a.q || !a.sasw || !a.biasi || (a.N & 3) || (a.s0_ctot & 15) || (a.s0_coff & 15))
+    return hipErrorInvalidValue;
+  if (cfg >= kNumCfg) {
+    if (strict) return hipErrorInvalidValue;
+    cfg = -1;
+  }
+  return launch_id(cfg >= 0 ? cfg : choose_cfg(a), a, kind, st);
+}
+
+hipError_t ym_launch_stem_i8(const ConvArgs& a, hipStream_t st) {
+  if (a.k != 3 || a.s != 2 || !a.nchw || a.shuffle || a.res || !a.q || a.Win % 4) return hipErrorInvalidValue;
+  switch (a.N) {
+    case 16: return launch_stem_g<1>(a, st);
+    case 32: return launch_stem_g<2>(a, st);
+    case 64: return launch_stem_g<4>(a, st);
+    case 96: return launch_stem_g<6>(a, st);
+  }
+  return hipErrorInvalidValue;
+}
+
+hipError_t ym_launch_dwconv_i8(const DwArgs& a, hipStream_t st) {
+  if (a.C % 8 || !a.q || !a.wq) return hipErrorInvalidValue;
+  const long total = (long)a.B * a.H * a.W * (a.C / 8);
+  hipLaunchKernelGGL(dwconv3x3_i8, dim3((total + 255) / 256), dim3(256), 0, st, a);
+  return hipGetLastError();
+}
+
+hipError_t ym_launch_attn_i8(const AttnArgs& a, hipStream_t st) {
+  if (a.kd > AKD || a.hd > AHD || !a.q || !a.pe_wq) return hipErrorInvalidValue;
+  const size_t budget = 150 * 1024;
+  auto lds = [&](int qb) { return ((size_t)qb * a.N + (size_t)qb * AKD + 64 * AHD) * sizeof(float); };
+  auto wgs = [&](int qb) { return (long)a.B * a.nh * ((a.N + qb - 1) / qb); };
+  if (lds(32) <= budget && wgs(32) >= 512)
+    hipLaunchKernelGGL((attn_psa_i8<32>), dim3(a.B * a.nh * ((a.N + 31) / 32)), dim3(256), lds(32), st, a);
+  else if (lds(16) <= budget && (wgs(16) >= 512 || lds(8) > budget))
+    hipLaunchKernelGGL((attn_psa_i8<16>), dim3(a.B * a.nh * ((a.N + 15) / 16)), dim3(256), lds(16), st, a);
+  else if (lds(8) <= budget)
+    hipLaunchKernelGGL((attn_psa_i8<8>), dim3(a.B * a.nh * ((a.N + 7) / 8)), dim3(256), lds(8), st, a);
+  else if (lds(4) <= budget)
+    hipLaunchKernelGGL((attn_psa_i8<4>), dim3(a.B * a.nh * ((a.N + 3) / 4)), dim3(256), lds(4), st, a);
+  else
+    return hipErrorInvalidValue;
+  return hipGetLastError();
+}
+
+hipError_t ym_launch_requant(const ReqArgs& a, hipStream_t st) {
+  if (a.C % 16 || a.s_coff % 16 || a.d_coff % 16 || a.s_ctot % 16 || a.d_ctot % 16 || !a.q) return hipErrorInvalidValue;
+  const long total = (long)a.B * a.H * a.W * (a.C / 16);
+  hipLaunchKernelGGL(requant_copy, dim3((total + 255) / 256), dim3(256), 0, st, a);
+  return hipGetLastError();
+}

@@ -82,6 +82,10 @@ __global__ __launch_bounds__(256) void dwconv3x3(const DwArgs a) {
 #pragma unroll
   for (int e = 0; e < 8; ++e) o[e] = (T)(a.act ? ym_silu(acc[e]) : acc[e]);
   Vec8<T>::store(static_cast<T*>(a.dst) + (size_t)(b * a.d_P + p) * a.d_ctot + a.d_coff + c0, o);
+  if (a.raw) {  // f32 calibration run: the pre-activation output
+#pragma unroll
+    for (int e = 0; e < 8; ++e) a.raw[(size_t)pix * a.C + c0 + e] = acc[e];
+  }
 }
 
 // ------------------------------------------------------------------------------------------------- SPPF pools
@@ -274,6 +278,7 @@ __global__ __launch_bounds__(256) void attn_psa(const AttnArgs a) {
       }
     }
     dst[((size_t)b * a.d_P + n) * a.d_ctot + a.d_coff + ch] = (T)(o[i] + pe);
+    if (a.raw) a.raw[((size_t)b * N + n) * a.C + ch] = pe;  // f32 calibration run: pe(v) before the add
   }
 }
 
@@ -544,6 +549,7 @@ hipError_t ym_launch_prep(int dtype, const PrepArgs& a, int* counts, int B, hipS
 }
 
 hipError_t ym_launch_dwconv(int dtype, const DwArgs& a, hipStream_t st) {
+  if (dtype == YM_DT_I8) return ym_launch_dwconv_i8(a, st);
   const long total = (long)a.B * a.H * a.W * (a.C / 8);
   const dim3 g((total + 255) / 256);
   if (a.C % 8) return hipErrorInvalidValue;
@@ -554,13 +560,14 @@ hipError_t ym_launch_dwconv(int dtype, const DwArgs& a, hipStream_t st) {
 
 hipError_t ym_launch_sppf(int dtype, const PoolArgs& a, hipStream_t st) {
   const size_t HW = (size_t)a.H * a.W;
-  const size_t img = HW * 8 * (dtype == YM_DT_F16 ? 2 : 4);
+  const size_t img = HW * 8 * (dtype == YM_DT_F16 ? 2 : (dtype == YM_DT_I8 ? 1 : 4));
   PoolArgs b = a;
   b.sep = 4 * img <= 128 * 1024;  // input + 3 row-max images, 8 channels
   const size_t lds = b.sep ? 4 * img : img;
   if (a.C % 8 || lds > 160 * 1024) return hipErrorInvalidValue;
   const dim3 g(a.B * (a.C / 8));
   if (dtype == YM_DT_F16) hipLaunchKernelGGL(sppf_pool<f16>, g, dim3(256), lds, st, b);
+  else if (dtype == YM_DT_I8) hipLaunchKernelGGL(sppf_pool<i8>, g, dim3(256), lds, st, b);  // max on q - 128: exact
   else hipLaunchKernelGGL(sppf_pool<float>, g, dim3(256), lds, st, b);
   return hipGetLastError();
 }
@@ -586,6 +593,7 @@ hipError_t launch_attn_t(const AttnArgs& a, hipStream_t st) {
 }
 
 hipError_t ym_launch_attn(int dtype, const AttnArgs& a, hipStream_t st) {
+  if (dtype == YM_DT_I8) return ym_launch_attn_i8(a, st);
   if (a.kd > AKD || a.hd > AHD) return hipErrorInvalidValue;
   return dtype == YM_DT_F16 ? launch_attn_t<f16>(a, st) : launch_attn_t<float>(a, st);
 }

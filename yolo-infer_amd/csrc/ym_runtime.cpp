@@ -40,7 +40,7 @@ constexpr int kHdr = 32, kBufRec = 8, kOpRec = 32, kNameLen = 48;
 constexpr int kSplitCounters = 16384;  // split-K tiles per conv launch (csrc/ym_conv_dma.hip)
 constexpr int kMaxLanes = 4;           // concurrent batch slices in one forward graph (<= GPU_MAX_HW_QUEUES)
 
-enum OpKind { OP_INPUT = 1, OP_CONV = 2, OP_DW = 3, OP_SPPF = 4, OP_ATTN = 5, OP_DECODE = 6, OP_NMS = 7 };
+enum OpKind { OP_INPUT = 1, OP_CONV = 2, OP_DW = 3, OP_SPPF = 4, OP_ATTN = 5, OP_DECODE = 6, OP_NMS = 7, OP_REQ = 8 };
 
 struct BufDesc {
   int C, f, f32;
@@ -100,6 +100,7 @@ struct ym_ctx {
   int lane = 0, lane_img0 = 0;  // lane / first image of the ops being launched
   std::vector<GraphEntry> graphs;
   std::vector<hipEvent_t> prof_events;
+  float* const* calib_raw = nullptr;  // ym_calibrate: per-op pre-activation output buffers (f32 plans)
   // per-shape, per-op conv tile configuration (-1 = heuristic); set by ym_tune / ym_set_op_cfg
   struct ShapeCfg {
     int B, H, W;
@@ -153,7 +154,11 @@ struct ym_ctx {
   }
   int buf_H(int b) const { return bufs[b].f == 0 ? 1 : cH / bufs[b].f; }
   int buf_Wd(int b) const { return bufs[b].f == 0 ? A : cW / bufs[b].f; }
-  int elem(int b) const { return (bufs[b].f32 || dtype == YM_DT_F32) ? 4 : 2; }
+  int elem(int b) const { return (bufs[b].f32 || dtype == YM_DT_F32) ? 4 : (dtype == YM_DT_I8 ? 1 : 2); }
+  template <typename T> const T* wptr(int32_t off) const {
+    return reinterpret_cast<const T*>(d_weights + (size_t)(uint32_t)off);
+  }
+  float* raw_of(const Op& op) const { return calib_raw ? calib_raw[&op - ops.data()] : nullptr; }
   // buffer b of the current lane: its image slice of the whole-batch buffer (all buffers are image-major)
   void* bptr(int b) const {
     return d_arena + buf_off[b] + (size_t)lane_img0 * buf_P(b) * bufs[b].C * elem(b);
@@ -245,6 +250,15 @@ int conv_args(ym_ctx* c, const Op& op, int B, const float* d_in, float in_eps, C
       a.Wo = (a.Win + 2 * a.pad - k) / s + 1;
       if (cin % 8 || (a.C0 + a.C1) != cin) return fail(YM_EBLOB, "op %s: cin %d not a multiple of 8", op.name, cin);
       a.Cin8 = cin / 8;
+      if (c->dtype == YM_DT_I8) {  // int8 plans: K chunks of 16 channels (the stem keeps its 8-padded taps)
+        if (b0 != c->input_buf) {
+          if (cin % 16) return fail(YM_EBLOB, "op %s: int8 cin %d not a multiple of 16", op.name, cin);
+          a.Cin8 = cin / 16;
+        }
+        a.q = c->wptr<QRec>(r[22]);
+        a.sasw = c->wptr<float>(r[23]);
+        a.biasi = c->wptr<int>(r[24]);
+      }
       a.Kc = k * k * a.Cin8;
       a.Kpad = r[21];
       a.N = cout;
@@ -271,7 +285,8 @@ int conv_args(ym_ctx* c, const Op& op, int B, const float* d_in, float in_eps, C
       a.M = B * a.Ho * a.Wo;
       a.fd_hw = ym_fdiv(a.Ho * a.Wo);
       a.fd_w = ym_fdiv(a.Wo);
-      out_f32 = c->bufs[bd].f32 && c->dtype == YM_DT_F16;
+      out_f32 = c->bufs[bd].f32 && c->dtype != YM_DT_F32;
+      a.raw = c->raw_of(op);
       a.s0_elems = (b0 == c->input_buf) ? 0 : (long)c->cB * c->buf_P(b0) * c->bufs[b0].C;
       a.s1_elems = b1 >= 0 ? (long)c->cB * c->buf_P(b1) * c->bufs[b1].C : 0;
       a.slab = reinterpret_cast<float*>(c->d_arena + c->off_slab + (size_t)c->lane * c->slab_bytes);
@@ -315,6 +330,13 @@ int launch_op(ym_ctx* c, const Op& op, int B, const float* d_in, const ym_infer_
       a.w = reinterpret_cast<const float*>(c->d_weights + (size_t)(uint32_t)r[19]);
       a.bias = reinterpret_cast<const float*>(c->d_weights + (size_t)(uint32_t)r[20]);
       a.C = r[3]; a.act = r[5]; a.H = c->buf_H(bs); a.W = c->buf_Wd(bs); a.B = B;
+      if (dt == YM_DT_I8) {
+        a.w = nullptr;
+        a.wq = c->wptr<i8>(r[19]);
+        a.q = c->wptr<QRec>(r[22]);
+        a.sasw = c->wptr<float>(r[23]);
+      }
+      a.raw = c->raw_of(op);
       e = ym_launch_dwconv(dt, a, st);
       break;
     }
@@ -336,7 +358,29 @@ int launch_op(ym_ctx* c, const Op& op, int B, const float* d_in, const ym_infer_
       a.C = r[3]; a.nh = r[4]; a.kd = r[5]; a.hd = r[9];
       a.H = c->buf_H(bq); a.W = c->buf_Wd(bq); a.N = a.H * a.W; a.B = B;
       memcpy(&a.scale, &r[21], 4);
+      if (dt == YM_DT_I8) {
+        a.pe_w = nullptr;
+        a.pe_wq = c->wptr<i8>(r[19]);
+        a.q = c->wptr<QRec>(r[22]);
+        a.pe_sasw = c->wptr<float>(r[23]);
+      }
+      a.raw = c->raw_of(op);
       e = ym_launch_attn(dt, a, st);
+      break;
+    }
+    case OP_REQ: {
+      if (dt != YM_DT_I8) return fail(YM_EBLOB, "op %s: requant in a non-int8 plan", op.name);
+      ReqArgs a{};
+      const int bs = r[6], bd = r[13];
+      a.src = static_cast<const i8*>(c->bptr(bs)); a.s_ctot = c->bufs[bs].C; a.s_coff = r[7]; a.s_P = c->buf_P(bs);
+      a.s_W = c->buf_Wd(bs); a.up = r[9];
+      a.dst = static_cast<i8*>(c->bptr(bd)); a.d_ctot = c->bufs[bd].C; a.d_coff = r[14]; a.d_P = c->buf_P(bd);
+      a.d_W = c->buf_Wd(bd);
+      a.C = r[3]; a.H = c->buf_H(bd); a.W = c->buf_Wd(bd); a.B = B;
+      if (c->buf_H(bs) * (a.up ? 2 : 1) != a.H || a.s_W * (a.up ? 2 : 1) != a.W)
+        return fail(YM_EBLOB, "op %s: requant source/destination shapes disagree", op.name);
+      a.q = c->wptr<QRec>(r[22]);
+      e = ym_launch_requant(a, st);
       break;
     }
     case OP_DECODE: {
@@ -439,7 +483,8 @@ int ym_load_weights(ym_ctx* c, const void* blob, size_t bytes) {
   const size_t woff = align_up(need, 256);
   if (bytes < woff + wbytes) return fail(YM_EBLOB, "blob truncated (%zu < %zu)", bytes, woff + wbytes);
   c->dtype = h[2];
-  if (c->dtype != YM_DT_F16 && c->dtype != YM_DT_F32) return fail(YM_EBLOB, "unknown dtype %d", c->dtype);
+  if (c->dtype != YM_DT_F16 && c->dtype != YM_DT_F32 && c->dtype != YM_DT_I8)
+    return fail(YM_EBLOB, "unknown dtype %d", c->dtype);
   c->task = h[3]; c->nc = h[4]; c->nm = h[5]; c->reg_max = h[6]; c->nl = h[7];
   if (c->nl < 1 || c->nl > 4) return fail(YM_EBLOB, "bad level count");
   for (int l = 0; l < c->nl; ++l) c->strides[l] = h[8 + l];
@@ -553,6 +598,22 @@ int ym_infer(ym_ctx* c, const float* d_in, int B, int H, int W, const ym_infer_a
   return YM_OK;
 }
 
+int ym_calibrate(ym_ctx* c, const float* d_in, int B, int H, int W, const ym_infer_args* args, float* d_dets,
+                 int* d_counts, float* const* d_raw, int n_ops, void* stream) {
+  int rc = check_call(c, d_in, B, H, W, args, d_dets, d_counts);
+  if (rc) return rc;
+  if (c->dtype != YM_DT_F32) return fail(YM_ESTATE, "ym_calibrate needs an f32 (parity) plan");
+  if (!d_raw || n_ops != (int)c->ops.size()) return fail(YM_EINVAL, "d_raw must hold %zu entries", c->ops.size());
+  HIPCK(hipSetDevice(c->device));
+  if ((rc = ensure_workspace(c, B, H, W))) return rc;
+  ym_infer_args one = *args;
+  one.lanes = 1;
+  c->calib_raw = d_raw;
+  rc = launch_forward(c, d_in, B, &one, d_dets, d_counts, static_cast<hipStream_t>(stream));
+  c->calib_raw = nullptr;
+  return rc;
+}
+
 int ym_profile(ym_ctx* c, const float* d_in, int B, int H, int W, const ym_infer_args* args, float* d_dets,
                int* d_counts, void* stream, float* op_ms, int n_ops) {
   int rc = check_call(c, d_in, B, H, W, args, d_dets, d_counts);
@@ -646,7 +707,7 @@ int ym_tune(ym_ctx* c, const float* d_in, int B, int H, int W, const ym_infer_ar
   hipEvent_t e0, e1;
   HIPCK(hipEventCreate(&e0));
   HIPCK(hipEventCreate(&e1));
-  const int ncfg = ym_conv_num_cfgs();
+  const int ncfg = c->dtype == YM_DT_I8 ? ym_conv_i8_num_cfgs() : ym_conv_num_cfgs();
   for (size_t i = 0; i < c->ops.size(); ++i) {
     const Op& op = c->ops[i];
     if (op.r[0] != OP_CONV) continue;

@@ -91,6 +91,11 @@ __global__ __launch_bounds__(256) void stem_conv3x3s2(const ConvArgs a) {
   T* dst = static_cast<T*>(a.dst) + (size_t)(b * a.d_P + oy * a.d_W + ox) * a.d_ctot + a.d_coff + n0;
   Vec8<T>::store(dst, o0);
   Vec8<T>::store(dst + 8, o1);
+  if (a.raw) {  // f32 calibration run: the pre-activation output, (M, N) row-major
+    float* r = a.raw + ((size_t)(b * a.Ho + oy) * a.Wo + ox) * N + n0;
+#pragma unroll
+    for (int e = 0; e < 16; ++e) r[e] = acc[e];
+  }
 }
 
 }  // namespace
@@ -118,6 +123,7 @@ hipError_t launch_t(const ConvArgs& a, hipStream_t st) {
 }
 
 hipError_t ym_launch_stem(int dtype, const ConvArgs& a, hipStream_t st) {
+  if (dtype == YM_DT_I8) return ym_launch_stem_i8(a, st);
   if (a.k != 3 || a.s != 2 || !a.nchw || a.shuffle || a.res || !a.act || a.Win % 4) return hipErrorInvalidValue;
   return dtype == YM_DT_F16 ? launch_t<f16>(a, st) : launch_t<float>(a, st);
 }

@@ -49,6 +49,15 @@ class Buffer:
     f: int            # spatial down-sampling factor w.r.t. the input (1, 2, ... 32); 0 = anchor-major buffer
     f32: bool = False  # storage fp32 regardless of activation dtype (head outputs)
     name: str = ""
+    # int8 plans: the quantisation point of the tensor this buffer stores (oracle/quant.py naming): "act:<qname>" =
+    # its own observer, "out:<qname>" = the output quantisation of the conv that writes it as is; None = float
+    qname: Optional[str] = None
+    qkind: str = "act"
+    Cs: int = 0         # storage channels (row stride): C, or C rounded up to 16 in int8 plans
+
+    @property
+    def qkey(self) -> Optional[str]:
+        return f"{self.qkind}:{self.qname}" if self.qname else None
 
 
 @dataclass
@@ -74,12 +83,14 @@ class Param:
 
 
 class GraphBuilder:
-    def __init__(self, scale: str = "n", task: str = "detect", nc: int = NC):
+    def __init__(self, scale: str = "n", task: str = "detect", nc: int = NC, quant: bool = False):
+        """quant=True builds the int8 (PTQ) plan: 16-channel storage granules and materialised concats (a concat is
+        one quantized tensor with its own observer, so the two-source A loader is replaced by requant copies)."""
         if scale not in SCALES:
             raise ValueError(f"Unsupported size: {scale}")
         if task not in ("detect", "segment"):
             raise ValueError(f"task {task!r} has no HIP plan (supported: detect, segment)")
-        self.scale, self.task, self.nc = scale, task, nc
+        self.scale, self.task, self.nc, self.quant = scale, task, nc, quant
         self.depth, self.width, self.max_ch = SCALES[scale]
         self.buffers: List[Buffer] = []
         self.ops: List[Op] = []
@@ -94,8 +105,9 @@ class GraphBuilder:
     def rep(self, n: int) -> int:
         return max(round(n * self.depth), 1) if n > 1 else n
 
-    def buf(self, C: int, f: int, name: str, f32: bool = False) -> Buffer:
-        b = Buffer(len(self.buffers), C, f, f32, name)
+    def buf(self, C: int, f: int, name: str, f32: bool = False, q: Optional[str] = None, qkind: str = "act") -> Buffer:
+        Cs = (C + 15) // 16 * 16 if (self.quant and not f32) else C
+        b = Buffer(len(self.buffers), C, f, f32, name, None if f32 else q, qkind, Cs)
         self.buffers.append(b)
         return b
 
@@ -116,14 +128,22 @@ class GraphBuilder:
 
     def conv(self, prefix: str, src: View, c2: int, k: int, s: int, dst: View, act: bool = True,
              res: Optional[View] = None, src1: Optional[View] = None, up0: bool = False, bn: bool = True,
-             bias_kind=None, extra=None, anchor_level: int = -1, shuffle2x2: bool = False):
+             bias_kind=None, extra=None, anchor_level: int = -1, shuffle2x2: bool = False,
+             catq: Optional[str] = None):
+        """catq: quantisation name of the concat a two-source conv reads (Ultralytics Concat module / cat tensor)."""
         c1 = src.C + (src1.C if src1 is not None else 0)
         self._conv_params(prefix, c1, c2, k, 1, bn, bias_kind, extra)
         assert dst.C == (4 * c2 if shuffle2x2 else c2) or anchor_level >= 0 or shuffle2x2
+        fin = src.buf.f * (2 if s == 2 else 1) // (2 if up0 else 1)
+        if self.quant and src1 is not None:  # int8: materialise the concat (requant copies into one tensor)
+            f_in = src.buf.f // (2 if up0 else 1)
+            cat = self.buf(c1, f_in, catq, q=catq)
+            self.ops.append(Op("requant", dict(src=src, up=up0, dst=View(cat, 0, src.C)), catq + ".req0"))
+            self.ops.append(Op("requant", dict(src=src1, up=False, dst=View(cat, src.C, src1.C)), catq + ".req1"))
+            src, src1, up0 = self.full(cat), None, False
         self.ops.append(Op("conv", dict(k=k, s=s, c1=c1, c2=c2, act=act, src0=src, up0=up0, src1=src1, dst=dst,
                                         res=res, anchor_level=anchor_level, shuffle2x2=shuffle2x2, bn=bn,
-                                        wkey=prefix), prefix))
-        fin = src.buf.f * (2 if s == 2 else 1) // (2 if up0 else 1)
+                                        wkey=prefix, catq=catq), prefix))
         self.flops_per_pixel.append((prefix, fin, k * k * c1 * c2))
 
     def dwconv(self, prefix: str, src: View, dst: View, act: bool = True):
@@ -135,26 +155,26 @@ class GraphBuilder:
     # ------------------------------------------------------------------ modules
     def Conv(self, i: int, x: View, c2: int, k: int, s: int) -> View:
         f = x.buf.f * s
-        out = self.buf(c2, f, f"L{i}")
+        out = self.buf(c2, f, f"L{i}", q=f"model.{i}")
         self.conv(f"model.{i}", x, c2, k, s, self.full(out))
         return self.full(out)
 
     def bottleneck(self, prefix: str, x: View, c: int, e: float, dst: View, f: int):
         c_ = int(c * e)
-        h = self.buf(c_, f, prefix + ".h")
+        h = self.buf(c_, f, prefix + ".h", q=prefix + ".cv1")
         self.conv(prefix + ".cv1", x, c_, 3, 1, self.full(h))
         self.conv(prefix + ".cv2", self.full(h), c, 3, 1, dst, res=x)
 
     def c3k(self, prefix: str, x: View, c: int, dst: View, f: int, n: int = 2):
         c_ = int(c * 0.5)
-        cat = self.buf(2 * c_, f, prefix + ".cat")
-        t = self.buf(c_, f, prefix + ".t0")
+        cat = self.buf(2 * c_, f, prefix + ".cat", q=prefix + ".cat")
+        t = self.buf(c_, f, prefix + ".t0", q=prefix + ".cv1")
         self.conv(prefix + ".cv1", x, c_, 1, 1, self.full(t))
         self.conv(prefix + ".cv2", x, c_, 1, 1, View(cat, c_, c_))
         cur = self.full(t)
         for j in range(n):
             last = j == n - 1
-            nxt = View(cat, 0, c_) if last else self.full(self.buf(c_, f, f"{prefix}.t{j + 1}"))
+            nxt = View(cat, 0, c_) if last else self.full(self.buf(c_, f, f"{prefix}.t{j + 1}", q=f"{prefix}.m.{j}"))
             self.bottleneck(f"{prefix}.m.{j}", cur, c_, 1.0, nxt, f)
             cur = nxt
         self.conv(prefix + ".cv3", self.full(cat), c, 1, 1, dst)
@@ -166,8 +186,9 @@ class GraphBuilder:
         n = self.rep(n)
         f = x.buf.f // (2 if up0 else 1)
         c = int(c2 * e)
-        cat = self.buf((2 + n) * c, f, f"L{i}.cat")
-        self.conv(f"model.{i}.cv1", x, 2 * c, 1, 1, View(cat, 0, 2 * c), src1=x1, up0=up0)
+        cat = self.buf((2 + n) * c, f, f"L{i}.cat", q=f"model.{i}.cat")
+        self.conv(f"model.{i}.cv1", x, 2 * c, 1, 1, View(cat, 0, 2 * c), src1=x1, up0=up0,
+                  catq=f"model.{i - 1}" if x1 is not None else None)
         prev = View(cat, c, c)
         for j in range(n):
             dst = View(cat, (2 + j) * c, c)
@@ -176,17 +197,17 @@ class GraphBuilder:
             else:
                 self.bottleneck(f"model.{i}.m.{j}", prev, c, 0.5, dst, f)
             prev = dst
-        out = self.buf(c2, f, f"L{i}")
+        out = self.buf(c2, f, f"L{i}", q=f"model.{i}")
         self.conv(f"model.{i}.cv2", self.full(cat), c2, 1, 1, self.full(out))
         return self.full(out)
 
     def SPPF(self, i: int, x: View, c2: int) -> View:
         c_ = x.C // 2
         f = x.buf.f
-        cat = self.buf(4 * c_, f, f"L{i}.cat")
+        cat = self.buf(4 * c_, f, f"L{i}.cat", q=f"model.{i}.cat")
         self.conv(f"model.{i}.cv1", x, c_, 1, 1, View(cat, 0, c_))
         self.ops.append(Op("sppf", dict(C=c_, src=View(cat, 0, c_), dst=cat), f"model.{i}.m"))
-        out = self.buf(c2, f, f"L{i}")
+        out = self.buf(c2, f, f"L{i}", q=f"model.{i}")
         self.conv(f"model.{i}.cv2", self.full(cat), c2, 1, 1, self.full(out))
         return self.full(out)
 
@@ -198,27 +219,27 @@ class GraphBuilder:
         hd = c // nh
         kd = int(hd * 0.5)
         h = c + 2 * nh * kd
-        cv1 = self.buf(2 * c, f, f"L{i}.cv1")
+        cv1 = self.buf(2 * c, f, f"L{i}.cv1", q=f"model.{i}.cv1")
         self.conv(f"model.{i}.cv1", x, 2 * c, 1, 1, self.full(cv1))
         b = View(cv1, c, c)
         for j in range(n):
             p = f"model.{i}.m.{j}"
-            qkv = self.buf(h, f, p + ".qkv")
+            qkv = self.buf(h, f, p + ".qkv", q=p + ".attn.qkv", qkind="out")
             self.conv(p + ".attn.qkv", b, h, 1, 1, self.full(qkv), act=False)
-            ao = self.buf(c, f, p + ".attn.o")
+            ao = self.buf(c, f, p + ".attn.o", q=p + ".attn.x")
             self._conv_params(p + ".attn.pe", c, c, 3, g=c)
             self.ops.append(Op("attn", dict(C=c, nh=nh, kd=kd, hd=hd, qkv=self.full(qkv), dst=self.full(ao),
                                             wkey=p + ".attn.pe"), p + ".attn"))
             self.flops_per_pixel.append((p + ".attn.pe", f, 9 * c))
-            b1 = self.buf(c, f, p + ".b1")
+            b1 = self.buf(c, f, p + ".b1", q=p + ".attn_add")
             self.conv(p + ".attn.proj", self.full(ao), c, 1, 1, self.full(b1), act=False, res=b)
-            ff = self.buf(2 * c, f, p + ".ffn")
+            ff = self.buf(2 * c, f, p + ".ffn", q=p + ".ffn.0")
             self.conv(p + ".ffn.0", self.full(b1), 2 * c, 1, 1, self.full(ff))
-            b2 = self.buf(c, f, p + ".b2")
+            b2 = self.buf(c, f, p + ".b2", q=p)
             self.conv(p + ".ffn.1", self.full(ff), c, 1, 1, self.full(b2), act=False, res=self.full(b1))
             b = self.full(b2)
-        out = self.buf(c2, f, f"L{i}")
-        self.conv(f"model.{i}.cv2", View(cv1, 0, c), c2, 1, 1, self.full(out), src1=b)
+        out = self.buf(c2, f, f"L{i}", q=f"model.{i}")
+        self.conv(f"model.{i}.cv2", View(cv1, 0, c), c2, 1, 1, self.full(out), src1=b, catq=f"model.{i}.cat")
         return self.full(out)
 
     def Detect(self, i: int, xs: List[View]):
@@ -235,18 +256,19 @@ class GraphBuilder:
         if self.task == "segment":  # Proto on P3 (Segment.forward computes it first)
             npr = make_divisible(min(256, self.max_ch) * self.width, 8)
             f = xs[0].buf.f
-            p1 = self.buf(npr, f, "proto.cv1")
+            p1 = self.buf(npr, f, "proto.cv1", q=f"{p}.proto.cv1")
             self.conv(f"{p}.proto.cv1", xs[0], npr, 3, 1, self.full(p1))
-            p2 = self.buf(npr, f // 2, "proto.up")
+            p2 = self.buf(npr, f // 2, "proto.up", q=f"{p}.proto.upsample", qkind="out")
             # ConvTranspose2d(npr, npr, 2, 2, bias): a 1x1 GEMM with N = 4*npr scattered 2x2 (pixel shuffle)
             self.params.append(Param(f"{p}.proto.upsample.weight", (npr, npr, 2, 2), "convT_w"))
             self.params.append(Param(f"{p}.proto.upsample.bias", (npr,), "bias"))
             self.ops.append(Op("conv", dict(k=1, s=1, c1=npr, c2=4 * npr, act=False, src0=self.full(p1), up0=False,
                                             src1=None, dst=self.full(p2), res=None, anchor_level=-1,
-                                            shuffle2x2=True, bn=False, wkey=f"{p}.proto.upsample", convT=True),
+                                            shuffle2x2=True, bn=False, wkey=f"{p}.proto.upsample", convT=True,
+                                            catq=None),
                                f"{p}.proto.upsample"))
             self.flops_per_pixel.append((f"{p}.proto.upsample", f, 4 * npr * npr))
-            p3 = self.buf(npr, f // 2, "proto.cv2")
+            p3 = self.buf(npr, f // 2, "proto.cv2", q=f"{p}.proto.cv2")
             self.conv(f"{p}.proto.cv2", self.full(p2), npr, 3, 1, self.full(p3))
             proto = self.buf(nm, f // 2, "proto", f32=True)
             self.conv(f"{p}.proto.cv3", self.full(p3), nm, 1, 1, self.full(proto))
@@ -254,29 +276,29 @@ class GraphBuilder:
         for l, x in enumerate(xs):
             f = x.buf.f
             # box branch cv2: Conv(x,c2,3) → Conv(c2,c2,3) → Conv2d(c2, 64, 1)
-            t1 = self.buf(c2, f, f"cv2.{l}.0")
+            t1 = self.buf(c2, f, f"cv2.{l}.0", q=f"{p}.cv2.{l}.0")
             self.conv(f"{p}.cv2.{l}.0", x, c2, 3, 1, self.full(t1))
-            t2 = self.buf(c2, f, f"cv2.{l}.1")
+            t2 = self.buf(c2, f, f"cv2.{l}.1", q=f"{p}.cv2.{l}.1")
             self.conv(f"{p}.cv2.{l}.1", self.full(t1), c2, 3, 1, self.full(t2))
             self.conv(f"{p}.cv2.{l}.2", self.full(t2), 4 * REG_MAX, 1, 1, View(anchor, 0, 4 * REG_MAX),
                       act=False, bn=False, bias_kind="box_b", anchor_level=l)
             # cls branch cv3: [DWConv(x,x,3) → Conv(x,c3,1)] → [DWConv(c3,c3,3) → Conv(c3,c3,1)] → Conv2d(c3, nc, 1)
-            d1 = self.buf(x.C, f, f"cv3.{l}.0.0")
+            d1 = self.buf(x.C, f, f"cv3.{l}.0.0", q=f"{p}.cv3.{l}.0.0")
             self.dwconv(f"{p}.cv3.{l}.0.0", x, self.full(d1))
-            e1 = self.buf(c3, f, f"cv3.{l}.0.1")
+            e1 = self.buf(c3, f, f"cv3.{l}.0.1", q=f"{p}.cv3.{l}.0.1")
             self.conv(f"{p}.cv3.{l}.0.1", self.full(d1), c3, 1, 1, self.full(e1))
-            d2 = self.buf(c3, f, f"cv3.{l}.1.0")
+            d2 = self.buf(c3, f, f"cv3.{l}.1.0", q=f"{p}.cv3.{l}.1.0")
             self.dwconv(f"{p}.cv3.{l}.1.0", self.full(e1), self.full(d2))
-            e2 = self.buf(c3, f, f"cv3.{l}.1.1")
+            e2 = self.buf(c3, f, f"cv3.{l}.1.1", q=f"{p}.cv3.{l}.1.1")
             self.conv(f"{p}.cv3.{l}.1.1", self.full(d2), c3, 1, 1, self.full(e2))
             self.conv(f"{p}.cv3.{l}.2", self.full(e2), nc, 1, 1, View(anchor, 4 * REG_MAX, nc), act=False,
                       bn=False, bias_kind="cls_b",
                       extra=dict(nc=nc, stride=STRIDES[l], shift=_cls_shift(self.scale)), anchor_level=l)
             if self.task == "segment":  # mask-coefficient branch cv4: Conv(x,c4,3) → Conv(c4,c4,3) → Conv2d(c4,nm,1)
                 c4 = max(ch0 // 4, nm)
-                m1 = self.buf(c4, f, f"cv4.{l}.0")
+                m1 = self.buf(c4, f, f"cv4.{l}.0", q=f"{p}.cv4.{l}.0")
                 self.conv(f"{p}.cv4.{l}.0", x, c4, 3, 1, self.full(m1))
-                m2 = self.buf(c4, f, f"cv4.{l}.1")
+                m2 = self.buf(c4, f, f"cv4.{l}.1", q=f"{p}.cv4.{l}.1")
                 self.conv(f"{p}.cv4.{l}.1", self.full(m1), c4, 3, 1, self.full(m2))
                 self.conv(f"{p}.cv4.{l}.2", self.full(m2), nm, 1, 1, View(anchor, no, nm), act=False, bn=False,
                           anchor_level=l)
@@ -286,7 +308,7 @@ class GraphBuilder:
 
     # ------------------------------------------------------------------ the graph
     def _build(self):
-        self.input = self.buf(8, 1, "input")  # RGB padded to 8 channels (16 B per pixel in fp16)
+        self.input = self.buf(8, 1, "input", q="input")  # RGB padded to 8 channels (16 B per pixel in fp16)
         self.ops.append(Op("input", dict(dst=self.input), "input"))
         x = View(self.input, 0, 3)
         ch = self.ch
@@ -349,6 +371,11 @@ class GraphBuilder:
                 N = (H // f) * (W // f)
                 fl = 2 * B * (N * N * a["nh"] * (a["kd"] + a["hd"]) + N * 9 * a["C"])
                 by = B * N * (a["qkv"].C + a["C"]) * act_bytes
+            elif op.kind == "requant":
+                s_, d_ = a["src"], a["dst"]
+                f = d_.buf.f
+                npx = B * (H // f) * (W // f)
+                by = 2 * npx * d_.C * act_bytes
             elif op.kind == "input":
                 by = B * H * W * (3 * 4 * 2 + 8 * act_bytes)
             elif op.kind == "decode":

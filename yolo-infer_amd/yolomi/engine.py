@@ -27,13 +27,16 @@ def tune_cache_dir() -> str:
 
 class Engine:
     def __init__(self, scale: str, task: str, state_dict: Dict[str, np.ndarray], device: torch.device,
-                 dtype: str = "f16", blob: Optional[bytes] = None):
+                 dtype: str = "f16", blob: Optional[bytes] = None, qparams: Optional[Dict] = None):
+        """dtype: 'f16' (throughput), 'f32' (exact parity mode) or 'i8' (PTQ int8; needs `qparams` from
+        yolomi.quant.calibrate, or an int8 `blob`)."""
         if device.type != "cuda":
             raise RuntimeError(f"the yolomi engine runs on a gfx950 GPU (got device {device}); there is no CPU path")
         self.scale, self.task, self.dtype = scale, task, dtype
         self.device = device
-        self.graph = GraphBuilder(scale, task)
-        self.blob = blob if blob is not None else pack_graph(self.graph, state_dict, dtype)
+        self.qparams = qparams
+        self.graph = GraphBuilder(scale, task, quant=dtype == "i8")
+        self.blob = blob if blob is not None else pack_graph(self.graph, state_dict, dtype, qparams)
         self.rt = Runtime(device.index if device.index is not None else torch.cuda.current_device(), self.blob)
         self.nm = self.graph.nm
         self._out: Dict[int, tuple] = {}
@@ -151,10 +154,42 @@ class Engine:
         return masks, nonempty, offs
 
     def read_buffer(self, buf_id: int, B: int) -> torch.Tensor:
-        """NHWC contents of plan buffer `buf_id` for the first B images (after run/profile), as a CPU float32 tensor."""
+        """NHWC contents of plan buffer `buf_id` for the first B images (after run/profile), as a CPU float32 tensor
+        (int8 plans: the quantized values q = stored byte + 128, over the storage channels)."""
         _, C, H, W, eb = self.rt.buffer_info(buf_id)
-        dt = torch.float16 if eb == 2 else torch.float32
+        dt = {1: torch.int8, 2: torch.float16, 4: torch.float32}[eb]
         out = torch.empty((B, H, W, C), dtype=dt)
         torch.cuda.synchronize(self.device)
         self.rt.read_buffer(buf_id, out.data_ptr(), out.numel() * out.element_size())
-        return out.float()
+        return out.float() + 128.0 if eb == 1 else out.float()
+
+    def raw_shapes(self, B: int, H: int, W: int) -> Dict[int, tuple]:
+        """(rows, cols) of every op's pre-activation output in a calibration run (ym_calibrate)."""
+        shapes = {}
+        for i, op in enumerate(self.graph.ops):
+            a = op.args
+            if op.kind == "conv":
+                fo = self.graph.out_factor(op)
+                shapes[i] = (B * (H // fo) * (W // fo), 4 * a["c2"] if a["shuffle2x2"] else a["c2"])
+            elif op.kind == "dwconv":
+                f = a["src"].buf.f
+                shapes[i] = (B * (H // f) * (W // f), a["C"])
+            elif op.kind == "attn":
+                f = a["qkv"].buf.f
+                shapes[i] = (B * (H // f) * (W // f), a["C"])
+        return shapes
+
+    def calibrate(self, x: torch.Tensor, **kw) -> Dict[int, torch.Tensor]:
+        """One eager f32 forward that also returns every conv-like op's pre-activation output (op index → (rows, C)
+        fp32 device tensor): the conv-output observers of PTQ calibration (yolomi.quant.calibrate)."""
+        assert x.is_cuda and x.dtype == torch.float32 and x.is_contiguous() and x.dim() == 4
+        B, _, H, W = x.shape
+        args = Runtime.make_args(use_graph=False, lanes=1, **kw)
+        dets, counts = self.outputs(B, args.max_det)
+        raws = {i: torch.empty(sh, dtype=torch.float32, device=self.device)
+                for i, sh in self.raw_shapes(B, H, W).items()}
+        ptrs = [raws[i].data_ptr() if i in raws else 0 for i in range(len(self.graph.ops))]
+        stream = torch.cuda.current_stream(self.device).cuda_stream
+        self.rt.calibrate(x.data_ptr(), B, H, W, args, dets.data_ptr(), counts.data_ptr(), ptrs, stream)
+        torch.cuda.synchronize(self.device)
+        return raws

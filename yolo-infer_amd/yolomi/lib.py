@@ -47,6 +47,7 @@ def load_library(path: os.PathLike = LIB_PATH):
         "ym_load_weights": (I, [P, P, C.c_size_t]),
         "ym_infer": (I, [P, P, I, I, I, C.POINTER(InferArgs), P, P, P]),
         "ym_profile": (I, [P, P, I, I, I, C.POINTER(InferArgs), P, P, P, F, I]),
+        "ym_calibrate": (I, [P, P, I, I, I, C.POINTER(InferArgs), P, P, C.POINTER(C.c_void_p), I, P]),
         "ym_profile_replay": (I, [P, P, I, I, I, C.POINTER(InferArgs), P, P, P, I, F, I]),
         "ym_tune": (I, [P, P, I, I, I, C.POINTER(InferArgs), P, P, P, I]),
         "ym_masks": (I, [P, P, I, I, P, I, I, I, P, P, P]),
@@ -70,7 +71,7 @@ def load_library(path: os.PathLike = LIB_PATH):
     return lib
 
 
-EXPORTED = ("ym_create", "ym_load_weights", "ym_infer", "ym_masks", "ym_profile", "ym_profile_replay", "ym_tune", "ym_get_op_cfg", "ym_set_op_cfg",
+EXPORTED = ("ym_create", "ym_load_weights", "ym_infer", "ym_calibrate", "ym_masks", "ym_profile", "ym_profile_replay", "ym_tune", "ym_get_op_cfg", "ym_set_op_cfg",
             "ym_num_ops", "ym_op_name", "ym_num_buffers",
             "ym_buffer_info", "ym_read_buffer", "ym_sync", "ym_last_error", "ym_destroy", "ym_version")
 
@@ -125,6 +126,11 @@ class Runtime:
         _check(self.lib.ym_profile_replay(self.ctx, C.c_void_p(x_ptr), B, H, W, C.byref(args), C.c_void_p(dets_ptr),
                                           C.c_void_p(counts_ptr), C.c_void_p(stream), reps, ms, self.n_ops))
         return list(ms)
+
+    def calibrate(self, x_ptr, B, H, W, args, dets_ptr, counts_ptr, raw_ptrs, stream):
+        arr = (C.c_void_p * len(raw_ptrs))(*[p or None for p in raw_ptrs])
+        _check(self.lib.ym_calibrate(self.ctx, C.c_void_p(x_ptr), B, H, W, C.byref(args), C.c_void_p(dets_ptr),
+                                     C.c_void_p(counts_ptr), arr, len(raw_ptrs), C.c_void_p(stream)))
 
     def masks(self, dets_ptr, B, max_det, offsets_ptr, total, H, W, masks_ptr, nonempty_ptr, stream):
         _check(self.lib.ym_masks(self.ctx, C.c_void_p(dets_ptr), B, max_det, C.c_void_p(offsets_ptr), total, H, W,

@@ -6,6 +6,12 @@ part — packing every conv as a K-contiguous GEMM B operand [N][Kpad] with K or
 implicit-GEMM loader (`csrc/ym_conv.hip`), the stem's Cin padded 3→8, ConvTranspose2d(2,2) re-laid out as a 1x1
 GEMM with N = 4·C (pixel-shuffle epilogue), depthwise weights as [9][C] fp32.
 
+int8 plans (dtype "i8", the runtime of the reference's PostTrainingQuantizer.convert,
+`optimization/quantization/quantizers.py:77`): weights quantized with the torch.ao observer of the calibrated
+backend, K padded to 16-channel granules per tap, and per op a `QRec` (csrc/ym_common.h: requantisation of the conv
+output, the 256-entry post-activation table, the stored tensor's / residual's / input's quantisation), the fp32
+s_in·s_w per output channel and the int32 zero-point correction Σ_k (128 - z_in)·w (activations are stored as q - 128).
+
 Blob layout (int32 little-endian; parsed by `csrc/ym_runtime.cpp:ym_load_weights`):
   header[32] | buffers[nbuf][8] | ops[nop][32] | names[nop][48 bytes] | pad to 256 | weights
 """
@@ -20,8 +26,8 @@ from .arch import REG_MAX, STRIDES, GraphBuilder
 
 MAGIC = 0x4C504D59
 VERSION = 1
-OP_IDS = {"input": 1, "conv": 2, "dwconv": 3, "sppf": 4, "attn": 5, "decode": 6, "nms": 7}
-DTYPES = {"f16": 0, "f32": 1}
+OP_IDS = {"input": 1, "conv": 2, "dwconv": 3, "sppf": 4, "attn": 5, "decode": 6, "nms": 7, "requant": 8}
+DTYPES = {"f16": 0, "f32": 1, "i8": 2}
 BK = 64  # conv K is padded to the kernel K step (csrc/ym_conv.hip KSTEP)
 
 
@@ -76,14 +82,36 @@ def _dw_weights(key: str, sd):
     return np.ascontiguousarray(w.reshape(C, 9).T).astype(np.float32), b  # [9][C]
 
 
-def pack_model(scale: str, task: str, sd: Dict[str, np.ndarray], dtype: str = "f16") -> bytes:
-    g = GraphBuilder(scale, task)
-    return pack_graph(g, sd, dtype)
+def _qrec(inv_sc, zc, qlo, qhi, mode, post, inv_so=1.0, zo=0, s_r=0.0, z_r=0, s_in=0.0, z_in=0, inv_s_in=0.0) -> bytes:
+    """csrc/ym_common.h `QRec` (1088 bytes)."""
+    head = struct.pack("<fiiiifififif4i", inv_sc, int(zc), int(qlo), int(qhi), int(mode), inv_so, int(zo), s_r,
+                       int(z_r), s_in, int(z_in), inv_s_in, 0, 0, 0, 0)
+    return head + np.asarray(post, np.float32).tobytes()
 
 
-def pack_graph(g: GraphBuilder, sd: Dict[str, np.ndarray], dtype: str = "f16") -> bytes:
+def pack_model(scale: str, task: str, sd: Dict[str, np.ndarray], dtype: str = "f16", qparams: Dict = None) -> bytes:
+    g = GraphBuilder(scale, task, quant=dtype == "i8")
+    return pack_graph(g, sd, dtype, qparams)
+
+
+def pack_graph(g: GraphBuilder, sd: Dict[str, np.ndarray], dtype: str = "f16", qparams: Dict = None) -> bytes:
     if dtype not in DTYPES:
         raise ValueError(f"dtype {dtype!r} not in {list(DTYPES)}")
+    quant = dtype == "i8"
+    if quant != bool(g.quant):
+        raise ValueError("int8 blobs need GraphBuilder(quant=True), float blobs quant=False")
+    if quant:
+        from .quant import BACKENDS, inv32, post_table, qrange, quantize_weight
+        if not qparams or qparams.get("backend") not in BACKENDS:
+            raise ValueError("dtype 'i8' needs calibrated qparams (yolomi.quant.calibrate) with a known backend")
+        per_channel = BACKENDS[qparams["backend"]][1]
+        qlo, qhi = qrange(qparams["backend"])
+
+        def qp(key):
+            if key not in qparams:
+                raise ValueError(f"qparams has no entry {key!r}")
+            s_, z_ = qparams[key]
+            return float(np.float32(s_)), int(z_)
     np_dt = np.float16 if dtype == "f16" else np.float32
     arena = _WeightArena()
     op_recs: List[List[int]] = []
@@ -96,14 +124,21 @@ def pack_graph(g: GraphBuilder, sd: Dict[str, np.ndarray], dtype: str = "f16") -
             w, b = _conv_weights(a, sd)  # (N, k, k, cin)
             src0 = a["src0"]
             C0 = src0.C
-            if src0.buf is g.input:  # stem: RGB padded to 8 channels
+            stem = src0.buf is g.input
+            if quant:
+                w, sw = quantize_weight(w, per_channel and not a.get("convT"))  # int8 (N, k, k, cin), fp32 (N,)
+            if stem:  # stem: RGB padded to 8 channels
                 pad = 8 - C0
-                w = np.concatenate([w, np.zeros(w.shape[:3] + (pad,), np.float32)], axis=3)
+                w = np.concatenate([w, np.zeros(w.shape[:3] + (pad,), w.dtype)], axis=3)
                 C0 = 8
+            elif quant and C0 % 16:  # int8 K chunks are 16 channels of one tap
+                pad = 16 - C0 % 16
+                w = np.concatenate([w, np.zeros(w.shape[:3] + (pad,), w.dtype)], axis=3)
+                C0 += pad
             N = w.shape[0]
             K = w.shape[1] * w.shape[2] * w.shape[3]
             Kpad = (K + BK - 1) // BK * BK
-            wp = np.zeros((N, Kpad), np.float32)
+            wp = np.zeros((N, Kpad), np.int8 if quant else np.float32)
             wp[:, :K] = w.reshape(N, K)
             src1 = a["src1"]
             C1 = src1.C if src1 is not None else 0
@@ -113,15 +148,40 @@ def pack_graph(g: GraphBuilder, sd: Dict[str, np.ndarray], dtype: str = "f16") -
             r[10:13] = [src1.buf.id, src1.coff, C1] if src1 is not None else [-1, 0, 0]
             r[13:17] = [dst.buf.id, dst.coff, a["anchor_level"], int(bool(a["shuffle2x2"]))]
             r[17:19] = [res.buf.id, res.coff] if res is not None else [-1, 0]
-            r[19] = arena.add(wp.astype(np_dt))
+            r[19] = arena.add(wp if quant else wp.astype(np_dt))
             r[20] = arena.add(b.astype(np.float32))
             r[21] = Kpad
+            if quant:
+                s_in, z_in = qp("act:input" if stem else src0.buf.qkey)
+                so, zo = qp("out:" + a["wkey"])
+                d = dst.buf
+                mode = 2 if d.f32 else (1 if d.qkind == "out" else 0)
+                s_b, z_b = (1.0, 0) if mode else qp(d.qkey)
+                s_r, z_r = qp(res.buf.qkey) if res is not None else (0.0, 0)
+                rec = _qrec(inv32(so), zo, qlo, qhi, mode, post_table(so, zo, bool(a["act"])), inv32(s_b), z_b, s_r,
+                            z_r, s_in, z_in, inv32(s_in))
+                biasi = np.zeros(N, np.int64) if stem else (128 - z_in) * wp.astype(np.int64).sum(1)
+                assert np.abs(biasi).max() < 2 ** 31
+                r[22] = arena.add(np.frombuffer(rec, np.uint8))
+                r[23] = arena.add((np.float32(s_in) * sw).astype(np.float32))
+                r[24] = arena.add(biasi.astype(np.int32))
         elif op.kind == "dwconv":
             w9, b = _dw_weights(a["wkey"], sd)
             r[3], r[5] = a["C"], int(bool(a["act"]))
             r[6], r[7] = a["src"].buf.id, a["src"].coff
             r[13], r[14] = a["dst"].buf.id, a["dst"].coff
-            r[19], r[20] = arena.add(w9), arena.add(b)
+            if quant:
+                wq, sw = quantize_weight(np.ascontiguousarray(w9.T), per_channel)  # (C, 9): per output channel
+                s_in, z_in = qp(a["src"].buf.qkey)
+                so, zo = qp("out:" + a["wkey"])
+                s_b, z_b = qp(a["dst"].buf.qkey)
+                rec = _qrec(inv32(so), zo, qlo, qhi, 0, post_table(so, zo, bool(a["act"])), inv32(s_b), z_b,
+                            s_in=s_in, z_in=z_in)
+                r[19], r[20] = arena.add(np.ascontiguousarray(wq.T)), arena.add(b)
+                r[22] = arena.add(np.frombuffer(rec, np.uint8))
+                r[23] = arena.add((np.float32(s_in) * sw).astype(np.float32))
+            else:
+                r[19], r[20] = arena.add(w9), arena.add(b)
         elif op.kind == "sppf":
             r[3] = a["C"]
             r[7] = a["src"].coff
@@ -131,8 +191,28 @@ def pack_graph(g: GraphBuilder, sd: Dict[str, np.ndarray], dtype: str = "f16") -
             r[3], r[4], r[5], r[9] = a["C"], a["nh"], a["kd"], a["hd"]
             r[6], r[7] = a["qkv"].buf.id, a["qkv"].coff
             r[13], r[14] = a["dst"].buf.id, a["dst"].coff
-            r[19], r[20] = arena.add(w9), arena.add(b)
             r[21] = struct.unpack("<i", struct.pack("<f", float(np.float32(a["kd"] ** -0.5))))[0]
+            if quant:
+                wq, sw = quantize_weight(np.ascontiguousarray(w9.T), per_channel)
+                s_in, z_in = qp(a["qkv"].buf.qkey)
+                so, zo = qp("out:" + a["wkey"])
+                s_b, z_b = qp(a["dst"].buf.qkey)
+                rec = _qrec(inv32(so), zo, qlo, qhi, 0, post_table(so, zo, False), inv32(s_b), z_b, s_in=s_in,
+                            z_in=z_in)
+                r[19], r[20] = arena.add(np.ascontiguousarray(wq.T)), arena.add(b)
+                r[22] = arena.add(np.frombuffer(rec, np.uint8))
+                r[23] = arena.add((np.float32(s_in) * sw).astype(np.float32))
+            else:
+                r[19], r[20] = arena.add(w9), arena.add(b)
+        elif op.kind == "requant":
+            src, dst = a["src"], a["dst"]
+            r[3] = dst.C
+            r[6], r[7], r[9] = src.buf.id, src.coff, int(bool(a["up"]))
+            r[13], r[14] = dst.buf.id, dst.coff
+            s_in, z_in = qp(src.buf.qkey)
+            s_b, z_b = qp(dst.buf.qkey)
+            rec = _qrec(1.0, 0, qlo, qhi, 0, np.zeros(256, np.float32), inv32(s_b), z_b, s_in=s_in, z_in=z_in)
+            r[22] = arena.add(np.frombuffer(rec, np.uint8))
         op_recs.append(r)
         nm = op.name.encode()[:47]
         names.append(nm + b"\0" * (48 - len(nm)))
@@ -149,7 +229,7 @@ def pack_graph(g: GraphBuilder, sd: Dict[str, np.ndarray], dtype: str = "f16") -
     hdr[17] = g.proto_buf.id if g.task == "segment" else -1
     hdr[18] = g.no
     head = struct.pack("<32i", *hdr)
-    bufs = b"".join(struct.pack("<8i", b.C, b.f, int(b.f32), 0, 0, 0, 0, 0) for b in g.buffers)
+    bufs = b"".join(struct.pack("<8i", b.Cs or b.C, b.f, int(b.f32), 0, 0, 0, 0, 0) for b in g.buffers)
     ops = b"".join(struct.pack("<32i", *rr) for rr in op_recs)
     meta = head + bufs + ops + b"".join(names)
     meta += b"\0" * ((-len(meta)) % 256)
