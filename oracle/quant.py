@@ -28,6 +28,9 @@ the build's explicit restatement of that qconfig on the BN-fused YOLO11 graph (A
     tensor's; terminal head outputs (Detect box/cls, Segment coefficients, Proto.cv3) are dequantised to float;
   * max-pool and nearest upsample act on the quantized values; DFL's fixed arange projection is part of the float
     decode; ConvTranspose2d weights are per-tensor on both backends;
+  * the attention core (q·kᵀ·scale, softmax, ·v, on the dequantised fp32 q/k/v) is evaluated in float64 and rounded
+    to fp32 once, at its output: an order-independent float island, so the int8 model is bit-reproducible across
+    implementations (fp32 accumulation would make one rounding flip cascade through the later int8 layers);
   * the weights quantized are the BN-fused fp32 weights of an elementwise fold (W * (g / sqrt(eps + var)),
     b' = beta - (g * mean) / sqrt(var + eps), eps 1e-3, IEEE-rounded sqrt): `fuse_conv_and_bn` without its
     diag-matrix BLAS product.
@@ -138,6 +141,7 @@ class _Ctx:
         self.obs: Dict[str, HistogramObserver] = {}
         self.qp = qparams or {}
         self.wcache: Dict[str, tuple] = {}
+        self.trace: Optional[Dict[str, "QT"]] = None  # quant mode: every stored tensor by quantisation key
 
     @property
     def quant(self) -> bool:
@@ -156,7 +160,10 @@ class _Ctx:
     def store(self, name: str, v: torch.Tensor):
         """A float tensor becomes a stored tensor (quantized with act:<name>)."""
         self._observe("act:" + name, v)
-        return self.qwith(name, v)
+        q = self.qwith(name, v)
+        if self.trace is not None and self.quant:
+            self.trace["act:" + name] = q
+        return q
 
     def qwith(self, name: str, v: torch.Tensor):
         """Quantize with act:<name> without observing (a member of a concat observed as a whole)."""
@@ -170,7 +177,10 @@ class _Ctx:
             c = torch.cat(parts, 1)
             self._observe("act:" + name, c)
             return c
-        return QT(torch.cat([p.q for p in parts], 1), parts[0].s, parts[0].z)
+        c = QT(torch.cat([p.q for p in parts], 1), parts[0].s, parts[0].z)
+        if self.trace is not None:
+            self.trace["act:" + name] = c
+        return c
 
     def deq(self, x):
         return x.deq() if self.quant else x
@@ -213,6 +223,9 @@ class _Ctx:
         y = y + mod.bias.detach().float().view(1, -1, 1, 1)
         so, zo = self.qp["out:" + name]
         stored = QT(quantize(y, so, zo, self.qmin, self.qmax), so, zo)
+        if self.trace is not None:
+            self.trace["out:" + name] = stored
+            self.trace["y:" + name] = y
         deq = stored.deq()
         return (silu64(deq) if act else deq), stored
 
@@ -279,8 +292,12 @@ def _psablock(ctx, p, blk, b):
     _, qkv = ctx.conv(p + ".attn.qkv", at.qkv.conv, b, False)  # stored as is (its own output quantisation)
     qkvf = ctx.deq(qkv)
     q, k, v = qkvf.view(B, nh, 2 * kd + hd, N).split([kd, kd, hd], dim=2)
-    attn = ((q.transpose(-2, -1) @ k) * at.scale).softmax(dim=-1)
-    o = (v @ attn.transpose(-2, -1)).view(B, C, H, W)
+    if ctx.quant:  # the float island of the int8 model, evaluated in float64 and rounded once (see module docstring)
+        s64 = (q.double().transpose(-2, -1) @ k.double()) * float(F32(at.scale))
+        o = (v.double() @ s64.softmax(dim=-1).transpose(-2, -1)).float().view(B, C, H, W)
+    else:
+        attn = ((q.transpose(-2, -1) @ k) * at.scale).softmax(dim=-1)
+        o = (v @ attn.transpose(-2, -1)).view(B, C, H, W)
     if ctx.quant:
         vq = QT(qkv.q.view(B, nh, 2 * kd + hd, N)[:, :, 2 * kd:, :].reshape(B, C, H, W), qkv.s, qkv.z)
     else:

@@ -1,12 +1,11 @@
 """GPU tests of the int8 PTQ path (csrc/ym_conv_i8.hip) through the C-ABI, against the int8 oracle
 (oracle/quant.py) and its committed fixtures.
 
-Parity bar: with the SAME calibrated qparams, every int8 tensor the GPU stores equals the oracle's bit for bit up to
-the C2PSA attention (pure integer / explicitly rounded fp32 arithmetic on both sides); the attention's float softmax
-and matmuls differ in summation order, so from there on a small fraction of stored values may differ by one
-quantisation step (bounded below); detections then match within 1e-3 px / 1e-3 score (>= 90 % matched, the rest an
-NMS/threshold flip of a near-tie).  The product's own calibration (exact-f32 plan + torch.ao observers on the host)
-reproduces the oracle's qparams.
+Parity bar: with the SAME calibrated qparams, every int8 tensor the GPU stores equals the oracle's BIT FOR BIT
+(integer MACs, one rounding per fp32 step on both sides, and the attention's float island evaluated in float64 and
+rounded once: only a float64 result straddling an fp32 rounding boundary — odds ~1e-8 per element — could differ),
+the fp32 head rows are identical, and so are the detections.  The product's own calibration (exact-f32 plan +
+torch.ao observers on the host) reproduces the oracle's qparams.
 """
 import json
 import os
@@ -67,15 +66,12 @@ def test_i8_stored_tensors_match_oracle(name):
         diff = (got - ref).abs()
         frac = float((diff > 0).float().mean())
         report.append((i, frac, float(diff.max())))
-        if i <= 9:  # before the float attention island: bit-exact
-            assert frac == 0.0, (b.name, frac, float(diff.max()))
-        else:
-            assert frac < 2e-3 and float(diff.max()) <= 3, (b.name, frac, float(diff.max()))
+        assert frac <= 1e-5, (b.name, frac, float(diff.max()), report)
     no = eng.graph.no
     ref_h = torch.cat([f.reshape(B, no, -1) for f in ex["feats"]], 2).transpose(1, 2)
     got_h = eng.read_buffer(eng.graph.anchor_buf.id, B).reshape(B, -1, eng.graph.anchor_buf.C)[..., :no]
     hd = (got_h - ref_h).abs()
-    assert float((hd > 1e-6).float().mean()) < 5e-3, report
+    assert float((hd > 0).float().mean()) <= 1e-5, report
 
 
 @pytest.mark.parametrize("name", list(I8_FIXTURES))
@@ -88,7 +84,7 @@ def test_i8_detections_match_golden(name):
         match_image(np.array(r, np.float32).reshape(-1, 6), got.boxes.data.cpu().numpy(), g["conf"], g["iou"], 1e-3,
                     1e-3, rep=rep)
     total = sum(len(d) for d in g["dets"])
-    assert rep.matched + rep.exempt >= 0.9 * total, (str(rep), rep.failures[:3])
+    assert rep.ok and rep.matched >= total - rep.exempt, (str(rep), rep.failures[:3])
 
 
 def test_i8_graph_replay_bitwise_equals_eager():

@@ -53,6 +53,25 @@ __device__ __forceinline__ int f2ord(float f) {
 }
 __device__ __forceinline__ float ord2f(int i) { return __int_as_float(i >= 0 ? i : i ^ 0x7FFFFFFF); }
 
+// The input statistics word of a forward (LoadTensor's batch max) is spread over YM_CTL_SLOTS atomicMax targets 64 B
+// apart (same-address atomics serialise at ~90 per µs); readers take the max of the slots.
+constexpr int YM_CTL_SLOTS = 16, YM_CTL_STRIDE = 16;  // ints
+__device__ __forceinline__ float ym_input_max(const float* ctl) {
+  const int* c = reinterpret_cast<const int*>(ctl);
+  int m = c[0];
+#pragma unroll
+  for (int s = 1; s < YM_CTL_SLOTS; ++s) m = max(m, c[s * YM_CTL_STRIDE]);
+  return ord2f(m);
+}
+
+// A value the compiler cannot see through: keeps `a * b` and a following `+ c` as two roundings.  hipcc compiles
+// with -ffp-contract=fast, which fuses across statements, ignores `#pragma clang fp contract`, and sees straight through
+// HIP's __fmul_rn / __fadd_rn (plain operators); parity with torch's separate fp32 ops needs the two roundings.
+__device__ __forceinline__ float ym_opaque(float x) {
+  asm volatile("" : "+v"(x));
+  return x;
+}
+
 __device__ __forceinline__ float ym_silu(float x) { return x / (1.0f + expf(-x)); }
 // SiLU from the hardware exp2 / reciprocal (each ~1 ulp): for epilogues whose outputs are rounded to fp16 anyway
 __device__ __forceinline__ float ym_silu_fast(float x) {

@@ -159,7 +159,7 @@ __global__ __launch_bounds__(WM * WN * WK * 64) void conv_igemm(const ConvArgs a
   }
 
   bool div255 = false;
-  if constexpr (KIND == 0) div255 = ord2f(*reinterpret_cast<const int*>(a.ctl)) > 1.0f + a.eps;
+  if constexpr (KIND == 0) div255 = ym_input_max(a.ctl) > 1.0f + a.eps;
   auto gather = [&](int i, int s) -> F {
     const int chunk = g * 2 * KS + 2 * s + h;
     if (!pv[i] || chunk >= a.Kc) return Vec8<T>::zero();

@@ -7,8 +7,8 @@
 //   Σ_k (128 - z_in)·w, which makes acc = Σ (q - z_in)·w exactly (3x3 padding taps read the byte z_in - 128, i.e.
 //   real zero); then y = float(acc)·(s_in·s_w) + bias, q_c = clamp(rint(y / s_out) + z_out), and the epilogue maps
 //   q_c through the op's 256-entry `post` table (SiLU or plain dequant of the requantised output), adds the residual
-//   ((q_r - z_r)·s_r), and quantizes into the stored tensor (or writes fp32 head rows).  All float steps use
-//   explicit __fmul_rn / __fadd_rn (no FMA contraction) so they round exactly as the oracle's torch fp32 ops.
+//   ((q_r - z_r)·s_r), and quantizes into the stored tensor (or writes fp32 head rows).  Every float step rounds
+//   once, as the oracle's separate torch fp32 ops do (ym_opaque keeps hipcc from fusing a multiply into an add).
 //
 // Kernels: conv_i8 (implicit GEMM over NHWC int8, same transposed orientation and tile structure as
 // csrc/ym_conv.hip: MFMA A = weights [N][Kpad], B = im2col gathered straight from NHWC, one 16-byte K chunk = 16
@@ -33,14 +33,14 @@ __device__ __forceinline__ int clampi(int v, int lo, int hi) { return v < lo ? l
 
 // quantized::conv2d output requantisation
 __device__ __forceinline__ int requant_out(int acc, float sasw, float bias, const QRec* Q) {
-  const float y = __fadd_rn(__fmul_rn((float)acc, sasw), bias);
+  const float y = ym_opaque((float)acc * sasw) + bias;  // two roundings (no FMA), as torch's mul then add
   return clampi((int)rintf(__fmul_rn(y, Q->inv_sc)) + Q->zc, Q->qlo, Q->qhi);
 }
 // quantize a float into a stored tensor: returns the int8 storage value q - 128
 __device__ __forceinline__ int quant_store(float v, float inv, int z, int lo, int hi) {
   return clampi((int)rintf(__fmul_rn(v, inv)) + z, lo, hi) - 128;
 }
-__device__ __forceinline__ float deq(int q, int z, float s) { return __fmul_rn((float)(q - z), s); }
+__device__ __forceinline__ float deq(int q, int z, float s) { return ym_opaque((float)(q - z) * s); }
 __device__ __forceinline__ int pack4(const int* v) {
   return (v[0] & 0xFF) | ((v[1] & 0xFF) << 8) | ((v[2] & 0xFF) << 16) | ((unsigned)(v[3] & 0xFF) << 24);
 }
@@ -346,7 +346,7 @@ __global__ __launch_bounds__(256) void stem_i8(const ConvArgs a) {
   const int b = bid / tiles_y;
   const int oy0 = ty * TH, ox0 = tx * TW;
   const int iy0 = 2 * oy0 - 1, xs = 2 * ox0 - 4;
-  const bool div = ord2f(*reinterpret_cast<const int*>(a.ctl)) > 1.0f + a.eps;
+  const bool div = ym_input_max(a.ctl) > 1.0f + a.eps;
   const size_t HW = (size_t)a.Hin * a.Win;
   const float* img = a.nchw + (size_t)b * 3 * HW;
   const float inv = Q->inv_s_in;
@@ -473,18 +473,19 @@ __global__ __launch_bounds__(256) void dwconv3x3_i8(const DwArgs a) {
 
 // ------------------------------------------------------------------------------------------------- attention
 // C2PSA Attention on the int8 qkv tensor (stored in the qkv conv's own output quantisation): q, k, v dequantised to
-// fp32, S = q·kᵀ·scale, fp32 softmax, O = P·V (as csrc/ym_misc.hip attn_psa), + pe(v) as a quantized depthwise conv
-// (int MACs on the stored v bytes, requantised, dequantised), then the sum is quantized into the attn.x tensor.
+// fp32; S = q·kᵀ·scale, softmax and O = P·V evaluated in float64 and rounded to fp32 once (the oracle's definition of
+// the int8 model's float island: order-independent, so the int8 outputs are bit-reproducible); + pe(v) as a quantized
+// depthwise conv (int MACs on the stored v bytes, requantised, dequantised); the sum is quantized into attn.x.
 constexpr int AKD = 32, AHD = 64;
 
 template <int QB>
 __global__ __launch_bounds__(256) void attn_psa_i8(const AttnArgs a) {
-  extern __shared__ float S[];  // [QB][N], then Q [QB][AKD], then V chunk [64][AHD]
+  extern __shared__ double S[];  // [QB][N] doubles, then Q [QB][AKD] floats, then a V chunk [64][AHD] floats
   __shared__ float post[256];
   const QRec* Qr = a.q;
   post[threadIdx.x] = Qr->post[threadIdx.x];
   const int N = a.N;
-  float* Qs = S + (size_t)QB * N;
+  float* Qs = reinterpret_cast<float*>(S + (size_t)QB * N);
   const int nqb = (N + QB - 1) / QB;
   const int qb = blockIdx.x % nqb;
   const int bh = blockIdx.x / nqb;
@@ -497,6 +498,7 @@ __global__ __launch_bounds__(256) void attn_psa_i8(const AttnArgs a) {
   const int hq = a.q_coff + h * per;
   const float s_in = Qr->s_in;
   const int z_in = Qr->z_in;
+  const double scale = (double)a.scale;
   for (int i = tid; i < QB * AKD; i += 256) {
     const int r = i / AKD, c = i % AKD;
     const int n = qb * QB + r;
@@ -504,34 +506,35 @@ __global__ __launch_bounds__(256) void attn_psa_i8(const AttnArgs a) {
   }
   __syncthreads();
   for (int key = tid; key < N; key += 256) {
-    float k[AKD];
+    double k[AKD];
     const i8* kp = qkv + (img + key) * a.q_ctot + hq + a.kd;
 #pragma unroll
     for (int c8 = 0; c8 < AKD / 8; ++c8) {
       const Vec8<i8>::type v = Vec8<i8>::load(kp + c8 * 8);
 #pragma unroll
-      for (int e = 0; e < 8; ++e) k[c8 * 8 + e] = (c8 * 8 + e < a.kd) ? deq((int)v[e] + 128, z_in, s_in) : 0.f;
+      for (int e = 0; e < 8; ++e)
+        k[c8 * 8 + e] = (c8 * 8 + e < a.kd) ? (double)deq((int)v[e] + 128, z_in, s_in) : 0.0;
     }
-#pragma unroll 4
+#pragma unroll 2
     for (int q = 0; q < QB; ++q) {
-      float s = 0.f;
+      double s = 0.0;
 #pragma unroll
-      for (int c = 0; c < AKD; ++c) s = fmaf(Qs[q * AKD + c], k[c], s);
-      S[q * N + key] = s * a.scale;
+      for (int c = 0; c < AKD; ++c) s = fma((double)Qs[q * AKD + c], k[c], s);
+      S[q * N + key] = s * scale;
     }
   }
   __syncthreads();
   {
     constexpr int TPR = 256 / QB;
     const int q = tid / TPR, sub = tid % TPR;
-    float* row = S + (size_t)q * N;
-    float m = -INFINITY;
-    for (int j = sub; j < N; j += TPR) m = fmaxf(m, row[j]);
+    double* row = S + (size_t)q * N;
+    double m = -INFINITY;
+    for (int j = sub; j < N; j += TPR) m = fmax(m, row[j]);
 #pragma unroll
-    for (int o = TPR / 2; o > 0; o >>= 1) m = fmaxf(m, __shfl_xor(m, o));
-    float sum = 0.f;
+    for (int o = TPR / 2; o > 0; o >>= 1) m = fmax(m, __shfl_xor(m, o));
+    double sum = 0.0;
     for (int j = sub; j < N; j += TPR) {
-      const float e = expf(row[j] - m);
+      const double e = exp(row[j] - m);
       row[j] = e;
       sum += e;
     }
@@ -542,9 +545,9 @@ __global__ __launch_bounds__(256) void attn_psa_i8(const AttnArgs a) {
   __syncthreads();
   constexpr int QPG = QB / 4;
   const int d = tid & 63, qg = tid >> 6;
-  float o[QPG];
+  double o[QPG];
 #pragma unroll
-  for (int i = 0; i < QPG; ++i) o[i] = 0.f;
+  for (int i = 0; i < QPG; ++i) o[i] = 0.0;
   float* Vs = Qs + QB * AKD;
   for (int k0 = 0; k0 < N; k0 += 64) {
     __syncthreads();
@@ -564,9 +567,9 @@ __global__ __launch_bounds__(256) void attn_psa_i8(const AttnArgs a) {
     __syncthreads();
     const int kn = N - k0 < 64 ? N - k0 : 64;
     for (int kj = 0; kj < kn; ++kj) {
-      const float v = Vs[kj * AHD + d];
+      const double v = (double)Vs[kj * AHD + d];
 #pragma unroll
-      for (int i = 0; i < QPG; ++i) o[i] = fmaf(S[(qg + 4 * i) * N + k0 + kj], v, o[i]);
+      for (int i = 0; i < QPG; ++i) o[i] = fma(S[(qg + 4 * i) * N + k0 + kj], v, o[i]);
     }
   }
   if (d >= a.hd) return;
@@ -594,7 +597,7 @@ __global__ __launch_bounds__(256) void attn_psa_i8(const AttnArgs a) {
     }
     const float pe = post[requant_out(acc, sa, pb, Qr)];
     dst[((size_t)b * a.d_P + n) * a.d_ctot + a.d_coff + ch] =
-        (i8)quant_store(__fadd_rn(o[i], pe), Qr->inv_so, Qr->zo, Qr->qlo, Qr->qhi);
+        (i8)quant_store((float)o[i] + pe, Qr->inv_so, Qr->zo, Qr->qlo, Qr->qhi);
   }
 }
 
@@ -661,7 +664,7 @@ hipError_t ym_launch_dwconv_i8(const DwArgs& a, hipStream_t st) {
 hipError_t ym_launch_attn_i8(const AttnArgs& a, hipStream_t st) {
   if (a.kd > AKD || a.hd > AHD || !a.q || !a.pe_wq) return hipErrorInvalidValue;
   const size_t budget = 150 * 1024;
-  auto lds = [&](int qb) { return ((size_t)qb * a.N + (size_t)qb * AKD + 64 * AHD) * sizeof(float); };
+  auto lds = [&](int qb) { return (size_t)qb * a.N * sizeof(double) + ((size_t)qb * AKD + 64 * AHD) * sizeof(float); };
   auto wgs = [&](int qb) { return (long)a.B * a.nh * ((a.N + qb - 1) / qb); };
   if (lds(32) <= budget && wgs(32) >= 512)
     hipLaunchKernelGGL((attn_psa_i8<32>), dim3(a.B * a.nh * ((a.N + 31) / 32)), dim3(256), lds(32), st, a);

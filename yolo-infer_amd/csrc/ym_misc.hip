@@ -11,18 +11,27 @@ namespace {
 // LoadTensor._single_check: `if im.max() > 1 + finfo(dtype).eps: im = im.float() / 255` over the WHOLE batch.
 // ctl[0] holds max as an order-preserving int; ctl is reset by the init kernel at the start of every forward.
 // The division itself happens in the stem conv's loader (csrc/ym_conv.hip KIND 0), which reads the NCHW batch.
-__global__ void init_ctl(float* ctl, int* counts, int B, int* cnt, int cnt_len) {
-  const int t = threadIdx.x;
-  if (t == 0) reinterpret_cast<int*>(ctl)[0] = f2ord(-INFINITY);
-  for (int b = t; b < B; b += blockDim.x) counts[b] = 0;
-  for (int i = t; i < cnt_len; i += blockDim.x) cnt[i] = 0;  // split-K tile counters (csrc/ym_conv_dma.hip)
+__global__ __launch_bounds__(256) void init_ctl(float* ctl, int* counts, int B, int* cnt, int cnt_len) {
+  const int t = blockIdx.x * blockDim.x + threadIdx.x;
+  if (t < YM_CTL_SLOTS) reinterpret_cast<int*>(ctl)[t * YM_CTL_STRIDE] = f2ord(-INFINITY);
+  for (int b = t; b < B; b += gridDim.x * blockDim.x) counts[b] = 0;
+  int4* c4 = reinterpret_cast<int4*>(cnt);  // split-K tile counters (csrc/ym_conv_dma.hip)
+  for (int i = t; i < cnt_len / 4; i += gridDim.x * blockDim.x) c4[i] = make_int4(0, 0, 0, 0);
 }
 
 __global__ __launch_bounds__(256) void max_reduce(const float* __restrict__ x, long n, float* ctl) {
   float m = -INFINITY;
   const long n4 = n >> 2;
   const f32x4* x4 = reinterpret_cast<const f32x4*>(x);
-  for (long i = blockIdx.x * (long)blockDim.x + threadIdx.x; i < n4; i += (long)gridDim.x * blockDim.x) {
+  const long step = (long)gridDim.x * blockDim.x;
+  long i = blockIdx.x * (long)blockDim.x + threadIdx.x;
+  for (; i + 3 * step < n4; i += 4 * step) {  // four independent 16-byte loads in flight per lane
+    const f32x4 v0 = x4[i], v1 = x4[i + step], v2 = x4[i + 2 * step], v3 = x4[i + 3 * step];
+    const f32x4 a = {fmaxf(v0[0], v1[0]), fmaxf(v0[1], v1[1]), fmaxf(v0[2], v1[2]), fmaxf(v0[3], v1[3])};
+    const f32x4 b = {fmaxf(v2[0], v3[0]), fmaxf(v2[1], v3[1]), fmaxf(v2[2], v3[2]), fmaxf(v2[3], v3[3])};
+    m = fmaxf(m, fmaxf(fmaxf(fmaxf(a[0], b[0]), fmaxf(a[1], b[1])), fmaxf(fmaxf(a[2], b[2]), fmaxf(a[3], b[3]))));
+  }
+  for (; i < n4; i += step) {
     const f32x4 v = x4[i];
     m = fmaxf(m, fmaxf(fmaxf(v[0], v[1]), fmaxf(v[2], v[3])));
   }
@@ -35,7 +44,7 @@ __global__ __launch_bounds__(256) void max_reduce(const float* __restrict__ x, l
   __syncthreads();
   if (threadIdx.x == 0) {
     m = fmaxf(fmaxf(wm[0], wm[1]), fmaxf(wm[2], wm[3]));
-    atomicMax(reinterpret_cast<int*>(ctl), f2ord(m));
+    atomicMax(reinterpret_cast<int*>(ctl) + (blockIdx.x % YM_CTL_SLOTS) * YM_CTL_STRIDE, f2ord(m));
   }
 }
 
@@ -336,28 +345,43 @@ __global__ __launch_bounds__(256) void decode_anchors(const DecodeArgs a) {
   const int base = threadIdx.x & 60;
   const float d0 = __shfl(dist, base), d1 = __shfl(dist, base + 1), d2 = __shfl(dist, base + 2),
               d3 = __shfl(dist, base + 3);
-  if (sub != 0 || !valid) return;
-  int l = 0;
-  while (l + 1 < a.nl && ai >= a.lvl_off[l + 1]) ++l;
-  const int p = ai - a.lvl_off[l];
-  const float ax = (float)(p % a.lvl_W[l]) + 0.5f;
-  const float ay = (float)(p / a.lvl_W[l]) + 0.5f;
-  const float st = a.lvl_stride[l];
-  const float x1 = ax - d0, y1 = ay - d1;
-  const float x2 = ax + d2, y2 = ay + d3;
-  const float cx = (x1 + x2) / 2.0f * st, cy = (y1 + y2) / 2.0f * st;
-  const float w = (x2 - x1) * st, hh = (y2 - y1) * st;
-  const float hw = w / 2.0f, hh2 = hh / 2.0f;
-  a.boxes[idx] = make_float4(cx - hw, cy - hh2, cx + hw, cy + hh2);
-  a.scores[idx] = best;
-  a.cls[idx] = bi;
-  bool cand = best > a.conf;
-  if (cand && a.has_classes) cand = (a.classes[bi >> 5] >> (bi & 31)) & 1u;
-  if (cand) {
-    const int slot = atomicAdd(&a.counts[b], 1);
-    a.keys[(size_t)b * a.kstride + slot] =
-        ((unsigned long long)__float_as_uint(best) << 32) | (unsigned long long)(0xFFFFFFFFu - (unsigned)ai);
+  // candidates are appended per workgroup: LDS slots first, then ONE global atomic per (workgroup, image) — the 64
+  // anchors of a workgroup span at most 5 images (A >= 21).  (Per-candidate atomics on the B per-image counters serialised:
+  // thousands of same-address atomics at ~90 per µs.)
+  __shared__ int wg_cnt[8], wg_base[8];
+  if (threadIdx.x < 8) wg_cnt[threadIdx.x] = 0;
+  __syncthreads();
+  const int b_first = (int)(a0 / a.A);
+  bool cand = false;
+  int slot = 0;
+  unsigned long long key = 0;
+  if (sub == 0 && valid) {
+    int l = 0;
+    while (l + 1 < a.nl && ai >= a.lvl_off[l + 1]) ++l;
+    const int p = ai - a.lvl_off[l];
+    const float ax = (float)(p % a.lvl_W[l]) + 0.5f;
+    const float ay = (float)(p / a.lvl_W[l]) + 0.5f;
+    const float st = a.lvl_stride[l];
+    const float x1 = ax - d0, y1 = ay - d1;
+    const float x2 = ax + d2, y2 = ay + d3;
+    const float cx = (x1 + x2) / 2.0f * st, cy = (y1 + y2) / 2.0f * st;
+    const float w = (x2 - x1) * st, hh = (y2 - y1) * st;
+    const float hw = w / 2.0f, hh2 = hh / 2.0f;
+    a.boxes[idx] = make_float4(cx - hw, cy - hh2, cx + hw, cy + hh2);
+    a.scores[idx] = best;
+    a.cls[idx] = bi;
+    cand = best > a.conf;
+    if (cand && a.has_classes) cand = (a.classes[bi >> 5] >> (bi & 31)) & 1u;
+    if (cand) {
+      slot = atomicAdd(&wg_cnt[b - b_first], 1);
+      key = ((unsigned long long)__float_as_uint(best) << 32) | (unsigned long long)(0xFFFFFFFFu - (unsigned)ai);
   }
+  }
+  __syncthreads();
+  if (threadIdx.x < 8 && wg_cnt[threadIdx.x] > 0)
+    wg_base[threadIdx.x] = atomicAdd(&a.counts[b_first + threadIdx.x], wg_cnt[threadIdx.x]);
+  __syncthreads();
+  if (cand) a.keys[(size_t)b * a.kstride + wg_base[b - b_first] + slot] = key;
 }
 
 // ------------------------------------------------------------------------------------------------- NMS
@@ -389,7 +413,7 @@ __device__ __forceinline__ bool iou_gt(const float4 bi, float ai_area, const flo
   const float xx2 = fminf(bi.z, bj.z), yy2 = fminf(bi.w, bj.w);
   const float w = fmaxf(0.0f, __fsub_rn(xx2, xx1));
   const float h = fmaxf(0.0f, __fsub_rn(yy2, yy1));
-  const float inter = __fmul_rn(w, h);
+  const float inter = ym_opaque(w * h);  // one rounding per operation, as torchvision's CPU kernel (no fused FMA)
   const float ovr = __fdiv_rn(inter, __fsub_rn(__fadd_rn(ai_area, aj_area), inter));
   return (double)ovr > thr;
 }
@@ -538,11 +562,13 @@ hipError_t ym_launch_spin(int usec, hipStream_t st) {
 
 hipError_t ym_launch_prep(int dtype, const PrepArgs& a, int* counts, int B, hipStream_t st) {
   (void)dtype;
-  hipLaunchKernelGGL(init_ctl, dim3(1), dim3(256), 0, st, a.ctl, counts, B, a.cnt, a.cnt_len);
+  const int ib = (a.cnt_len / 4 + 255) / 256;
+  hipLaunchKernelGGL(init_ctl, dim3(ib < 1 ? 1 : (ib > 64 ? 64 : ib)), dim3(256), 0, st, a.ctl, counts, B, a.cnt,
+                     a.cnt_len);
   // one atomic per block: a few hundred same-address atomics, not thousands (one word takes ~90 per us)
   const long n = (long)a.B * a.C * a.H * a.W;
   long blocks = (n / 4 + 255) / 256;
-  if (blocks > 512) blocks = 512;
+  if (blocks > 1024) blocks = 1024;
   if (blocks < 1) blocks = 1;
   hipLaunchKernelGGL(max_reduce, dim3(blocks), dim3(256), 0, st, a.in, n, a.ctl);
   return hipGetLastError();

@@ -204,7 +204,7 @@ int ensure_workspace(ym_ctx* c, int B, int H, int W) {
   c->off_cls = off;    off = align_up(off + BA * 4, 256);
   c->off_keys = off;   off = align_up(off + (size_t)nB * c->kstride * 8, 256);
   c->off_counts = off; off = align_up(off + (size_t)nB * 4, 256);
-  c->off_ctl = off;    off = align_up(off + 256, 256);
+  c->off_ctl = off;    off = align_up(off + YM_CTL_SLOTS * YM_CTL_STRIDE * 4, 256);
   c->off_sboxes = off; off = align_up(off + BA * 16, 256);
   c->off_sareas = off; off = align_up(off + BA * 4, 256);
   c->off_sup = off;    off = align_up(off + BA, 256);

@@ -32,7 +32,7 @@ __global__ __launch_bounds__(256) void stem_conv3x3s2(const ConvArgs a) {
   const int b = bid / tiles_y;
   const int oy0 = ty * TH, ox0 = tx * TW;
   const int iy0 = 2 * oy0 - 1, xs = 2 * ox0 - 4;  // patch column 0 = input column xs (xs % 4 == 0)
-  const bool div = ord2f(*reinterpret_cast<const int*>(a.ctl)) > 1.0f + a.eps;
+  const bool div = ym_input_max(a.ctl) > 1.0f + a.eps;
   const size_t HW = (size_t)a.Hin * a.Win;
   const float* img = a.nchw + (size_t)b * 3 * HW;
   for (int i = threadIdx.x; i < 3 * PH * PW4; i += 256) {

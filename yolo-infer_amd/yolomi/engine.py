@@ -42,7 +42,9 @@ class Engine:
         self._out: Dict[int, tuple] = {}
         # Per-shape conv tile tables: on the first call of each (B, H, W) a table is taken from the writable tune
         # cache or the committed `tuned/` directory; failing both, ym_tune measures one on this GPU (and caches it).
-        self.autotune = os.environ.get("YM_AUTOTUNE", "1") != "0"
+        # The exact-f32 parity plan is never autotuned: its tiles (and so its fp32 summation orders) stay the fixed
+        # heuristic ones, so its results are reproducible from run to run.
+        self.autotune = os.environ.get("YM_AUTOTUNE", "1") != "0" and dtype != "f32"
         # Lanes: the batch runs as up to 4 concurrent image slices (parallel branches of one graph); conv tables are
         # per slice batch.  Default from YM_LANES (1).
         self.lanes = int(os.environ.get("YM_LANES", "1"))
