@@ -22,16 +22,20 @@ import sys
 
 ROOT = os.path.dirname(os.path.dirname(os.path.abspath(__file__)))
 PROF = os.path.join(ROOT, "profiles")
-CONV = re.compile(r"conv_igemm|conv_lds|conv_dma")
-STEM = re.compile(r"stem_conv3x3s2")
+CONV = re.compile(r"conv_igemm|conv_lds|conv_dma|conv_i8")
+STEM = re.compile(r"stem_conv3x3s2|stem_i8")
+CALIB = re.compile(r"conv_igemm<float, float|conv_igemmIffL")  # the f32 calibration forwards of an int8 run
 
 
 def family(name):
+    if CALIB.search(name):
+        return "calib_f32_conv"
     if STEM.search(name):
         return "stem"
     if CONV.search(name):
         return "conv"
-    for k in ("dwconv3x3", "sppf", "attn_psa", "decode_anchors", "nms_image", "init_ctl", "max_reduce", "spin_wait"):
+    for k in ("dwconv3x3", "sppf", "attn_psa", "decode_anchors", "nms_image", "init_ctl", "max_reduce", "spin_wait", "requant_copy",
+              "copyBuffer"):
         if k in name:
             return k
     return "other"
