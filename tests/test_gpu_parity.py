@@ -219,6 +219,7 @@ def test_results_contract_and_benchmark():
 
 # ------------------------------------------------------------------------------------------------ LDS-DMA conv configs
 DMA_FIRST = 17  # csrc/ym_conv.hip: ids >= 17 are the LDS-DMA / split-K kernels of csrc/ym_conv_dma.hip
+STREAM_FIRST = DMA_FIRST + 18  # then the streaming 1x1 / 3x3 kernels of csrc/ym_conv_stream.hip (15 configs)
 
 
 def _force_cfg(eng, x, cfg):
@@ -228,9 +229,10 @@ def _force_cfg(eng, x, cfg):
     eng.rt.set_op_cfg(B, H, W, [cfg if op.kind == "conv" else -1 for op in eng.graph.ops])
 
 
-@pytest.mark.parametrize("cfg", list(range(DMA_FIRST, DMA_FIRST + 18)))
+@pytest.mark.parametrize("cfg", list(range(DMA_FIRST, STREAM_FIRST + 15)))
 def test_dma_conv_configs_match_oracle(cfg):
-    """Every conv of yolo11n (1x1 two-source/upsampled, 3x3 s1/s2, residual, fp32 Detect rows) on one DMA config."""
+    """Every conv of yolo11n (1x1 two-source/upsampled, 3x3 s1/s2, residual, fp32 Detect rows) on one DMA or
+    streaming config (ops a config does not apply to fall back to the heuristic choice)."""
     m = model("n", "f16")
     eng = m.model.engine
     x = make_input("uniform", (11, 12), 640)

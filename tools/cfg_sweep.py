@@ -22,7 +22,7 @@ def main():
     ap.add_argument("--batch", type=int, default=8)
     ap.add_argument("--size", type=int, default=640)
     ap.add_argument("--ops", default=".")
-    ap.add_argument("--cfgs", default="0-34")
+    ap.add_argument("--cfgs", default="0-40")
     a = ap.parse_args()
     os.environ["YM_AUTOTUNE"] = "0"
     os.environ["YM_TUNE_TABLES"] = "0"
@@ -33,8 +33,10 @@ def main():
     x = synthetic_batch(a.batch, a.size, 1000, torch.device("cuda", 0))
     B, S = a.batch, a.size
     eng.run(x)
-    lo, hi = map(int, a.cfgs.split("-"))
-    cfgs = list(range(lo, hi + 1))
+    cfgs = []
+    for part in a.cfgs.split(","):
+        lo, _, hi = part.partition("-")
+        cfgs += list(range(int(lo), int(hi or lo) + 1))
     ops = eng.graph.ops
     sel = [i for i, op in enumerate(ops) if op.kind == "conv" and i > 1 and re.search(a.ops, op.name)]
     tab = {}

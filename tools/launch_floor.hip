@@ -40,15 +40,19 @@ double time_graph(hipStream_t st, int nk, F launch) {
 int main() {
   hipStream_t st;
   CK(hipStreamCreate(&st));
-  const int n = (8 << 20) / 16;
+  const int n = (8 << 20) / 16, nbig = (64 << 20) / 16;
   float4 *a, *b;
-  CK(hipMalloc(&a, n * 16));
-  CK(hipMalloc(&b, n * 16));
+  CK(hipMalloc(&a, nbig * 16));
+  CK(hipMalloc(&b, nbig * 16));
   const int NK = 100;
   printf("empty 1 block      : %.2f us/kernel\n", time_graph(st, NK, [](hipStream_t s) { hipLaunchKernelGGL(k_empty, 1, 64, 0, s); }));
   printf("empty 1024 blocks  : %.2f us/kernel\n", time_graph(st, NK, [](hipStream_t s) { hipLaunchKernelGGL(k_empty, 1024, 256, 0, s); }));
   printf("copy 8MB 512 blocks: %.2f us/kernel\n", time_graph(st, NK, [&](hipStream_t s) { hipLaunchKernelGGL(k_touch, 512, 256, 0, s, a, b, n); }));
   printf("copy 8MB + 48KB LDS: %.2f us/kernel\n", time_graph(st, NK, [&](hipStream_t s) { hipLaunchKernelGGL(k_touch_lds, 512, 256, 48 * 1024, s, a, b, n); }));
   printf("copy 64KB 16 blocks: %.2f us/kernel\n", time_graph(st, NK, [&](hipStream_t s) { hipLaunchKernelGGL(k_touch, 16, 256, 0, s, a, b, 4096); }));
+  for (int blocks : {2048, 4096, 8192}) {
+    const double us = time_graph(st, NK, [&](hipStream_t s) { hipLaunchKernelGGL(k_touch, blocks, 256, 0, s, a, b, nbig); });
+    printf("copy 64MB %5d blocks: %.2f us/kernel = %.0f GB/s (read+write)\n", blocks, us, 2.0 * 64 * 1048576 / us / 1e3);
+  }
   return 0;
 }

@@ -25,12 +25,17 @@ def main():
     ap.add_argument("--size", type=int, default=640)
     ap.add_argument("--dtype", default="f16")
     ap.add_argument("--reps", type=int, default=3)
+    ap.add_argument("--ops-out", default=None, help="write the op names of one forward, in launch order, to this file")
     a = ap.parse_args()
     from bench import synthetic_batch
     from core.model import YOLO11Model
     m = YOLO11Model(task=a.task, size=a.model, device="cuda:0", dtype=a.dtype)
     x = synthetic_batch(a.batch, a.size, 1000, torch.device("cuda", 0))
     eng = m.model.engine
+    if a.ops_out:
+        with open(a.ops_out, "w") as f:
+            for op in eng.graph.ops:
+                f.write(f"{op.name}\t{op.kind}\n")
     eng.run(x, use_graph=False)  # table lookup (or tuning) happens here
     torch.cuda.synchronize()
     for _ in range(a.reps):

@@ -125,6 +125,7 @@ struct ConvArgs {
   int Hin, Win, Ho, Wo, k, s, pad, Cin8, Kc, N, Kpad, act, shuffle, npr, M, tiles_n;
   // stem only: read the caller's NCHW fp32 input directly, applying LoadTensor's /255 rule on load
   const float* nchw; const float* ctl; float eps;
+  const float* wstem;          // stem weights, fp32 [27][N] (tap (ky, kx, c)-major), re-laid out at load
   // LDS-DMA kernels (csrc/ym_conv_dma.hip): operand extents (elements) and the split-K slab/counter workspace
   long s0_elems, s1_elems;
   FDiv fd_hw, fd_w;            // division by Ho*Wo and by Wo
@@ -219,11 +220,12 @@ hipError_t ym_launch_stem(int dtype, const ConvArgs& a, hipStream_t st);
 hipError_t ym_launch_spin(int usec, hipStream_t st);  // profiling: park the stream for usec (wall clock)
 hipError_t ym_launch_conv_dma(int out_f32, const ConvArgs& a, int i, hipStream_t st);  // f16 plans only
 int ym_conv_dma_num_cfgs();
+hipError_t ym_launch_conv_stream(int out_f32, const ConvArgs& a, int i, hipStream_t st);  // f16 1x1 only
+int ym_conv_stream_num_cfgs();
 hipError_t ym_launch_masks(const MaskArgs& a, hipStream_t st);  // Segment: process_mask(upsample=True)
 // int8 (PTQ) plans: csrc/ym_conv_i8.hip
 hipError_t ym_launch_conv_i8(const ConvArgs& a, int cfg, hipStream_t st, bool strict);
 int ym_conv_i8_num_cfgs();
-hipError_t ym_launch_stem_i8(const ConvArgs& a, hipStream_t st);
 hipError_t ym_launch_dwconv_i8(const DwArgs& a, hipStream_t st);
 hipError_t ym_launch_attn_i8(const AttnArgs& a, hipStream_t st);
 hipError_t ym_launch_requant(const ReqArgs& a, hipStream_t st);

@@ -320,7 +320,8 @@ __global__ __launch_bounds__(WM * WN * WK * 64) void conv_igemm(const ConvArgs a
 #pragma unroll
         for (int e = 0; e < 4; ++e) {
           const float x = acc[i][j][4 * q + e] + bias[j][q][e];
-          v[e] = (a.act ? ym_silu(x) : x) + resv[i][j][q][e];
+          // f16 plans: the fp16-rounded output does not see the fast SiLU's ~1 ulp (fp32) error
+          v[e] = (a.act ? (sizeof(T) == 2 ? ym_silu_fast(x) : ym_silu(x)) : x) + resv[i][j][q][e];
           if (a.raw) a.raw[(size_t)(pbase + i * 32 + l32) * a.N + n + e] = x;  // f32 calibration run
         }
         if (a.shuffle) {
@@ -513,7 +514,7 @@ __global__ __launch_bounds__(256) void conv_lds(const ConvArgs a) {
 #pragma unroll
         for (int e = 0; e < 4; ++e) {
           const float x = acc[i][j][4 * q + e] + b4[e];
-          v[e] = a.act ? ym_silu(x) : x;
+          v[e] = a.act ? ym_silu_fast(x) : x;  // f16 plans only (LDS variants)
         }
         if (a.shuffle) {
           const int sub = n / a.npr;
@@ -616,8 +617,9 @@ int choose_cfg(const ConvArgs& a) {
 
 }  // namespace
 
-// ids [0, 17): first-generation kernels above; [17, 17 + ym_conv_dma_num_cfgs()): LDS-DMA / split-K kernels
-int ym_conv_num_cfgs() { return kNumAllCfg + ym_conv_dma_num_cfgs(); }
+// ids [0, 17): first-generation kernels above; [17, 17 + ym_conv_dma_num_cfgs()): LDS-DMA / split-K kernels;
+// then ym_conv_stream_num_cfgs() streaming 1x1 kernels (csrc/ym_conv_stream.hip)
+int ym_conv_num_cfgs() { return kNumAllCfg + ym_conv_dma_num_cfgs() + ym_conv_stream_num_cfgs(); }
 
 hipError_t ym_launch_conv(int dtype, int out_f32, const ConvArgs& a, int cfg, hipStream_t st, bool strict) {
   int kind;
@@ -632,8 +634,11 @@ hipError_t ym_launch_conv(int dtype, int out_f32, const ConvArgs& a, int cfg, hi
   if (cfg >= kNumAllCfg) {
     // a DMA config that does not apply to this op (checked before anything is launched): the tuner skips the
     // candidate (strict); a pinned table falls back to the heuristic
-    const hipError_t e = dtype == YM_DT_F16 ? ym_launch_conv_dma(out_f32, a, cfg - kNumAllCfg, st)
-                                            : hipErrorInvalidValue;
+    const int ndma = ym_conv_dma_num_cfgs();
+    hipError_t e = hipErrorInvalidValue;
+    if (dtype == YM_DT_F16)
+      e = cfg - kNumAllCfg < ndma ? ym_launch_conv_dma(out_f32, a, cfg - kNumAllCfg, st)
+                                  : ym_launch_conv_stream(out_f32, a, cfg - kNumAllCfg - ndma, st);
     if (e != hipErrorInvalidValue || strict) return e;
     cfg = -1;
   }

@@ -12,7 +12,8 @@
 //
 // Kernels: conv_i8 (implicit GEMM over NHWC int8, same transposed orientation and tile structure as
 // csrc/ym_conv.hip: MFMA A = weights [N][Kpad], B = im2col gathered straight from NHWC, one 16-byte K chunk = 16
-// channels of one input pixel), stem_i8 (the image → int8 quantisation folded into the 3x3 s2 stem),
+// channels of one input pixel) — the int8 stem (the image's quantisation folded into the 3x3 s2 conv) is in
+// csrc/ym_stem.hip —
 // dwconv3x3_i8, attn_psa_i8 (float attention on dequantised q/k/v + int8 positional depthwise conv), requant (the
 // materialised concats of an int8 plan).
 #include <stdlib.h>
@@ -320,107 +321,6 @@ int choose_cfg(const ConvArgs& a) {
   return steps >= 4 ? 4 : 6;
 }
 
-// ------------------------------------------------------------------------------------------------- stem
-// Conv(3, c, 3, 2) on the caller's NCHW fp32 batch: LoadTensor's /255 rule, then the image's int8 quantisation
-// (q = clamp(rint(x / s_in) + z_in)) folded into the LDS patch as q - z_in (0 for padding), integer MACs in fp32
-// (|partial sums| < 2^24: exact), the quantized-conv epilogue, 16 channels (16 bytes) per thread.
-constexpr int TH = 8;
-
-template <int G>
-__global__ __launch_bounds__(256) void stem_i8(const ConvArgs a) {
-  constexpr int TW = 32 / G;
-  constexpr int PH = 2 * TH + 1;
-  constexpr int PW4 = (2 * TW + 4 + 3) / 4 + 1;
-  constexpr int PW = PW4 * 4;
-  constexpr int N = 16 * G;
-  extern __shared__ float sm[];
-  float* patch = sm;                // [3][PH][PW]
-  float* wl = patch + 3 * PH * PW;  // [27][N]
-  float* post = wl + 27 * N;        // [256]
-  const QRec* Q = a.q;
-  const int tiles_x = (a.Wo + TW - 1) / TW, tiles_y = (a.Ho + TH - 1) / TH;
-  int bid = blockIdx.x;
-  const int tx = bid % tiles_x;
-  bid /= tiles_x;
-  const int ty = bid % tiles_y;
-  const int b = bid / tiles_y;
-  const int oy0 = ty * TH, ox0 = tx * TW;
-  const int iy0 = 2 * oy0 - 1, xs = 2 * ox0 - 4;
-  const bool div = ym_input_max(a.ctl) > 1.0f + a.eps;
-  const size_t HW = (size_t)a.Hin * a.Win;
-  const float* img = a.nchw + (size_t)b * 3 * HW;
-  const float inv = Q->inv_s_in;
-  const int zi = Q->z_in, lo = Q->qlo, hi = Q->qhi;
-  for (int i = threadIdx.x; i < 3 * PH * PW4; i += 256) {
-    const int c = i / (PH * PW4), r = i - c * (PH * PW4);
-    const int py = r / PW4, q = r - (r / PW4) * PW4;
-    const int iy = iy0 + py, ix = xs + 4 * q;
-    f32x4 v = {0.f, 0.f, 0.f, 0.f};
-    if ((unsigned)iy < (unsigned)a.Hin && (unsigned)ix < (unsigned)a.Win) {
-      v = *reinterpret_cast<const f32x4*>(img + c * HW + (size_t)iy * a.Win + ix);
-#pragma unroll
-      for (int e = 0; e < 4; ++e) {
-        float x = v[e];
-        if (div) x = x / 255.0f;
-        v[e] = (float)(clampi((int)rintf(__fmul_rn(x, inv)) + zi, lo, hi) - zi);
-      }
-    }
-    *reinterpret_cast<f32x4*>(patch + (c * PH + py) * PW + 4 * q) = v;
-  }
-  const i8* W = static_cast<const i8*>(a.w);
-  for (int i = threadIdx.x; i < 27 * N; i += 256) {
-    const int tap = i / N, n = i - (i / N) * N;
-    const int kk = tap / 3, c = tap - (tap / 3) * 3;
-    wl[i] = (float)W[(size_t)n * a.Kpad + kk * 8 + c];
-  }
-  for (int i = threadIdx.x; i < 256; i += 256) post[i] = Q->post[i];
-  __syncthreads();
-  const int t = threadIdx.x;
-  if (t >= TH * TW * G) return;
-  const int g = t % G, pix = t / G;
-  const int ly = pix / TW, lx = pix - (pix / TW) * TW;
-  const int oy = oy0 + ly, ox = ox0 + lx;
-  if (oy >= a.Ho || ox >= a.Wo) return;
-  float x[27];
-#pragma unroll
-  for (int ky = 0; ky < 3; ++ky)
-#pragma unroll
-    for (int kx = 0; kx < 3; ++kx)
-#pragma unroll
-      for (int c = 0; c < 3; ++c)
-        x[(ky * 3 + kx) * 3 + c] = patch[(c * PH + 2 * ly + ky) * PW + 2 * lx + kx + 3];
-  const int n0 = g * 16;
-  float acc[16];
-#pragma unroll
-  for (int e = 0; e < 16; ++e) acc[e] = 0.f;
-#pragma unroll
-  for (int k = 0; k < 27; ++k) {
-    const float* wr = wl + k * N + n0;
-#pragma unroll
-    for (int e = 0; e < 16; ++e) acc[e] = fmaf(x[k], wr[e], acc[e]);
-  }
-  int ov[16];
-#pragma unroll
-  for (int e = 0; e < 16; ++e) {
-    const int qc = requant_out((int)acc[e] + a.biasi[n0 + e], a.sasw[n0 + e], a.bias[n0 + e], Q);
-    ov[e] = quant_store(post[qc], Q->inv_so, Q->zo, lo, hi);
-  }
-  const i32x4 o{pack4(ov), pack4(ov + 4), pack4(ov + 8), pack4(ov + 12)};
-  i8* dst = static_cast<i8*>(a.dst) + (size_t)(b * a.d_P + oy * a.d_W + ox) * a.d_ctot + a.d_coff + n0;
-  *reinterpret_cast<i32x4*>(dst) = o;
-}
-
-template <int G>
-hipError_t launch_stem_g(const ConvArgs& a, hipStream_t st) {
-  constexpr int TW = 32 / G;
-  constexpr int PW = ((2 * TW + 4 + 3) / 4 + 1) * 4;
-  const int B = a.M / (a.Ho * a.Wo);
-  const dim3 grid(B * ((a.Ho + TH - 1) / TH) * ((a.Wo + TW - 1) / TW));
-  const size_t lds = ((size_t)3 * (2 * TH + 1) * PW + 27 * 16 * G + 256) * sizeof(float);
-  hipLaunchKernelGGL((stem_i8<G>), grid, dim3(256), lds, st, a);
-  return hipGetLastError();
-}
-
 // ------------------------------------------------------------------------------------------------- depthwise
 // DWConv 3x3 (Detect cv3): one thread = 8 channels of one pixel; acc = Σ over in-image taps (q - z_in)·w, then the
 // quantized-conv epilogue (mode 0).
@@ -641,17 +541,6 @@ hipError_t ym_launch_conv_i8(const ConvArgs& a, int cfg, hipStream_t st, bool st
     cfg = -1;
   }
   return launch_id(cfg >= 0 ? cfg : choose_cfg(a), a, kind, st);
-}
-
-hipError_t ym_launch_stem_i8(const ConvArgs& a, hipStream_t st) {
-  if (a.k != 3 || a.s != 2 || !a.nchw || a.shuffle || a.res || !a.q || a.Win % 4) return hipErrorInvalidValue;
-  switch (a.N) {
-    case 16: return launch_stem_g<1>(a, st);
-    case 32: return launch_stem_g<2>(a, st);
-    case 64: return launch_stem_g<4>(a, st);
-    case 96: return launch_stem_g<6>(a, st);
-  }
-  return hipErrorInvalidValue;
 }
 
 hipError_t ym_launch_dwconv_i8(const DwArgs& a, hipStream_t st) {

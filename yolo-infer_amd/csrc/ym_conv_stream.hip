@@ -1,0 +1,201 @@
+// Streaming 1x1 / 3x3 conv for the large-M, small-K/N layers (f16 plans) — the HBM-bound half of the Conv launches
+// (C3k2 cv1/cv2 and Bottleneck 3x3s at 160² and 80², the stride-2 downsamples, the FPN merges of the neck, the P3
+// Detect-head convs).
+//
+// The first-generation and LDS-DMA kernels (csrc/ym_conv.hip, ym_conv_dma.hip) give each wave one small output tile
+// and retire: on these layers a wave does a few MFMAs between a prologue (tile coordinates, weight rows, bias) and
+// an epilogue, and its lifetime is one memory round trip.  Here a persistent grid of waves streams over the pixels:
+//   * the whole weight matrix [N][Kpad] (<= 80 KB) is staged in LDS once per workgroup, rows padded by 16 bytes so
+//     the MFMA A-fragment reads (ds_read_b128, 16 rows at one K offset) spread over the banks; bias in LDS too;
+//   * a wave takes PX groups of 16 consecutive pixels per iteration; their B fragments (one 16-byte load = 8
+//     channels of one pixel per lane; 1x1: concat sources and the nearest-2x upsample folded into the row address,
+//     3x3: the im2col gather of tap (ky, kx) straight from NHWC, zero padding by predicate) for the NEXT iteration
+//     are in flight while the current one computes — two iterations of loads per wave in flight;
+//   * v_mfma_f32_16x16x32_f16 in the transposed orientation (A = weights): a lane ends with 4 consecutive output
+//     channels of one pixel → + bias, SiLU, (+ residual), one 8-byte (fp16) or 16-byte (fp32 head buffer) store.
+// Results are identical in kind to the other conv kernels (fp32 accumulation of fp16 products, one rounding to the
+// output type); only the summation order differs.
+#include "ym_common.h"
+
+namespace {
+
+typedef _Float16 h8 __attribute__((ext_vector_type(8)));
+
+struct SCfg {
+  int kind, ks, px, cap;  // kind 1 = 1x1 s1, 3 = 3x3; K steps of 32 (Kpad / 32); 16-pixel groups per wave
+};                        // iteration; workgroup cap of the persistent grid
+#define YM_STREAM_CFGS(X)                                                                                        \
+  X(0, 1, 2, 1, 1024) X(1, 1, 2, 2, 1024) X(2, 1, 2, 1, 4096) X(3, 1, 4, 1, 1024) X(4, 1, 4, 2, 1024)            \
+  X(5, 1, 8, 1, 1024) X(6, 1, 4, 1, 4096) X(7, 3, 4, 1, 1024) X(8, 3, 6, 1, 1024) X(9, 3, 10, 1, 1024)          \
+  X(10, 3, 18, 1, 1024) X(11, 3, 4, 1, 4096) X(12, 3, 6, 1, 4096) X(13, 3, 10, 1, 4096) X(14, 3, 18, 1, 4096)
+constexpr SCfg kStream[] = {
+#define YM_X(id, kind, ks, px, cap) {kind, ks, px, cap},
+    YM_STREAM_CFGS(YM_X)
+#undef YM_X
+};
+constexpr int kNumStream = sizeof(kStream) / sizeof(kStream[0]);
+constexpr int kMaxWBytes = 80 * 1024;
+
+template <typename OutT, int KIND, int KS, int PX>
+__global__ __launch_bounds__(256) void conv_stream(const ConvArgs a) {
+  constexpr int KP = KS * 32;      // Kpad
+  constexpr int LDW = KP + 8;      // LDS row pitch (halves): +16 bytes
+  extern __shared__ __attribute__((aligned(16))) f16 ws[];  // [N][LDW], then bias [N] f32
+  float* bs = reinterpret_cast<float*>(ws + ((a.N + 15) & ~15) * LDW);
+  const int tid = threadIdx.x, lane = tid & 63, wave = tid >> 6;
+  const int g = lane >> 4, col = lane & 15;
+  const f16* W = static_cast<const f16*>(a.w);
+  const int NP = (a.N + 15) & ~15;  // rows padded to the 16-row MFMA block (zero weights, outputs not stored)
+  for (int i = tid; i < NP * (KP / 8); i += 256) {
+    const int n = i / (KP / 8), c = i - n * (KP / 8);
+    *reinterpret_cast<f16x8*>(ws + n * LDW + 8 * c) =
+        n < a.N ? *reinterpret_cast<const f16x8*>(W + (size_t)n * KP + 8 * c) : Vec8<f16>::zero();
+  }
+  for (int i = tid; i < NP; i += 256) bs[i] = i < a.N ? a.bias[i] : 0.f;
+
+  const int HW = a.Ho * a.Wo;
+  const int G = (a.M + 15) >> 4;  // 16-pixel groups
+  const int nw = gridDim.x * 4;
+  const f16* s0 = static_cast<const f16*>(a.src0);
+  const f16* s1 = static_cast<const f16*>(a.src1);
+  const int K = a.C0 + a.C1;
+  const int lc8 = __builtin_ctz(a.Cin8);  // 3x3: Cin / 8 is a power of two (checked on the host)
+
+  // B fragments of the iteration starting at group gb: [PX][KS]
+  auto load = [&](int gb, h8 (&bf)[PX][KS]) {
+#pragma unroll
+    for (int p = 0; p < PX; ++p) {
+      const int m = (gb + p) * 16 + col;
+      const bool ok = gb + p < G && m < a.M;
+      const int mm = ok ? m : 0;
+      const int b = ym_div(mm, a.fd_hw), rem = mm - b * HW;
+      const int y = ym_div(rem, a.fd_w), x = rem - y * a.Wo;
+      if constexpr (KIND == 1) {
+        const size_t p0 = a.up0 ? (size_t)b * a.s0_P + (y >> 1) * a.s0_W + (x >> 1) : (size_t)b * a.s0_P + y * a.s0_W + x;
+        const size_t p1 = (size_t)b * a.s1_P + y * a.Win + x;
+#pragma unroll
+        for (int ks = 0; ks < KS; ++ks) {
+          const int k0 = 32 * ks + 8 * g;
+          h8 v = Vec8<f16>::zero();
+          if (ok && k0 < K)
+            v = k0 < a.C0 ? Vec8<f16>::load(s0 + p0 * a.s0_ctot + a.s0_coff + k0)
+                          : Vec8<f16>::load(s1 + p1 * a.s1_ctot + a.s1_coff + (k0 - a.C0));
+          bf[p][ks] = v;
+        }
+      } else {  // 3x3, pad 1, stride a.s: chunk c = 4 ks + g is tap c >> lc8, channels 8 (c & (Cin8 - 1)) ..
+        const f16* img = s0 + (size_t)b * a.s0_P * a.s0_ctot + a.s0_coff;
+        const int iy0 = y * a.s - 1, ix0 = x * a.s - 1;
+#pragma unroll
+        for (int ks = 0; ks < KS; ++ks) {
+          const int c = 4 * ks + g;
+          const int t = c >> lc8, cb = c & (a.Cin8 - 1);
+          const int ky = t >= 6 ? 2 : (t >= 3 ? 1 : 0), kx = t - 3 * ky;
+          const int iy = iy0 + ky, ix = ix0 + kx;
+          h8 v = Vec8<f16>::zero();
+          if (ok && c < a.Kc && (unsigned)iy < (unsigned)a.Hin && (unsigned)ix < (unsigned)a.Win)
+            v = Vec8<f16>::load(img + (size_t)(iy * a.Win + ix) * a.s0_ctot + 8 * cb);
+          bf[p][ks] = v;
+        }
+      }
+    }
+  };
+
+  int gb = (blockIdx.x * 4 + wave) * PX;
+  h8 cur[PX][KS], nxt[PX][KS];
+  load(gb, cur);
+  __syncthreads();
+  OutT* dst = static_cast<OutT*>(a.dst);
+  const f16* res = static_cast<const f16*>(a.res);
+  for (; gb < G; gb += nw * PX) {
+    if (gb + nw * PX < G) load(gb + nw * PX, nxt);
+    int ob[PX], rb[PX];  // output / residual pixel index of this lane's pixel in group p (ob -1: none)
+#pragma unroll
+    for (int p = 0; p < PX; ++p) {
+      const int m = (gb + p) * 16 + col;
+      const int b = ym_div(m, a.fd_hw), rem = m - b * HW;
+      const int y = ym_div(rem, a.fd_w), x = rem - y * a.Wo;
+      ob[p] = (gb + p < G && m < a.M) ? b * a.d_P + a.d_pixoff + y * a.d_W + x : -1;
+      rb[p] = b * a.r_P + y * a.Wo + x;
+    }
+    for (int nb = 0; nb < NP / 16; ++nb) {
+      h8 af[KS];
+#pragma unroll
+      for (int ks = 0; ks < KS; ++ks)
+        af[ks] = *reinterpret_cast<const h8*>(ws + (16 * nb + col) * LDW + 32 * ks + 8 * g);
+      const int n0 = 16 * nb + 4 * g;
+      const f32x4 b4 = *reinterpret_cast<const f32x4*>(bs + n0);
+#pragma unroll
+      for (int p = 0; p < PX; ++p) {
+        f32x4 acc = {0.f, 0.f, 0.f, 0.f};
+#pragma unroll
+        for (int ks = 0; ks < KS; ++ks) acc = __builtin_amdgcn_mfma_f32_16x16x32_f16(af[ks], cur[p][ks], acc, 0, 0, 0);
+        if (ob[p] < 0 || n0 >= a.N) continue;
+        float v[4];
+#pragma unroll
+        for (int r = 0; r < 4; ++r) {
+          const float xv = acc[r] + b4[r];
+          v[r] = a.act ? ym_silu_fast(xv) : xv;
+        }
+        if (res) {
+          const f16x4 rv = *reinterpret_cast<const f16x4*>(res + (size_t)rb[p] * a.r_ctot + a.r_coff + n0);
+#pragma unroll
+          for (int r = 0; r < 4; ++r) v[r] += (float)rv[r];
+        }
+        OutT* o = dst + (size_t)ob[p] * a.d_ctot + a.d_coff + n0;
+        if constexpr (sizeof(OutT) == 2) *reinterpret_cast<f16x4*>(o) = f16x4{(f16)v[0], (f16)v[1], (f16)v[2], (f16)v[3]};
+        else *reinterpret_cast<f32x4*>(o) = f32x4{v[0], v[1], v[2], v[3]};
+      }
+    }
+#pragma unroll
+    for (int p = 0; p < PX; ++p)
+#pragma unroll
+      for (int ks = 0; ks < KS; ++ks) cur[p][ks] = nxt[p][ks];
+  }
+}
+
+template <typename OutT, int KIND, int KS, int PX, int CAP>
+hipError_t launch(const ConvArgs& a, hipStream_t st) {
+  if (a.Kpad != KS * 32 || a.k != KIND) return hipErrorInvalidValue;
+  const int G = (a.M + 15) / 16;
+  long wgs = (G + 4 * PX - 1) / (4 * PX);
+  if (wgs > CAP) wgs = CAP;  // the persistent grid: CAP workgroups, the rest streams through them
+  const int NP = (a.N + 15) & ~15;
+  const size_t lds = (size_t)NP * (KS * 32 + 8) * sizeof(f16) + (size_t)NP * sizeof(float);
+  if (lds > kMaxWBytes) return hipErrorInvalidValue;
+  hipLaunchKernelGGL((conv_stream<OutT, KIND, KS, PX>), dim3(wgs), dim3(256), lds, st, a);
+  return hipGetLastError();
+}
+
+template <typename OutT>
+hipError_t dispatch(const ConvArgs& a, int i, hipStream_t st) {
+  switch (i) {
+#define YM_X(id, kind, ks, px, cap) \
+  case id: return launch<OutT, kind, ks, px, cap>(a, st);
+    YM_STREAM_CFGS(YM_X)
+#undef YM_X
+  }
+  return hipErrorInvalidValue;
+}
+
+}  // namespace
+
+int ym_conv_stream_num_cfgs() { return kNumStream; }
+
+// Host-side applicability: f16 plans; 1x1 stride-1 convs without pixel shuffle (8-channel-aligned concat split) or
+// 3x3 convs on one plain source with Cin / 8 a power of two; N % 4 == 0 and 4-aligned output channel slices
+// (8/16-byte stores); weights + bias <= 80 KB of LDS.
+hipError_t ym_launch_conv_stream(int out_f32, const ConvArgs& a, int i, hipStream_t st) {
+  if (i < 0 || i >= kNumStream) return hipErrorInvalidValue;
+  if (a.shuffle || a.raw || a.nchw || !a.src0 || (a.N & 3) || a.Kpad % 32) return hipErrorInvalidValue;
+  if (a.k == 1) {
+    if (a.s != 1 || a.C0 % 8 || a.C1 % 8) return hipErrorInvalidValue;
+    if (a.src1 && (a.s1_coff % 8 || a.s1_ctot % 8)) return hipErrorInvalidValue;
+  } else if (a.k == 3) {
+    if (a.src1 || a.up0 || a.pad != 1 || (a.Cin8 & (a.Cin8 - 1))) return hipErrorInvalidValue;
+  } else {
+    return hipErrorInvalidValue;
+  }
+  if ((a.d_ctot & 3) || (a.d_coff & 3) || (a.res && ((a.r_ctot & 3) || (a.r_coff & 3)))) return hipErrorInvalidValue;
+  if (a.s0_coff % 8 || a.s0_ctot % 8) return hipErrorInvalidValue;
+  return out_f32 ? dispatch<float>(a, i, st) : dispatch<f16>(a, i, st);
+}

@@ -291,6 +291,132 @@ __global__ __launch_bounds__(256) void attn_psa(const AttnArgs a) {
   }
 }
 
+// f16 plans, kd = 32 / hd = 64 (every YOLO11 scale) and N <= 512 tokens (inputs up to 724 px): the same Attention on
+// MFMA.  One workgroup = (image, head, 64 queries), one wave = 16 queries:
+//   1. V of the whole (image, head) is staged transposed in LDS, V^T [64][LDV] f16 (row pitch 16*NKT + 4 halves:
+//      the 8-byte fragment reads below hit 32 distinct banks);
+//   2. S^T = K·Q^T: one v_mfma_f32_16x16x32_f16 per 16 keys (K = kd = 32), A = K rows, B = the wave's 16 query rows,
+//      both plain 16-byte loads; the lane holds S^T[key 16t + 4(l>>4) + r][query l&15], all N keys in registers;
+//   3. softmax over keys: in-lane over the tiles, then across the 4 lane groups (fp32, max-subtracted, as torch);
+//   4. O^T = V^T·P^T, K = 32 keys per MFMA in the lane-group order of step 2 (slot j of group g is key
+//      32s + 4g + j, or 32s + 16 + 4g + j - 4), so P comes straight from the softmax registers (rounded to fp16)
+//      and V^T as two 8-byte LDS reads; a lane ends with 4 consecutive channels of one query: 8-byte NHWC stores;
+//   5. + pe(v) (depthwise 3x3 + folded BN) from the staged V^T, store.
+typedef _Float16 h8v __attribute__((ext_vector_type(8)));
+
+template <int NKT>  // key tiles of 16 (even): N <= 16 NKT
+__global__ __launch_bounds__(256) void attn_psa_mfma(const AttnArgs a) {
+  extern __shared__ __attribute__((aligned(16))) f16 vt[];  // [64][LDV]
+  constexpr int LDV = 16 * NKT + 4;
+  const int N = a.N;
+  const int nqb = (N + 63) / 64;
+  const int qb = blockIdx.x % nqb, bh = blockIdx.x / nqb;
+  const int h = bh % a.nh, b = bh / a.nh;
+  const int tid = threadIdx.x, lane = tid & 63, wave = tid >> 6;
+  const int g = lane >> 4, c = lane & 15;
+  const f16* qkv = static_cast<const f16*>(a.qkv);
+  const size_t img = (size_t)b * a.q_P;
+  const int hq = a.q_coff + h * 128;  // per head: q 32, k 32, v 64 channels
+  // 1. V^T (keys >= N zero)
+  {  // all loads in flight before the first LDS store (one memory latency, not NIT)
+    constexpr int NIT = (16 * NKT * 8 + 255) / 256;
+    f16x8 v[NIT];
+#pragma unroll
+    for (int it = 0; it < NIT; ++it) {
+      const int i = tid + 256 * it, key = i >> 3, d0 = (i & 7) * 8;
+      v[it] = key < N ? Vec8<f16>::load(qkv + (img + key) * a.q_ctot + hq + 64 + d0) : Vec8<f16>::zero();
+    }
+#pragma unroll
+    for (int it = 0; it < NIT; ++it) {
+      const int i = tid + 256 * it, key = i >> 3, d0 = (i & 7) * 8;
+      if (key >= 16 * NKT) break;
+#pragma unroll
+      for (int e = 0; e < 8; ++e) vt[(d0 + e) * LDV + key] = v[it][e];
+    }
+  }
+  // 2. scores
+  const int q = qb * 64 + wave * 16 + c;
+  h8v qf = Vec8<f16>::zero();
+  if (q < N) qf = Vec8<f16>::load(qkv + (img + q) * a.q_ctot + hq + 8 * g);
+  float s[NKT][4];
+#pragma unroll
+  for (int t = 0; t < NKT; ++t) {
+    const int key = 16 * t + c;
+    h8v kf = Vec8<f16>::zero();
+    if (key < N) kf = Vec8<f16>::load(qkv + (img + key) * a.q_ctot + hq + 32 + 8 * g);
+    const f32x4 d = __builtin_amdgcn_mfma_f32_16x16x32_f16(kf, qf, f32x4{0.f, 0.f, 0.f, 0.f}, 0, 0, 0);
+#pragma unroll
+    for (int r = 0; r < 4; ++r) s[t][r] = 16 * t + 4 * g + r < N ? d[r] * a.scale : -INFINITY;
+  }
+  // 3. softmax over the keys of query l&15
+  float m = -INFINITY;
+#pragma unroll
+  for (int t = 0; t < NKT; ++t)
+#pragma unroll
+    for (int r = 0; r < 4; ++r) m = fmaxf(m, s[t][r]);
+  m = fmaxf(m, __shfl_xor(m, 16));
+  m = fmaxf(m, __shfl_xor(m, 32));
+  float sum = 0.f;
+#pragma unroll
+  for (int t = 0; t < NKT; ++t)
+#pragma unroll
+    for (int r = 0; r < 4; ++r) {
+      s[t][r] = expf(s[t][r] - m);
+      sum += s[t][r];
+    }
+  sum += __shfl_xor(sum, 16);
+  sum += __shfl_xor(sum, 32);
+  const float rs = 1.0f / sum;
+  __syncthreads();
+  // 4. O^T = V^T P^T
+  f32x4 o[4];
+#pragma unroll
+  for (int dt = 0; dt < 4; ++dt) o[dt] = f32x4{0.f, 0.f, 0.f, 0.f};
+#pragma unroll
+  for (int ks = 0; ks < NKT / 2; ++ks) {
+    h8v pf;
+#pragma unroll
+    for (int r = 0; r < 4; ++r) {
+      pf[r] = (f16)(s[2 * ks][r] * rs);
+      pf[4 + r] = (f16)(s[2 * ks + 1][r] * rs);
+    }
+#pragma unroll
+    for (int dt = 0; dt < 4; ++dt) {
+      const f16* vr = vt + (16 * dt + c) * LDV + 32 * ks + 4 * g;
+      const f16x4 lo = *reinterpret_cast<const f16x4*>(vr), hi = *reinterpret_cast<const f16x4*>(vr + 16);
+      const h8v vf = {lo[0], lo[1], lo[2], lo[3], hi[0], hi[1], hi[2], hi[3]};
+      o[dt] = __builtin_amdgcn_mfma_f32_16x16x32_f16(vf, pf, o[dt], 0, 0, 0);
+    }
+  }
+  // 5. + pe(v), store: lane = channels 16dt + 4g .. +3 of query q
+  if (q >= N) return;
+  const int y = q / a.W, x = q - (q / a.W) * a.W;
+  f16* dst = static_cast<f16*>(a.dst) + ((size_t)b * a.d_P + q) * a.d_ctot + a.d_coff + h * 64;
+#pragma unroll
+  for (int dt = 0; dt < 4; ++dt) {
+    const int d0 = 16 * dt + 4 * g, ch0 = h * 64 + d0;
+    float pe[4];
+#pragma unroll
+    for (int r = 0; r < 4; ++r) pe[r] = a.pe_b[ch0 + r];
+    for (int ky = 0; ky < 3; ++ky) {
+      const int iy = y + ky - 1;
+      if ((unsigned)iy >= (unsigned)a.H) continue;
+      for (int kx = 0; kx < 3; ++kx) {
+        const int ix = x + kx - 1;
+        if ((unsigned)ix >= (unsigned)a.W) continue;
+        const int nb = iy * a.W + ix;
+        const float* w = a.pe_w + (ky * 3 + kx) * a.C + ch0;
+#pragma unroll
+        for (int r = 0; r < 4; ++r) pe[r] = fmaf((float)vt[(d0 + r) * LDV + nb], w[r], pe[r]);
+      }
+    }
+    f16x4 out;
+#pragma unroll
+    for (int r = 0; r < 4; ++r) out[r] = (f16)(o[dt][r] + pe[r]);
+    *reinterpret_cast<f16x4*>(dst + d0) = out;
+  }
+}
+
 // ------------------------------------------------------------------------------------------------- decode
 // Detect._inference + the candidate stage of non_max_suppression; 4 lanes per anchor (lane s: DFL side s and a
 // quarter of the classes):
@@ -618,8 +744,23 @@ hipError_t launch_attn_t(const AttnArgs& a, hipStream_t st) {
   return hipGetLastError();
 }
 
+template <int NKT>
+hipError_t launch_attn_mfma(const AttnArgs& a, hipStream_t st) {
+  const size_t lds = (size_t)64 * (16 * NKT + 4) * sizeof(f16);
+  hipLaunchKernelGGL((attn_psa_mfma<NKT>), dim3(a.B * a.nh * ((a.N + 63) / 64)), dim3(256), lds, st, a);
+  return hipGetLastError();
+}
+
 hipError_t ym_launch_attn(int dtype, const AttnArgs& a, hipStream_t st) {
   if (dtype == YM_DT_I8) return ym_launch_attn_i8(a, st);
+  if (dtype == YM_DT_F16 && a.kd == 32 && a.hd == 64 && !a.raw && a.nh * 128 <= a.q_ctot && a.d_ctot % 4 == 0 &&
+      a.d_coff % 4 == 0 && a.q_ctot % 8 == 0 && a.q_coff % 8 == 0) {
+    const int nkt = (a.N + 15) / 16;
+    if (nkt <= 8) return launch_attn_mfma<8>(a, st);
+    if (nkt <= 16) return launch_attn_mfma<16>(a, st);
+    if (nkt <= 26) return launch_attn_mfma<26>(a, st);
+    if (nkt <= 32) return launch_attn_mfma<32>(a, st);
+  }
   if (a.kd > AKD || a.hd > AHD) return hipErrorInvalidValue;
   return dtype == YM_DT_F16 ? launch_attn_t<f16>(a, st) : launch_attn_t<float>(a, st);
 }

@@ -82,6 +82,7 @@ struct ym_ctx {
   std::vector<BufDesc> bufs;
   std::vector<Op> ops;
   char* d_weights = nullptr;
+  size_t off_wstem = 0;       // stem weights re-laid out as fp32 [27][N] behind the blob's weights (ym_stem.hip)
   size_t wbytes = 0;
   // workspace for the current (B, H, W)
   int cB = 0, cH = 0, cW = 0;
@@ -236,6 +237,7 @@ int conv_args(ym_ctx* c, const Op& op, int B, const float* d_in, float in_eps, C
         a.nchw = d_in;
         a.ctl = reinterpret_cast<const float*>(c->d_arena + c->off_ctl);
         a.eps = in_eps;
+        a.wstem = reinterpret_cast<const float*>(c->d_weights + c->off_wstem);
       }
       a.s0_W = c->buf_Wd(b0); a.s0_P = c->buf_P(b0); a.up0 = up0;
       a.Hin = c->buf_H(b0) * (up0 ? 2 : 1);
@@ -506,9 +508,36 @@ int ym_load_weights(ym_ctx* c, const void* blob, size_t bytes) {
   c->clear_graphs();
   if (c->d_weights) HIPCK(hipFree(c->d_weights));
   c->d_weights = nullptr;
-  hipError_t e = hipMalloc(&c->d_weights, wbytes ? wbytes : 256);
-  if (e != hipSuccess) return fail(YM_ENOMEM, "weights hipMalloc(%zu): %s", wbytes, hipGetErrorString(e));
+  // The stem conv's weights, re-laid out on the host as fp32 [27][N] (tap-major: (ky, kx, c), N contiguous) so the
+  // stem kernel reads them with wave-uniform (scalar) loads; the blob packs them as [N][Kpad] GEMM rows with the
+  // 3 input channels padded to 8 per tap.  int8 plans keep the integer weight values (exact in fp32).
+  std::vector<float> wstem;
+  for (const Op& o : c->ops) {
+    if (o.r[0] != OP_CONV || o.r[6] != c->input_buf) continue;
+    const int N = o.r[4], Kpad = o.r[21];
+    if (o.r[1] != 3 || o.r[3] != 8 || Kpad < 72) return fail(YM_EBLOB, "op %s: unexpected stem geometry", o.name);
+    const char* w = static_cast<const char*>(blob) + woff + (size_t)(uint32_t)o.r[19];
+    const size_t esz = c->dtype == YM_DT_F32 ? 4 : (c->dtype == YM_DT_F16 ? 2 : 1);
+    if ((size_t)(uint32_t)o.r[19] + (size_t)N * Kpad * esz > wbytes) return fail(YM_EBLOB, "stem weights out of range");
+    wstem.assign((size_t)27 * N, 0.f);
+    for (int n = 0; n < N; ++n)
+      for (int t = 0; t < 27; ++t) {
+        const size_t i = (size_t)n * Kpad + (t / 3) * 8 + t % 3;
+        float v;
+        if (c->dtype == YM_DT_F32) memcpy(&v, w + 4 * i, 4);
+        else if (c->dtype == YM_DT_F16) { _Float16 h16; memcpy(&h16, w + 2 * i, 2); v = (float)h16; }
+        else v = (float)reinterpret_cast<const int8_t*>(w)[i];
+        wstem[(size_t)t * N + n] = v;
+      }
+    break;
+  }
+  c->off_wstem = align_up(wbytes, 256);
+  const size_t dbytes = c->off_wstem + wstem.size() * sizeof(float);
+  hipError_t e = hipMalloc(&c->d_weights, dbytes ? dbytes : 256);
+  if (e != hipSuccess) return fail(YM_ENOMEM, "weights hipMalloc(%zu): %s", dbytes, hipGetErrorString(e));
   HIPCK(hipMemcpy(c->d_weights, static_cast<const char*>(blob) + woff, wbytes, hipMemcpyHostToDevice));
+  if (!wstem.empty())
+    HIPCK(hipMemcpy(c->d_weights + c->off_wstem, wstem.data(), wstem.size() * sizeof(float), hipMemcpyHostToDevice));
   c->wbytes = wbytes;
   c->loaded = true;
   return YM_OK;

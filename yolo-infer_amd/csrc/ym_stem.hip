@@ -1,37 +1,162 @@
-// Stem conv of YOLO11 (layer 0: Conv(3, c, 3, 2) = conv2d → folded BN → SiLU) straight from the caller's NCHW fp32
-// batch — the `LoadTensor` /255 rule (/root/reference/core/model.py:133 → ultralytics LoadTensor._single_check) and
-// the NCHW → NHWC change of layout are folded into its loader, so the input is read exactly once.
+// Stem conv: Conv(3, C, 3, 2) + SiLU on the caller's NCHW fp32 batch.  LoadTensor's /255 rule
+// (ultralytics/data/loaders.py LoadTensor) and the NCHW → NHWC change of layout are folded into its
+// loader, so the input is read exactly once.
 //
-// It is HBM-bound (27 MACs per output channel): a direct VALU kernel, not MFMA.  A workgroup computes an 8-row x
-// TW-column output tile; the 17 x (2*TW+1) x 3 input patch is staged in LDS with coalesced row loads, the
-// [27][Cout] weights are broadcast from LDS, and each thread writes 16 channels of one pixel as 16-byte vectors.
+// A workgroup computes an 8-row x 32-column output tile.  The 17 x 68 x 3 input patch is staged in LDS with
+// coalesced float4 row loads (the rows start 4 floats left of the window: 16-byte aligned, W % 4 == 0).
+//
+// f16 / int8 plans — stem_mfma: the 27-tap contraction (K = 27, padded to 32) is ONE v_mfma_f32_16x16x32_f16 per
+// 16 pixels x 16 channels, in the transposed orientation of csrc/ym_conv.hip (A = weights, so a lane owns 4
+// consecutive output channels of one pixel: 8-byte NHWC stores).  The patch is kept in fp16: the activation storage
+// precision of the f16 plan, and for int8 plans the exact integers q - z_in (|v| <= 255) — int8 weights are exact in
+// fp16 as well, products are exact in fp32 and the 27-term sums stay below 2^24, so the int8 accumulator is exact.
+// Each lane gathers its 8 K values of one pixel from the LDS patch through per-lane tap offsets.
+// int8 plans quantize the image on load (q = clamp(rint(x / s_in) + z_in), patch = q - z_in, padding 0), then run the
+// quantized-conv epilogue (csrc/ym_conv_i8.hip; numerics oracle/quant.py).
+//
+// f32 parity plan — stem_valu: one thread per output pixel, fp32 FMAs, weights read with wave-uniform addresses;
+// optionally the pre-activation output for the calibration runs.
 #include "ym_common.h"
 
 namespace {
 
-constexpr int TH = 8;
+constexpr int TH = 8, TW = 32;
+constexpr int PH = 2 * TH + 1;             // patch rows
+constexpr int PW4 = (2 * TW + 4) / 4 + 1;  // 4-wide groups per patch row: columns x0-4 .. x0+2TW+3
+constexpr int PW = PW4 * 4;
 
-// G = Cout/16 channel groups per pixel, TW = 32/G output columns per tile.  The patch starts 4 floats left of the
-// window (16-byte aligned, W % 32 == 0) and is loaded as float4 rows: [3][17][PW4*4].
-template <typename T, int G>
-__global__ __launch_bounds__(256) void stem_conv3x3s2(const ConvArgs a) {
-  constexpr int TW = 32 / G;
-  constexpr int PH = 2 * TH + 1;
-  constexpr int PW4 = (2 * TW + 4 + 3) / 4 + 1;  // float4s per patch row (covers x0-4 .. x0+2TW)
-  constexpr int PW = PW4 * 4;
-  constexpr int N = 16 * G;
-  extern __shared__ float sm[];
-  float* patch = sm;                   // [3][PH][PW]
-  float* wl = patch + 3 * PH * PW;     // [27][N]
-  float* bl = wl + 27 * N;             // [N]
+__device__ __forceinline__ int clampi(int v, int lo, int hi) { return v < lo ? lo : (v > hi ? hi : v); }
+
+__device__ __forceinline__ void tile_of(const ConvArgs& a, int& b, int& oy0, int& ox0) {
   const int tiles_x = (a.Wo + TW - 1) / TW, tiles_y = (a.Ho + TH - 1) / TH;
   int bid = blockIdx.x;
   const int tx = bid % tiles_x;
   bid /= tiles_x;
   const int ty = bid % tiles_y;
-  const int b = bid / tiles_y;
-  const int oy0 = ty * TH, ox0 = tx * TW;
-  const int iy0 = 2 * oy0 - 1, xs = 2 * ox0 - 4;  // patch column 0 = input column xs (xs % 4 == 0)
+  b = bid / tiles_y;
+  oy0 = ty * TH;
+  ox0 = tx * TW;
+}
+
+// ------------------------------------------------------------------------------------------------ MFMA (f16, i8)
+typedef _Float16 h8 __attribute__((ext_vector_type(8)));
+
+template <typename T, int NT>  // NT = Cout / 16 channel tiles
+__global__ __launch_bounds__(256) void stem_mfma(const ConvArgs a) {
+  constexpr bool QUANT = sizeof(T) == 1;
+  __shared__ __attribute__((aligned(16))) f16 patch[3 * PH * PW];
+  __shared__ float post[QUANT ? 256 : 1];
+  int b, oy0, ox0;
+  tile_of(a, b, oy0, ox0);
+  const int iy0 = 2 * oy0 - 1, xs = 2 * ox0 - 4;
+  const bool div = ym_input_max(a.ctl) > 1.0f + a.eps;
+  const size_t HW = (size_t)a.Hin * a.Win;
+  const float* img = a.nchw + (size_t)b * 3 * HW;
+  const QRec* Q = a.q;
+  float inv = 0.f;
+  int zi = 0, lo = 0, hi = 0;
+  if constexpr (QUANT) {
+    inv = Q->inv_s_in;
+    zi = Q->z_in;
+    lo = Q->qlo;
+    hi = Q->qhi;
+    post[threadIdx.x] = Q->post[threadIdx.x];
+  }
+  // all of a thread's patch loads are issued before the first is consumed (one memory latency, not NIT)
+  constexpr int NIT = (3 * PH * PW4 + 255) / 256;
+  f32x4 v[NIT];
+  bool in[NIT];
+#pragma unroll
+  for (int it = 0; it < NIT; ++it) {
+    const int i = threadIdx.x + 256 * it;
+    const int c = i / (PH * PW4), r = i - c * (PH * PW4);
+    const int py = r / PW4, q = r - (r / PW4) * PW4;
+    const int iy = iy0 + py, ix = xs + 4 * q;
+    in[it] = i < 3 * PH * PW4 && (unsigned)iy < (unsigned)a.Hin && (unsigned)ix < (unsigned)a.Win;
+    v[it] = in[it] ? *reinterpret_cast<const f32x4*>(img + c * HW + (size_t)iy * a.Win + ix) : f32x4{0.f, 0.f, 0.f, 0.f};
+  }
+#pragma unroll
+  for (int it = 0; it < NIT; ++it) {
+    const int i = threadIdx.x + 256 * it;
+    if (i >= 3 * PH * PW4) break;
+    f16x4 h = {0, 0, 0, 0};
+    if (in[it]) {
+#pragma unroll
+      for (int e = 0; e < 4; ++e) {
+        float x = v[it][e];
+        if (div) x = x / 255.0f;
+        if constexpr (QUANT) h[e] = (f16)(float)(clampi((int)rintf(__fmul_rn(x, inv)) + zi, lo, hi) - zi);
+        else h[e] = (f16)x;  // the activation storage precision, as the NHWC input of the MFMA path
+      }
+    }
+    *reinterpret_cast<f16x4*>(patch + 4 * i) = h;  // i = (c*PH + py)*PW4 + q
+  }
+  // Per-lane K slots: lane l covers K = 8(l>>4) .. +7 of pixel column l&15; K = tap (ky*3 + kx)*3 + c (the wstem row
+  // order), K >= 27 zero weights (their patch reads point at a valid element).
+  const int lane = threadIdx.x & 63, wave = threadIdx.x >> 6;
+  const int kg = lane >> 4, col = lane & 15;
+  int off[8];
+  h8 wf[NT];
+#pragma unroll
+  for (int j = 0; j < 8; ++j) {
+    const int k = 8 * kg + j;
+    const int kk = k / 3, c = k - (k / 3) * 3;
+    const int ky = kk / 3, kx = kk - (kk / 3) * 3;
+    off[j] = k < 27 ? (c * PH + ky) * PW + kx + 3 : 3;  // +3: the patch starts at x0 - 4, the window at x0 - 1
+#pragma unroll
+    for (int t = 0; t < NT; ++t) wf[t][j] = k < 27 ? (f16)a.wstem[k * a.N + 16 * t + col] : (f16)0.f;
+  }
+  float bias[NT][4], sasw[NT][4];
+#pragma unroll
+  for (int t = 0; t < NT; ++t)
+#pragma unroll
+    for (int r = 0; r < 4; ++r) {
+      bias[t][r] = a.bias[16 * t + 4 * kg + r];
+      if constexpr (QUANT) sasw[t][r] = a.sasw[16 * t + 4 * kg + r];
+    }
+  __syncthreads();
+  // wave w: pixel groups 4w .. 4w+3 of the tile's 16 (16 consecutive columns of one row each)
+#pragma unroll
+  for (int gi = 0; gi < 4; ++gi) {
+    const int g = 4 * wave + gi;
+    const int ly = g >> 1, lx = (g & 1) * 16 + col;
+    const f16* pp = patch + 2 * ly * PW + 2 * lx;
+    h8 bf;
+#pragma unroll
+    for (int j = 0; j < 8; ++j) bf[j] = pp[off[j]];
+    const int oy = oy0 + ly, ox = ox0 + lx;
+    const bool ok = oy < a.Ho && ox < a.Wo;
+    T* dst = static_cast<T*>(a.dst) + (size_t)(b * a.d_P + oy * a.d_W + ox) * a.d_ctot + a.d_coff + 4 * kg;
+#pragma unroll
+    for (int t = 0; t < NT; ++t) {
+      const f32x4 acc = __builtin_amdgcn_mfma_f32_16x16x32_f16(wf[t], bf, f32x4{0.f, 0.f, 0.f, 0.f}, 0, 0, 0);
+      if (!ok) continue;
+      if constexpr (QUANT) {
+        int ov[4];
+#pragma unroll
+        for (int r = 0; r < 4; ++r) {
+          const float y = ym_opaque(acc[r] * sasw[t][r]) + bias[t][r];  // two roundings, as the oracle's mul + add
+          const int qc = clampi((int)rintf(__fmul_rn(y, Q->inv_sc)) + Q->zc, lo, hi);
+          ov[r] = clampi((int)rintf(__fmul_rn(post[qc], Q->inv_so)) + Q->zo, lo, hi) - 128;
+        }
+        *reinterpret_cast<int*>(dst + 16 * t) =
+            (ov[0] & 0xFF) | ((ov[1] & 0xFF) << 8) | ((ov[2] & 0xFF) << 16) | ((unsigned)(ov[3] & 0xFF) << 24);
+      } else {
+        f16x4 o;
+#pragma unroll
+        for (int r = 0; r < 4; ++r) o[r] = (f16)ym_silu_fast(acc[r] + bias[t][r]);
+        *reinterpret_cast<f16x4*>(dst + 16 * t) = o;
+      }
+    }
+  }
+}
+
+// ------------------------------------------------------------------------------------------------ VALU (f32 parity)
+__global__ __launch_bounds__(256) void stem_valu(const ConvArgs a) {
+  __shared__ __attribute__((aligned(16))) float patch[3 * PH * PW];
+  int b, oy0, ox0;
+  tile_of(a, b, oy0, ox0);
+  const int iy0 = 2 * oy0 - 1, xs = 2 * ox0 - 4;
   const bool div = ym_input_max(a.ctl) > 1.0f + a.eps;
   const size_t HW = (size_t)a.Hin * a.Win;
   const float* img = a.nchw + (size_t)b * 3 * HW;
@@ -40,28 +165,18 @@ __global__ __launch_bounds__(256) void stem_conv3x3s2(const ConvArgs a) {
     const int py = r / PW4, q = r - (r / PW4) * PW4;
     const int iy = iy0 + py, ix = xs + 4 * q;
     f32x4 v = {0.f, 0.f, 0.f, 0.f};
-    if ((unsigned)iy < (unsigned)a.Hin && (unsigned)ix < (unsigned)a.Win)
+    if ((unsigned)iy < (unsigned)a.Hin && (unsigned)ix < (unsigned)a.Win) {
       v = *reinterpret_cast<const f32x4*>(img + c * HW + (size_t)iy * a.Win + ix);
+      if (div) {
 #pragma unroll
-    for (int e = 0; e < 4; ++e) {
-      float x = v[e];
-      if (div) x = x / 255.0f;
-      v[e] = (float)(T)x;  // the activation storage precision, as the NHWC input of the MFMA path
+        for (int e = 0; e < 4; ++e) v[e] = v[e] / 255.0f;
+      }
     }
     *reinterpret_cast<f32x4*>(patch + (c * PH + py) * PW + 4 * q) = v;
   }
-  const T* W = static_cast<const T*>(a.w);
-  for (int i = threadIdx.x; i < 27 * N; i += 256) {
-    const int tap = i / N, n = i - (i / N) * N;  // tap = (ky*3 + kx)*3 + c
-    const int kk = tap / 3, c = tap - (tap / 3) * 3;
-    wl[i] = (float)W[(size_t)n * a.Kpad + kk * 8 + c];
-  }
-  for (int i = threadIdx.x; i < N; i += 256) bl[i] = a.bias[i];
   __syncthreads();
   const int t = threadIdx.x;
-  if (t >= TH * TW * G) return;
-  const int g = t % G, pix = t / G;
-  const int ly = pix / TW, lx = pix - (pix / TW) * TW;
+  const int ly = t / TW, lx = t - (t / TW) * TW;
   const int oy = oy0 + ly, ox = ox0 + lx;
   if (oy >= a.Ho || ox >= a.Wo) return;
   float x[27];
@@ -72,58 +187,57 @@ __global__ __launch_bounds__(256) void stem_conv3x3s2(const ConvArgs a) {
 #pragma unroll
       for (int c = 0; c < 3; ++c)
         x[(ky * 3 + kx) * 3 + c] = patch[(c * PH + 2 * ly + ky) * PW + 2 * lx + kx + 3];  // +3: xs = x0 - 4
-  const int n0 = g * 16;
-  float acc[16];
+  const size_t pix = (size_t)(b * a.Ho + oy) * a.Wo + ox;
+  const float* __restrict__ Wt = a.wstem;  // [27][N] fp32, wave-uniform addresses
+  for (int g = 0; g < a.N; g += 16) {
+    float acc[16];
 #pragma unroll
-  for (int e = 0; e < 16; ++e) acc[e] = bl[n0 + e];
+    for (int e = 0; e < 16; ++e) acc[e] = a.bias[g + e];
 #pragma unroll
-  for (int k = 0; k < 27; ++k) {
-    const float* wr = wl + k * N + n0;
+    for (int k = 0; k < 27; ++k)
 #pragma unroll
-    for (int e = 0; e < 16; ++e) acc[e] = fmaf(x[k], wr[e], acc[e]);
+      for (int e = 0; e < 16; ++e) acc[e] = fmaf(x[k], Wt[k * a.N + g + e], acc[e]);
+    float* dst = static_cast<float*>(a.dst) + (size_t)(b * a.d_P + oy * a.d_W + ox) * a.d_ctot + a.d_coff + g;
+    f32x8 o0, o1;
+#pragma unroll
+    for (int e = 0; e < 8; ++e) {
+      o0[e] = ym_silu(acc[e]);
+      o1[e] = ym_silu(acc[8 + e]);
+    }
+    Vec8<float>::store(dst, o0);
+    Vec8<float>::store(dst + 8, o1);
+    if (a.raw) {  // f32 calibration run: the pre-activation output, (M, N) row-major
+#pragma unroll
+      for (int e = 0; e < 16; ++e) a.raw[pix * a.N + g + e] = acc[e];
+    }
   }
-  typename Vec8<T>::type o0, o1;
-#pragma unroll
-  for (int e = 0; e < 8; ++e) {
-    o0[e] = (T)ym_silu(acc[e]);
-    o1[e] = (T)ym_silu(acc[8 + e]);
+}
+
+dim3 grid_of(const ConvArgs& a) {
+  const int B = a.M / (a.Ho * a.Wo);
+  return dim3(B * ((a.Ho + TH - 1) / TH) * ((a.Wo + TW - 1) / TW));
+}
+
+template <typename T>
+hipError_t launch_mfma(const ConvArgs& a, hipStream_t st) {
+  switch (a.N / 16) {
+    case 1: hipLaunchKernelGGL((stem_mfma<T, 1>), grid_of(a), dim3(256), 0, st, a); break;
+    case 2: hipLaunchKernelGGL((stem_mfma<T, 2>), grid_of(a), dim3(256), 0, st, a); break;
+    case 4: hipLaunchKernelGGL((stem_mfma<T, 4>), grid_of(a), dim3(256), 0, st, a); break;
+    case 6: hipLaunchKernelGGL((stem_mfma<T, 6>), grid_of(a), dim3(256), 0, st, a); break;
+    default: return hipErrorInvalidValue;
   }
-  T* dst = static_cast<T*>(a.dst) + (size_t)(b * a.d_P + oy * a.d_W + ox) * a.d_ctot + a.d_coff + n0;
-  Vec8<T>::store(dst, o0);
-  Vec8<T>::store(dst + 8, o1);
-  if (a.raw) {  // f32 calibration run: the pre-activation output, (M, N) row-major
-    float* r = a.raw + ((size_t)(b * a.Ho + oy) * a.Wo + ox) * N + n0;
-#pragma unroll
-    for (int e = 0; e < 16; ++e) r[e] = acc[e];
-  }
+  return hipGetLastError();
 }
 
 }  // namespace
 
-template <typename T, int G>
-hipError_t launch_g(const ConvArgs& a, hipStream_t st) {
-  constexpr int TW = 32 / G;
-  constexpr int PW = ((2 * TW + 4 + 3) / 4 + 1) * 4;
-  const int B = a.M / (a.Ho * a.Wo);
-  const dim3 grid(B * ((a.Ho + TH - 1) / TH) * ((a.Wo + TW - 1) / TW));
-  const size_t lds = ((size_t)3 * (2 * TH + 1) * PW + 28 * 16 * G) * sizeof(float);
-  hipLaunchKernelGGL((stem_conv3x3s2<T, G>), grid, dim3(256), lds, st, a);
-  return hipGetLastError();
-}
-
-template <typename T>
-hipError_t launch_t(const ConvArgs& a, hipStream_t st) {
-  switch (a.N) {
-    case 16: return launch_g<T, 1>(a, st);
-    case 32: return launch_g<T, 2>(a, st);
-    case 64: return launch_g<T, 4>(a, st);
-    case 96: return launch_g<T, 6>(a, st);
-  }
-  return hipErrorInvalidValue;
-}
-
 hipError_t ym_launch_stem(int dtype, const ConvArgs& a, hipStream_t st) {
-  if (dtype == YM_DT_I8) return ym_launch_stem_i8(a, st);
-  if (a.k != 3 || a.s != 2 || !a.nchw || a.shuffle || a.res || !a.act || a.Win % 4) return hipErrorInvalidValue;
-  return dtype == YM_DT_F16 ? launch_t<f16>(a, st) : launch_t<float>(a, st);
+  if (a.k != 3 || a.s != 2 || !a.nchw || a.shuffle || a.res || !a.act || a.Win % 4 || !a.wstem || a.N % 16 ||
+      a.M % (a.Ho * a.Wo))
+    return hipErrorInvalidValue;
+  if (dtype == YM_DT_I8) return a.q && a.sasw ? launch_mfma<i8>(a, st) : hipErrorInvalidValue;
+  if (dtype == YM_DT_F16) return a.raw ? hipErrorInvalidValue : launch_mfma<f16>(a, st);
+  hipLaunchKernelGGL(stem_valu, grid_of(a), dim3(256), 0, st, a);
+  return hipGetLastError();
 }
