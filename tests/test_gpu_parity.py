@@ -109,6 +109,16 @@ def test_predict_kwargs_f32(kw):
         assert len(res[0]) <= kw["max_det"]
 
 
+@pytest.mark.parametrize("conf", [0.5, 0.3, 0.15, 0.06, 0.02, 0.004])
+def test_nms_paths_f32(conf):
+    """Candidate counts from a few dozen to thousands per image: the one-wave (<= 64), bit-matrix (<= 512) and
+    LDS / global-scratch (> 512) NMS paths of csrc/ym_misc.hip nms_image all reproduce torchvision's greedy order."""
+    x = make_input("uniform", (31, 32), 640)
+    ref = oracle().predict(x, conf=conf)
+    res = model("n", "f32").predict(x.to(DEV), conf=conf)
+    check(ref, res, conf, 0.7, 1e-3, 1e-3)
+
+
 @pytest.mark.parametrize("S,B", [(320, 3), (1280, 1), (640, 8)])
 def test_sizes_and_batches_f32(S, B):
     x = make_input("uniform", tuple(range(31, 31 + B)), S)
@@ -219,7 +229,7 @@ def test_results_contract_and_benchmark():
 
 # ------------------------------------------------------------------------------------------------ LDS-DMA conv configs
 DMA_FIRST = 17  # csrc/ym_conv.hip: ids >= 17 are the LDS-DMA / split-K kernels of csrc/ym_conv_dma.hip
-STREAM_FIRST = DMA_FIRST + 18  # then the streaming 1x1 / 3x3 kernels of csrc/ym_conv_stream.hip (15 configs)
+STREAM_FIRST = DMA_FIRST + 18  # then csrc/ym_conv_stream.hip: 15 streaming 1x1 / 3x3 configs, 12 small-M split-K ones
 
 
 def _force_cfg(eng, x, cfg):
@@ -229,7 +239,7 @@ def _force_cfg(eng, x, cfg):
     eng.rt.set_op_cfg(B, H, W, [cfg if op.kind == "conv" else -1 for op in eng.graph.ops])
 
 
-@pytest.mark.parametrize("cfg", list(range(DMA_FIRST, STREAM_FIRST + 15)))
+@pytest.mark.parametrize("cfg", list(range(DMA_FIRST, STREAM_FIRST + 27)))
 def test_dma_conv_configs_match_oracle(cfg):
     """Every conv of yolo11n (1x1 two-source/upsampled, 3x3 s1/s2, residual, fp32 Detect rows) on one DMA or
     streaming config (ops a config does not apply to fall back to the heuristic choice)."""

@@ -59,7 +59,7 @@ __global__ __launch_bounds__(256) void conv_stream(const ConvArgs a) {
   const f16* s0 = static_cast<const f16*>(a.src0);
   const f16* s1 = static_cast<const f16*>(a.src1);
   const int K = a.C0 + a.C1;
-  const int lc8 = __builtin_ctz(a.Cin8);  // 3x3: Cin / 8 is a power of two (checked on the host)
+  const unsigned c8m = (0x1000000u + a.Cin8 - 1) / a.Cin8;  // 3x3: tap = (chunk * c8m) >> 24 (chunk < 9 Cin8)
 
   // B fragments of the iteration starting at group gb: [PX][KS]
   auto load = [&](int gb, h8 (&bf)[PX][KS]) {
@@ -82,13 +82,13 @@ __global__ __launch_bounds__(256) void conv_stream(const ConvArgs a) {
                           : Vec8<f16>::load(s1 + p1 * a.s1_ctot + a.s1_coff + (k0 - a.C0));
           bf[p][ks] = v;
         }
-      } else {  // 3x3, pad 1, stride a.s: chunk c = 4 ks + g is tap c >> lc8, channels 8 (c & (Cin8 - 1)) ..
+      } else {  // 3x3, pad 1, stride a.s: chunk c = 4 ks + g is tap c / Cin8, channels 8 (c % Cin8) ..
         const f16* img = s0 + (size_t)b * a.s0_P * a.s0_ctot + a.s0_coff;
         const int iy0 = y * a.s - 1, ix0 = x * a.s - 1;
 #pragma unroll
         for (int ks = 0; ks < KS; ++ks) {
           const int c = 4 * ks + g;
-          const int t = c >> lc8, cb = c & (a.Cin8 - 1);
+          const int t = (int)(((unsigned)c * c8m) >> 24), cb = c - t * a.Cin8;
           const int ky = t >= 6 ? 2 : (t >= 3 ? 1 : 0), kx = t - 3 * ky;
           const int iy = iy0 + ky, ix = ix0 + kx;
           h8 v = Vec8<f16>::zero();
@@ -153,6 +153,132 @@ __global__ __launch_bounds__(256) void conv_stream(const ConvArgs a) {
   }
 }
 
+// ------------------------------------------------------------------------------------------------ small-M convs
+// The 20x20 / 40x40 layers (M = B·400 … B·1600 pixels): too few output tiles to fill 256 CUs with whole-K tiles,
+// so their time is one tile's dependent memory round trips.  conv_small puts one 16-pixel x 16-channel output
+// block (PXG blocks along M) on a 4-wave workgroup that splits K four ways: every wave issues ALL of its A (weight
+// rows, 16 B per lane) and B (im2col, 16 B per lane) fragments at once, runs its MFMAs, and the partial blocks meet
+// in LDS — one memory latency per launch.  Grid = ceil(M / 16 PXG) x ceil(N / 16) workgroups.
+#define YM_SMALL_CFGS(X)                                                                                          \
+  X(0, 1, 2, 1) X(1, 1, 4, 1) X(2, 1, 8, 1) X(3, 1, 16, 1) X(4, 1, 2, 2) X(5, 1, 4, 2) X(6, 1, 8, 2)             \
+  X(7, 3, 5, 1) X(8, 3, 9, 1) X(9, 3, 18, 1) X(10, 3, 5, 2) X(11, 3, 9, 2)
+struct MCfg {
+  int kind, ksw, pxg;  // 1x1 / 3x3; max K steps of 32 per wave (Kpad <= 128 KSW); 16-pixel blocks per workgroup
+};
+constexpr MCfg kSmall[] = {
+#define YM_X(id, kind, ksw, pxg) {kind, ksw, pxg},
+    YM_SMALL_CFGS(YM_X)
+#undef YM_X
+};
+constexpr int kNumSmall = sizeof(kSmall) / sizeof(kSmall[0]);
+
+template <typename OutT, int KIND, int KSW, int PXG>
+__global__ __launch_bounds__(256) void conv_small(const ConvArgs a) {
+  __shared__ f32x4 red[3][PXG][64];
+  const int tid = threadIdx.x, lane = tid & 63, wave = tid >> 6;
+  const int g = lane >> 4, col = lane & 15;
+  const int ntn = (a.N + 15) >> 4;
+  const int tn = blockIdx.x % ntn, tm = blockIdx.x / ntn;
+  const int KS = a.Kpad >> 5;
+  const int HW = a.Ho * a.Wo;
+  const f16* s0 = static_cast<const f16*>(a.src0);
+  const f16* s1 = static_cast<const f16*>(a.src1);
+  const int K = a.C0 + a.C1;
+  const unsigned c8m = (0x1000000u + a.Cin8 - 1) / a.Cin8;
+  const int nrow = 16 * tn + col;
+  const f16* wr = static_cast<const f16*>(a.w) + (size_t)(nrow < a.N ? nrow : 0) * a.Kpad + 8 * g;
+  h8 af[KSW];
+#pragma unroll
+  for (int j = 0; j < KSW; ++j) {
+    const int ks = wave + 4 * j;
+    af[j] = (ks < KS && nrow < a.N) ? Vec8<f16>::load(wr + 32 * ks) : Vec8<f16>::zero();
+  }
+  h8 bf[PXG][KSW];
+  int b[PXG], y[PXG], x[PXG];
+  bool ok[PXG];
+#pragma unroll
+  for (int p = 0; p < PXG; ++p) {
+    const int m = (tm * PXG + p) * 16 + col;
+    ok[p] = m < a.M;
+    const int mm = ok[p] ? m : 0;
+    b[p] = ym_div(mm, a.fd_hw);
+    const int rem = mm - b[p] * HW;
+    y[p] = ym_div(rem, a.fd_w);
+    x[p] = rem - y[p] * a.Wo;
+    if constexpr (KIND == 1) {
+      const size_t p0 = a.up0 ? (size_t)b[p] * a.s0_P + (y[p] >> 1) * a.s0_W + (x[p] >> 1)
+                              : (size_t)b[p] * a.s0_P + y[p] * a.s0_W + x[p];
+      const size_t p1 = (size_t)b[p] * a.s1_P + y[p] * a.Win + x[p];
+#pragma unroll
+      for (int j = 0; j < KSW; ++j) {
+        const int k0 = 32 * (wave + 4 * j) + 8 * g;
+        h8 v = Vec8<f16>::zero();
+        if (ok[p] && k0 < K)
+          v = k0 < a.C0 ? Vec8<f16>::load(s0 + p0 * a.s0_ctot + a.s0_coff + k0)
+                        : Vec8<f16>::load(s1 + p1 * a.s1_ctot + a.s1_coff + (k0 - a.C0));
+        bf[p][j] = v;
+      }
+    } else {
+      const f16* img = s0 + (size_t)b[p] * a.s0_P * a.s0_ctot + a.s0_coff;
+      const int iy0 = y[p] * a.s - 1, ix0 = x[p] * a.s - 1;
+#pragma unroll
+      for (int j = 0; j < KSW; ++j) {
+        const int c = 4 * (wave + 4 * j) + g;
+        const int t = (int)(((unsigned)c * c8m) >> 24), cb = c - t * a.Cin8;
+        const int ky = t >= 6 ? 2 : (t >= 3 ? 1 : 0), kx = t - 3 * ky;
+        const int iy = iy0 + ky, ix = ix0 + kx;
+        h8 v = Vec8<f16>::zero();
+        if (ok[p] && c < a.Kc && (unsigned)iy < (unsigned)a.Hin && (unsigned)ix < (unsigned)a.Win)
+          v = Vec8<f16>::load(img + (size_t)(iy * a.Win + ix) * a.s0_ctot + 8 * cb);
+        bf[p][j] = v;
+      }
+    }
+  }
+  f32x4 acc[PXG];
+#pragma unroll
+  for (int p = 0; p < PXG; ++p) {
+    acc[p] = f32x4{0.f, 0.f, 0.f, 0.f};
+#pragma unroll
+    for (int j = 0; j < KSW; ++j) acc[p] = __builtin_amdgcn_mfma_f32_16x16x32_f16(af[j], bf[p][j], acc[p], 0, 0, 0);
+    if (wave > 0) red[wave - 1][p][lane] = acc[p];
+  }
+  __syncthreads();
+  if (wave > 0) return;
+  const int n0 = 16 * tn + 4 * g;
+  if (n0 >= a.N) return;
+  const f32x4 b4 = *reinterpret_cast<const f32x4*>(a.bias + n0);
+  OutT* dst = static_cast<OutT*>(a.dst);
+  const f16* res = static_cast<const f16*>(a.res);
+#pragma unroll
+  for (int p = 0; p < PXG; ++p) {
+    if (!ok[p]) continue;
+    const f32x4 r = acc[p] + red[0][p][lane] + red[1][p][lane] + red[2][p][lane];
+    float v[4];
+#pragma unroll
+    for (int e = 0; e < 4; ++e) {
+      const float xv = r[e] + b4[e];
+      v[e] = a.act ? ym_silu_fast(xv) : xv;
+    }
+    if (res) {
+      const f16x4 rv = *reinterpret_cast<const f16x4*>(
+          res + (size_t)(b[p] * a.r_P + y[p] * a.Wo + x[p]) * a.r_ctot + a.r_coff + n0);
+#pragma unroll
+      for (int e = 0; e < 4; ++e) v[e] += (float)rv[e];
+    }
+    OutT* o = dst + (size_t)(b[p] * a.d_P + a.d_pixoff + y[p] * a.d_W + x[p]) * a.d_ctot + a.d_coff + n0;
+    if constexpr (sizeof(OutT) == 2) *reinterpret_cast<f16x4*>(o) = f16x4{(f16)v[0], (f16)v[1], (f16)v[2], (f16)v[3]};
+    else *reinterpret_cast<f32x4*>(o) = f32x4{v[0], v[1], v[2], v[3]};
+  }
+}
+
+template <typename OutT, int KIND, int KSW, int PXG>
+hipError_t launch_small(const ConvArgs& a, hipStream_t st) {
+  if (a.k != KIND || a.Kpad > 128 * KSW) return hipErrorInvalidValue;
+  const long wgs = (long)((a.M + 16 * PXG - 1) / (16 * PXG)) * ((a.N + 15) / 16);
+  hipLaunchKernelGGL((conv_small<OutT, KIND, KSW, PXG>), dim3(wgs), dim3(256), 0, st, a);
+  return hipGetLastError();
+}
+
 template <typename OutT, int KIND, int KS, int PX, int CAP>
 hipError_t launch(const ConvArgs& a, hipStream_t st) {
   if (a.Kpad != KS * 32 || a.k != KIND) return hipErrorInvalidValue;
@@ -174,24 +300,30 @@ hipError_t dispatch(const ConvArgs& a, int i, hipStream_t st) {
     YM_STREAM_CFGS(YM_X)
 #undef YM_X
   }
+  switch (i - kNumStream) {
+#define YM_X(id, kind, ksw, pxg) \
+  case id: return launch_small<OutT, kind, ksw, pxg>(a, st);
+    YM_SMALL_CFGS(YM_X)
+#undef YM_X
+  }
   return hipErrorInvalidValue;
 }
 
 }  // namespace
 
-int ym_conv_stream_num_cfgs() { return kNumStream; }
+int ym_conv_stream_num_cfgs() { return kNumStream + kNumSmall; }
 
 // Host-side applicability: f16 plans; 1x1 stride-1 convs without pixel shuffle (8-channel-aligned concat split) or
-// 3x3 convs on one plain source with Cin / 8 a power of two; N % 4 == 0 and 4-aligned output channel slices
+// 3x3 convs on one plain source; N % 4 == 0 and 4-aligned output channel slices
 // (8/16-byte stores); weights + bias <= 80 KB of LDS.
 hipError_t ym_launch_conv_stream(int out_f32, const ConvArgs& a, int i, hipStream_t st) {
-  if (i < 0 || i >= kNumStream) return hipErrorInvalidValue;
+  if (i < 0 || i >= kNumStream + kNumSmall) return hipErrorInvalidValue;
   if (a.shuffle || a.raw || a.nchw || !a.src0 || (a.N & 3) || a.Kpad % 32) return hipErrorInvalidValue;
   if (a.k == 1) {
     if (a.s != 1 || a.C0 % 8 || a.C1 % 8) return hipErrorInvalidValue;
     if (a.src1 && (a.s1_coff % 8 || a.s1_ctot % 8)) return hipErrorInvalidValue;
   } else if (a.k == 3) {
-    if (a.src1 || a.up0 || a.pad != 1 || (a.Cin8 & (a.Cin8 - 1))) return hipErrorInvalidValue;
+    if (a.src1 || a.up0 || a.pad != 1 || a.Cin8 > 1024) return hipErrorInvalidValue;
   } else {
     return hipErrorInvalidValue;
   }

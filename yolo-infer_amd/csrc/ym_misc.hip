@@ -430,11 +430,21 @@ __global__ __launch_bounds__(256) void decode_anchors(const DecodeArgs a) {
   const long total = (long)a.B * a.A;
   const long a0 = blockIdx.x * 64L;
   const int nrow = total - a0 < 64 ? (int)(total - a0) : 64;
-  {
+  {  // every load in flight before the first LDS store (no_tot <= 192: at most 12 per thread)
     const f32x4* src = reinterpret_cast<const f32x4*>(a.anchors + a0 * a.no_tot);
     f32x4* dst = reinterpret_cast<f32x4*>(rows);
     const int n4 = nrow * a.no_tot / 4;
-    for (int i = threadIdx.x; i < n4; i += 256) dst[i] = src[i];
+    f32x4 v[12];
+#pragma unroll
+    for (int it = 0; it < 12; ++it) {
+      const int i = threadIdx.x + 256 * it;
+      if (i < n4) v[it] = src[i];
+    }
+#pragma unroll
+    for (int it = 0; it < 12; ++it) {
+      const int i = threadIdx.x + 256 * it;
+      if (i < n4) dst[i] = v[it];
+    }
   }
   __syncthreads();
   const long gidx = a0 + (threadIdx.x >> 2);
@@ -518,6 +528,7 @@ __global__ __launch_bounds__(256) void decode_anchors(const DecodeArgs a) {
 // larger candidate sets fall back to the same algorithm on global scratch.
 constexpr int NMS_T = 1024;
 constexpr int NMS_LDS = 4096;
+constexpr int NMS_BM = 512;  // bit-matrix path: 512 x 8 words of 64 bits (32 KB) behind the first 512 boxes
 
 __device__ void bitonic_sort_desc(unsigned long long* k, int n2, int tid) {
   for (int size = 2; size <= n2; size <<= 1) {
@@ -608,6 +619,77 @@ __global__ __launch_bounds__(NMS_T) void nms_image(const NmsArgs a) {
       for (int m = 0; m < a.nm; ++m) r[6 + m] = a.anchors[(ib + ai) * a.no_tot + a.mask_off + m];
     }
     if (lane == 0) a.out_counts[b] = kept;
+    return;
+  }
+  if (n <= NMS_BM) {
+    // 64 < n <= 512: rank sort (one barrier), the IoU > iou bit matrix computed by all 1024 threads, then ONE
+    // wave scans it greedily (torchvision's loop: keep i unless a kept earlier box suppressed it) — no barrier
+    // per kept box.  Keys are unique (anchor index in the low word), so the ranks are a permutation.
+    unsigned long long* sorted = sk + NMS_BM;
+    unsigned long long* mask = reinterpret_cast<unsigned long long*>(sbx + NMS_BM);  // [ne][W]
+    unsigned long long ki = 0;
+    if (tid < n) sk[tid] = ki = gk[tid];
+    __syncthreads();
+    if (tid < n) {
+      int r = 0;
+      for (int j = 0; j < n; ++j) r += sk[j] > ki;
+      sorted[r] = ki;
+    }
+    __syncthreads();
+    const int ne = n < a.max_nms ? n : a.max_nms;
+    const int W = (ne + 63) >> 6;
+    if (tid < ne) {
+      const unsigned ai = 0xFFFFFFFFu - (unsigned)(sorted[tid] & 0xFFFFFFFFull);
+      const float4 v = a.boxes[ib + ai];
+      const float off = a.agnostic ? 0.0f : (float)a.cls[ib + ai] * a.max_wh;
+      const float4 o = make_float4(v.x + off, v.y + off, v.z + off, v.w + off);
+      sbx[tid] = o;
+      sar[tid] = __fmul_rn(__fsub_rn(o.z, o.x), __fsub_rn(o.w, o.y));
+    }
+    __syncthreads();
+    for (int pq = tid; pq < ne * W; pq += NMS_T) {
+      const int i = pq / W, w = pq - i * W;
+      unsigned long long bits = 0;
+      if (64 * w + 63 > i) {
+        const float4 bi = sbx[i];
+        const float ai_area = sar[i];
+        for (int jj = 0; jj < 64; ++jj) {
+          const int j = 64 * w + jj;
+          if (j > i && j < ne && iou_gt(bi, ai_area, sbx[j], sar[j], a.iou)) bits |= 1ull << jj;
+        }
+      }
+      mask[pq] = bits;
+    }
+    __syncthreads();
+    __shared__ int keep_bm[NMS_BM], kept_bm;
+    if (tid < 64) {
+      const int cap = a.max_det;
+      unsigned long long rem = 0;
+      int kept = 0;
+      for (int i = 0; i < ne && kept < cap; ++i) {
+        const unsigned long long wv = __shfl(rem, i >> 6);
+        if ((wv >> (i & 63)) & 1ull) continue;
+        if (tid == 0) keep_bm[kept] = i;
+        ++kept;
+        if (tid < W) rem |= mask[i * W + tid];
+      }
+      if (tid == 0) kept_bm = kept;
+    }
+    __syncthreads();
+    const int kept = kept_bm;
+    for (int q = tid; q < kept; q += NMS_T) {
+      const unsigned ai = 0xFFFFFFFFu - (unsigned)(sorted[keep_bm[q]] & 0xFFFFFFFFull);
+      const float4 v = a.boxes[ib + ai];
+      float* r = out + (size_t)q * rowlen;
+      r[0] = fminf(fmaxf(v.x, 0.f), a.img_w);
+      r[1] = fminf(fmaxf(v.y, 0.f), a.img_h);
+      r[2] = fminf(fmaxf(v.z, 0.f), a.img_w);
+      r[3] = fminf(fmaxf(v.w, 0.f), a.img_h);
+      r[4] = a.scores[ib + ai];
+      r[5] = (float)a.cls[ib + ai];
+      for (int m = 0; m < a.nm; ++m) r[6 + m] = a.anchors[(ib + ai) * a.no_tot + a.mask_off + m];
+    }
+    if (tid == 0) a.out_counts[b] = kept;
     return;
   }
   int n2 = 1;
