@@ -155,6 +155,31 @@ def test_graph_replay_bitwise_equals_eager():
     assert torch.equal(c1, c2) and torch.equal(d1, d2)
 
 
+@pytest.mark.parametrize("dtype,scale", [("f16", "n"), ("f16", "s"), ("f32", "n")])
+def test_branch_schedule_bitwise_equals_serial(dtype, scale):
+    """The one-lane branch schedule (csrc/ym_runtime.cpp build_schedule: Detect-head chains on their own streams
+    beside the neck) computes exactly what the serial launch order computes: same kernels, so bit-equal outputs."""
+    from core.model import YOLO11Model
+    x = make_input("uniform", tuple(range(41, 49)), 640).to(DEV)
+    m = model(scale, dtype)
+    eng = m.model.engine
+    d1, c1 = eng.run(x, use_graph=True)
+    d1, c1 = d1.clone(), c1.clone()
+    h1 = eng.read_buffer(eng.graph.anchor_buf.id, 8)
+    os.environ["YM_BRANCHES"] = "1"
+    try:
+        ms = YOLO11Model(size=scale, device="cuda:0", dtype=dtype, verbose=False)
+    finally:
+        del os.environ["YM_BRANCHES"]
+    es = ms.model.engine
+    for use_graph in (False, True):
+        d2, c2 = es.run(x, use_graph=use_graph)
+        assert torch.equal(c1, c2), use_graph
+        for b, n in enumerate(c1.tolist()):  # rows past the count are whatever an earlier call left there
+            assert torch.equal(d1[b, :n], d2[b, :n]), (use_graph, b)
+    assert torch.equal(h1, es.read_buffer(es.graph.anchor_buf.id, 8))
+
+
 def test_batch_independence():
     """An image's detections do not depend on its batch neighbours (per-pixel work only; the tuned tiles may differ
     between B=8 and B=1, so compare with the f32 tolerance)."""

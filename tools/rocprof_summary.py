@@ -22,8 +22,8 @@ import sys
 
 ROOT = os.path.dirname(os.path.dirname(os.path.abspath(__file__)))
 PROF = os.path.join(ROOT, "profiles")
-CONV = re.compile(r"conv_igemm|conv_lds|conv_dma|conv_i8")
-STEM = re.compile(r"stem_conv3x3s2|stem_i8")
+CONV = re.compile(r"conv_igemm|conv_lds|conv_dma|conv_i8|conv_stream|conv_small")
+STEM = re.compile(r"stem_conv3x3s2|stem_i8|stem_mfma|stem_valu")
 CALIB = re.compile(r"conv_igemm<float, float|conv_igemmIffL")  # the f32 calibration forwards of an int8 run
 
 

@@ -196,7 +196,7 @@ class YOLO11Model:
         if self.task != "segment":
             dt = (time.perf_counter() - t0) * 1e3
             speed = {"preprocess": 0.0, "inference": dt, "postprocess": 0.0}
-            return [Results(im[b], names, out[b, : n[b], :6], path=f"image{b}.jpg", speed=speed) for b in range(B)]
+            return [Results.from_batch(im, b, names, out, n[b], path=f"image{b}.jpg", speed=speed) for b in range(B)]
         # Segment: process_mask(upsample=True) on the GPU, then the predictor keeps only non-empty masks
         H, W = im.shape[2:]
         masks, nonempty, offs = eng.masks(out, n, H, W)

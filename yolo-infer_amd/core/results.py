@@ -131,6 +131,45 @@ class Results:
         self.keypoints = None
         self.obb = None
 
+    @classmethod
+    def from_batch(cls, batch: torch.Tensor, b: int, names: Dict[int, str], dets: torch.Tensor, n: int,
+                   path: str = "image0.jpg", speed=None) -> "Results":
+        """Image b of a predict() batch: boxes = dets[b, :n, :6] and the input slice batch[b], both taken (as tensor
+        views) on first access, so building the B Results of a call costs no tensor operations."""
+        r = cls.__new__(cls)
+        r._batch, r._b, r._dets, r._n = batch, b, dets, n
+        r._orig_tensor_v = None
+        r._orig_img = None
+        r.orig_shape = tuple(batch.shape[-2:])
+        r.names = names
+        r._boxes = None
+        r.masks = None
+        r.path = path
+        r.speed = speed or {"preprocess": None, "inference": None, "postprocess": None}
+        r.probs = r.keypoints = r.obb = None
+        return r
+
+    @property
+    def _orig_tensor(self):
+        if self._orig_tensor_v is None and getattr(self, "_batch", None) is not None:
+            self._orig_tensor_v = self._batch[self._b]
+        return self._orig_tensor_v
+
+    @_orig_tensor.setter
+    def _orig_tensor(self, t):
+        self._orig_tensor_v = t
+        self._batch = None
+
+    @property
+    def boxes(self) -> "Boxes":
+        if self._boxes is None:
+            self._boxes = Boxes(self._dets[self._b, : self._n, :6], self.orig_shape)
+        return self._boxes
+
+    @boxes.setter
+    def boxes(self, b):
+        self._boxes = b
+
     @property
     def orig_img(self) -> np.ndarray:
         """HWC uint8 copy of the input image, as upstream `convert_torch2numpy_batch` makes it

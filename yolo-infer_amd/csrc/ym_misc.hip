@@ -89,7 +89,10 @@ __global__ __launch_bounds__(256) void dwconv3x3(const DwArgs a) {
     for (int e = 0; e < 8; ++e) acc[e] = fmaf((float)v[t][e], w[t][e >> 2][e & 3], acc[e]);
   typename Vec8<T>::type o;
 #pragma unroll
-  for (int e = 0; e < 8; ++e) o[e] = (T)(a.act ? ym_silu(acc[e]) : acc[e]);
+  for (int e = 0; e < 8; ++e) {  // f16 plans: the fp16 rounding hides the fast SiLU's ~1 ulp (fp32)
+    const float sv = sizeof(T) == 2 ? ym_silu_fast(acc[e]) : ym_silu(acc[e]);
+    o[e] = (T)(a.act ? sv : acc[e]);
+  }
   Vec8<T>::store(static_cast<T*>(a.dst) + (size_t)(b * a.d_P + p) * a.d_ctot + a.d_coff + c0, o);
   if (a.raw) {  // f32 calibration run: the pre-activation output
 #pragma unroll
@@ -102,6 +105,9 @@ __global__ __launch_bounds__(256) void dwconv3x3(const DwArgs a) {
 // wider window).  Separable: row maxima of radius 2/4/6 in one pass over the 13-wide row window, then column
 // maxima.  One workgroup = one image x 8 channels; pixels move as 16-byte vectors and stay in LDS in the storage
 // type (max is exact in any precision).
+template <typename V>
+__device__ __forceinline__ V vmax(V x, V y) { return __builtin_elementwise_max(x, y); }  // v_pk_max_f16 for fp16
+
 template <typename T>
 __global__ __launch_bounds__(256) void sppf_pool(const PoolArgs a) {
   typedef typename Vec8<T>::type V;
@@ -113,8 +119,21 @@ __global__ __launch_bounds__(256) void sppf_pool(const PoolArgs a) {
   const int b = blockIdx.x / ng;
   const int c0 = (blockIdx.x % ng) * 8;
   T* buf = static_cast<T*>(a.buf);
-  for (int p = threadIdx.x; p < HW; p += 256)
-    in[p] = Vec8<T>::load(buf + (size_t)(b * a.P + p) * a.ctot + a.coff + c0);
+  {  // all loads in flight before the first LDS store (HW <= 1024 on the separable path's maps)
+    V v[4];
+#pragma unroll
+    for (int it = 0; it < 4; ++it) {
+      const int p = threadIdx.x + 256 * it;
+      if (p < HW) v[it] = Vec8<T>::load(buf + (size_t)(b * a.P + p) * a.ctot + a.coff + c0);
+    }
+#pragma unroll
+    for (int it = 0; it < 4; ++it) {
+      const int p = threadIdx.x + 256 * it;
+      if (p < HW) in[p] = v[it];
+    }
+    for (int p = threadIdx.x + 1024; p < HW; p += 256)
+      in[p] = Vec8<T>::load(buf + (size_t)(b * a.P + p) * a.ctot + a.coff + c0);
+  }
   __syncthreads();
   if (!a.sep) {  // LDS holds only the input image (large maps in f32): direct 2-D windows
     for (int it = threadIdx.x; it < 3 * HW; it += 256) {
@@ -123,11 +142,7 @@ __global__ __launch_bounds__(256) void sppf_pool(const PoolArgs a) {
       const int y = p / a.W, x = p - (p / a.W) * a.W;
       V m = in[p];
       for (int yy = y - r < 0 ? 0 : y - r; yy <= y + r && yy < a.H; ++yy)
-        for (int xx = x - r < 0 ? 0 : x - r; xx <= x + r && xx < a.W; ++xx) {
-          const V v = in[yy * a.W + xx];
-#pragma unroll
-          for (int e = 0; e < 8; ++e) m[e] = v[e] > m[e] ? v[e] : m[e];
-        }
+        for (int xx = x - r < 0 ? 0 : x - r; xx <= x + r && xx < a.W; ++xx) m = vmax(m, in[yy * a.W + xx]);
       Vec8<T>::store(buf + (size_t)(b * a.P + p) * a.ctot + a.coff + (j + 1) * a.C + c0, m);
     }
     return;
@@ -140,12 +155,9 @@ __global__ __launch_bounds__(256) void sppf_pool(const PoolArgs a) {
       if (dx == 0 || (unsigned)xx >= (unsigned)a.W) continue;
       const V v = in[y * a.W + xx];
       const int ad = dx < 0 ? -dx : dx;
-#pragma unroll
-      for (int e = 0; e < 8; ++e) {
-        m6[e] = v[e] > m6[e] ? v[e] : m6[e];
-        if (ad <= 4) m4[e] = v[e] > m4[e] ? v[e] : m4[e];
-        if (ad <= 2) m2[e] = v[e] > m2[e] ? v[e] : m2[e];
-      }
+      m6 = vmax(m6, v);
+      if (ad <= 4) m4 = vmax(m4, v);
+      if (ad <= 2) m2 = vmax(m2, v);
     }
     hr[p] = m2;
     hr[HW + p] = m4;
@@ -161,9 +173,7 @@ __global__ __launch_bounds__(256) void sppf_pool(const PoolArgs a) {
     for (int dy = -r; dy <= r; ++dy) {
       const int yy = y + dy;
       if (dy == 0 || (unsigned)yy >= (unsigned)a.H) continue;
-      const V v = h[yy * a.W + x];
-#pragma unroll
-      for (int e = 0; e < 8; ++e) m[e] = v[e] > m[e] ? v[e] : m[e];
+      m = vmax(m, h[yy * a.W + x]);
     }
     Vec8<T>::store(buf + (size_t)(b * a.P + p) * a.ctot + a.coff + (j + 1) * a.C + c0, m);
   }
@@ -293,21 +303,26 @@ __global__ __launch_bounds__(256) void attn_psa(const AttnArgs a) {
 
 // f16 plans, kd = 32 / hd = 64 (every YOLO11 scale) and N <= 512 tokens (inputs up to 724 px): the same Attention on
 // MFMA.  One workgroup = (image, head, 64 queries), one wave = 16 queries:
-//   1. V of the whole (image, head) is staged transposed in LDS, V^T [64][LDV] f16 (row pitch 16*NKT + 4 halves:
-//      the 8-byte fragment reads below hit 32 distinct banks);
-//   2. S^T = K·Q^T: one v_mfma_f32_16x16x32_f16 per 16 keys (K = kd = 32), A = K rows, B = the wave's 16 query rows,
-//      both plain 16-byte loads; the lane holds S^T[key 16t + 4(l>>4) + r][query l&15], all N keys in registers;
-//   3. softmax over keys: in-lane over the tiles, then across the 4 lane groups (fp32, max-subtracted, as torch);
+//   1. K [N][32] and V^T [64][N] of the whole (image, head) are staged in LDS with every load in flight at once
+//      (K rows padded to 80 bytes, V^T rows to 16 NKT + 4 halves: the fragment reads below spread over the banks);
+//   2. S^T = K·Q^T: one v_mfma_f32_16x16x32_f16 per 16 keys (K = kd = 32), A = K rows from LDS, B = the wave's 16
+//      query rows (one 16-byte load); the lane holds S^T[key 16t + 4(l>>4) + r][query l&15], all N keys in registers;
+//   3. softmax over keys: in-lane over the tiles, then across the 4 lane groups (fp32, max-subtracted, v_exp_f32
+//      on log2-scaled scores);
 //   4. O^T = V^T·P^T, K = 32 keys per MFMA in the lane-group order of step 2 (slot j of group g is key
 //      32s + 4g + j, or 32s + 16 + 4g + j - 4), so P comes straight from the softmax registers (rounded to fp16)
 //      and V^T as two 8-byte LDS reads; a lane ends with 4 consecutive channels of one query: 8-byte NHWC stores;
-//   5. + pe(v) (depthwise 3x3 + folded BN) from the staged V^T, store.
+//   5. + pe(v) (depthwise 3x3 + folded BN) from the staged V^T and LDS taps, store.
 typedef _Float16 h8v __attribute__((ext_vector_type(8)));
 
 template <int NKT>  // key tiles of 16 (even): N <= 16 NKT
 __global__ __launch_bounds__(256) void attn_psa_mfma(const AttnArgs a) {
-  extern __shared__ __attribute__((aligned(16))) f16 vt[];  // [64][LDV]
+  // LDS: V^T [64][LDV] f16, K [16 NKT][LDK] f16, pe weights [9][64] + bias [64] f32
+  extern __shared__ __attribute__((aligned(16))) f16 vt[];
   constexpr int LDV = 16 * NKT + 4;
+  constexpr int LDK = 40;  // 80-byte K rows: the 16-row fragment reads spread over the banks
+  f16* kl = vt + 64 * LDV;
+  float* pw = reinterpret_cast<float*>(kl + 16 * NKT * LDK);
   const int N = a.N;
   const int nqb = (N + 63) / 64;
   const int qb = blockIdx.x % nqb, bh = blockIdx.x / nqb;
@@ -317,36 +332,43 @@ __global__ __launch_bounds__(256) void attn_psa_mfma(const AttnArgs a) {
   const f16* qkv = static_cast<const f16*>(a.qkv);
   const size_t img = (size_t)b * a.q_P;
   const int hq = a.q_coff + h * 128;  // per head: q 32, k 32, v 64 channels
-  // 1. V^T (keys >= N zero)
-  {  // all loads in flight before the first LDS store (one memory latency, not NIT)
-    constexpr int NIT = (16 * NKT * 8 + 255) / 256;
+  // 1. K and V^T of the (image, head) into LDS (keys >= N zero), this head's positional-conv taps and bias
+  for (int i = tid; i < 640; i += 256)
+    pw[i] = i < 576 ? a.pe_w[(i >> 6) * a.C + h * 64 + (i & 63)] : a.pe_b[h * 64 + i - 576];
+  {  // all loads in flight before the first LDS store (one memory latency, not NIT): 12 chunks of 8 per key
+    constexpr int NIT = (16 * NKT * 12 + 255) / 256;
     f16x8 v[NIT];
 #pragma unroll
     for (int it = 0; it < NIT; ++it) {
-      const int i = tid + 256 * it, key = i >> 3, d0 = (i & 7) * 8;
-      v[it] = key < N ? Vec8<f16>::load(qkv + (img + key) * a.q_ctot + hq + 64 + d0) : Vec8<f16>::zero();
+      const int i = tid + 256 * it, key = i / 12, ch = i - key * 12;
+      v[it] = key < N ? Vec8<f16>::load(qkv + (img + key) * a.q_ctot + hq + 32 + 8 * ch) : Vec8<f16>::zero();
     }
 #pragma unroll
     for (int it = 0; it < NIT; ++it) {
-      const int i = tid + 256 * it, key = i >> 3, d0 = (i & 7) * 8;
+      const int i = tid + 256 * it, key = i / 12, ch = i - key * 12;
       if (key >= 16 * NKT) break;
+      if (ch < 4) {
+        *reinterpret_cast<f16x8*>(kl + key * LDK + 8 * ch) = v[it];
+      } else {
+        const int d0 = 8 * (ch - 4);
 #pragma unroll
-      for (int e = 0; e < 8; ++e) vt[(d0 + e) * LDV + key] = v[it][e];
+        for (int e = 0; e < 8; ++e) vt[(d0 + e) * LDV + key] = v[it][e];
+      }
     }
   }
-  // 2. scores
   const int q = qb * 64 + wave * 16 + c;
   h8v qf = Vec8<f16>::zero();
   if (q < N) qf = Vec8<f16>::load(qkv + (img + q) * a.q_ctot + hq + 8 * g);
+  __syncthreads();
+  // 2. scores, in log2 units (scale·log2 e folded in: softmax by exp2)
+  const float sl2 = a.scale * 1.4426950408889634f;
   float s[NKT][4];
 #pragma unroll
   for (int t = 0; t < NKT; ++t) {
-    const int key = 16 * t + c;
-    h8v kf = Vec8<f16>::zero();
-    if (key < N) kf = Vec8<f16>::load(qkv + (img + key) * a.q_ctot + hq + 32 + 8 * g);
+    const h8v kf = *reinterpret_cast<const h8v*>(kl + (16 * t + c) * LDK + 8 * g);
     const f32x4 d = __builtin_amdgcn_mfma_f32_16x16x32_f16(kf, qf, f32x4{0.f, 0.f, 0.f, 0.f}, 0, 0, 0);
 #pragma unroll
-    for (int r = 0; r < 4; ++r) s[t][r] = 16 * t + 4 * g + r < N ? d[r] * a.scale : -INFINITY;
+    for (int r = 0; r < 4; ++r) s[t][r] = 16 * t + 4 * g + r < N ? d[r] * sl2 : -INFINITY;
   }
   // 3. softmax over the keys of query l&15
   float m = -INFINITY;
@@ -361,13 +383,12 @@ __global__ __launch_bounds__(256) void attn_psa_mfma(const AttnArgs a) {
   for (int t = 0; t < NKT; ++t)
 #pragma unroll
     for (int r = 0; r < 4; ++r) {
-      s[t][r] = expf(s[t][r] - m);
+      s[t][r] = __builtin_amdgcn_exp2f(s[t][r] - m);  // v_exp_f32 (~1 ulp; P is rounded to fp16 below)
       sum += s[t][r];
     }
   sum += __shfl_xor(sum, 16);
   sum += __shfl_xor(sum, 32);
   const float rs = 1.0f / sum;
-  __syncthreads();
   // 4. O^T = V^T P^T
   f32x4 o[4];
 #pragma unroll
@@ -394,21 +415,18 @@ __global__ __launch_bounds__(256) void attn_psa_mfma(const AttnArgs a) {
   f16* dst = static_cast<f16*>(a.dst) + ((size_t)b * a.d_P + q) * a.d_ctot + a.d_coff + h * 64;
 #pragma unroll
   for (int dt = 0; dt < 4; ++dt) {
-    const int d0 = 16 * dt + 4 * g, ch0 = h * 64 + d0;
+    const int d0 = 16 * dt + 4 * g;
     float pe[4];
 #pragma unroll
-    for (int r = 0; r < 4; ++r) pe[r] = a.pe_b[ch0 + r];
-    for (int ky = 0; ky < 3; ++ky) {
-      const int iy = y + ky - 1;
-      if ((unsigned)iy >= (unsigned)a.H) continue;
-      for (int kx = 0; kx < 3; ++kx) {
-        const int ix = x + kx - 1;
-        if ((unsigned)ix >= (unsigned)a.W) continue;
-        const int nb = iy * a.W + ix;
-        const float* w = a.pe_w + (ky * 3 + kx) * a.C + ch0;
+    for (int r = 0; r < 4; ++r) pe[r] = pw[576 + d0 + r];
 #pragma unroll
-        for (int r = 0; r < 4; ++r) pe[r] = fmaf((float)vt[(d0 + r) * LDV + nb], w[r], pe[r]);
-      }
+    for (int t = 0; t < 9; ++t) {  // taps in (ky, kx) order; out-of-image taps skipped, as the zero-padded conv
+      const int iy = y + t / 3 - 1, ix = x + t % 3 - 1;
+      if ((unsigned)iy >= (unsigned)a.H || (unsigned)ix >= (unsigned)a.W) continue;
+      const int nb = iy * a.W + ix;
+      const f32x4 w = *reinterpret_cast<const f32x4*>(pw + 64 * t + d0);
+#pragma unroll
+      for (int r = 0; r < 4; ++r) pe[r] = fmaf((float)vt[(d0 + r) * LDV + nb], w[r], pe[r]);
     }
     f16x4 out;
 #pragma unroll
@@ -426,14 +444,16 @@ __global__ __launch_bounds__(256) void attn_psa_mfma(const AttnArgs a) {
 // score-descending order with ties broken by ascending anchor index (torchvision's stable sort).
 __global__ __launch_bounds__(256) void decode_anchors(const DecodeArgs a) {
   // the workgroup's 64 anchor rows are contiguous: stage them in LDS with coalesced 16-byte loads
-  extern __shared__ float rows[];  // [64][no_tot]
+  extern __shared__ float rows[];  // [64][no_tot + 1]
   const long total = (long)a.B * a.A;
   const long a0 = blockIdx.x * 64L;
   const int nrow = total - a0 < 64 ? (int)(total - a0) : 64;
+  // LDS rows are padded to an odd pitch (no_tot + 1 floats): the 16 anchors x 4 sides of a wave read 16-float
+  // strided bins, which on a 144-float pitch fell into two banks (32-way conflicts)
+  const int ldr = a.no_tot + 1;
   {  // every load in flight before the first LDS store (no_tot <= 192: at most 12 per thread)
     const f32x4* src = reinterpret_cast<const f32x4*>(a.anchors + a0 * a.no_tot);
-    f32x4* dst = reinterpret_cast<f32x4*>(rows);
-    const int n4 = nrow * a.no_tot / 4;
+    const int n4 = nrow * a.no_tot / 4, r4 = a.no_tot / 4;
     f32x4 v[12];
 #pragma unroll
     for (int it = 0; it < 12; ++it) {
@@ -443,7 +463,11 @@ __global__ __launch_bounds__(256) void decode_anchors(const DecodeArgs a) {
 #pragma unroll
     for (int it = 0; it < 12; ++it) {
       const int i = threadIdx.x + 256 * it;
-      if (i < n4) dst[i] = v[it];
+      if (i < n4) {
+        const int rr = i / r4, cc = 4 * (i - rr * r4);
+        float* d = rows + rr * ldr + cc;
+        d[0] = v[it][0]; d[1] = v[it][1]; d[2] = v[it][2]; d[3] = v[it][3];
+      }
     }
   }
   __syncthreads();
@@ -453,22 +477,33 @@ __global__ __launch_bounds__(256) void decode_anchors(const DecodeArgs a) {
   const long idx = valid ? gidx : 0;
   const int b = idx / a.A;
   const int ai = idx - (long)b * a.A;
-  const float* row = rows + (valid ? (threadIdx.x >> 2) : 0) * a.no_tot;
+  const float* row = rows + (valid ? (threadIdx.x >> 2) : 0) * ldr;
   float dist;
-  {
+  {  // DFL: softmax over the bins, expectation of the bin index (one exp per bin, one division)
     const float* r = row + sub * a.reg_max;
     float mx = -INFINITY;
     for (int i = 0; i < a.reg_max; ++i) mx = fmaxf(mx, r[i]);
     float den = 0.f, num = 0.f;
-    for (int i = 0; i < a.reg_max; ++i) den += expf(r[i] - mx);
-    for (int i = 0; i < a.reg_max; ++i) num = fmaf(expf(r[i] - mx) / den, (float)i, num);
-    dist = num;
+    for (int i = 0; i < a.reg_max; ++i) {
+      const float e = expf(r[i] - mx);
+      den += e;
+      num = fmaf(e, (float)i, num);
+    }
+    dist = num / den;
   }
+  // class score = max sigmoid, first index on ties (torch max).  Sigmoid is monotonic, so only logits near the
+  // quarter's max can reach its value: those within 0.5 of it while it is < 10 (there sigmoid' > 4e-5, so a logit
+  // 0.5 lower is many ulps lower), every logit otherwise (saturation).
   const int q = (a.nc + 3) / 4;
   const float* cl = row + 4 * a.reg_max;
+  const int c0 = sub * q, c1 = (sub + 1) * q < a.nc ? (sub + 1) * q : a.nc;
+  float lmax = -INFINITY;
+  for (int c = c0; c < c1; ++c) lmax = fmaxf(lmax, cl[c]);
+  const float lthr = lmax < 10.0f ? lmax - 0.5f : -INFINITY;
   float best = -INFINITY;
   int bi = 0x7FFFFFFF;
-  for (int c = sub * q; c < a.nc && c < (sub + 1) * q; ++c) {
+  for (int c = c0; c < c1; ++c) {
+    if (!(cl[c] >= lthr)) continue;
     const float sc = ym_sigmoid(cl[c]);
     if (sc > best) { best = sc; bi = c; }
   }
@@ -828,7 +863,7 @@ hipError_t launch_attn_t(const AttnArgs& a, hipStream_t st) {
 
 template <int NKT>
 hipError_t launch_attn_mfma(const AttnArgs& a, hipStream_t st) {
-  const size_t lds = (size_t)64 * (16 * NKT + 4) * sizeof(f16);
+  const size_t lds = ((size_t)64 * (16 * NKT + 4) + (size_t)16 * NKT * 40) * sizeof(f16) + 640 * sizeof(float);
   hipLaunchKernelGGL((attn_psa_mfma<NKT>), dim3(a.B * a.nh * ((a.N + 63) / 64)), dim3(256), lds, st, a);
   return hipGetLastError();
 }
@@ -850,7 +885,7 @@ hipError_t ym_launch_attn(int dtype, const AttnArgs& a, hipStream_t st) {
 hipError_t ym_launch_decode(const DecodeArgs& a, hipStream_t st) {
   const long total = (long)a.B * a.A;
   if (a.no_tot % 4) return hipErrorInvalidValue;
-  hipLaunchKernelGGL(decode_anchors, dim3((total + 63) / 64), dim3(256), (size_t)64 * a.no_tot * sizeof(float), st,
+  hipLaunchKernelGGL(decode_anchors, dim3((total + 63) / 64), dim3(256), (size_t)64 * (a.no_tot + 1) * sizeof(float), st,
                      a);
   return hipGetLastError();
 }

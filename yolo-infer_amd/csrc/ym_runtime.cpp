@@ -82,7 +82,13 @@ struct ym_ctx {
   std::vector<BufDesc> bufs;
   std::vector<Op> ops;
   char* d_weights = nullptr;
-  size_t off_wstem = 0;       // stem weights re-laid out as fp32 [27][N] behind the blob's weights (ym_stem.hip)
+  size_t off_wstem = 0;
+  // branch schedule of a one-lane forward (ops of independent DAG branches on up to kMaxLanes streams)
+  int nbr = 1;
+  std::vector<int> br_of;                // per op: branch stream
+  std::vector<std::vector<int>> br_wait; // per op: earlier ops (other streams) whose events it waits for
+  std::vector<char> br_rec;              // per op: record its event after it
+  std::vector<hipEvent_t> op_ev;       // stem weights re-laid out as fp32 [27][N] behind the blob's weights (ym_stem.hip)
   size_t wbytes = 0;
   // workspace for the current (B, H, W)
   int cB = 0, cH = 0, cW = 0;
@@ -140,6 +146,7 @@ struct ym_ctx {
       if (join_ev[l]) (void)hipEventDestroy(join_ev[l]);
     }
     if (fork_ev) (void)hipEventDestroy(fork_ev);
+    for (hipEvent_t e : op_ev) (void)hipEventDestroy(e);
   }
   void clear_graphs() {
     for (auto& g : graphs) {
@@ -474,6 +481,78 @@ int ym_create(int device, const ym_model_desc* desc, ym_ctx** out) {
   return YM_OK;
 }
 
+
+// Static branch schedule (one-lane forwards): op i depends on every earlier op that writes a buffer it reads
+// (buffer granularity; the planner never rewrites a buffer region within a forward, so RAW is the only hazard).
+// Ops go in program order onto up to kMaxLanes streams: an op continues the stream of its latest dependency when
+// that dependency is the stream's tail, else opens an unused stream, else joins the stream whose tail is oldest.
+// Cross-stream dependencies become event waits (skipped when already implied by an earlier wait).  The Detect-head
+// chains of P3/P4 then run beside the neck's latency-bound 40x40/20x20 layers.
+static void build_schedule(ym_ctx* c) {
+  const int nop = (int)c->ops.size(), nbuf = (int)c->bufs.size();
+  const int P_DEC = nbuf, P_OUT = nbuf + 1;  // pseudo buffers: decode scratch, detections
+  auto rw = [&](const Op& o, std::vector<int>& rd, std::vector<int>& wr) {
+    const int32_t* r = o.r;
+    rd.clear(); wr.clear();
+    switch (r[0]) {
+      case OP_INPUT: wr.push_back(c->input_buf); break;
+      case OP_CONV: rd.push_back(r[6]); if (r[10] >= 0) rd.push_back(r[10]); if (r[17] >= 0) rd.push_back(r[17]);
+                    wr.push_back(r[13]); break;
+      case OP_DW: case OP_ATTN: case OP_REQ: rd.push_back(r[6]); wr.push_back(r[13]); break;
+      case OP_SPPF: rd.push_back(r[13]); wr.push_back(r[13]); break;
+      case OP_DECODE: rd.push_back(c->anchor_buf); wr.push_back(P_DEC); break;
+      case OP_NMS: rd.push_back(P_DEC); rd.push_back(c->anchor_buf); wr.push_back(P_OUT); break;
+      default: rd.push_back(-2); break;  // unknown: serialise behind everything
+    }
+  };
+  const int S = kMaxLanes;
+  c->br_of.assign(nop, 0);
+  c->br_wait.assign(nop, {});
+  c->br_rec.assign(nop, 0);
+  std::vector<std::vector<int>> writers(nbuf + 2);
+  std::vector<int> tail(S, -1);
+  std::vector<std::vector<int>> known(S, std::vector<int>(S, -1));  // known[s][t]: ops of stream t done before s
+  std::vector<std::vector<int>> snap(nop);                          // known vector of an op's stream after it
+  std::vector<int> rd, wr;
+  int used = 1;
+  const char* env = getenv("YM_BRANCHES");
+  const int maxs = env && *env ? (atoi(env) < 1 ? 1 : (atoi(env) > S ? S : atoi(env))) : S;
+  for (int i = 0; i < nop; ++i) {
+    rw(c->ops[i], rd, wr);
+    std::vector<int> deps;
+    bool all = false;
+    for (int b : rd) {
+      if (b == -2) all = true;
+      else if (b >= 0 && b < nbuf + 2) deps.insert(deps.end(), writers[b].begin(), writers[b].end());
+    }
+    if (all) for (int j = 0; j < i; ++j) deps.push_back(j);
+    int jmax = -1;
+    for (int j : deps) jmax = j > jmax ? j : jmax;
+    int s = -1;
+    if (jmax >= 0 && tail[c->br_of[jmax]] == jmax) s = c->br_of[jmax];
+    if (s < 0 && jmax >= 0 && used < maxs) s = used++;
+    if (s < 0) {  // the stream whose tail is oldest
+      s = 0;
+      for (int t = 1; t < used; ++t) if (tail[t] < tail[s]) s = t;
+    }
+    if (i == 0) s = 0;
+    for (int j : deps) {
+      const int t = c->br_of[j];
+      if (t == s || known[s][t] >= j) continue;
+      c->br_wait[i].push_back(j);
+      c->br_rec[j] = 1;
+      known[s][t] = j;
+      for (int u = 0; u < S; ++u) if (snap[j][u] > known[s][u]) known[s][u] = snap[j][u];
+    }
+    c->br_of[i] = s;
+    tail[s] = i;
+    known[s][s] = i;
+    snap[i] = known[s];
+    for (int b : wr) if (b >= 0 && b < nbuf + 2) writers[b].push_back(i);
+  }
+  c->nbr = used;
+}
+
 int ym_load_weights(ym_ctx* c, const void* blob, size_t bytes) {
   if (!c || !blob) return fail(YM_EINVAL, "null argument");
   HIPCK(hipSetDevice(c->device));
@@ -505,6 +584,12 @@ int ym_load_weights(ym_ctx* c, const void* blob, size_t bytes) {
   }
   if (c->input_buf < 0 || c->input_buf >= nbuf || c->anchor_buf < 0 || c->anchor_buf >= nbuf)
     return fail(YM_EBLOB, "bad input/anchor buffer ids");
+  build_schedule(c);
+  while (c->op_ev.size() < c->ops.size()) {
+    hipEvent_t ev;
+    HIPCK(hipEventCreateWithFlags(&ev, hipEventDisableTiming));
+    c->op_ev.push_back(ev);
+  }
   c->clear_graphs();
   if (c->d_weights) HIPCK(hipFree(c->d_weights));
   c->d_weights = nullptr;
@@ -560,6 +645,24 @@ static int launch_forward(ym_ctx* c, const float* d_in, int B, const ym_infer_ar
   lane_split(args, B, L, Bl);
   c->lane = 0;
   c->lane_img0 = 0;
+  if (L == 1 && c->nbr > 1) {  // one lane: the branch schedule (build_schedule)
+    hipStream_t bs[kMaxLanes] = {st};
+    for (int s = 1; s < kMaxLanes; ++s) bs[s] = c->lane_streams[s];
+    for (size_t i = 0; i < c->ops.size(); ++i) {
+      const int s = c->br_of[i];
+      for (int j : c->br_wait[i]) HIPCK(hipStreamWaitEvent(bs[s], c->op_ev[j], 0));
+      c->lane = s;  // split-K slab / counter region of this stream
+      rc = launch_op(c, c->ops[i], B, d_in, args, d_dets, d_counts, bs[s]);
+      c->lane = 0;
+      if (rc) return rc;
+      if (c->br_rec[i]) HIPCK(hipEventRecord(c->op_ev[i], bs[s]));
+    }
+    for (int s = 1; s < c->nbr; ++s) {  // every branch joins back into the caller's stream
+      HIPCK(hipEventRecord(c->join_ev[s], bs[s]));
+      HIPCK(hipStreamWaitEvent(st, c->join_ev[s], 0));
+    }
+    return YM_OK;
+  }
   size_t o = 0;
   for (o = 0; o < c->ops.size() && c->ops[o].r[0] == OP_INPUT; ++o)
     if ((rc = launch_op(c, c->ops[o], B, d_in, args, d_dets, d_counts, st))) return rc;

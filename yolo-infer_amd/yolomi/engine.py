@@ -49,6 +49,7 @@ class Engine:
         # per slice batch.  Default from YM_LANES (1).
         self.lanes = int(os.environ.get("YM_LANES", "1"))
         self._tuned = set()
+        self._args_cache = {}
         self.tune_source: Dict[tuple, str] = {}
 
     def _table_name(self, B, H, W):
@@ -110,7 +111,15 @@ class Engine:
         if in_eps is None:
             in_eps = torch.finfo(torch.float32).eps
         lanes = self.lanes if lanes is None else lanes
-        args = Runtime.make_args(conf, iou, max_det, max_nms, agnostic, max_wh, in_eps, classes, use_graph, lanes)
+        # the ctypes argument block of a repeated call is reused (predict loops pass the same thresholds)
+        akey = (conf, iou, max_det, max_nms, agnostic, max_wh, in_eps, tuple(classes) if classes is not None else None,
+                use_graph, lanes)
+        args = self._args_cache.get(akey)
+        if args is None:
+            if len(self._args_cache) > 64:
+                self._args_cache.clear()
+            args = self._args_cache[akey] = Runtime.make_args(conf, iou, max_det, max_nms, agnostic, max_wh, in_eps,
+                                                              classes, use_graph, lanes)
         dets, counts = self.outputs(B, max_det)
         stream = torch.cuda.current_stream(self.device).cuda_stream
         Bl = self.lane_batch(B, lanes)
