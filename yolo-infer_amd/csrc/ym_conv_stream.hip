@@ -27,7 +27,8 @@ struct SCfg {
 #define YM_STREAM_CFGS(X)                                                                                        \
   X(0, 1, 2, 1, 1024) X(1, 1, 2, 2, 1024) X(2, 1, 2, 1, 4096) X(3, 1, 4, 1, 1024) X(4, 1, 4, 2, 1024)            \
   X(5, 1, 8, 1, 1024) X(6, 1, 4, 1, 4096) X(7, 3, 4, 1, 1024) X(8, 3, 6, 1, 1024) X(9, 3, 10, 1, 1024)          \
-  X(10, 3, 18, 1, 1024) X(11, 3, 4, 1, 4096) X(12, 3, 6, 1, 4096) X(13, 3, 10, 1, 4096) X(14, 3, 18, 1, 4096)
+  X(10, 3, 18, 1, 1024) X(11, 3, 4, 1, 4096) X(12, 3, 6, 1, 4096) X(13, 3, 10, 1, 4096) X(14, 3, 18, 1, 4096)         \
+  X(15, 1, 2, 2, 4096) X(16, 1, 2, 4, 4096) X(17, 1, 4, 2, 4096) X(18, 3, 4, 2, 4096) X(19, 3, 6, 2, 4096)
 constexpr SCfg kStream[] = {
 #define YM_X(id, kind, ks, px, cap) {kind, ks, px, cap},
     YM_STREAM_CFGS(YM_X)

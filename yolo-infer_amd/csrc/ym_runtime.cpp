@@ -515,8 +515,10 @@ static void build_schedule(ym_ctx* c) {
   std::vector<std::vector<int>> snap(nop);                          // known vector of an op's stream after it
   std::vector<int> rd, wr;
   int used = 1;
+  // opt-in (YM_BRANCHES=2..4): measured on MI355X, graph replays gain nothing (0.732 vs 0.734 ms per yolo11n B=8
+  // forward, tools/branch_check.py) and eager launches lose (0.774 vs 0.727 ms), so the serial order is the default
   const char* env = getenv("YM_BRANCHES");
-  const int maxs = env && *env ? (atoi(env) < 1 ? 1 : (atoi(env) > S ? S : atoi(env))) : S;
+  const int maxs = env && *env ? (atoi(env) < 1 ? 1 : (atoi(env) > S ? S : atoi(env))) : 1;
   for (int i = 0; i < nop; ++i) {
     rw(c->ops[i], rd, wr);
     std::vector<int> deps;

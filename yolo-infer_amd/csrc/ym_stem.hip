@@ -2,8 +2,9 @@
 // (ultralytics/data/loaders.py LoadTensor) and the NCHW → NHWC change of layout are folded into its
 // loader, so the input is read exactly once.
 //
-// A workgroup computes an 8-row x 32-column output tile.  The 17 x 68 x 3 input patch is staged in LDS with
-// coalesced float4 row loads (the rows start 4 floats left of the window: 16-byte aligned, W % 4 == 0).
+// A workgroup computes a TH-row x 32-column output tile (TH = 16 on the MFMA path, 8 on the VALU path).  The
+// (2 TH + 1) x 68 x 3 input patch is staged in LDS with coalesced float4 row loads, all in flight at once (the rows
+// start 4 floats left of the window: 16-byte aligned, W % 4 == 0).
 //
 // f16 / int8 plans — stem_mfma: the 27-tap contraction (K = 27, padded to 32) is ONE v_mfma_f32_16x16x32_f16 per
 // 16 pixels x 16 channels, in the transposed orientation of csrc/ym_conv.hip (A = weights, so a lane owns 4
@@ -20,13 +21,13 @@
 
 namespace {
 
-constexpr int TH = 8, TW = 32;
-constexpr int PH = 2 * TH + 1;             // patch rows
+constexpr int TW = 32;
 constexpr int PW4 = (2 * TW + 4) / 4 + 1;  // 4-wide groups per patch row: columns x0-4 .. x0+2TW+3
 constexpr int PW = PW4 * 4;
 
 __device__ __forceinline__ int clampi(int v, int lo, int hi) { return v < lo ? lo : (v > hi ? hi : v); }
 
+template <int TH>
 __device__ __forceinline__ void tile_of(const ConvArgs& a, int& b, int& oy0, int& ox0) {
   const int tiles_x = (a.Wo + TW - 1) / TW, tiles_y = (a.Ho + TH - 1) / TH;
   int bid = blockIdx.x;
@@ -41,13 +42,16 @@ __device__ __forceinline__ void tile_of(const ConvArgs& a, int& b, int& oy0, int
 // ------------------------------------------------------------------------------------------------ MFMA (f16, i8)
 typedef _Float16 h8 __attribute__((ext_vector_type(8)));
 
+constexpr int MTH = 16;  // MFMA path: 16 output rows per workgroup (32 groups of 16 pixels, 8 per wave)
+
 template <typename T, int NT>  // NT = Cout / 16 channel tiles
 __global__ __launch_bounds__(256) void stem_mfma(const ConvArgs a) {
   constexpr bool QUANT = sizeof(T) == 1;
+  constexpr int TH = MTH, PH = 2 * TH + 1;
   __shared__ __attribute__((aligned(16))) f16 patch[3 * PH * PW];
   __shared__ float post[QUANT ? 256 : 1];
   int b, oy0, ox0;
-  tile_of(a, b, oy0, ox0);
+  tile_of<TH>(a, b, oy0, ox0);
   const int iy0 = 2 * oy0 - 1, xs = 2 * ox0 - 4;
   const bool div = ym_input_max(a.ctl) > 1.0f + a.eps;
   const size_t HW = (size_t)a.Hin * a.Win;
@@ -115,10 +119,10 @@ __global__ __launch_bounds__(256) void stem_mfma(const ConvArgs a) {
       if constexpr (QUANT) sasw[t][r] = a.sasw[16 * t + 4 * kg + r];
     }
   __syncthreads();
-  // wave w: pixel groups 4w .. 4w+3 of the tile's 16 (16 consecutive columns of one row each)
+  // wave w: pixel groups 8w .. 8w+7 of the tile's 32 (16 consecutive columns of one row each)
 #pragma unroll
-  for (int gi = 0; gi < 4; ++gi) {
-    const int g = 4 * wave + gi;
+  for (int gi = 0; gi < 8; ++gi) {
+    const int g = 8 * wave + gi;
     const int ly = g >> 1, lx = (g & 1) * 16 + col;
     const f16* pp = patch + 2 * ly * PW + 2 * lx;
     h8 bf;
@@ -153,9 +157,10 @@ __global__ __launch_bounds__(256) void stem_mfma(const ConvArgs a) {
 
 // ------------------------------------------------------------------------------------------------ VALU (f32 parity)
 __global__ __launch_bounds__(256) void stem_valu(const ConvArgs a) {
+  constexpr int TH = 8, PH = 2 * TH + 1;  // one thread per output pixel: 8 x 32
   __shared__ __attribute__((aligned(16))) float patch[3 * PH * PW];
   int b, oy0, ox0;
-  tile_of(a, b, oy0, ox0);
+  tile_of<TH>(a, b, oy0, ox0);
   const int iy0 = 2 * oy0 - 1, xs = 2 * ox0 - 4;
   const bool div = ym_input_max(a.ctl) > 1.0f + a.eps;
   const size_t HW = (size_t)a.Hin * a.Win;
@@ -213,7 +218,7 @@ __global__ __launch_bounds__(256) void stem_valu(const ConvArgs a) {
   }
 }
 
-dim3 grid_of(const ConvArgs& a) {
+dim3 grid_of(const ConvArgs& a, int TH) {
   const int B = a.M / (a.Ho * a.Wo);
   return dim3(B * ((a.Ho + TH - 1) / TH) * ((a.Wo + TW - 1) / TW));
 }
@@ -221,10 +226,10 @@ dim3 grid_of(const ConvArgs& a) {
 template <typename T>
 hipError_t launch_mfma(const ConvArgs& a, hipStream_t st) {
   switch (a.N / 16) {
-    case 1: hipLaunchKernelGGL((stem_mfma<T, 1>), grid_of(a), dim3(256), 0, st, a); break;
-    case 2: hipLaunchKernelGGL((stem_mfma<T, 2>), grid_of(a), dim3(256), 0, st, a); break;
-    case 4: hipLaunchKernelGGL((stem_mfma<T, 4>), grid_of(a), dim3(256), 0, st, a); break;
-    case 6: hipLaunchKernelGGL((stem_mfma<T, 6>), grid_of(a), dim3(256), 0, st, a); break;
+    case 1: hipLaunchKernelGGL((stem_mfma<T, 1>), grid_of(a, MTH), dim3(256), 0, st, a); break;
+    case 2: hipLaunchKernelGGL((stem_mfma<T, 2>), grid_of(a, MTH), dim3(256), 0, st, a); break;
+    case 4: hipLaunchKernelGGL((stem_mfma<T, 4>), grid_of(a, MTH), dim3(256), 0, st, a); break;
+    case 6: hipLaunchKernelGGL((stem_mfma<T, 6>), grid_of(a, MTH), dim3(256), 0, st, a); break;
     default: return hipErrorInvalidValue;
   }
   return hipGetLastError();
@@ -238,6 +243,6 @@ hipError_t ym_launch_stem(int dtype, const ConvArgs& a, hipStream_t st) {
     return hipErrorInvalidValue;
   if (dtype == YM_DT_I8) return a.q && a.sasw ? launch_mfma<i8>(a, st) : hipErrorInvalidValue;
   if (dtype == YM_DT_F16) return a.raw ? hipErrorInvalidValue : launch_mfma<f16>(a, st);
-  hipLaunchKernelGGL(stem_valu, grid_of(a), dim3(256), 0, st, a);
+  hipLaunchKernelGGL(stem_valu, grid_of(a, 8), dim3(256), 0, st, a);
   return hipGetLastError();
 }
