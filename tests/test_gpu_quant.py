@@ -97,13 +97,15 @@ def test_i8_graph_replay_bitwise_equals_eager():
     assert torch.equal(c1, c2) and torch.equal(d1, d2)
 
 
-@pytest.mark.parametrize("cfg", list(range(12)))
+@pytest.mark.parametrize("cfg", list(range(12 + 15 + 8)))
 def test_i8_conv_tile_configs_agree(cfg):
-    """Every int8 conv tile configuration (incl. the intra-workgroup split-K ones) gives the same int8 tensors."""
+    """Every int8 conv configuration — conv_i8 tiles (incl. intra-workgroup split-K), the streaming and the small-M
+    kernels of csrc/ym_conv_i8_stream.hip (ids >= 12) — gives the same int8 tensors and the same fp32 head rows."""
     eng = i8_model("det_n_i8_fbgemm_320").model.engine
     x = make_input("uniform", (71,), 320).to(DEV)
     eng.run(x, use_graph=False)
-    ref = {b.id: eng.read_buffer(b.id, 1) for b in eng.graph.buffers if b.name.startswith("L") and b.name[1:].isdigit()}
+    ref = {b.id: eng.read_buffer(b.id, 1) for b in eng.graph.buffers
+           if (b.name.startswith("L") and b.name[1:].isdigit()) or b.id == eng.graph.anchor_buf.id}
     B, _, H, W = x.shape
     try:
         eng.rt.set_op_cfg(B, H, W, [cfg if op.kind == "conv" else -1 for op in eng.graph.ops])

@@ -25,14 +25,25 @@ def main():
     a = ap.parse_args()
     from bench import PEAK_HBM_GBS, PEAK_TFLOPS, synthetic_batch
     from core.model import YOLO11Model
-    m = YOLO11Model(task=a.task, size=a.model, device="cuda:0", dtype=a.dtype)
+    blob = None
+    if a.dtype == "i8":  # the PTQ plan of bench.py: calibration through the exact-f32 plan, qnnpack qconfig
+        from yolomi.engine import Engine
+        from yolomi.plan import pack_model
+        from yolomi.quant import calibrate
+        from yolomi.synth import synth_weights
+        dev = torch.device("cuda", 0)
+        ce = Engine(a.model, a.task, synth_weights(a.model, a.task, 0), dev, "f32")
+        qp = calibrate(ce, [synthetic_batch(a.batch, a.size, 500 + i, dev) for i in range(4)], "qnnpack")
+        del ce
+        blob = pack_model(a.model, a.task, synth_weights(a.model, a.task, 0), "i8", qp)
+    m = YOLO11Model(task=a.task, size=a.model, device="cuda:0", dtype=a.dtype, weights_blob=blob)
     eng = m.model.engine
     x = synthetic_batch(a.batch, a.size, 1000, torch.device("cuda", 0))
     eng.run(x)
     B, S = a.batch, a.size
     cfg = eng.rt.get_op_cfg(B, S, S) or [-1] * eng.rt.n_ops
     t = eng.profile_replay(x, reps=20)
-    costs = eng.graph.op_costs(B, S, S, 2 if a.dtype == "f16" else 4)
+    costs = eng.graph.op_costs(B, S, S, {"f16": 2, "f32": 4, "i8": 1}[a.dtype])
     tot = floor = 0.0
     print(f"yolo11{a.model} {a.task} B={B} {S}^2 {a.dtype}; tune source {eng.tune_source}")
     print(f"{'op':26s} {'kind':6s} {'shape':28s} {'cfg':>4s} {'us':>7s} {'floor':>6s} {'TF/s':>7s} {'GB/s':>7s}")

@@ -226,6 +226,8 @@ hipError_t ym_launch_masks(const MaskArgs& a, hipStream_t st);  // Segment: proc
 // int8 (PTQ) plans: csrc/ym_conv_i8.hip
 hipError_t ym_launch_conv_i8(const ConvArgs& a, int cfg, hipStream_t st, bool strict);
 int ym_conv_i8_num_cfgs();
+hipError_t ym_launch_conv_i8_stream(const ConvArgs& a, int i, hipStream_t st);
+int ym_conv_i8_stream_num_cfgs();
 hipError_t ym_launch_dwconv_i8(const DwArgs& a, hipStream_t st);
 hipError_t ym_launch_attn_i8(const AttnArgs& a, hipStream_t st);
 hipError_t ym_launch_requant(const ReqArgs& a, hipStream_t st);

@@ -19,10 +19,9 @@
 #include <stdlib.h>
 
 #include "ym_common.h"
+#include "ym_quant.h"
 
-typedef int i32x4 __attribute__((ext_vector_type(4)));
 typedef int i32x16 __attribute__((ext_vector_type(16)));
-typedef signed char i8x16 __attribute__((ext_vector_type(16)));
 
 namespace {
 
@@ -30,21 +29,6 @@ constexpr int KSTEP = 64;        // K bytes per step: two 32-deep MFMAs per 32x3
 constexpr int KS = KSTEP / 32;
 
 __device__ __forceinline__ i8x16 ld16(const i8* p) { return *reinterpret_cast<const i8x16*>(p); }
-__device__ __forceinline__ int clampi(int v, int lo, int hi) { return v < lo ? lo : (v > hi ? hi : v); }
-
-// quantized::conv2d output requantisation
-__device__ __forceinline__ int requant_out(int acc, float sasw, float bias, const QRec* Q) {
-  const float y = ym_opaque((float)acc * sasw) + bias;  // two roundings (no FMA), as torch's mul then add
-  return clampi((int)rintf(__fmul_rn(y, Q->inv_sc)) + Q->zc, Q->qlo, Q->qhi);
-}
-// quantize a float into a stored tensor: returns the int8 storage value q - 128
-__device__ __forceinline__ int quant_store(float v, float inv, int z, int lo, int hi) {
-  return clampi((int)rintf(__fmul_rn(v, inv)) + z, lo, hi) - 128;
-}
-__device__ __forceinline__ float deq(int q, int z, float s) { return ym_opaque((float)(q - z) * s); }
-__device__ __forceinline__ int pack4(const int* v) {
-  return (v[0] & 0xFF) | ((v[1] & 0xFF) << 8) | ((v[2] & 0xFF) << 16) | ((unsigned)(v[3] & 0xFF) << 24);
-}
 
 __device__ __forceinline__ bool xcd_tile(const ConvArgs& a, int BM, int& tm, int& tn) {
   const int bid = blockIdx.x;
@@ -527,7 +511,8 @@ __global__ __launch_bounds__(256) void requant_copy(const ReqArgs a) {
 
 }  // namespace
 
-int ym_conv_i8_num_cfgs() { return kNumCfg; }
+// ids [0, kNumCfg): conv_i8 above; then the streaming / small-M int8 kernels (csrc/ym_conv_i8_stream.hip)
+int ym_conv_i8_num_cfgs() { return kNumCfg + ym_conv_i8_stream_num_cfgs(); }
 
 hipError_t ym_launch_conv_i8(const ConvArgs& a, int cfg, hipStream_t st, bool strict) {
   int kind;
@@ -537,8 +522,9 @@ hipError_t ym_launch_conv_i8(const ConvArgs& a, int cfg, hipStream_t st, bool st
   if (a.Kpad % KSTEP || !a.q || !a.sasw || !a.biasi || (a.N & 3) || (a.s0_ctot & 15) || (a.s0_coff & 15))
     return hipErrorInvalidValue;
   if (cfg >= kNumCfg) {
-    if (strict) return hipErrorInvalidValue;
-    cfg = -1;
+    const hipError_t e = ym_launch_conv_i8_stream(a, cfg - kNumCfg, st);
+    if (e != hipErrorInvalidValue || strict) return e;
+    cfg = -1;  // a pinned table entry that does not apply: the heuristic
   }
   return launch_id(cfg >= 0 ? cfg : choose_cfg(a), a, kind, st);
 }
