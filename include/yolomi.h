@@ -121,6 +121,16 @@ int ym_read_buffer(ym_ctx* ctx, int buf, void* dst, size_t bytes);
 int ym_masks(ym_ctx* ctx, const float* d_dets, int B, int max_det, const int* d_offsets, int total, int H, int W,
              unsigned char* d_masks, int* d_nonempty, void* stream);
 
+/* Image sources: Ultralytics `LetterBox` + predictor preprocessing of ONE HWC uint8 image already
+ * in device memory (d_src, rows row_bytes apart, 3 channels; bgr = 1 for cv2.imread order).  The image is resized to
+ * uh x uw with OpenCV's 8-bit INTER_LINEAR fixed-point arithmetic (skipped when the size does not change), placed at
+ * (top, left) of an Hn x Wn canvas filled with 114, converted to RGB planes and divided by 255 into d_dst (3 x Hn x Wn
+ * fp32: one image of the batch ym_infer reads).  The geometry is the caller's (LetterBox arithmetic, see
+ * yolomi/preprocess.py).  Asynchronous on `stream`.  Replaces the reference's cv2-based preprocessing under
+ * YOLO11Model.predict(path | ndarray) (/root/reference/core/model.py:118-133, demos/detection_demo.py:87-93). */
+int ym_letterbox(ym_ctx* ctx, const void* d_src, int h, int w, int row_bytes, int bgr, int uh, int uw, int top,
+                 int left, float* d_dst, int Hn, int Wn, void* stream);
+
 int ym_sync(ym_ctx* ctx);
 const char* ym_last_error(void);
 void ym_destroy(ym_ctx* ctx);

@@ -180,6 +180,50 @@ def test_branch_schedule_bitwise_equals_serial(dtype, scale):
     assert torch.equal(h1, es.read_buffer(es.graph.anchor_buf.id, 8))
 
 
+# ------------------------------------------------------------------------------------------------ image sources
+LB_SHAPES = [(853, 1280), (480, 640), (100, 37), (640, 640), (1000, 700)]
+
+
+def _images(shapes, seed):
+    rng = np.random.default_rng(seed)
+    return [rng.integers(0, 256, s + (3,), dtype=np.uint8) for s in shapes]
+
+
+@pytest.mark.parametrize("shapes", [[s] for s in LB_SHAPES] + [LB_SHAPES[:3], [(853, 1280)] * 3])
+def test_letterbox_kernel_matches_oracle(shapes):
+    """csrc/ym_letterbox.hip (fixed-point INTER_LINEAR, 114 border, BGR->RGB, /255) == oracle/letterbox.py, bit for
+    bit, for single images, mixed-shape batches (auto=False: 640x640 canvases) and same-shape batches (auto=True)."""
+    from oracle import letterbox as olb
+    from yolomi.preprocess import letterbox_batch
+    imgs = _images(shapes, 17)
+    eng = model("n", "f32").model.engine
+    got, _ = letterbox_batch(eng.rt, imgs, DEV, stream=torch.cuda.current_stream().cuda_stream)
+    ref = torch.from_numpy(olb.preprocess(imgs))
+    assert got.shape == ref.shape and torch.equal(got.cpu(), ref)
+
+
+def test_predict_image_sources_match_oracle(tmp_path):
+    """predict(list of HWC BGR ndarrays) and predict(path) = the oracle's preprocess -> predict -> scale_boxes."""
+    from PIL import Image
+    from oracle import letterbox as olb
+    from oracle.postprocess import scale_boxes as oscale
+    imgs = _images([(853, 1280), (853, 1280)], 23)
+    x = torch.from_numpy(olb.preprocess(imgs))
+    ref = oracle().predict(x)
+    for r in ref:
+        r["boxes"] = r["boxes"].clone()
+        oscale(tuple(x.shape[2:]), r["boxes"][:, :4], (853, 1280))
+    m = model("n", "f32")
+    res = m.predict(imgs)
+    assert res[0].orig_shape == (853, 1280) and res[0].orig_img is imgs[0]
+    check(ref, res, 0.25, 0.7, 2e-3, 1e-3)  # coordinates scaled by 1/gain = 2
+    p = tmp_path / "img.png"
+    Image.fromarray(imgs[1][..., ::-1].copy()).save(p)
+    rp = m.predict(str(p))
+    assert rp[0].path == str(p)
+    check(ref[1:], rp, 0.25, 0.7, 2e-3, 1e-3)
+
+
 def test_batch_independence():
     """An image's detections do not depend on its batch neighbours (per-pixel work only; the tuned tiles may differ
     between B=8 and B=1, so compare with the f32 tolerance)."""

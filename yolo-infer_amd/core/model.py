@@ -155,12 +155,17 @@ class YOLO11Model:
         return _ModelHandle(sd, engine, COCO_NAMES)
 
     # ------------------------------------------------------------------ hot path
-    def _as_batch(self, source) -> (torch.Tensor, float):
+    def _as_batch(self, source, imgsz: int = 640):
+        """(batch tensor on the device, LoadTensor eps, image-source info or None).  Tensors follow LoadTensor; paths,
+        directories, HWC uint8 BGR ndarrays and PIL images are letterboxed on the GPU (yolomi/preprocess.py)."""
         if isinstance(source, (list, tuple)) and source and all(isinstance(s, torch.Tensor) for s in source):
             source = torch.stack(list(source))
         if not isinstance(source, torch.Tensor):
-            raise NotImplementedError("only torch.Tensor sources (BCHW/CHW) run on the MI355X path this round; "
-                                      "file/ndarray sources need the letterbox kernel (SURVEY §8f)")
+            from yolomi.preprocess import expand_sources, letterbox_batch
+            imgs, paths = expand_sources(source)
+            stream = torch.cuda.current_stream(self._dev).cuda_stream
+            im, shapes = letterbox_batch(self.model.engine.rt, imgs, self._dev, imgsz=imgsz, stream=stream)
+            return im, torch.finfo(torch.float32).eps, (imgs, paths, shapes)
         im = source
         if im.dim() != 4:
             if im.dim() != 3:
@@ -176,7 +181,7 @@ class YOLO11Model:
         if im.device != self._dev:
             im = im.to(self._dev)
         im = im.float().contiguous()
-        return im, eps
+        return im, eps, None
 
     def predict(self, source, **kwargs) -> List[Results]:
         conf = float(kwargs.get("conf", 0.25))
@@ -184,31 +189,44 @@ class YOLO11Model:
         max_det = int(kwargs.get("max_det", 300))
         classes = kwargs.get("classes", None)
         agnostic = bool(kwargs.get("agnostic_nms", False))
-        im, eps = self._as_batch(source)
-        eng = self.model.engine
         t0 = time.perf_counter()
+        im, eps, imsrc = self._as_batch(source, int(kwargs.get("imgsz", 640)))
+        t1 = time.perf_counter()
+        eng = self.model.engine
         dets, counts = eng.run(im, conf=conf, iou=iou, max_det=max_det, classes=classes, agnostic=agnostic,
                                in_eps=eps)
         B = im.shape[0]
         out = dets[:B].clone()
         n = counts[:B].tolist()  # the device→host sync of a predict call
         names = self.model.names
-        if self.task != "segment":
-            dt = (time.perf_counter() - t0) * 1e3
-            speed = {"preprocess": 0.0, "inference": dt, "postprocess": 0.0}
-            return [Results.from_batch(im, b, names, out, n[b], path=f"image{b}.jpg", speed=speed) for b in range(B)]
-        # Segment: process_mask(upsample=True) on the GPU, then the predictor keeps only non-empty masks
-        H, W = im.shape[2:]
-        masks, nonempty, offs = eng.masks(out, n, H, W)
-        keep = nonempty.tolist()
-        dt = (time.perf_counter() - t0) * 1e3
-        speed = {"preprocess": 0.0, "inference": dt, "postprocess": 0.0}
-        res = []
+        masks = None
+        if self.task == "segment":  # process_mask(upsample=True) on the GPU, in letterboxed coordinates
+            H, W = im.shape[2:]
+            masks, nonempty, offs = eng.masks(out, n, H, W)
+            keep = nonempty.tolist()
+        if imsrc is not None:  # ops.scale_boxes back to each original image
+            from yolomi.preprocess import scale_boxes
+            for b in range(B):
+                if n[b]:
+                    scale_boxes(im.shape[2:], out[b, : n[b], :4], imsrc[2][b])
+        t2 = time.perf_counter()
+        speed = {"preprocess": (t1 - t0) * 1e3, "inference": (t2 - t1) * 1e3, "postprocess": 0.0}
+        if masks is None:
+            if imsrc is None:
+                return [Results.from_batch(im, b, names, out, n[b], path=f"image{b}.jpg", speed=speed)
+                        for b in range(B)]
+            return [Results.from_image(imsrc[0][b], imsrc[1][b], names, out[b, : n[b], :6], speed=speed)
+                    for b in range(B)]
+        res = []  # Segment: the predictor keeps only non-empty masks
         for b in range(B):
             idx = [i for i in range(n[b]) if keep[offs[b] + i]]
             sel = torch.tensor(idx, dtype=torch.long, device=out.device)
-            res.append(Results(im[b], names, out[b].index_select(0, sel)[:, :6], path=f"image{b}.jpg", speed=speed,
-                               masks=masks[offs[b]:offs[b + 1]].index_select(0, sel).bool()))
+            bx = out[b].index_select(0, sel)[:, :6]
+            mk = masks[offs[b]:offs[b + 1]].index_select(0, sel).bool()
+            if imsrc is None:
+                res.append(Results(im[b], names, bx, path=f"image{b}.jpg", speed=speed, masks=mk))
+            else:
+                res.append(Results.from_image(imsrc[0][b], imsrc[1][b], names, bx, speed=speed, masks=mk))
         return res
 
     def __call__(self, source, **kwargs):

@@ -149,6 +149,19 @@ class Results:
         r.probs = r.keypoints = r.obb = None
         return r
 
+    @classmethod
+    def from_image(cls, img_bgr: np.ndarray, path: str, names: Dict[int, str], boxes: torch.Tensor,
+                   masks: Optional[torch.Tensor] = None, speed=None) -> "Results":
+        """An image-file / ndarray source: `orig_img` is the HWC uint8 BGR image as loaded (cv2.imread order),
+        boxes are in its coordinates (already mapped back by scale_boxes)."""
+        r = cls(None, names, boxes, masks=masks, path=path, speed=speed)
+        r._orig_img = img_bgr
+        r.orig_shape = tuple(img_bgr.shape[:2])
+        r.boxes.orig_shape = r.orig_shape
+        if r.masks is not None:
+            r.masks.orig_shape = r.orig_shape
+        return r
+
     @property
     def _orig_tensor(self):
         if self._orig_tensor_v is None and getattr(self, "_batch", None) is not None:
@@ -182,16 +195,23 @@ class Results:
     def __len__(self):
         return len(self.boxes)
 
-    def __getitem__(self, idx):
-        r = Results(self._orig_tensor, self.names, self.boxes.data[idx],
-                    self.masks.data[idx] if self.masks is not None else None, self.path, self.speed)
+    def _like(self, orig_tensor, boxes, masks):
+        r = Results(orig_tensor, self.names, boxes, masks, self.path, self.speed)
+        if orig_tensor is None:  # image-file / ndarray source: keep the loaded image and its shape
+            r._orig_img = self._orig_img
+            r.orig_shape = self.orig_shape
+            r.boxes.orig_shape = self.orig_shape
+            if r.masks is not None:
+                r.masks.orig_shape = self.orig_shape
         return r
 
+    def __getitem__(self, idx):
+        return self._like(self._orig_tensor, self.boxes.data[idx],
+                          self.masks.data[idx] if self.masks is not None else None)
+
     def cpu(self):
-        r = Results(self._orig_tensor.cpu() if self._orig_tensor is not None else None, self.names,
-                    self.boxes.data.cpu(), self.masks.data.cpu() if self.masks is not None else None, self.path,
-                    self.speed)
-        return r
+        return self._like(self._orig_tensor.cpu() if self._orig_tensor is not None else None, self.boxes.data.cpu(),
+                          self.masks.data.cpu() if self.masks is not None else None)
 
     def summary(self, normalize=False, decimals=5):
         out = []

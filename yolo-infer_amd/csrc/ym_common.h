@@ -188,6 +188,13 @@ struct NmsArgs {
   double iou;
 };
 
+struct LetterboxArgs {
+  const unsigned char* src; int h, w, row_bytes, bgr;  // HWC uint8 image (3 channels), BGR or RGB order
+  int uh, uw, top, left;                               // resized (unpadded) size and its offset in the canvas
+  double scale_x, scale_y;                             // 1 / ((double)uw / w), 1 / ((double)uh / h)
+  float* dst; int Hn, Wn;                              // one image of the fp32 NCHW batch (3 planes of Hn x Wn)
+};
+
 struct PrepArgs {
   const float* in; void* out;  // NCHW fp32 → NHWC act dtype, 8 channels (3 real + 5 zero)
   float* ctl;                  // ctl[0] = running max (ordered-int encoded) of the input
@@ -217,6 +224,7 @@ hipError_t ym_launch_prep(int dtype, const PrepArgs& a, int* counts, int B, hipS
 hipError_t ym_launch_decode(const DecodeArgs& a, hipStream_t st);
 hipError_t ym_launch_nms(const NmsArgs& a, hipStream_t st);
 hipError_t ym_launch_stem(int dtype, const ConvArgs& a, hipStream_t st);
+hipError_t ym_launch_letterbox(const LetterboxArgs& a, hipStream_t st);
 hipError_t ym_launch_spin(int usec, hipStream_t st);  // profiling: park the stream for usec (wall clock)
 hipError_t ym_launch_conv_dma(int out_f32, const ConvArgs& a, int i, hipStream_t st);  // f16 plans only
 int ym_conv_dma_num_cfgs();

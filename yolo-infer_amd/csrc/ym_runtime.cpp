@@ -82,13 +82,13 @@ struct ym_ctx {
   std::vector<BufDesc> bufs;
   std::vector<Op> ops;
   char* d_weights = nullptr;
-  size_t off_wstem = 0;
+  size_t off_wstem = 0;  // stem weights re-laid out as fp32 [27][N] behind the blob's weights (ym_stem.hip)
   // branch schedule of a one-lane forward (ops of independent DAG branches on up to kMaxLanes streams)
   int nbr = 1;
   std::vector<int> br_of;                // per op: branch stream
   std::vector<std::vector<int>> br_wait; // per op: earlier ops (other streams) whose events it waits for
   std::vector<char> br_rec;              // per op: record its event after it
-  std::vector<hipEvent_t> op_ev;       // stem weights re-laid out as fp32 [27][N] behind the blob's weights (ym_stem.hip)
+  std::vector<hipEvent_t> op_ev;
   size_t wbytes = 0;
   // workspace for the current (B, H, W)
   int cB = 0, cH = 0, cW = 0;
@@ -927,6 +927,26 @@ int ym_read_buffer(ym_ctx* c, int b, void* dst, size_t bytes) {
   HIPCK(hipSetDevice(c->device));
   HIPCK(hipDeviceSynchronize());
   HIPCK(hipMemcpy(dst, c->bptr(b), bytes, hipMemcpyDefault));
+  return YM_OK;
+}
+
+int ym_letterbox(ym_ctx* c, const void* d_src, int h, int w, int row_bytes, int bgr, int uh, int uw, int top,
+                 int left, float* d_dst, int Hn, int Wn, void* stream) {
+  if (!c) return fail(YM_EINVAL, "null context");
+  if (!d_src || !d_dst || h < 1 || w < 1 || uh < 1 || uw < 1 || top < 0 || left < 0 || top + uh > Hn ||
+      left + uw > Wn || row_bytes < 3 * w)
+    return fail(YM_EINVAL, "bad ym_letterbox geometry (%dx%d -> %dx%d at (%d, %d) in %dx%d)", h, w, uh, uw, top, left,
+                Hn, Wn);
+  HIPCK(hipSetDevice(c->device));
+  LetterboxArgs a{};
+  a.src = static_cast<const unsigned char*>(d_src);
+  a.h = h; a.w = w; a.row_bytes = row_bytes; a.bgr = bgr ? 1 : 0;
+  a.uh = uh; a.uw = uw; a.top = top; a.left = left;
+  a.scale_x = 1.0 / ((double)uw / w);  // cv2: scale_x = 1. / inv_scale_x, inv_scale_x = (double)dsize.width / ssize.width
+  a.scale_y = 1.0 / ((double)uh / h);
+  a.dst = d_dst; a.Hn = Hn; a.Wn = Wn;
+  hipError_t e = ym_launch_letterbox(a, static_cast<hipStream_t>(stream));
+  if (e != hipSuccess) return fail(YM_EHIP, "letterbox launch: %s", hipGetErrorString(e));
   return YM_OK;
 }
 

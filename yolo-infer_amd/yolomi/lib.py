@@ -51,6 +51,7 @@ def load_library(path: os.PathLike = LIB_PATH):
         "ym_profile_replay": (I, [P, P, I, I, I, C.POINTER(InferArgs), P, P, P, I, F, I]),
         "ym_tune": (I, [P, P, I, I, I, C.POINTER(InferArgs), P, P, P, I]),
         "ym_masks": (I, [P, P, I, I, P, I, I, I, P, P, P]),
+        "ym_letterbox": (I, [P, P, I, I, I, I, I, I, I, I, P, I, I, P]),
         "ym_get_op_cfg": (I, [P, I, I, I, C.POINTER(I), I]),
         "ym_set_op_cfg": (I, [P, I, I, I, C.POINTER(I), I]),
         "ym_num_ops": (I, [P]),
@@ -71,7 +72,7 @@ def load_library(path: os.PathLike = LIB_PATH):
     return lib
 
 
-EXPORTED = ("ym_create", "ym_load_weights", "ym_infer", "ym_calibrate", "ym_masks", "ym_profile", "ym_profile_replay", "ym_tune", "ym_get_op_cfg", "ym_set_op_cfg",
+EXPORTED = ("ym_create", "ym_load_weights", "ym_infer", "ym_calibrate", "ym_masks", "ym_letterbox", "ym_profile", "ym_profile_replay", "ym_tune", "ym_get_op_cfg", "ym_set_op_cfg",
             "ym_num_ops", "ym_op_name", "ym_num_buffers",
             "ym_buffer_info", "ym_read_buffer", "ym_sync", "ym_last_error", "ym_destroy", "ym_version")
 
@@ -135,6 +136,10 @@ class Runtime:
     def masks(self, dets_ptr, B, max_det, offsets_ptr, total, H, W, masks_ptr, nonempty_ptr, stream):
         _check(self.lib.ym_masks(self.ctx, C.c_void_p(dets_ptr), B, max_det, C.c_void_p(offsets_ptr), total, H, W,
                                  C.c_void_p(masks_ptr), C.c_void_p(nonempty_ptr), C.c_void_p(stream)))
+
+    def letterbox(self, src_ptr, h, w, row_bytes, bgr, uh, uw, top, left, dst_ptr, Hn, Wn, stream):
+        _check(self.lib.ym_letterbox(self.ctx, C.c_void_p(src_ptr), h, w, row_bytes, int(bool(bgr)), uh, uw, top, left,
+                                     C.c_void_p(dst_ptr), Hn, Wn, C.c_void_p(stream)))
 
     def tune(self, x_ptr, B, H, W, args, dets_ptr, counts_ptr, stream, reps=8):
         _check(self.lib.ym_tune(self.ctx, C.c_void_p(x_ptr), B, H, W, C.byref(args), C.c_void_p(dets_ptr),
