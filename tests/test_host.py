@@ -174,3 +174,31 @@ def test_dma_kernels_issue_exactly_the_counted_loads():
     r = subprocess.run([sys.executable, os.path.join(ROOT, "tools", "check_dma_asm.py")], capture_output=True,
                        text=True, timeout=300)
     assert r.returncode == 0, r.stdout[-2000:] + r.stderr[-2000:]
+
+
+def test_save_detection_results_formats(tmp_path):
+    """utils.visualization.save_detection_results writes the reference's txt/json/csv formats
+    (/root/reference/utils/visualization.py:342-437): checked against a per-box restatement of those formats."""
+    import csv as _csv
+    from core.results import Results
+    from utils.visualization import save_detection_results
+    rng = np.random.default_rng(9)
+    d = torch.from_numpy(np.concatenate([rng.uniform(0, 640, (5, 4)), rng.uniform(0.25, 1, (5, 1)),
+                                         rng.integers(0, 80, (5, 1))], 1).astype(np.float32))
+    r = Results(torch.zeros(3, 64, 64), {i: str(i) for i in range(80)}, d)
+    per_box = [(int(b.cls[0].item()), float(b.conf[0].item()), [float(v) for v in b.xyxy[0].tolist()]) for b in r.boxes]
+    save_detection_results(r, str(tmp_path / "o" / "a.txt"), "txt")
+    want = "".join(f"{c} {s:.6f} {x[0]:.6f} {x[1]:.6f} {x[2]:.6f} {x[3]:.6f}\n" for c, s, x in per_box)
+    assert (tmp_path / "o" / "a.txt").read_text() == want
+    save_detection_results(r, str(tmp_path / "a.json"), "json")
+    got = json.loads((tmp_path / "a.json").read_text())
+    assert got == {"detections": [{"class_id": c, "confidence": s, "bbox": x} for c, s, x in per_box]}
+    save_detection_results(r, str(tmp_path / "a.csv"), "CSV")
+    rows = list(_csv.reader(open(tmp_path / "a.csv")))
+    assert rows[0] == ["class_id", "confidence", "x1", "y1", "x2", "y2"]
+    assert rows[1:] == [[str(c), str(s)] + [str(v) for v in x] for c, s, x in per_box]
+    empty = Results(torch.zeros(3, 64, 64), {}, torch.zeros(0, 6))
+    save_detection_results(empty, str(tmp_path / "e.csv"), "csv")
+    assert len(list(_csv.reader(open(tmp_path / "e.csv")))) == 1
+    with pytest.raises(ValueError):
+        save_detection_results(r, str(tmp_path / "a.xml"), "xml")
