@@ -421,3 +421,19 @@ def test_segment_masks_match_oracle(dtype, agree, min_frac):
             a = (r["masks"][i] == g.masks.data[j].cpu()).float().mean().item()
             assert a >= agree, (i, j, a)
     assert total > 0 and matched >= min_frac * total - 1, (matched, total)
+
+
+def test_ultralytics_pt_model_path(tmp_path):
+    """YOLO11Model(model_path=<Ultralytics .pt>) runs the checkpoint's weights (yolomi/ptimport.py): the same
+    detections as a model packed from those (fp16-rounded) weights directly."""
+    from core.model import YOLO11Model
+    from tests.test_ptimport import _fake_checkpoint
+    sd = synth_weights("n", "detect", 3)
+    p = tmp_path / "yolo11n.pt"
+    _fake_checkpoint(p, sd)
+    sd16 = {k: (np.asarray(v).astype(np.float16).astype(np.float32) if np.asarray(v).dtype.kind == "f" else v)
+            for k, v in sd.items()}
+    x = make_input("uniform", (5,), 640).to(DEV)
+    a = YOLO11Model(model_path=str(p), size="n", device="cuda:0", dtype="f32").predict(x)
+    b = YOLO11Model(size="n", device="cuda:0", dtype="f32", state_dict=sd16).predict(x)
+    assert len(a[0]) == len(b[0]) and torch.equal(a[0].boxes.data, b[0].boxes.data)

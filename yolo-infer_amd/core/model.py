@@ -76,13 +76,17 @@ def _load_state_dict(path: Path) -> Dict[str, np.ndarray]:
         with np.load(path, allow_pickle=False) as z:
             return {k: z[k] for k in z.files}
     if suf == ".pt":
-        obj = torch.load(path, map_location="cpu", weights_only=True)
+        try:
+            obj = torch.load(path, map_location="cpu", weights_only=True)
+        except Exception:  # a pickled Ultralytics model (YOLO('yolo11n.pt') checkpoints): restricted unpickler
+            from yolomi.ptimport import load_ultralytics_checkpoint
+            return load_ultralytics_checkpoint(str(path))
         if isinstance(obj, dict) and "state_dict" in obj:
             obj = obj["state_dict"]
-        if not isinstance(obj, dict):
+        if not isinstance(obj, dict) or not all(isinstance(v, torch.Tensor) for v in obj.values()):
             raise ValueError(f"{path}: expected a state dict of tensors")
         return {k: v.float().numpy() if v.is_floating_point() else v.numpy() for k, v in obj.items()}
-    raise ValueError(f"unsupported weights file {path} (use .safetensors, .npz or a state-dict .pt)")
+    raise ValueError(f"unsupported weights file {path} (use an Ultralytics .pt, a state-dict .pt, .safetensors or .npz)")
 
 
 class YOLO11Model:
