@@ -99,10 +99,19 @@ __global__ __launch_bounds__(256) void conv_stream_i8(const ConvArgs a) {
   const int g = lane >> 4, col = lane & 15;
   const QRec* Q = a.q;
   const i8* W = static_cast<const i8*>(a.w);
-  for (int i = tid; i < NP * (KP / 16); i += 256) {
-    const int n = i / (KP / 16), c = i - n * (KP / 16);
-    *reinterpret_cast<i8x16*>(ws + n * LDW + 16 * c) =
-        n < a.N ? *reinterpret_cast<const i8x16*>(W + (size_t)n * KP + 16 * c) : __builtin_bit_cast(i8x16, i32x4{0, 0, 0, 0});
+  for (int i0 = tid; i0 < NP * (KP / 16); i0 += 256 * 8) {  // 8 loads in flight per thread and round
+    i8x16 v[8];
+#pragma unroll
+    for (int u = 0; u < 8; ++u) {
+      const int i = i0 + 256 * u, n = i / (KP / 16), c = i - n * (KP / 16);
+      v[u] = (i < NP * (KP / 16) && n < a.N) ? *reinterpret_cast<const i8x16*>(W + (size_t)n * KP + 16 * c)
+                                              : __builtin_bit_cast(i8x16, i32x4{0, 0, 0, 0});
+    }
+#pragma unroll
+    for (int u = 0; u < 8; ++u) {
+      const int i = i0 + 256 * u, n = i / (KP / 16), c = i - n * (KP / 16);
+      if (i < NP * (KP / 16)) *reinterpret_cast<i8x16*>(ws + n * LDW + 16 * c) = v[u];
+    }
   }
   post[tid] = Q->post[tid];
   for (int i = tid; i < NP; i += 256) {
@@ -210,6 +219,10 @@ __global__ __launch_bounds__(256) void conv_small_i8(const ConvArgs a) {
     const int ks = wave + 4 * j;
     af[j] = (ks < KS && nrow < a.N) ? *reinterpret_cast<const i8x16*>(wr + 64 * ks) : zero;
   }
+  const int nq = 16 * tn + 4 * g < a.N ? 16 * tn + 4 * g : 0;  // the epilogue's parameters, fetched up front
+  const i32x4 bi = *reinterpret_cast<const i32x4*>(a.biasi + nq);
+  const f32x4 sa = *reinterpret_cast<const f32x4*>(a.sasw + nq);
+  const f32x4 bf = *reinterpret_cast<const f32x4*>(a.bias + nq);
   const i8* s0 = static_cast<const i8*>(a.src0) + a.s0_coff;
   i8x16 bfr[PXG][KSW];
   int b[PXG], y[PXG], x[PXG];
@@ -242,9 +255,6 @@ __global__ __launch_bounds__(256) void conv_small_i8(const ConvArgs a) {
   if (wave > 0) return;
   const int n0 = 16 * tn + 4 * g;
   if (n0 >= a.N) return;
-  const i32x4 bi = *reinterpret_cast<const i32x4*>(a.biasi + n0);
-  const f32x4 sa = *reinterpret_cast<const f32x4*>(a.sasw + n0);
-  const f32x4 bf = *reinterpret_cast<const f32x4*>(a.bias + n0);
   const int biv[4] = {bi[0], bi[1], bi[2], bi[3]};
   const float sav[4] = {sa[0], sa[1], sa[2], sa[3]}, bfv[4] = {bf[0], bf[1], bf[2], bf[3]};
   const int mode = Q->mode;

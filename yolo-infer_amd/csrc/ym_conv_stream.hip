@@ -47,10 +47,19 @@ __global__ __launch_bounds__(256) void conv_stream(const ConvArgs a) {
   const int g = lane >> 4, col = lane & 15;
   const f16* W = static_cast<const f16*>(a.w);
   const int NP = (a.N + 15) & ~15;  // rows padded to the 16-row MFMA block (zero weights, outputs not stored)
-  for (int i = tid; i < NP * (KP / 8); i += 256) {
-    const int n = i / (KP / 8), c = i - n * (KP / 8);
-    *reinterpret_cast<f16x8*>(ws + n * LDW + 8 * c) =
-        n < a.N ? *reinterpret_cast<const f16x8*>(W + (size_t)n * KP + 8 * c) : Vec8<f16>::zero();
+  for (int i0 = tid; i0 < NP * (KP / 8); i0 += 256 * 8) {  // 8 loads in flight per thread and round
+    f16x8 v[8];
+#pragma unroll
+    for (int u = 0; u < 8; ++u) {
+      const int i = i0 + 256 * u, n = i / (KP / 8), c = i - n * (KP / 8);
+      v[u] = (i < NP * (KP / 8) && n < a.N) ? *reinterpret_cast<const f16x8*>(W + (size_t)n * KP + 8 * c)
+                                             : Vec8<f16>::zero();
+    }
+#pragma unroll
+    for (int u = 0; u < 8; ++u) {
+      const int i = i0 + 256 * u, n = i / (KP / 8), c = i - n * (KP / 8);
+      if (i < NP * (KP / 8)) *reinterpret_cast<f16x8*>(ws + n * LDW + 8 * c) = v[u];
+    }
   }
   for (int i = tid; i < NP; i += 256) bs[i] = i < a.N ? a.bias[i] : 0.f;
 
@@ -194,6 +203,9 @@ __global__ __launch_bounds__(256) void conv_small(const ConvArgs a) {
     const int ks = wave + 4 * j;
     af[j] = (ks < KS && nrow < a.N) ? Vec8<f16>::load(wr + 32 * ks) : Vec8<f16>::zero();
   }
+  // the epilogue's bias, fetched with the operands (4-aligned n0 < N: in range; clamped otherwise)
+  const int nb4 = 16 * tn + 4 * g < a.N ? 16 * tn + 4 * g : 0;
+  const f32x4 b4 = *reinterpret_cast<const f32x4*>(a.bias + nb4);
   h8 bf[PXG][KSW];
   int b[PXG], y[PXG], x[PXG];
   bool ok[PXG];
@@ -247,7 +259,6 @@ __global__ __launch_bounds__(256) void conv_small(const ConvArgs a) {
   if (wave > 0) return;
   const int n0 = 16 * tn + 4 * g;
   if (n0 >= a.N) return;
-  const f32x4 b4 = *reinterpret_cast<const f32x4*>(a.bias + n0);
   OutT* dst = static_cast<OutT*>(a.dst);
   const f16* res = static_cast<const f16*>(a.res);
 #pragma unroll

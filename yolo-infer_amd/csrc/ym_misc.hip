@@ -664,10 +664,16 @@ __global__ __launch_bounds__(NMS_T) void nms_image(const NmsArgs a) {
     unsigned long long* mask = reinterpret_cast<unsigned long long*>(sbx + NMS_BM);  // [ne][W]
     unsigned long long ki = 0;
     if (tid < n) sk[tid] = ki = gk[tid];
+    if (tid == n) sk[n] = 0ull;  // pad to an even count (keys are > 0: the score bits of a candidate are)
     __syncthreads();
     if (tid < n) {
       int r = 0;
-      for (int j = 0; j < n; ++j) r += sk[j] > ki;
+      const int n2 = (n + 1) >> 1;
+#pragma unroll 4
+      for (int j = 0; j < n2; ++j) {  // 16-byte LDS reads, two keys each
+        const unsigned long long k0 = sk[2 * j], k1 = sk[2 * j + 1];
+        r += (k0 > ki) + (k1 > ki);
+      }
       sorted[r] = ki;
     }
     __syncthreads();
@@ -698,17 +704,38 @@ __global__ __launch_bounds__(NMS_T) void nms_image(const NmsArgs a) {
     __syncthreads();
     __shared__ int keep_bm[NMS_BM], kept_bm;
     if (tid < 64) {
-      const int cap = a.max_det;
+      // greedy scan, 64 candidates per block: lane w holds removed-word w; within block k the rows' own word k
+      // (lane l: row 64k + l) decides sequentially from registers (readlane), then the block's kept rows are
+      // OR-reduced across the wave into the later words
+      const int lane = tid, cap = a.max_det;
       unsigned long long rem = 0;
       int kept = 0;
-      for (int i = 0; i < ne && kept < cap; ++i) {
-        const unsigned long long wv = __shfl(rem, i >> 6);
-        if ((wv >> (i & 63)) & 1ull) continue;
-        if (tid == 0) keep_bm[kept] = i;
-        ++kept;
-        if (tid < W) rem |= mask[i * W + tid];
+      bool stop = false;
+      for (int k = 0; k < W && !stop; ++k) {
+        const int row = 64 * k + lane;
+        const unsigned long long diag = row < ne ? mask[row * W + k] : 0ull;
+        const unsigned dlo = (unsigned)diag, dhi = (unsigned)(diag >> 32);
+        unsigned long long remk = __shfl(rem, k);
+        unsigned long long keepbits = 0;
+        const int jn = ne - 64 * k < 64 ? ne - 64 * k : 64;
+        for (int j = 0; j < jn; ++j) {
+          if ((remk >> j) & 1ull) continue;
+          if (kept >= cap) { stop = true; break; }
+          keepbits |= 1ull << j;
+          if (lane == 0) keep_bm[kept] = 64 * k + j;
+          ++kept;
+          remk |= ((unsigned long long)__builtin_amdgcn_readlane(dhi, j) << 32) |
+                  (unsigned long long)(unsigned)__builtin_amdgcn_readlane(dlo, j);
+        }
+        const bool mine = (keepbits >> lane) & 1ull;
+        for (int w = k + 1; w < W; ++w) {
+          unsigned long long v = (mine && row < ne) ? mask[row * W + w] : 0ull;
+#pragma unroll
+          for (int o = 32; o > 0; o >>= 1) v |= __shfl_xor(v, o);
+          if (lane == w) rem |= v;
+        }
       }
-      if (tid == 0) kept_bm = kept;
+      if (lane == 0) kept_bm = kept;
     }
     __syncthreads();
     const int kept = kept_bm;

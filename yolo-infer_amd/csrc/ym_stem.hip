@@ -66,6 +66,31 @@ __global__ __launch_bounds__(256) void stem_mfma(const ConvArgs a) {
     hi = Q->qhi;
     post[threadIdx.x] = Q->post[threadIdx.x];
   }
+  // Per-lane K slots: lane l covers K = 8(l>>4) .. +7 of pixel column l&15; K = tap (ky*3 + kx)*3 + c (the wstem row
+  // order), K >= 27 zero weights (their patch reads point at a valid element).  The weight / bias loads are
+  // unconditional (clamped rows) and issued before the patch loads, so their latency hides behind the staging.
+  const int lane = threadIdx.x & 63, wave = threadIdx.x >> 6;
+  const int kg = lane >> 4, col = lane & 15;
+  int off[8];
+  float wraw[NT][8];
+#pragma unroll
+  for (int j = 0; j < 8; ++j) {
+    const int k = 8 * kg + j;
+    const int kk = k / 3, c = k - (k / 3) * 3;
+    const int ky = kk / 3, kx = kk - (kk / 3) * 3;
+    off[j] = k < 27 ? (c * PH + ky) * PW + kx + 3 : 3;  // +3: the patch starts at x0 - 4, the window at x0 - 1
+    const int kr = k < 27 ? k : 26;
+#pragma unroll
+    for (int t = 0; t < NT; ++t) wraw[t][j] = a.wstem[kr * a.N + 16 * t + col];
+  }
+  float bias[NT][4], sasw[NT][4];
+#pragma unroll
+  for (int t = 0; t < NT; ++t)
+#pragma unroll
+    for (int r = 0; r < 4; ++r) {
+      bias[t][r] = a.bias[16 * t + 4 * kg + r];
+      if constexpr (QUANT) sasw[t][r] = a.sasw[16 * t + 4 * kg + r];
+    }
   // all of a thread's patch loads are issued before the first is consumed (one memory latency, not NIT)
   constexpr int NIT = (3 * PH * PW4 + 255) / 256;
   f32x4 v[NIT];
@@ -95,29 +120,11 @@ __global__ __launch_bounds__(256) void stem_mfma(const ConvArgs a) {
     }
     *reinterpret_cast<f16x4*>(patch + 4 * i) = h;  // i = (c*PH + py)*PW4 + q
   }
-  // Per-lane K slots: lane l covers K = 8(l>>4) .. +7 of pixel column l&15; K = tap (ky*3 + kx)*3 + c (the wstem row
-  // order), K >= 27 zero weights (their patch reads point at a valid element).
-  const int lane = threadIdx.x & 63, wave = threadIdx.x >> 6;
-  const int kg = lane >> 4, col = lane & 15;
-  int off[8];
   h8 wf[NT];
 #pragma unroll
-  for (int j = 0; j < 8; ++j) {
-    const int k = 8 * kg + j;
-    const int kk = k / 3, c = k - (k / 3) * 3;
-    const int ky = kk / 3, kx = kk - (kk / 3) * 3;
-    off[j] = k < 27 ? (c * PH + ky) * PW + kx + 3 : 3;  // +3: the patch starts at x0 - 4, the window at x0 - 1
+  for (int j = 0; j < 8; ++j)
 #pragma unroll
-    for (int t = 0; t < NT; ++t) wf[t][j] = k < 27 ? (f16)a.wstem[k * a.N + 16 * t + col] : (f16)0.f;
-  }
-  float bias[NT][4], sasw[NT][4];
-#pragma unroll
-  for (int t = 0; t < NT; ++t)
-#pragma unroll
-    for (int r = 0; r < 4; ++r) {
-      bias[t][r] = a.bias[16 * t + 4 * kg + r];
-      if constexpr (QUANT) sasw[t][r] = a.sasw[16 * t + 4 * kg + r];
-    }
+    for (int t = 0; t < NT; ++t) wf[t][j] = 8 * kg + j < 27 ? (f16)wraw[t][j] : (f16)0.f;
   __syncthreads();
   // wave w: pixel groups 8w .. 8w+7 of the tile's 32 (16 consecutive columns of one row each)
 #pragma unroll

@@ -17,7 +17,7 @@ from .lib import Runtime
 from .plan import pack_graph
 
 # Bump when the meaning of a conv config index (csrc/ym_conv.hip kCfgs) changes: stale tables are then ignored.
-TUNE_VERSION = 8
+TUNE_VERSION = 9
 TUNED_DIR = os.path.join(os.path.dirname(os.path.abspath(__file__)), "tuned")  # committed tables
 
 
