@@ -314,14 +314,14 @@ __global__ __launch_bounds__(256) void dwconv3x3_i8(const DwArgs a) {
   post[threadIdx.x] = Q->post[threadIdx.x];
   __syncthreads();
   const int C8 = a.C >> 3;
-  const long idx = blockIdx.x * (long)blockDim.x + threadIdx.x;
-  const long total = (long)a.B * a.H * a.W * C8;
+  const int idx = blockIdx.x * blockDim.x + threadIdx.x;  // 32-bit index math (checked < 2^31 on the host)
+  const int total = a.B * a.H * a.W * C8;
   if (idx >= total) return;
-  const int cg = idx % C8;
-  const long pix = idx / C8;
+  const int pix = idx / C8;
+  const int cg = idx - pix * C8;
   const int HW = a.H * a.W;
   const int b = pix / HW;
-  const int p = pix - (long)b * HW;
+  const int p = pix - b * HW;
   const int y = p / a.W, x = p - (p / a.W) * a.W;
   const int c0 = cg * 8;
   const i8* src = static_cast<const i8*>(a.src);
@@ -337,6 +337,10 @@ __global__ __launch_bounds__(256) void dwconv3x3_i8(const DwArgs a) {
     w[t] = Vec8<i8>::load(a.wq + t * a.C + c0);
   }
   const int zi = Q->z_in;
+  const f32x4 sa0 = *reinterpret_cast<const f32x4*>(a.sasw + c0), sa1 = *reinterpret_cast<const f32x4*>(a.sasw + c0 + 4);
+  const f32x4 bb0 = *reinterpret_cast<const f32x4*>(a.bias + c0), bb1 = *reinterpret_cast<const f32x4*>(a.bias + c0 + 4);
+  const float sav[8] = {sa0[0], sa0[1], sa0[2], sa0[3], sa1[0], sa1[1], sa1[2], sa1[3]};
+  const float bbv[8] = {bb0[0], bb0[1], bb0[2], bb0[3], bb1[0], bb1[1], bb1[2], bb1[3]};
   int acc[8];
 #pragma unroll
   for (int e = 0; e < 8; ++e) acc[e] = 0;
@@ -349,7 +353,7 @@ __global__ __launch_bounds__(256) void dwconv3x3_i8(const DwArgs a) {
   V o;
 #pragma unroll
   for (int e = 0; e < 8; ++e) {
-    const int qc = requant_out(acc[e], a.sasw[c0 + e], a.bias[c0 + e], Q);
+    const int qc = requant_out(acc[e], sav[e], bbv[e], Q);
     o[e] = (i8)quant_store(post[qc], Q->inv_so, Q->zo, Q->qlo, Q->qhi);
   }
   Vec8<i8>::store(static_cast<i8*>(a.dst) + (size_t)(b * a.d_P + p) * a.d_ctot + a.d_coff + c0, o);
@@ -532,6 +536,7 @@ hipError_t ym_launch_conv_i8(const ConvArgs& a, int cfg, hipStream_t st, bool st
 hipError_t ym_launch_dwconv_i8(const DwArgs& a, hipStream_t st) {
   if (a.C % 8 || !a.q || !a.wq) return hipErrorInvalidValue;
   const long total = (long)a.B * a.H * a.W * (a.C / 8);
+  if (total >= 0x7FFFFFFFL - 256) return hipErrorInvalidValue;  // the kernel indexes in 32 bits
   hipLaunchKernelGGL(dwconv3x3_i8, dim3((total + 255) / 256), dim3(256), 0, st, a);
   return hipGetLastError();
 }

@@ -56,14 +56,14 @@ __global__ __launch_bounds__(256) void max_reduce(const float* __restrict__ x, l
 template <typename T>
 __global__ __launch_bounds__(256) void dwconv3x3(const DwArgs a) {
   const int C8 = a.C >> 3;
-  const long idx = blockIdx.x * (long)blockDim.x + threadIdx.x;
-  const long total = (long)a.B * a.H * a.W * C8;
+  const int idx = blockIdx.x * blockDim.x + threadIdx.x;  // 32-bit index math (checked < 2^31 on the host)
+  const int total = a.B * a.H * a.W * C8;
   if (idx >= total) return;
-  const int cg = idx % C8;
-  const long pix = idx / C8;
+  const int pix = idx / C8;
+  const int cg = idx - pix * C8;
   const int HW = a.H * a.W;
   const int b = pix / HW;
-  const int p = pix - (long)b * HW;
+  const int p = pix - b * HW;
   const int y = p / a.W, x = p - (p / a.W) * a.W;
   const int c0 = cg * 8;
   const T* src = static_cast<const T*>(a.src);
@@ -847,6 +847,7 @@ hipError_t ym_launch_prep(int dtype, const PrepArgs& a, int* counts, int B, hipS
 hipError_t ym_launch_dwconv(int dtype, const DwArgs& a, hipStream_t st) {
   if (dtype == YM_DT_I8) return ym_launch_dwconv_i8(a, st);
   const long total = (long)a.B * a.H * a.W * (a.C / 8);
+  if (total >= 0x7FFFFFFFL - 256) return hipErrorInvalidValue;  // the kernel indexes in 32 bits
   const dim3 g((total + 255) / 256);
   if (a.C % 8) return hipErrorInvalidValue;
   if (dtype == YM_DT_F16) hipLaunchKernelGGL(dwconv3x3<f16>, g, dim3(256), 0, st, a);
