@@ -40,7 +40,7 @@ def main():
         out = dets.clone()
         n = counts.tolist()
         t2 = time.perf_counter()
-        _ = [Results(x[b], m.model.names, out[b, :n[b], :6]) for b in range(8)]
+        _ = [Results.from_batch(x, b, m.model.names, out, n[b]) for b in range(8)]
         t3 = time.perf_counter()
         t_enq += t1 - t0
         t_sync += t2 - t1
@@ -49,6 +49,12 @@ def main():
     k = 1e6 / a.iters
     print(f"lanes {a.lanes}: enqueue {t_enq * k:.1f} us, clone+sync {t_sync * k:.1f} us, Results {t_res * k:.1f} us, "
           f"total {t_tot * k:.1f} us per predict")
+    torch.cuda.synchronize()
+    t0 = time.perf_counter()
+    for _ in range(a.iters):
+        m.predict(x)
+    t1 = time.perf_counter()
+    print(f"lanes {a.lanes}: predict() loop {(t1 - t0) * k:.1f} us per call")
     torch.cuda.synchronize()
     t0 = time.perf_counter()
     for _ in range(a.iters):
