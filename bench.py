@@ -51,7 +51,8 @@ def pmc_traffic(workload):
             j = json.load(open(p))
         except (OSError, ValueError):
             continue
-        if j.get("workload") == workload and "conv" in j.get("families", {}):
+        # the summary names the network/batch/dtype; the bench line appends how it was driven (", predict() loop")
+        if j.get("workload") == workload.split(",")[0] and "conv" in j.get("families", {}):
             best = (p, j)
     if best is None:
         return None, None

@@ -10,7 +10,7 @@ namespace {
 // ------------------------------------------------------------------------------------------------- input stats
 // LoadTensor._single_check: `if im.max() > 1 + finfo(dtype).eps: im = im.float() / 255` over the WHOLE batch.
 // ctl[0] holds max as an order-preserving int; ctl is reset by the init kernel at the start of every forward.
-// The division itself happens in the stem conv's loader (csrc/ym_conv.hip KIND 0), which reads the NCHW batch.
+// The division itself happens in the stem conv's loader (csrc/ym_stem.hip), which reads the NCHW batch.
 __global__ __launch_bounds__(256) void init_ctl(float* ctl, int* counts, int B, int* cnt, int cnt_len) {
   const int t = blockIdx.x * blockDim.x + threadIdx.x;
   if (t < YM_CTL_SLOTS) reinterpret_cast<int*>(ctl)[t * YM_CTL_STRIDE] = f2ord(-INFINITY);
@@ -25,11 +25,12 @@ __global__ __launch_bounds__(256) void max_reduce(const float* __restrict__ x, l
   const f32x4* x4 = reinterpret_cast<const f32x4*>(x);
   const long step = (long)gridDim.x * blockDim.x;
   long i = blockIdx.x * (long)blockDim.x + threadIdx.x;
-  for (; i + 3 * step < n4; i += 4 * step) {  // four independent 16-byte loads in flight per lane
-    const f32x4 v0 = x4[i], v1 = x4[i + step], v2 = x4[i + 2 * step], v3 = x4[i + 3 * step];
-    const f32x4 a = {fmaxf(v0[0], v1[0]), fmaxf(v0[1], v1[1]), fmaxf(v0[2], v1[2]), fmaxf(v0[3], v1[3])};
-    const f32x4 b = {fmaxf(v2[0], v3[0]), fmaxf(v2[1], v3[1]), fmaxf(v2[2], v3[2]), fmaxf(v2[3], v3[3])};
-    m = fmaxf(m, fmaxf(fmaxf(fmaxf(a[0], b[0]), fmaxf(a[1], b[1])), fmaxf(fmaxf(a[2], b[2]), fmaxf(a[3], b[3]))));
+  for (; i + 7 * step < n4; i += 8 * step) {  // eight independent 16-byte loads in flight per lane
+    f32x4 v[8];
+#pragma unroll
+    for (int u = 0; u < 8; ++u) v[u] = __builtin_nontemporal_load(x4 + i + u * step);
+#pragma unroll
+    for (int u = 0; u < 8; ++u) m = fmaxf(m, fmaxf(fmaxf(v[u][0], v[u][1]), fmaxf(v[u][2], v[u][3])));
   }
   for (; i < n4; i += step) {
     const f32x4 v = x4[i];
@@ -838,7 +839,7 @@ hipError_t ym_launch_prep(int dtype, const PrepArgs& a, int* counts, int B, hipS
   // one atomic per block: a few hundred same-address atomics, not thousands (one word takes ~90 per us)
   const long n = (long)a.B * a.C * a.H * a.W;
   long blocks = (n / 4 + 255) / 256;
-  if (blocks > 1024) blocks = 1024;
+  if (blocks > 2048) blocks = 2048;
   if (blocks < 1) blocks = 1;
   hipLaunchKernelGGL(max_reduce, dim3(blocks), dim3(256), 0, st, a.in, n, a.ctl);
   return hipGetLastError();
