@@ -437,3 +437,47 @@ def test_ultralytics_pt_model_path(tmp_path):
     a = YOLO11Model(model_path=str(p), size="n", device="cuda:0", dtype="f32").predict(x)
     b = YOLO11Model(size="n", device="cuda:0", dtype="f32", state_dict=sd16).predict(x)
     assert len(a[0]) == len(b[0]) and torch.equal(a[0].boxes.data, b[0].boxes.data)
+
+
+# ------------------------------------------------------------------------------------------------ fused conv pairs
+SPLIT_TAG = 1 << 20  # csrc/ym_runtime.cpp kSplitTag: op cfg of a fused pair run as its two convs
+
+
+def test_fused_pairs_split_equals_unfused_plan():
+    """The fused f16 plan (yolomi/arch.py fuse_pairs + the C3k cv1 ‖ cv2 merge) with its pairs run as two launches
+    (op cfg SPLIT_TAG + ...) and with its pairs on the fused streaming kernel both match the unfused f16 plan on the
+    Detect rows within fp16 storage error (the merge and the fused second GEMM change fp32 summation order only)."""
+    from core.model import YOLO11Model
+    x = make_input("uniform", (5, 6), 640).to(DEV)
+    B, _, H, W = x.shape
+    os.environ["YM_FUSE"] = "0"
+    try:
+        mu = YOLO11Model(size="n", device="cuda:0", dtype="f16", verbose=False)
+    finally:
+        del os.environ["YM_FUSE"]
+    eu, ef = mu.model.engine, model("n", "f16").model.engine
+    assert not any(op.args.get("pair") for op in eu.graph.ops)
+    assert sum(bool(op.args.get("pair")) for op in ef.graph.ops) >= 6
+    cfg = 29  # one LDS-DMA config for every conv (inapplicable ops fall back to the heuristic choice)
+    eu.run(x, use_graph=False)
+    eu.rt.set_op_cfg(B, H, W, [cfg if op.kind == "conv" else -1 for op in eu.graph.ops])
+    ef.run(x, use_graph=False)
+    fused = ef.rt.get_op_cfg(B, H, W)
+    try:
+        ef.rt.set_op_cfg(B, H, W, [(SPLIT_TAG + 128 * cfg + cfg if op.args.get("pair") else cfg)
+                                   if op.kind == "conv" else -1 for op in ef.graph.ops])
+        eu.run(x, use_graph=False)
+        ef.run(x, use_graph=False)
+        hu = eu.read_buffer(eu.graph.anchor_buf.id, B)
+        hs = ef.read_buffer(ef.graph.anchor_buf.id, B)
+        ef.rt.set_op_cfg(B, H, W, [(35 if op.args.get("pair") else cfg) if op.kind == "conv" else -1
+                                   for op in ef.graph.ops])
+        ef.run(x, use_graph=False)
+        hf = ef.read_buffer(ef.graph.anchor_buf.id, B)
+    finally:
+        if fused is not None:
+            ef.rt.set_op_cfg(B, H, W, fused)
+        ef._tuned.discard((B, H, W))
+        eu._tuned.discard((B, H, W))
+    rel = lambda a, b: (a - b).abs().max().item() / b.abs().max().item()  # noqa: E731
+    assert rel(hs, hu) < 1e-2 and rel(hf, hu) < 1e-2

@@ -12,7 +12,7 @@ import torch
 from tests.matching import MatchReport, match_image
 from yolomi.arch import GraphBuilder, param_specs
 from yolomi.metrics import evaluate
-from yolomi.plan import MAGIC, fuse_conv_bn, pack_model
+from yolomi.plan import MAGIC, fuse_conv_bn, fuse_default, pack_model
 from yolomi.synth import splitmix64, synth_weights, uniform
 
 ROOT = os.path.dirname(os.path.dirname(os.path.abspath(__file__)))
@@ -58,7 +58,7 @@ def test_blob_layout(scale, task, dtype):
     sd = synth_weights(scale, task, 0)
     blob = pack_model(scale, task, sd, dtype)
     h = struct.unpack("<32i", blob[:128])
-    g = GraphBuilder(scale, task)
+    g = GraphBuilder(scale, task, fuse=fuse_default(dtype))
     assert h[0] == MAGIC and h[1] == 1 and h[2] == (0 if dtype == "f16" else 1)
     assert h[3] == (1 if task == "segment" else 0) and h[4] == 80 and h[5] == g.nm and h[6] == 16
     assert h[8:11] == (8, 16, 32) and h[11] == len(g.buffers) and h[12] == len(g.ops)
@@ -71,6 +71,9 @@ def test_blob_layout(scale, task, dtype):
         if r[0] == 2:
             assert r[3] % 8 == 0 and r[21] % 64 == 0 and r[21] >= r[1] * r[1] * r[3]
             assert 0 <= r[19] < wb and 0 <= r[20] < wb
+            if r[30]:  # fused 1x1 successor: W2 [N2][Kpad2] with K = this conv's N
+                assert dtype == "f16" and r[27] > 0 and r[29] % 64 == 0 and r[29] >= r[4]
+                assert 0 <= r[25] < wb and 0 <= r[26] < wb
 
 
 def test_capi_exports_every_declared_symbol():
@@ -202,3 +205,37 @@ def test_save_detection_results_formats(tmp_path):
     assert len(list(_csv.reader(open(tmp_path / "e.csv")))) == 1
     with pytest.raises(ValueError):
         save_detection_results(r, str(tmp_path / "a.xml"), "xml")
+
+
+@pytest.mark.parametrize("scale,task", [("n", "detect"), ("s", "detect"), ("s", "segment")])
+def test_fused_pairs(scale, task):
+    """GraphBuilder.fuse_pairs: each fused op is a conv followed by a 1x1 conv that was the only reader of the
+    conv's output; the work (MACs) is unchanged, the intermediate tensor leaves the byte count and no op reads it."""
+    g0, g = GraphBuilder(scale, task), GraphBuilder(scale, task, fuse=True)
+    pairs = [op for op in g.ops if op.args.get("pair")]
+    names0 = [op.name for op in g0.ops]
+    merged = [op for op in g.ops if op.args.get("wkeys")]  # C3k cv1 ‖ cv2
+    assert [op.name for op in merged] == [f"model.{i}.m.0.cv1+cv2" for i in (6, 8, 22)]
+    assert len(g.ops) == len(g0.ops) - len(pairs) - len(merged)
+    assert g.macs_per_image() == g0.macs_per_image()
+    heads = {f"model.23.cv2.{l}.1+2" for l in range(3)} | {f"model.23.cv3.{l}.1.1+2" for l in range(3)}
+    assert heads <= {op.name for op in pairs}
+    for op in pairs:
+        first = op.name.split("+")[0]
+        i = names0.index(first)
+        nxt = g0.ops[i + 1]
+        assert nxt.args["k"] == 1 and nxt.args["src0"].buf.name == op.args["pair"]["mid"].buf.name
+        assert (op.args["dst"].buf.name, op.args["dst"].coff) == (nxt.args["dst"].buf.name, nxt.args["dst"].coff)
+        mid = op.args["pair"]["mid"].buf
+        for o in g.ops:
+            for k in ("src0", "src1", "res", "src", "qkv"):
+                v = o.args.get(k)
+                assert not (v is not None and hasattr(v, "buf") and v.buf is mid), (op.name, o.name)
+    c0, c1 = g0.op_costs(8, 640, 640), g.op_costs(8, 640, 640)
+    assert sum(c[0] for c in c0) == sum(c[0] for c in c1)
+    saved = sum(c[1] for c in c0) - sum(c[1] for c in c1)
+    mids = sum(op.args["pair"]["mid"].C * 8 * (640 // g.out_factor(op)) ** 2 * 2 * 2 for op in pairs)
+    xs = sum(op.args["src0"].C * 8 * (640 // g.out_factor(op)) ** 2 * 2 for op in merged)
+    assert saved == mids + xs  # each intermediate was written and read once, each merged input read once, at 2 B
+    with pytest.raises(ValueError):
+        GraphBuilder(scale, task, quant=True, fuse=True)

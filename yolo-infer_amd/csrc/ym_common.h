@@ -134,6 +134,10 @@ struct ConvArgs {
   // int8 plans: quantisation record, per-channel s_in·s_w and the int32 zero-point correction Σ_k (128 - z_in)·w
   const QRec* q; const float* sasw; const int* biasi;
   float* raw;                  // f32 calibration runs: pre-activation conv output, (M, N) row-major, or null
+  // fused pair (f16 streaming kernels): a following 1x1 conv consumes this conv's activated output straight from
+  // registers — out = act2(W2 · h + bias2) (+ res) with h = fp16(act(W · x + bias)); dst/res then describe the
+  // second conv's output.  w2 [N2][Kpad2] (K = this conv's N output channels), null for a single conv.
+  const void* w2; const float* bias2; int N2, Kpad2, act2;
 };
 
 struct DwArgs {

@@ -631,6 +631,21 @@ hipError_t ym_launch_conv(int dtype, int out_f32, const ConvArgs& a, int cfg, hi
   if (dtype == YM_DT_I8) return ym_launch_conv_i8(a, cfg, st, strict);  // csrc/ym_conv_i8.hip
   // (concat/upsample sources only feed 1x1 convs; YOLO11 has k in {1, 3})
   if (a.Kpad % KSTEP) return hipErrorInvalidValue;
+  if (a.w2) {  // fused pair: only the streaming kernels hold a whole N in one wave (csrc/ym_conv_stream.hip)
+    if (dtype != YM_DT_F16) return hipErrorInvalidValue;
+    const int sbase = kNumAllCfg + ym_conv_dma_num_cfgs(), ns = ym_conv_stream_num_cfgs();
+    if (cfg >= sbase && cfg < sbase + ns) {
+      const hipError_t e = ym_launch_conv_stream(out_f32, a, cfg - sbase, st);
+      if (e != hipErrorInvalidValue || strict) return e;
+    } else if (strict) {
+      return hipErrorInvalidValue;
+    }
+    for (int i = 0; i < ns; ++i) {  // untuned: the first streaming variant that takes the shape
+      const hipError_t e = ym_launch_conv_stream(out_f32, a, i, st);
+      if (e != hipErrorInvalidValue) return e;
+    }
+    return hipErrorInvalidValue;
+  }
   if (cfg >= kNumAllCfg) {
     // a DMA config that does not apply to this op (checked before anything is launched): the tuner skips the
     // candidate (strict); a pinned table falls back to the heuristic

@@ -36,13 +36,26 @@ constexpr SCfg kStream[] = {
 };
 constexpr int kNumStream = sizeof(kStream) / sizeof(kStream[0]);
 constexpr int kMaxWBytes = 80 * 1024;
+constexpr int kMaxFusedBytes = 112 * 1024;  // fused pairs: both weight matrices
 
-template <typename OutT, int KIND, int KS, int PX>
+// FUSE: the fused pair (ConvArgs::w2) — the first conv's activated output block nb (16 channels x 16 pixels, lane
+// (g, col) holding channels 16 nb + 4 g .. + 3 of pixel col) is exactly the B operand of a 16x16x16 MFMA with K chunk
+// nb, so the following 1x1 conv runs from registers: no LDS round trip, no HBM write/read of the intermediate, one
+// launch fewer.  The intermediate is rounded to fp16 like the stored tensor of the unfused pair.
+constexpr int kFuseMaxN = 128;  // first conv's N (= second conv's K) held in registers: 8 blocks of 16
+
+template <typename OutT, int KIND, int KS, int PX, bool FUSE>
 __global__ __launch_bounds__(256) void conv_stream(const ConvArgs a) {
   constexpr int KP = KS * 32;      // Kpad
   constexpr int LDW = KP + 8;      // LDS row pitch (halves): +16 bytes
-  extern __shared__ __attribute__((aligned(16))) f16 ws[];  // [N][LDW], then bias [N] f32
+  constexpr int NBF = FUSE ? kFuseMaxN / 16 : 1;
+  extern __shared__ __attribute__((aligned(16))) f16 ws[];  // [N][LDW], then bias [N] f32 (FUSE: then W2, bias2)
   float* bs = reinterpret_cast<float*>(ws + ((a.N + 15) & ~15) * LDW);
+  const int NB = (a.N + 15) >> 4;
+  const int LDW2 = 16 * NB + 4;  // W2 row pitch (halves): the 8-byte A reads of 16 rows spread over the banks
+  f16* w2s = reinterpret_cast<f16*>(bs + 16 * NB);
+  const int NB2 = FUSE ? (a.N2 + 15) >> 4 : 0;
+  float* bs2 = reinterpret_cast<float*>(w2s + 16 * NB2 * LDW2);
   const int tid = threadIdx.x, lane = tid & 63, wave = tid >> 6;
   const int g = lane >> 4, col = lane & 15;
   const f16* W = static_cast<const f16*>(a.w);
@@ -62,6 +75,17 @@ __global__ __launch_bounds__(256) void conv_stream(const ConvArgs a) {
     }
   }
   for (int i = tid; i < NP; i += 256) bs[i] = i < a.N ? a.bias[i] : 0.f;
+  if constexpr (FUSE) {  // W2 [16 NB2][LDW2]: row n2, K = first-conv channel (zero past N / N2)
+    const f16* W2 = static_cast<const f16*>(a.w2);
+    const int q4 = 4 * NB;  // 4-channel quads per row
+    for (int i = tid; i < 16 * NB2 * q4; i += 256) {
+      const int n = i / q4, c = 4 * (i - n * q4);
+      f16x4 v = {0, 0, 0, 0};
+      if (n < a.N2 && c < a.N) v = *reinterpret_cast<const f16x4*>(W2 + (size_t)n * a.Kpad2 + c);
+      *reinterpret_cast<f16x4*>(w2s + n * LDW2 + c) = v;
+    }
+    for (int i = tid; i < 16 * NB2; i += 256) bs2[i] = i < a.N2 ? a.bias2[i] : 0.f;
+  }
 
   const int HW = a.Ho * a.Wo;
   const int G = (a.M + 15) >> 4;  // 16-pixel groups
@@ -127,6 +151,59 @@ __global__ __launch_bounds__(256) void conv_stream(const ConvArgs a) {
       ob[p] = (gb + p < G && m < a.M) ? b * a.d_P + a.d_pixoff + y * a.d_W + x : -1;
       rb[p] = b * a.r_P + y * a.Wo + x;
     }
+    if constexpr (FUSE) {
+      f16x4 h[PX][NBF];  // the first conv's activated output, fp16, in registers
+#pragma unroll
+      for (int nb = 0; nb < NBF; ++nb) {
+        if (nb >= NB) break;
+        h8 af[KS];
+#pragma unroll
+        for (int ks = 0; ks < KS; ++ks)
+          af[ks] = *reinterpret_cast<const h8*>(ws + (16 * nb + col) * LDW + 32 * ks + 8 * g);
+        const f32x4 b4 = *reinterpret_cast<const f32x4*>(bs + 16 * nb + 4 * g);
+#pragma unroll
+        for (int p = 0; p < PX; ++p) {
+          f32x4 acc = {0.f, 0.f, 0.f, 0.f};
+#pragma unroll
+          for (int ks = 0; ks < KS; ++ks) acc = __builtin_amdgcn_mfma_f32_16x16x32_f16(af[ks], cur[p][ks], acc, 0, 0, 0);
+#pragma unroll
+          for (int r = 0; r < 4; ++r) {
+            const float xv = acc[r] + b4[r];
+            h[p][nb][r] = (f16)(a.act ? ym_silu_fast(xv) : xv);
+          }
+        }
+      }
+      for (int nb2 = 0; nb2 < NB2; ++nb2) {
+        f16x4 a2[NBF];
+#pragma unroll
+        for (int nb = 0; nb < NBF; ++nb)
+          if (nb < NB) a2[nb] = *reinterpret_cast<const f16x4*>(w2s + (16 * nb2 + col) * LDW2 + 16 * nb + 4 * g);
+        const int n0 = 16 * nb2 + 4 * g;
+        const f32x4 b4 = *reinterpret_cast<const f32x4*>(bs2 + n0);
+#pragma unroll
+        for (int p = 0; p < PX; ++p) {
+          f32x4 acc = {0.f, 0.f, 0.f, 0.f};
+#pragma unroll
+          for (int nb = 0; nb < NBF; ++nb)
+            if (nb < NB) acc = __builtin_amdgcn_mfma_f32_16x16x16f16(a2[nb], h[p][nb], acc, 0, 0, 0);
+          if (ob[p] < 0 || n0 >= a.N2) continue;
+          float v[4];
+#pragma unroll
+          for (int r = 0; r < 4; ++r) {
+            const float xv = acc[r] + b4[r];
+            v[r] = a.act2 ? ym_silu_fast(xv) : xv;
+          }
+          if (res) {
+            const f16x4 rv = *reinterpret_cast<const f16x4*>(res + (size_t)rb[p] * a.r_ctot + a.r_coff + n0);
+#pragma unroll
+            for (int r = 0; r < 4; ++r) v[r] += (float)rv[r];
+          }
+          OutT* o = dst + (size_t)ob[p] * a.d_ctot + a.d_coff + n0;
+          if constexpr (sizeof(OutT) == 2) *reinterpret_cast<f16x4*>(o) = f16x4{(f16)v[0], (f16)v[1], (f16)v[2], (f16)v[3]};
+          else *reinterpret_cast<f32x4*>(o) = f32x4{v[0], v[1], v[2], v[3]};
+        }
+      }
+    } else
     for (int nb = 0; nb < NP / 16; ++nb) {
       h8 af[KS];
 #pragma unroll
@@ -285,6 +362,7 @@ __global__ __launch_bounds__(256) void conv_small(const ConvArgs a) {
 
 template <typename OutT, int KIND, int KSW, int PXG>
 hipError_t launch_small(const ConvArgs& a, hipStream_t st) {
+  if (a.w2) return hipErrorInvalidValue;  // one 16-channel block per workgroup: no fused pairs
   if (a.k != KIND || a.Kpad > 128 * KSW) return hipErrorInvalidValue;
   const long wgs = (long)((a.M + 16 * PXG - 1) / (16 * PXG)) * ((a.N + 15) / 16);
   hipLaunchKernelGGL((conv_small<OutT, KIND, KSW, PXG>), dim3(wgs), dim3(256), 0, st, a);
@@ -298,9 +376,16 @@ hipError_t launch(const ConvArgs& a, hipStream_t st) {
   long wgs = (G + 4 * PX - 1) / (4 * PX);
   if (wgs > CAP) wgs = CAP;  // the persistent grid: CAP workgroups, the rest streams through them
   const int NP = (a.N + 15) & ~15;
-  const size_t lds = (size_t)NP * (KS * 32 + 8) * sizeof(f16) + (size_t)NP * sizeof(float);
+  size_t lds = (size_t)NP * (KS * 32 + 8) * sizeof(f16) + (size_t)NP * sizeof(float);
   if (lds > kMaxWBytes) return hipErrorInvalidValue;
-  hipLaunchKernelGGL((conv_stream<OutT, KIND, KS, PX>), dim3(wgs), dim3(256), lds, st, a);
+  if (a.w2) {  // fused pair: + W2 [N2P][NP + 4] and bias2 (checked by ym_launch_conv_stream: N <= 128)
+    const int N2P = (a.N2 + 15) & ~15;
+    lds += (size_t)N2P * (NP + 4) * sizeof(f16) + (size_t)N2P * sizeof(float);
+    if (lds > kMaxFusedBytes) return hipErrorInvalidValue;
+    hipLaunchKernelGGL((conv_stream<OutT, KIND, KS, PX, true>), dim3(wgs), dim3(256), lds, st, a);
+  } else {
+    hipLaunchKernelGGL((conv_stream<OutT, KIND, KS, PX, false>), dim3(wgs), dim3(256), lds, st, a);
+  }
   return hipGetLastError();
 }
 
@@ -341,5 +426,6 @@ hipError_t ym_launch_conv_stream(int out_f32, const ConvArgs& a, int i, hipStrea
   }
   if ((a.d_ctot & 3) || (a.d_coff & 3) || (a.res && ((a.r_ctot & 3) || (a.r_coff & 3)))) return hipErrorInvalidValue;
   if (a.s0_coff % 8 || a.s0_ctot % 8) return hipErrorInvalidValue;
+  if (a.w2 && (a.N > kFuseMaxN || (a.N2 & 3) || a.Kpad2 < a.N || (a.Kpad2 & 3) || !a.bias2)) return hipErrorInvalidValue;
   return out_f32 ? dispatch<float>(a, i, st) : dispatch<f16>(a, i, st);
 }

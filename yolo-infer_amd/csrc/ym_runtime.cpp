@@ -274,6 +274,16 @@ int conv_args(ym_ctx* c, const Op& op, int B, const float* d_in, float in_eps, C
       a.w = c->d_weights + (size_t)(uint32_t)r[19];
       a.bias = reinterpret_cast<const float*>(c->d_weights + (size_t)(uint32_t)r[20]);
       a.act = r[5];
+      if (r[30]) {  // fused pair (yolomi/arch.py fuse_pairs): a following 1x1 conv, output in dst/res
+        if (c->dtype != YM_DT_F16) return fail(YM_EBLOB, "op %s: fused conv pairs are f16-only", op.name);
+        a.w2 = c->d_weights + (size_t)(uint32_t)r[25];
+        a.bias2 = reinterpret_cast<const float*>(c->d_weights + (size_t)(uint32_t)r[26]);
+        a.N2 = r[27]; a.act2 = r[28]; a.Kpad2 = r[29];
+        if (a.N2 <= 0 || a.Kpad2 < cout || r[31] < 0 || r[31] >= (int)c->bufs.size() || cout % 8 ||
+            c->buf_H(r[31]) != a.Ho || c->buf_Wd(r[31]) != a.Wo || c->bufs[r[31]].C != cout || c->bufs[r[31]].f32)
+          return fail(YM_EBLOB, "op %s: bad fused-pair geometry", op.name);
+        if (ym_conv_num_cfgs() > 127) return fail(YM_EBLOB, "split cfg encoding needs < 128 conv configs");
+      }
       a.shuffle = r[16];
       a.npr = a.shuffle ? cout / 4 : cout;
       a.dst = c->bptr(bd); a.d_ctot = c->bufs[bd].C; a.d_coff = r[14]; a.d_P = c->buf_P(bd);
@@ -305,6 +315,34 @@ int conv_args(ym_ctx* c, const Op& op, int B, const float* d_in, float in_eps, C
       return YM_OK;
 }
 
+// A fused pair (ConvArgs::w2) run as its two convs: A writes the intermediate buffer (record r[31]), B reads it.
+// The tuner picks this when the two tuned single launches beat every fused variant (op cfg kSplitTag + ...).
+constexpr int kSplitTag = 1 << 20;  // op cfg = kSplitTag + 128 * cfg(A) + cfg(B)
+void split_args(ym_ctx* c, const Op& op, const ConvArgs& a, ConvArgs& A, ConvArgs& Bc) {
+  const int mid = op.r[31];
+  A = a;
+  A.w2 = nullptr; A.bias2 = nullptr; A.res = nullptr;
+  A.dst = c->bptr(mid); A.d_ctot = c->bufs[mid].C; A.d_coff = 0; A.d_P = c->buf_P(mid); A.d_pixoff = 0;
+  A.d_W = c->buf_Wd(mid);
+  Bc = a;
+  Bc.w2 = nullptr; Bc.bias2 = nullptr;
+  Bc.src0 = c->bptr(mid); Bc.s0_ctot = c->bufs[mid].C; Bc.s0_coff = 0; Bc.C0 = a.N; Bc.s0_W = c->buf_Wd(mid);
+  Bc.s0_P = c->buf_P(mid); Bc.up0 = 0;
+  Bc.src1 = nullptr; Bc.C1 = 0; Bc.s1_elems = 0;
+  Bc.Hin = a.Ho; Bc.Win = a.Wo; Bc.k = 1; Bc.s = 1; Bc.pad = 0;
+  Bc.Cin8 = a.N / 8; Bc.Kc = Bc.Cin8; Bc.Kpad = a.Kpad2; Bc.N = a.N2; Bc.npr = a.N2;
+  Bc.w = a.w2; Bc.bias = a.bias2; Bc.act = a.act2;
+  Bc.s0_elems = (long)c->cB * c->buf_P(mid) * c->bufs[mid].C;
+}
+
+hipError_t launch_fused(ym_ctx* c, const Op& op, const ConvArgs& a, int out_f32, int cfg, hipStream_t st) {
+  if (cfg < kSplitTag) return ym_launch_conv(c->dtype, out_f32, a, cfg, st);
+  ConvArgs A, Bc;
+  split_args(c, op, a, A, Bc);
+  const hipError_t e = ym_launch_conv(c->dtype, 0, A, ((cfg - kSplitTag) >> 7) & 127, st);
+  return e != hipSuccess ? e : ym_launch_conv(c->dtype, out_f32, Bc, (cfg - kSplitTag) & 127, st);
+}
+
 int launch_op(ym_ctx* c, const Op& op, int B, const float* d_in, const ym_infer_args* args, float* d_dets,
               int* d_counts, hipStream_t st) {
   const int32_t* r = op.r;
@@ -328,7 +366,9 @@ int launch_op(ym_ctx* c, const Op& op, int B, const float* d_in, const ym_infer_
       int out_f32 = 0;
       const int rc = conv_args(c, op, B, d_in, args->in_eps, a, out_f32);
       if (rc) return rc;
-      e = a.nchw ? ym_launch_stem(dt, a, st) : ym_launch_conv(dt, out_f32, a, c->op_cfg(&op - c->ops.data(), B), st);
+      const int cfg = c->op_cfg(&op - c->ops.data(), B);
+      e = a.nchw ? ym_launch_stem(dt, a, st)
+                 : (a.w2 ? launch_fused(c, op, a, out_f32, cfg, st) : ym_launch_conv(dt, out_f32, a, cfg, st));
       break;
     }
     case OP_DW: {
@@ -849,31 +889,46 @@ int ym_tune(ym_ctx* c, const float* d_in, int B, int H, int W, const ym_infer_ar
     int out_f32 = 0;
     if ((rc = conv_args(c, op, B, d_in, args->in_eps, a, out_f32))) return rc;
     if (a.nchw) continue;  // the stem has its own kernel (csrc/ym_stem.hip)
-    float bt = 1e30f;
-    for (int cf = 0; cf < ncfg; ++cf) {
-      // time `reps` back-to-back launches of this candidate as one graph: device-bound even for tiny kernels
-      hipGraph_t g = nullptr;
-      hipGraphExec_t ge = nullptr;
-      HIPCK(hipStreamBeginCapture(c->cap_stream, hipStreamCaptureModeRelaxed));
-      hipError_t le = hipSuccess;
-      for (int r = 0; r < reps && le == hipSuccess; ++r) le = ym_launch_conv(c->dtype, out_f32, a, cf, c->cap_stream, true);
-      HIPCK(hipStreamEndCapture(c->cap_stream, &g));
-      if (le != hipSuccess) {
+    // best config of one conv launch: time `reps` back-to-back launches of each candidate as one graph
+    // (device-bound even for tiny kernels)
+    auto tune_one = [&](const ConvArgs& ca, int of32, int& bcf) -> float {
+      float bt = 1e30f;
+      bcf = -1;
+      for (int cf = 0; cf < ncfg; ++cf) {
+        hipGraph_t g = nullptr;
+        hipGraphExec_t ge = nullptr;
+        HIPCK(hipStreamBeginCapture(c->cap_stream, hipStreamCaptureModeRelaxed));
+        hipError_t le = hipSuccess;
+        for (int r = 0; r < reps && le == hipSuccess; ++r) le = ym_launch_conv(c->dtype, of32, ca, cf, c->cap_stream, true);
+        HIPCK(hipStreamEndCapture(c->cap_stream, &g));
+        if (le != hipSuccess) {
+          (void)hipGraphDestroy(g);
+          continue;
+        }
+        HIPCK(hipGraphInstantiate(&ge, g, nullptr, nullptr, 0));
+        HIPCK(hipGraphLaunch(ge, st));
+        HIPCK(hipEventRecord(e0, st));
+        HIPCK(hipGraphLaunch(ge, st));
+        HIPCK(hipGraphLaunch(ge, st));
+        HIPCK(hipEventRecord(e1, st));
+        HIPCK(hipEventSynchronize(e1));
+        float ms = 0.f;
+        HIPCK(hipEventElapsedTime(&ms, e0, e1));
+        (void)hipGraphExecDestroy(ge);
         (void)hipGraphDestroy(g);
-        continue;
+        if (ms < bt) { bt = ms; bcf = cf; }
       }
-      HIPCK(hipGraphInstantiate(&ge, g, nullptr, nullptr, 0));
-      HIPCK(hipGraphLaunch(ge, st));
-      HIPCK(hipEventRecord(e0, st));
-      HIPCK(hipGraphLaunch(ge, st));
-      HIPCK(hipGraphLaunch(ge, st));
-      HIPCK(hipEventRecord(e1, st));
-      HIPCK(hipEventSynchronize(e1));
-      float ms = 0.f;
-      HIPCK(hipEventElapsedTime(&ms, e0, e1));
-      (void)hipGraphExecDestroy(ge);
-      (void)hipGraphDestroy(g);
-      if (ms < bt) { bt = ms; best[i] = cf; }
+      return bt;
+    };
+    int cf = -1;
+    const float tf = tune_one(a, out_f32, cf);
+    best[i] = cf;
+    if (a.w2) {  // fused pair: also the two convs as separate tuned launches
+      ConvArgs A, Bc;
+      split_args(c, op, a, A, Bc);
+      int ca = -1, cb = -1;
+      const float ta = tune_one(A, 0, ca), tb = tune_one(Bc, out_f32, cb);
+      if (ca >= 0 && cb >= 0 && ta + tb < tf) best[i] = kSplitTag + 128 * ca + cb;
     }
   }
   (void)hipEventDestroy(e0);
@@ -892,8 +947,12 @@ int ym_get_op_cfg(ym_ctx* c, int B, int H, int W, int* cfg, int n) {
 
 int ym_set_op_cfg(ym_ctx* c, int B, int H, int W, const int* cfg, int n) {
   if (!c || !cfg || n != (int)c->ops.size()) return fail(YM_EINVAL, "cfg array must hold %zu entries", c ? c->ops.size() : 0);
-  for (int i = 0; i < n; ++i)
+  for (int i = 0; i < n; ++i) {
+    if (cfg[i] >= kSplitTag && c->ops[i].r[0] == OP_CONV && c->ops[i].r[30] &&
+        ((cfg[i] - kSplitTag) >> 7) < ym_conv_num_cfgs() && ((cfg[i] - kSplitTag) & 127) < ym_conv_num_cfgs())
+      continue;  // a fused pair run as two launches
     if (cfg[i] >= ym_conv_num_cfgs()) return fail(YM_EINVAL, "cfg[%d] = %d out of range", i, cfg[i]);
+  }
   c->put_cfg(B, H, W, std::vector<int>(cfg, cfg + n));
   c->clear_graphs();
   return YM_OK;

@@ -83,9 +83,12 @@ class Param:
 
 
 class GraphBuilder:
-    def __init__(self, scale: str = "n", task: str = "detect", nc: int = NC, quant: bool = False):
+    def __init__(self, scale: str = "n", task: str = "detect", nc: int = NC, quant: bool = False,
+                 fuse: bool = False):
         """quant=True builds the int8 (PTQ) plan: 16-channel storage granules and materialised concats (a concat is
-        one quantized tensor with its own observer, so the two-source A loader is replaced by requant copies)."""
+        one quantized tensor with its own observer, so the two-source A loader is replaced by requant copies).
+        fuse=True (f16 plans) merges each conv that feeds only a following 1x1 conv into one launch (fuse_pairs)
+        and runs C3k's two 1x1 convs on the same input as one GEMM."""
         if scale not in SCALES:
             raise ValueError(f"Unsupported size: {scale}")
         if task not in ("detect", "segment"):
@@ -96,7 +99,12 @@ class GraphBuilder:
         self.ops: List[Op] = []
         self.params: List[Param] = []
         self.flops_per_pixel: List[Tuple[str, int, int]] = []  # (op name, factor, MACs per output pixel)
+        self.fuse = fuse
         self._build()
+        if fuse:
+            if quant:
+                raise ValueError("fused conv pairs are f16-only (int8 plans requantise every conv output)")
+            self.fuse_pairs()
 
     # ------------------------------------------------------------------ helpers
     def ch(self, c: int) -> int:
@@ -168,10 +176,22 @@ class GraphBuilder:
     def c3k(self, prefix: str, x: View, c: int, dst: View, f: int, n: int = 2):
         c_ = int(c * 0.5)
         cat = self.buf(2 * c_, f, prefix + ".cat", q=prefix + ".cat")
-        t = self.buf(c_, f, prefix + ".t0", q=prefix + ".cv1")
-        self.conv(prefix + ".cv1", x, c_, 1, 1, self.full(t))
-        self.conv(prefix + ".cv2", x, c_, 1, 1, View(cat, c_, c_))
-        cur = self.full(t)
+        if self.fuse:
+            # cv1 ‖ cv2 (both 1x1 on x) as one GEMM with N = 2c_: cv1's output lands in cat[0:c_], which nothing
+            # reads after the first Bottleneck until the last one writes its output there; cv2's in cat[c_:2c_]
+            self._conv_params(prefix + ".cv1", x.C, c_, 1)
+            self._conv_params(prefix + ".cv2", x.C, c_, 1)
+            self.ops.append(Op("conv", dict(k=1, s=1, c1=x.C, c2=2 * c_, act=True, src0=x, up0=False, src1=None,
+                                            dst=self.full(cat), res=None, anchor_level=-1, shuffle2x2=False, bn=True,
+                                            wkey=prefix + ".cv1", wkeys=[prefix + ".cv1", prefix + ".cv2"],
+                                            catq=None), prefix + ".cv1+cv2"))
+            self.flops_per_pixel.append((prefix + ".cv1+cv2", f, x.C * 2 * c_))
+            cur = View(cat, 0, c_)
+        else:
+            t = self.buf(c_, f, prefix + ".t0", q=prefix + ".cv1")
+            self.conv(prefix + ".cv1", x, c_, 1, 1, self.full(t))
+            self.conv(prefix + ".cv2", x, c_, 1, 1, View(cat, c_, c_))
+            cur = self.full(t)
         for j in range(n):
             last = j == n - 1
             nxt = View(cat, 0, c_) if last else self.full(self.buf(c_, f, f"{prefix}.t{j + 1}", q=f"{prefix}.m.{j}"))
@@ -333,6 +353,69 @@ class GraphBuilder:
         self.Detect(23, [L16, L19, L22])
         # the stem reads 3 real channels out of the 8-channel padded input: pad its weights' Cin to 8 at pack time
 
+    # ------------------------------------------------------------------ fused pairs (f16 plans)
+    STREAM_KS = {1: (2, 4, 8), 3: (4, 6, 10, 18)}  # csrc/ym_conv_stream.hip K steps of 32 per kind
+    FUSE_MAX_N = 128                                 # csrc/ym_conv_stream.hip kFuseMaxN
+    FUSE_MAX_LDS = 112 * 1024                        # csrc/ym_conv_stream.hip kMaxFusedBytes
+
+    def _readers(self, buf: Buffer) -> int:
+        n = 0
+        for op in self.ops:
+            a = op.args
+            views = [a.get(k) for k in ("src0", "src1", "res", "src", "qkv")]
+            n += sum(1 for v in views if isinstance(v, View) and v.buf is buf)
+            if op.kind == "sppf" and a["dst"] is buf:
+                n += 1
+        return n
+
+    def fuse_pairs(self):
+        """Merge conv A → 1x1 conv B when B immediately follows A and is the only reader of A's whole output
+        buffer (the Detect/Segment head chains: cv2.l.1 → cv2.l.2, cv3.l.1.1 → cv3.l.2, cv4.l.1 → cv4.l.2).  The
+        fused op runs A's conv, rounds its activated output to fp16 like the stored tensor, and multiplies it by
+        B's weights in the same streaming kernel (csrc/ym_conv_stream.hip FUSE); A's output buffer is never
+        written.  Same arithmetic as the unfused pair up to fp32 summation order in B."""
+        out: List[Op] = []
+        i = 0
+        while i < len(self.ops):
+            op = self.ops[i]
+            nxt = self.ops[i + 1] if i + 1 < len(self.ops) else None
+            if nxt is not None and self._fusable(op, nxt):
+                a, b = op.args, nxt.args
+                args = dict(a)
+                args.update(dst=b["dst"], res=b["res"], anchor_level=b["anchor_level"],
+                            pair=dict(k=1, c1=b["c1"], c2=b["c2"], act=b["act"], bn=b["bn"], wkey=b["wkey"],
+                                      dst=b["dst"], res=b["res"], mid=a["dst"]))
+                out.append(Op("conv", args, f"{op.name}+{nxt.name.rsplit('.', 1)[-1]}"))
+                i += 2
+                continue
+            out.append(op)
+            i += 1
+        self.ops = out
+
+    def _fusable(self, A: Op, B: Op) -> bool:
+        if A.kind != "conv" or B.kind != "conv":
+            return False
+        a, b = A.args, B.args
+        if a.get("pair") or a.get("convT") or a["shuffle2x2"] or a["res"] is not None or a["anchor_level"] >= 0:
+            return False
+        if b["k"] != 1 or b["s"] != 1 or b["src1"] is not None or b["up0"] or b["shuffle2x2"] or b.get("convT"):
+            return False
+        mid = a["dst"]
+        if b["src0"].buf is not mid.buf or mid.coff != 0 or mid.C != mid.buf.C or b["src0"].C != mid.C:
+            return False
+        if self._readers(mid.buf) != 1:
+            return False
+        if a["k"] == 3 and (a["src1"] is not None or a["up0"]):
+            return False
+        N, N2 = a["c2"], b["c2"]
+        kpad = -(-a["k"] * a["k"] * a["c1"] // 64) * 64
+        if N > self.FUSE_MAX_N or N % 4 or N2 % 4 or kpad // 32 not in self.STREAM_KS[a["k"]]:
+            return False
+        NP, N2P = -(-N // 16) * 16, -(-N2 // 16) * 16
+        if NP * (kpad + 8) * 2 + NP * 4 > 80 * 1024:
+            return False
+        return NP * (kpad + 8) * 2 + NP * 4 + N2P * (NP + 4) * 2 + N2P * 4 <= self.FUSE_MAX_LDS
+
     # ------------------------------------------------------------------ accounting
     def op_costs(self, B: int, H: int, W: int, act_bytes: int = 2):
         """Per op (aligned with self.ops): (algorithmic FLOPs, algorithmic HBM bytes) for one forward of B images.
@@ -353,10 +436,15 @@ class GraphBuilder:
                     f1 = a["src1"].buf.f
                     by += B * (H // f1) * (W // f1) * a["src1"].C * act_bytes
                 by += a["k"] * a["k"] * cin * a["c2"] * act_bytes + a["c2"] * 4
+                c_out = a["c2"]
+                if a.get("pair"):  # + the second 1x1 conv; its input (this conv's output) never reaches HBM
+                    c_out = a["pair"]["c2"]
+                    fl += 2 * npx * a["c2"] * c_out
+                    by += a["c2"] * c_out * act_bytes + c_out * 4
                 ob = 4 if a["dst"].buf.f32 else act_bytes
-                by += npx * a["c2"] * ob
+                by += npx * c_out * ob
                 if a["res"] is not None:
-                    by += npx * a["c2"] * act_bytes
+                    by += npx * c_out * act_bytes
             elif op.kind == "dwconv":
                 f = a["src"].buf.f
                 npx = B * (H // f) * (W // f)
@@ -393,6 +481,8 @@ class GraphBuilder:
                 fo = self.out_factor(op)
                 npx = (H // fo) * (W // fo)
                 tot += npx * a["k"] * a["k"] * (a["c1"] if op.name != "model.0" else 3) * a["c2"]
+                if a.get("pair"):
+                    tot += npx * a["c2"] * a["pair"]["c2"]
             elif op.kind == "dwconv":
                 f = a["src"].buf.f
                 tot += (H // f) * (W // f) * 9 * a["C"]

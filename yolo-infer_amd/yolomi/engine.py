@@ -14,7 +14,7 @@ import torch
 
 from .arch import GraphBuilder
 from .lib import Runtime
-from .plan import pack_graph
+from .plan import fuse_default, pack_graph
 
 # Bump when the meaning of a conv config index (csrc/ym_conv.hip kCfgs) changes: stale tables are then ignored.
 TUNE_VERSION = 9
@@ -35,7 +35,7 @@ class Engine:
         self.scale, self.task, self.dtype = scale, task, dtype
         self.device = device
         self.qparams = qparams
-        self.graph = GraphBuilder(scale, task, quant=dtype == "i8")
+        self.graph = GraphBuilder(scale, task, quant=dtype == "i8", fuse=fuse_default(dtype))
         self.blob = blob if blob is not None else pack_graph(self.graph, state_dict, dtype, qparams)
         self.rt = Runtime(device.index if device.index is not None else torch.cuda.current_device(), self.blob)
         self.nm = self.graph.nm

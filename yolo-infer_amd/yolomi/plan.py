@@ -59,6 +59,9 @@ class _WeightArena:
 
 
 def _conv_weights(a: dict, sd: Dict[str, np.ndarray]):
+    if a.get("wkeys"):  # sibling convs on one input merged into one GEMM (arch.py C3k): output channels concatenated
+        parts = [_conv_weights(dict(a, wkeys=None, wkey=k), sd) for k in a["wkeys"]]
+        return np.concatenate([w for w, _ in parts]), np.concatenate([b for _, b in parts])
     key = a["wkey"]
     if a.get("convT"):
         wt = sd[key + ".weight"].astype(np.float32)  # (in, out, 2, 2)
@@ -89,8 +92,14 @@ def _qrec(inv_sc, zc, qlo, qhi, mode, post, inv_so=1.0, zo=0, s_r=0.0, z_r=0, s_
     return head + np.asarray(post, np.float32).tobytes()
 
 
+def fuse_default(dtype: str) -> bool:
+    """Fused conv pairs (GraphBuilder.fuse_pairs) in f16 plans unless YM_FUSE=0."""
+    import os
+    return dtype == "f16" and os.environ.get("YM_FUSE", "1") != "0"
+
+
 def pack_model(scale: str, task: str, sd: Dict[str, np.ndarray], dtype: str = "f16", qparams: Dict = None) -> bytes:
-    g = GraphBuilder(scale, task, quant=dtype == "i8")
+    g = GraphBuilder(scale, task, quant=dtype == "i8", fuse=fuse_default(dtype))
     return pack_graph(g, sd, dtype, qparams)
 
 
@@ -151,6 +160,18 @@ def pack_graph(g: GraphBuilder, sd: Dict[str, np.ndarray], dtype: str = "f16", q
             r[19] = arena.add(wp if quant else wp.astype(np_dt))
             r[20] = arena.add(b.astype(np.float32))
             r[21] = Kpad
+            pair = a.get("pair")
+            if pair is not None:  # fused 1x1 successor (GraphBuilder.fuse_pairs): W2 [N2][Kpad2], K = this conv's N
+                if dtype != "f16":
+                    raise ValueError(f"op {op.name}: fused conv pairs are f16-only")
+                w2, b2 = _conv_weights(pair, sd)  # (N2, 1, 1, N)
+                N2 = w2.shape[0]
+                assert w2.shape[3] == N
+                Kpad2 = (N + BK - 1) // BK * BK
+                w2p = np.zeros((N2, Kpad2), np.float32)
+                w2p[:, :N] = w2.reshape(N2, N)
+                r[25], r[26] = arena.add(w2p.astype(np.float16)), arena.add(b2.astype(np.float32))
+                r[27:32] = [N2, int(bool(pair["act"])), Kpad2, 1, pair["mid"].buf.id]
             if quant:
                 s_in, z_in = qp("act:input" if stem else src0.buf.qkey)
                 so, zo = qp("out:" + a["wkey"])
