@@ -101,6 +101,65 @@ __global__ __launch_bounds__(256) void dwconv3x3(const DwArgs a) {
   }
 }
 
+// Row variant: one thread = 8 channels of PXT consecutive pixels of one row (W % PXT == 0).  The 3 x (PXT + 2)
+// activation window and the 9 x 8 weights are loaded once for PXT outputs: (3 (PXT + 2) + 20) vector loads per
+// PXT pixels instead of 29 per pixel — the single-pixel kernel is bound by load-instruction issue, not bytes.
+// Same fmaf order per output as dwconv3x3 (bias, then taps 0..8): bit-identical results.
+template <typename T, int PXT>
+__global__ __launch_bounds__(256) void dwconv3x3_row(const DwArgs a) {
+  const int C8 = a.C >> 3;
+  const int Wq = a.W / PXT;
+  const int idx = blockIdx.x * blockDim.x + threadIdx.x;
+  const int total = a.B * a.H * Wq * C8;
+  if (idx >= total) return;
+  const int q = idx / C8;
+  const int cg = idx - q * C8;
+  const int row = q / Wq;  // b * H + y
+  const int x0 = (q - row * Wq) * PXT;
+  const int b = row / a.H, y = row - b * a.H;
+  const int c0 = cg * 8;
+  const T* src = static_cast<const T*>(a.src) + (size_t)b * a.s_P * a.s_ctot + a.s_coff + c0;
+  typename Vec8<T>::type v[3][PXT + 2];
+#pragma unroll
+  for (int r = 0; r < 3; ++r) {
+    const int iy = y + r - 1;
+#pragma unroll
+    for (int cc = 0; cc < PXT + 2; ++cc) {
+      const int ix = x0 + cc - 1;
+      v[r][cc] = ((unsigned)iy < (unsigned)a.H && (unsigned)ix < (unsigned)a.W)
+                     ? Vec8<T>::load(src + (size_t)(iy * a.W + ix) * a.s_ctot)
+                     : Vec8<T>::zero();
+    }
+  }
+  f32x4 w[9][2];
+#pragma unroll
+  for (int t = 0; t < 9; ++t) {
+    w[t][0] = *reinterpret_cast<const f32x4*>(a.w + t * a.C + c0);
+    w[t][1] = *reinterpret_cast<const f32x4*>(a.w + t * a.C + c0 + 4);
+  }
+  const f32x4 b0 = *reinterpret_cast<const f32x4*>(a.bias + c0), b1 = *reinterpret_cast<const f32x4*>(a.bias + c0 + 4);
+#pragma unroll
+  for (int px = 0; px < PXT; ++px) {
+    float acc[8] = {b0[0], b0[1], b0[2], b0[3], b1[0], b1[1], b1[2], b1[3]};
+#pragma unroll
+    for (int t = 0; t < 9; ++t)
+#pragma unroll
+      for (int e = 0; e < 8; ++e) acc[e] = fmaf((float)v[t / 3][px + t % 3][e], w[t][e >> 2][e & 3], acc[e]);
+    typename Vec8<T>::type o;
+#pragma unroll
+    for (int e = 0; e < 8; ++e) {
+      const float sv = sizeof(T) == 2 ? ym_silu_fast(acc[e]) : ym_silu(acc[e]);
+      o[e] = (T)(a.act ? sv : acc[e]);
+    }
+    const int p = y * a.W + x0 + px;
+    Vec8<T>::store(static_cast<T*>(a.dst) + (size_t)(b * a.d_P + p) * a.d_ctot + a.d_coff + c0, o);
+    if (a.raw) {
+#pragma unroll
+      for (int e = 0; e < 8; ++e) a.raw[((size_t)b * a.H * a.W + p) * a.C + c0 + e] = acc[e];
+    }
+  }
+}
+
 // ------------------------------------------------------------------------------------------------- SPPF pools
 // y1 = max5(y0), y2 = max5(y1) = max9(y0), y3 = max13(y0) (stride 1, -inf padding: the cascade is exactly the
 // wider window).  Separable: row maxima of radius 2/4/6 in one pass over the 13-wide row window, then column
@@ -851,7 +910,16 @@ hipError_t ym_launch_dwconv(int dtype, const DwArgs& a, hipStream_t st) {
   if (total >= 0x7FFFFFFFL - 256) return hipErrorInvalidValue;  // the kernel indexes in 32 bits
   const dim3 g((total + 255) / 256);
   if (a.C % 8) return hipErrorInvalidValue;
-  if (dtype == YM_DT_F16) hipLaunchKernelGGL(dwconv3x3<f16>, g, dim3(256), 0, st, a);
+  // pixels per thread: 4 where that still leaves >= 128 workgroups (measured best at 80²/160²), else 2 (20²/40²)
+  static const int env_pxt = [] { const char* e = getenv("YM_DW_PXT"); return e ? atoi(e) : 0; }();
+  const int pxt = env_pxt ? env_pxt : (total / 4 >= 128 * 256 ? 4 : 2);
+  if (dtype == YM_DT_F16 && pxt == 4 && a.W % 4 == 0)
+    hipLaunchKernelGGL((dwconv3x3_row<f16, 4>), dim3((total / 4 + 255) / 256), dim3(256), 0, st, a);
+  else if (pxt >= 2 && a.W % 2 == 0 && dtype == YM_DT_F16)
+    hipLaunchKernelGGL((dwconv3x3_row<f16, 2>), dim3((total / 2 + 255) / 256), dim3(256), 0, st, a);
+  else if (pxt >= 2 && a.W % 2 == 0)
+    hipLaunchKernelGGL((dwconv3x3_row<float, 2>), dim3((total / 2 + 255) / 256), dim3(256), 0, st, a);
+  else if (dtype == YM_DT_F16) hipLaunchKernelGGL(dwconv3x3<f16>, g, dim3(256), 0, st, a);
   else hipLaunchKernelGGL(dwconv3x3<float>, g, dim3(256), 0, st, a);
   return hipGetLastError();
 }
