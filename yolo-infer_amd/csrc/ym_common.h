@@ -116,6 +116,16 @@ struct QRec {
 // ------------------------------------------------------------------------------------------------------------
 // Kernel argument blocks (plain structs passed by value).
 
+// XCD-contiguous block order: the dispatcher deals workgroups round-robin over the 8 XCDs (bid % 8), each with its
+// own L2.  Renumber so XCD x runs one contiguous range of logical blocks: neighbouring output tiles (whose 3x3
+// windows share input rows) then read those rows through the same L2 instead of fetching them from HBM once per
+// XCD.  A bijection for any grid size; placement only affects speed, never results.  Used by the stem (yolo11n
+// B=8: 22.7 -> 19.8 us); measured neutral-to-negative on the conv families, whose orders stay as they are.
+__device__ __forceinline__ int ym_xcd_block(int bid, int n) {
+  const int q = n >> 3, r = n & 7, x = bid & 7;
+  return x * q + (x < r ? x : r) + (bid >> 3);
+}
+
 struct ConvArgs {
   const void* src0; int s0_ctot, s0_coff, C0, s0_W, s0_P, up0;  // first A source; up0: read at (y>>1, x>>1)
   const void* src1; int s1_ctot, s1_coff, C1, s1_P;             // optional second A source (concat tail)

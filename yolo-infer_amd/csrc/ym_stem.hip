@@ -30,7 +30,7 @@ __device__ __forceinline__ int clampi(int v, int lo, int hi) { return v < lo ? l
 template <int TH>
 __device__ __forceinline__ void tile_of(const ConvArgs& a, int& b, int& oy0, int& ox0) {
   const int tiles_x = (a.Wo + TW - 1) / TW, tiles_y = (a.Ho + TH - 1) / TH;
-  int bid = blockIdx.x;
+  int bid = ym_xcd_block(blockIdx.x, gridDim.x);  // neighbouring tiles (shared halo lines) on one XCD
   const int tx = bid % tiles_x;
   bid /= tiles_x;
   const int ty = bid % tiles_y;
