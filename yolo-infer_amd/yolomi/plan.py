@@ -14,6 +14,10 @@ s_in·s_w per output channel and the int32 zero-point correction Σ_k (128 - z_i
 
 Blob layout (int32 little-endian; parsed by `csrc/ym_runtime.cpp:ym_load_weights`):
   header[32] | buffers[nbuf][8] | ops[nop][32] | names[nop][48 bytes] | pad to 256 | weights
+Conv op record: [1..5] k, s, Cin, N, act | [6..9] src0 buf, coff, C, up0 | [10..12] src1 | [13..16] dst buf, coff,
+anchor level, pixel shuffle | [17..18] residual | [19..21] weight / bias offsets, Kpad | [22..24] int8 QRec, s_in·s_w,
+int32 bias | [25..31] fused 1x1 successor (f16 plans, GraphBuilder.fuse_pairs): W2 / bias2 offsets, N2, act2, Kpad2,
+flag, intermediate buffer (used when the tuner runs the pair as two launches).
 """
 from __future__ import annotations
 
