@@ -10,7 +10,7 @@ from core.model import YOLO11Model
 m = YOLO11Model(size="n", device="cuda:0", dtype="f16", verbose=False)
 eng = m.model.engine
 x = synthetic_batch(8, 640, 1000, torch.device("cuda", 0))
-for conf in (0.99, 0.5, 0.25, 0.1):
+for conf in [float(c) for c in os.environ.get("NMS_CONFS", "0.99,0.5,0.25,0.1").split(",")]:
     for _ in range(20):
         eng.run(x, conf=conf, use_graph=False)
     torch.cuda.synchronize()

@@ -502,70 +502,117 @@ __global__ __launch_bounds__(256) void attn_psa_mfma(const AttnArgs a) {
 //   sigmoid class scores → (max, first argmax); candidate iff max > conf (and class in the filter).
 // Candidates are appended to a per-image key list: key = score bits << 32 | ~anchor, so a descending sort gives
 // score-descending order with ties broken by ascending anchor index (torchvision's stable sort).
+// DIRECT (reg_max 16, nc 80: the YOLO11 heads): no LDS staging — lane s of an anchor loads its 16 DFL bins and its
+// 20 class logits straight into registers (4 + 5 float4; the 4 lanes of an anchor cover its 576-byte row, so a wave's
+// loads are 9.2 KB contiguous), no barrier before the math, and a small LDS footprint (more workgroups in flight).
+// Same per-element arithmetic in the same order as the staged variant.
+template <bool DIRECT>
 __global__ __launch_bounds__(256) void decode_anchors(const DecodeArgs a) {
-  // the workgroup's 64 anchor rows are contiguous: stage them in LDS with coalesced 16-byte loads
-  extern __shared__ float rows[];  // [64][no_tot + 1]
+  float dist, best;
+  int bi, b, ai, sub;
+  long idx;
+  bool valid;
   const long total = (long)a.B * a.A;
   const long a0 = blockIdx.x * 64L;
-  const int nrow = total - a0 < 64 ? (int)(total - a0) : 64;
-  // LDS rows are padded to an odd pitch (no_tot + 1 floats): the 16 anchors x 4 sides of a wave read 16-float
-  // strided bins, which on a 144-float pitch fell into two banks (32-way conflicts)
-  const int ldr = a.no_tot + 1;
-  {  // every load in flight before the first LDS store (no_tot <= 192: at most 12 per thread)
-    const f32x4* src = reinterpret_cast<const f32x4*>(a.anchors + a0 * a.no_tot);
-    const int n4 = nrow * a.no_tot / 4, r4 = a.no_tot / 4;
-    f32x4 v[12];
+  if constexpr (DIRECT) {
+    const long gidx = a0 + (threadIdx.x >> 2);
+    sub = threadIdx.x & 3;
+    valid = gidx < total;
+    idx = valid ? gidx : 0;
+    b = idx / a.A;
+    ai = idx - (long)b * a.A;
+    const f32x4* row = reinterpret_cast<const f32x4*>(a.anchors + idx * a.no_tot);
+    f32x4 bv[4], cv[5];
 #pragma unroll
-    for (int it = 0; it < 12; ++it) {
-      const int i = threadIdx.x + 256 * it;
-      if (i < n4) v[it] = src[i];
-    }
+    for (int i = 0; i < 4; ++i) bv[i] = row[4 * sub + i];
 #pragma unroll
-    for (int it = 0; it < 12; ++it) {
-      const int i = threadIdx.x + 256 * it;
-      if (i < n4) {
-        const int rr = i / r4, cc = 4 * (i - rr * r4);
-        float* d = rows + rr * ldr + cc;
-        d[0] = v[it][0]; d[1] = v[it][1]; d[2] = v[it][2]; d[3] = v[it][3];
-      }
-    }
-  }
-  __syncthreads();
-  const long gidx = a0 + (threadIdx.x >> 2);
-  const int sub = threadIdx.x & 3;
-  const bool valid = gidx < total;
-  const long idx = valid ? gidx : 0;
-  const int b = idx / a.A;
-  const int ai = idx - (long)b * a.A;
-  const float* row = rows + (valid ? (threadIdx.x >> 2) : 0) * ldr;
-  float dist;
-  {  // DFL: softmax over the bins, expectation of the bin index (one exp per bin, one division)
-    const float* r = row + sub * a.reg_max;
+    for (int i = 0; i < 5; ++i) cv[i] = row[16 + 5 * sub + i];
     float mx = -INFINITY;
-    for (int i = 0; i < a.reg_max; ++i) mx = fmaxf(mx, r[i]);
+#pragma unroll
+    for (int i = 0; i < 16; ++i) mx = fmaxf(mx, bv[i >> 2][i & 3]);
     float den = 0.f, num = 0.f;
-    for (int i = 0; i < a.reg_max; ++i) {
-      const float e = expf(r[i] - mx);
+#pragma unroll
+    for (int i = 0; i < 16; ++i) {
+      const float e = expf(bv[i >> 2][i & 3] - mx);
       den += e;
       num = fmaf(e, (float)i, num);
     }
     dist = num / den;
-  }
-  // class score = max sigmoid, first index on ties (torch max).  Sigmoid is monotonic, so only logits near the
-  // quarter's max can reach its value: those within 0.5 of it while it is < 10 (there sigmoid' > 4e-5, so a logit
-  // 0.5 lower is many ulps lower), every logit otherwise (saturation).
-  const int q = (a.nc + 3) / 4;
-  const float* cl = row + 4 * a.reg_max;
-  const int c0 = sub * q, c1 = (sub + 1) * q < a.nc ? (sub + 1) * q : a.nc;
-  float lmax = -INFINITY;
-  for (int c = c0; c < c1; ++c) lmax = fmaxf(lmax, cl[c]);
-  const float lthr = lmax < 10.0f ? lmax - 0.5f : -INFINITY;
-  float best = -INFINITY;
-  int bi = 0x7FFFFFFF;
-  for (int c = c0; c < c1; ++c) {
-    if (!(cl[c] >= lthr)) continue;
-    const float sc = ym_sigmoid(cl[c]);
-    if (sc > best) { best = sc; bi = c; }
+    float lmax = -INFINITY;
+#pragma unroll
+    for (int c = 0; c < 20; ++c) lmax = fmaxf(lmax, cv[c >> 2][c & 3]);
+    const float lthr = lmax < 10.0f ? lmax - 0.5f : -INFINITY;
+    best = -INFINITY;
+    bi = 0x7FFFFFFF;
+#pragma unroll
+    for (int c = 0; c < 20; ++c) {
+      const float l = cv[c >> 2][c & 3];
+      if (!(l >= lthr)) continue;
+      const float sc = ym_sigmoid(l);
+      if (sc > best) { best = sc; bi = 20 * sub + c; }
+    }
+  } else {
+    // the workgroup's 64 anchor rows are contiguous: stage them in LDS with coalesced 16-byte loads
+    extern __shared__ float rows[];  // [64][no_tot + 1]
+    const int nrow = total - a0 < 64 ? (int)(total - a0) : 64;
+    // LDS rows are padded to an odd pitch (no_tot + 1 floats): the 16 anchors x 4 sides of a wave read 16-float
+    // strided bins, which on a 144-float pitch fell into two banks (32-way conflicts)
+    const int ldr = a.no_tot + 1;
+    {  // every load in flight before the first LDS store (no_tot <= 192: at most 12 per thread)
+      const f32x4* src = reinterpret_cast<const f32x4*>(a.anchors + a0 * a.no_tot);
+      const int n4 = nrow * a.no_tot / 4, r4 = a.no_tot / 4;
+      f32x4 v[12];
+#pragma unroll
+      for (int it = 0; it < 12; ++it) {
+        const int i = threadIdx.x + 256 * it;
+        if (i < n4) v[it] = src[i];
+      }
+#pragma unroll
+      for (int it = 0; it < 12; ++it) {
+        const int i = threadIdx.x + 256 * it;
+        if (i < n4) {
+          const int rr = i / r4, cc = 4 * (i - rr * r4);
+          float* d = rows + rr * ldr + cc;
+          d[0] = v[it][0]; d[1] = v[it][1]; d[2] = v[it][2]; d[3] = v[it][3];
+        }
+      }
+    }
+    __syncthreads();
+    const long gidx = a0 + (threadIdx.x >> 2);
+    sub = threadIdx.x & 3;
+    valid = gidx < total;
+    idx = valid ? gidx : 0;
+    b = idx / a.A;
+    ai = idx - (long)b * a.A;
+    const float* row = rows + (valid ? (threadIdx.x >> 2) : 0) * ldr;
+    {  // DFL: softmax over the bins, expectation of the bin index (one exp per bin, one division)
+      const float* r = row + sub * a.reg_max;
+      float mx = -INFINITY;
+      for (int i = 0; i < a.reg_max; ++i) mx = fmaxf(mx, r[i]);
+      float den = 0.f, num = 0.f;
+      for (int i = 0; i < a.reg_max; ++i) {
+        const float e = expf(r[i] - mx);
+        den += e;
+        num = fmaf(e, (float)i, num);
+      }
+      dist = num / den;
+    }
+    // class score = max sigmoid, first index on ties (torch max).  Sigmoid is monotonic, so only logits near the
+    // quarter's max can reach its value: those within 0.5 of it while it is < 10 (there sigmoid' > 4e-5, so a logit
+    // 0.5 lower is many ulps lower), every logit otherwise (saturation).
+    const int q = (a.nc + 3) / 4;
+    const float* cl = row + 4 * a.reg_max;
+    const int c0 = sub * q, c1 = (sub + 1) * q < a.nc ? (sub + 1) * q : a.nc;
+    float lmax = -INFINITY;
+    for (int c = c0; c < c1; ++c) lmax = fmaxf(lmax, cl[c]);
+    const float lthr = lmax < 10.0f ? lmax - 0.5f : -INFINITY;
+    best = -INFINITY;
+    bi = 0x7FFFFFFF;
+    for (int c = c0; c < c1; ++c) {
+      if (!(cl[c] >= lthr)) continue;
+      const float sc = ym_sigmoid(cl[c]);
+      if (sc > best) { best = sc; bi = c; }
+    }
   }
 #pragma unroll
   for (int o = 1; o < 4; o <<= 1) {
@@ -692,12 +739,14 @@ __global__ __launch_bounds__(NMS_T) void nms_image(const NmsArgs a) {
     }
     int sup = lane >= ne;
     int keep = 0, kept = 0;
+    // candidate i is wave-uniform: v_readlane (a VALU -> SGPR move) instead of ds_bpermute round trips
+    auto rl = [](float v, int i) { return __int_as_float(__builtin_amdgcn_readlane(__float_as_int(v), i)); };
     for (int i = 0; i < ne && kept < a.max_det; ++i) {
-      if (__shfl(sup, i)) continue;
+      if (__builtin_amdgcn_readlane(sup, i)) continue;
       ++kept;
       if (lane == i) keep = 1;
-      const float4 bi = make_float4(__shfl(bx.x, i), __shfl(bx.y, i), __shfl(bx.z, i), __shfl(bx.w, i));
-      const float ai_area = __shfl(ar, i);
+      const float4 bi = make_float4(rl(bx.x, i), rl(bx.y, i), rl(bx.z, i), rl(bx.w, i));
+      const float ai_area = rl(ar, i);
       if (lane > i && !sup && iou_gt(bi, ai_area, bx, ar, a.iou)) sup = 1;
     }
     const unsigned long long km = __ballot(keep);
@@ -748,18 +797,15 @@ __global__ __launch_bounds__(NMS_T) void nms_image(const NmsArgs a) {
       sar[tid] = __fmul_rn(__fsub_rn(o.z, o.x), __fsub_rn(o.w, o.y));
     }
     __syncthreads();
-    for (int pq = tid; pq < ne * W; pq += NMS_T) {
-      const int i = pq / W, w = pq - i * W;
-      unsigned long long bits = 0;
-      if (64 * w + 63 > i) {
-        const float4 bi = sbx[i];
-        const float ai_area = sar[i];
-        for (int jj = 0; jj < 64; ++jj) {
-          const int j = 64 * w + jj;
-          if (j > i && j < ne && iou_gt(bi, ai_area, sbx[j], sar[j], a.iou)) bits |= 1ull << jj;
-        }
+    {  // one IoU per lane: wave item (i, w) has lane l test box j = 64 w + l against row i; the ballot IS word w
+      const int wv = tid >> 6, ln = tid & 63;
+      for (int pq = wv; pq < ne * W; pq += NMS_T / 64) {
+        const int i = pq / W, w = pq - i * W;
+        const int j = 64 * w + ln;
+        const bool s = 64 * w + 63 > i && j > i && j < ne && iou_gt(sbx[i], sar[i], sbx[j], sar[j], a.iou);
+        const unsigned long long bits = __ballot(s);
+        if (ln == 0) mask[pq] = bits;
       }
-      mask[pq] = bits;
     }
     __syncthreads();
     __shared__ int keep_bm[NMS_BM], kept_bm;
@@ -982,7 +1028,11 @@ hipError_t ym_launch_attn(int dtype, const AttnArgs& a, hipStream_t st) {
 hipError_t ym_launch_decode(const DecodeArgs& a, hipStream_t st) {
   const long total = (long)a.B * a.A;
   if (a.no_tot % 4) return hipErrorInvalidValue;
-  hipLaunchKernelGGL(decode_anchors, dim3((total + 63) / 64), dim3(256), (size_t)64 * (a.no_tot + 1) * sizeof(float), st,
+  if (a.reg_max == 16 && a.nc == 80) {
+    hipLaunchKernelGGL(decode_anchors<true>, dim3((total + 63) / 64), dim3(256), 0, st, a);
+    return hipGetLastError();
+  }
+  hipLaunchKernelGGL(decode_anchors<false>, dim3((total + 63) / 64), dim3(256), (size_t)64 * (a.no_tot + 1) * sizeof(float), st,
                      a);
   return hipGetLastError();
 }
