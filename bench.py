@@ -1,24 +1,31 @@
 #!/usr/bin/env python3
 """Headline benchmark: images/s of batched YOLO11 inference at 640x640 on MI355X (+ mAP50-95 vs the CPU oracle).
 
-    python bench.py [--gpus N] [--steps K] [--warmup W] [--model n] [--batch 8] [--size 640] [--dtype f16]
+    python bench.py [--gpus N] [--steps K] [--warmup W] [--model s] [--batch 8] [--size 640] [--dtype f16]
     python -m torch.distributed.run --nproc-per-node N --master-addr 127.0.0.1 bench.py --gpus N
 
-One step = one `YOLO11Model.predict(batch)` call (the reference's timed unit: core/model.py:277-282,
-benchmarks/speed_benchmark.py:330-335) over B=8 synthetic U[0,1) 640x640 images already resident in HBM:
-input /255 rule → yolo11n forward (one HIP-graph replay) → decode → NMS → per-image Results (one D2H sync).
-Multi-GPU: one process per GPU, rank 0 packs the weights once and broadcasts the blob over RCCL (xGMI); each rank
-then runs its own batch shard with no per-step collective ("weak" scaling: 8 images per GPU per step).
+Default workload = BASELINE.json config 3, the one the 1/2/4/8-GPU metric is quoted on: yolo11s detect, 640x640,
+batch 8 per GPU, fp16 (`--model n` gives config 2, `--dtype i8` config 4, `--model s --task segment --batch 4`
+config 5).  One step = one `YOLO11Model.predict(batch)` call (the reference's timed unit: core/model.py:277-282,
+benchmarks/speed_benchmark.py:330-335) over synthetic U[0,1) 640x640 images already resident in HBM: input /255
+rule → forward (one HIP-graph replay) → decode → NMS → per-image Results (one D2H sync).
+Multi-GPU: one process per GPU (`--gpus N` without a launcher spawns the N ranks itself through
+torch.distributed.run, as a child process); rank 0 packs the weights once and broadcasts the blob over RCCL (xGMI,
+yolomi.dist.broadcast_blob); each rank runs its own batch shard; per step the ranks exchange one fp32 (all-reduce MAX:
+LoadTensor's /255 rule over the global batch, yolomi.dist.GlobalBatchMax) — "weak" scaling, 8 images per GPU.
 
 Rank 0 prints ONE JSON line.  Extra fields: `roofline` (conv implicit-GEMM kernels, live HIP-event timing),
-`cpu_baseline` (the oracle on host cores, N=1 only), `accuracy` (mAP50-95 of GPU detections against oracle
-detections as pseudo ground truth, N=1 only), `device_images_per_s` (back-to-back graph replays, no host sync).
+`kernels` (per-kind device time and achieved HBM GB/s of the non-conv kernels), `cpu_baseline` (the oracle on host
+cores, N=1 only, B=1 and B=8 samples), `accuracy` (mAP50-95 of GPU detections against oracle detections as pseudo
+ground truth, N=1 only), `device_images_per_s` (back-to-back graph replays, no host sync).
 """
 from __future__ import annotations
 
 import argparse
 import json
 import os
+import socket
+import subprocess
 import sys
 import time
 
@@ -103,9 +110,66 @@ def conv_roofline(model, x, dtype, workload, reps=20):
     }
 
 
+def pmc_family_bytes(workload):
+    """Per-forward HBM-side bytes of every kernel family in the newest committed PMC summary of this workload."""
+    import glob
+    best = None
+    for p in sorted(glob.glob(os.path.join(ROOT, "profiles", "*_pmc.json"))):
+        try:
+            j = json.load(open(p))
+        except (OSError, ValueError):
+            continue
+        if j.get("workload") == workload.split(",")[0]:
+            best = (p, j)
+    if best is None:
+        return {}, None
+    return {k: v.get("bytes_corrected") for k, v in best[1].get("families", {}).items()}, os.path.relpath(best[0], ROOT)
+
+
+# op kind (yolomi/arch.py) → the rocprof kernel family of tools/rocprof_summary.py
+KIND_FAMILY = {"stem": "stem", "dwconv": "dwconv3x3", "sppf": "sppf", "attn": "attn_psa", "decode": "decode_anchors",
+               "input": "max_reduce", "nms": "nms_image"}
+
+
+def kernel_table(model, x, dtype, workload):
+    """Device time and achieved HBM GB/s of the non-conv kernel families of one forward (pointwise /
+    pooling / decode kernels are judged against HBM, not MFMA).  Times: one eager forward with a HIP event pair
+    around every op on the launch stream (ym_profile), the median of 5; bytes: algorithmic (each input element read
+    once, each output written once, yolomi/arch.py op_costs) and, when a committed PMC summary of this workload
+    exists, the measured HBM-side bytes."""
+    eng = model.model.engine
+    B, _, H, W = x.shape
+    costs = eng.graph.op_costs(B, H, W, ACT_BYTES[dtype])
+    runs = np.array([eng.profile(x) for _ in range(5)])
+    t = np.median(runs, axis=0)
+    pmc, src = pmc_family_bytes(workload)
+    agg = {}
+    for i, op in enumerate(eng.graph.ops):
+        kind = "stem" if op.kind == "conv" and op.args["src0"].buf is eng.graph.input else op.kind
+        if kind not in KIND_FAMILY:
+            continue
+        e = agg.setdefault(kind, {"launches": 0, "us": 0.0, "bytes": 0})
+        e["launches"] += 1
+        e["us"] += float(t[i]) * 1e3
+        e["bytes"] += int(costs[i][1])
+    out = {}
+    for kind, e in agg.items():
+        d = {"launches": e["launches"], "us_per_forward": round(e["us"], 2), "bytes_algorithmic": e["bytes"]}
+        if e["bytes"] and e["us"] > 0:
+            gbs = e["bytes"] / (e["us"] * 1e-6) / 1e9
+            d.update(GBps_algorithmic=round(gbs, 1), hbm_frac=round(gbs / PEAK_HBM_GBS, 4))
+        pb = pmc.get(KIND_FAMILY[kind])
+        if pb and e["us"] > 0:
+            d.update(bytes_pmc=int(pb), GBps_pmc=round(pb / (e["us"] * 1e-6) / 1e9, 1))
+        out[kind] = d
+    return {"timing": "eager forward, HIP event pair per op on the launch stream (ym_profile), median of 5",
+            "peak_GBps": PEAK_HBM_GBS, "pmc_source": src, "by_kind": out}
+
+
 def cpu_baseline(scale, task, x_gpu_dets, xs, seconds, qparams=None):
-    """Oracle (torch CPU fp32, fused; or the int8 oracle of oracle/quant.py for an int8 run) timed on this host; also
-    mAP of the GPU dets against the oracle's dets (and, for int8, against the float oracle's: the quantisation loss)."""
+    """Oracle (torch CPU fp32, fused; or the int8 oracle of oracle/quant.py for an int8 run) timed on this host at
+    B=1 and at B=8 (half the time budget each); also mAP of the GPU dets against the oracle's dets (and, for int8,
+    against the float oracle's: the quantisation loss)."""
     from oracle.predict import OracleModel
     from yolomi.metrics import evaluate
     from yolomi.synth import synth_weights
@@ -116,13 +180,16 @@ def cpu_baseline(scale, task, x_gpu_dets, xs, seconds, qparams=None):
         om = Int8OracleModel(scale, task, synth_weights(scale, task, 0), qparams)
     else:
         om = OracleModel(scale, task, synth_weights(scale, task, 0))
-    x1 = xs[:1].cpu()
-    om.predict(x1)  # warm-up
-    n, t0 = 0, time.perf_counter()
-    while time.perf_counter() - t0 < seconds:
-        om.predict(x1)
-        n += 1
-    dt = time.perf_counter() - t0
+    rates = {}
+    for B in (1, min(8, xs.shape[0])):
+        xb = xs[:B].cpu()
+        om.predict(xb)  # warm-up
+        n, t0 = 0, time.perf_counter()
+        while time.perf_counter() - t0 < seconds / 2:
+            om.predict(xb)
+            n += B
+        dt = time.perf_counter() - t0
+        rates[B] = (n, dt)
     ref = om.predict(xs.cpu())
     gts = [r["boxes"].numpy() for r in ref]
     m = evaluate(x_gpu_dets, gts)
@@ -132,9 +199,14 @@ def cpu_baseline(scale, task, x_gpu_dets, xs, seconds, qparams=None):
     except OSError:
         cpu_name = "unknown"
     what = "int8 oracle (oracle/quant.py: integer convs as exact float64 convs)" if qparams else "oracle"
-    base = {"value": round(n / dt, 3), "unit": "images/s", "cores": nthreads, "kind": "port",
-            "sample": f"{what} predict yolo11{scale} B=1 640x640 U[0,1): {n} images in {dt:.1f}s on {cpu_name} "
-                      f"(os.cpu_count={os.cpu_count()})"}
+    bmax = max(rates)
+    n8, dt8 = rates[bmax]
+    n1, dt1 = rates[1]
+    base = {"value": round(n8 / dt8, 3), "unit": "images/s", "cores": nthreads, "kind": "port",
+            "value_b1": round(n1 / dt1, 3),
+            "sample": f"{what} predict yolo11{scale} {task} 640x640 U[0,1) on {cpu_name} (os.cpu_count="
+                      f"{os.cpu_count()}): B={bmax}: {n8} images in {dt8:.1f}s (value); B=1: {n1} images in "
+                      f"{dt1:.1f}s (value_b1)"}
     acc = {"map50_95": round(m["map"], 4), "map50": round(m["map50"], 4), "images": len(gts),
            "gt": ("int8 oracle (CPU) detections, same qparams, as pseudo ground truth" if qparams else
                   "oracle (CPU fp32) detections as pseudo ground truth"),
@@ -146,36 +218,94 @@ def cpu_baseline(scale, task, x_gpu_dets, xs, seconds, qparams=None):
     return base, acc
 
 
+def _free_port():
+    s = socket.socket()
+    s.bind(("127.0.0.1", 0))
+    p = s.getsockname()[1]
+    s.close()
+    return p
+
+
+def spawn_ranks(n: int) -> int:
+    """`--gpus N` without a launcher: run this script under torch.distributed.run with N ranks (the driver's own
+    form), as a CHILD process — this process has not touched the GPU and is never replaced by exec — and return
+    its exit status."""
+    cmd = [sys.executable, "-m", "torch.distributed.run", "--nnodes=1", f"--nproc-per-node={n}", "--master-addr",
+           "127.0.0.1", "--master-port", str(_free_port()), os.path.abspath(__file__)] + sys.argv[1:]
+    env = dict(os.environ, HSA_ENABLE_IPC_MODE_LEGACY=os.environ.get("HSA_ENABLE_IPC_MODE_LEGACY", "0"))
+    return subprocess.call(cmd, env=env)
+
+
+def plumbing(a, world, rank):
+    """--plumbing: the multi-rank protocol of the bench on CPU (gloo), no GPU: blob broadcast, global batch-max
+    all-reduce per step, barrier + max-over-ranks timing, one JSON line from rank 0 (tests/test_dist.py)."""
+    from yolomi.dist import GlobalBatchMax, broadcast_blob, digest
+    from yolomi.plan import pack_model
+    from yolomi.synth import synth_weights
+    dist.init_process_group("gloo")
+    dev = torch.device("cpu")
+    blob = pack_model(a.model, a.task, synth_weights(a.model, a.task, 0), "f16") if rank == 0 else None
+    blob = broadcast_blob(blob, dev)
+    h = torch.tensor(list(bytes.fromhex(digest(blob))), dtype=torch.uint8)
+    hs = [torch.zeros_like(h) for _ in range(world)]
+    dist.all_gather(hs, h)
+    rule = GlobalBatchMax(device=dev)
+    rule.local_max = lambda x: rule.buf.copy_(x.amax().reshape(1))
+    x = torch.rand(a.batch, 3, 32, 32) * (255.0 if rank == world - 1 else 1.0)
+    for _ in range(a.warmup):
+        rule(x)
+    dist.barrier()
+    t0 = time.perf_counter()
+    for _ in range(a.steps):
+        m = rule(x)
+    dist.barrier()
+    el = torch.tensor([time.perf_counter() - t0], dtype=torch.float64)
+    dist.all_reduce(el, op=dist.ReduceOp.MAX)
+    if rank == 0:
+        print(json.dumps({"metric": METRIC, "plumbing": True, "n_gpus": world, "steps": a.steps, "warmup": a.warmup,
+                          "value": round(world * a.batch * a.steps / float(el.item()), 2), "unit": "images/s",
+                          "blob_bytes": len(blob), "blob_equal_on_all_ranks": all(torch.equal(hs[0], y) for y in hs),
+                          "global_batch_max": float(m.item())}), flush=True)
+    dist.destroy_process_group()
+
+
 def main():
     ap = argparse.ArgumentParser()
     ap.add_argument("--gpus", type=int, default=1)
     ap.add_argument("--steps", type=int, default=200)
     ap.add_argument("--warmup", type=int, default=20)
-    ap.add_argument("--model", default="n")
+    ap.add_argument("--model", default="s", help="scale (default s: BASELINE config 3, the headline workload)")
     ap.add_argument("--task", default="detect")
     ap.add_argument("--batch", type=int, default=8, help="images per GPU per step")
     ap.add_argument("--size", type=int, default=640)
     ap.add_argument("--dtype", default="f16", choices=["f16", "f32", "i8"])
     ap.add_argument("--backend", default="qnnpack", choices=["qnnpack", "fbgemm"], help="i8: PTQ qconfig")
     ap.add_argument("--calib-batches", type=int, default=4, help="i8: calibration batches (B images each)")
-    ap.add_argument("--cpu-seconds", type=float, default=15.0)
+    ap.add_argument("--cpu-seconds", type=float, default=16.0)
     ap.add_argument("--no-cpu", action="store_true")
     ap.add_argument("--no-roofline", action="store_true")
+    ap.add_argument("--plumbing", action="store_true", help="CPU/gloo rehearsal of the multi-rank protocol (no GPU)")
     ap.add_argument("--lanes", type=int, default=int(os.environ.get("YM_LANES", "1")),
                     help="concurrent image slices per forward graph (yolomi lanes)")
     a = ap.parse_args()
 
+    if "WORLD_SIZE" not in os.environ and a.gpus > 1:
+        sys.exit(spawn_ranks(a.gpus))
     world = int(os.environ.get("WORLD_SIZE", "1"))
     rank = int(os.environ.get("RANK", "0"))
     local = int(os.environ.get("LOCAL_RANK", "0"))
-    if world != a.gpus and rank == 0:
-        print(f"[bench] note: --gpus {a.gpus} but WORLD_SIZE={world}; using WORLD_SIZE", file=sys.stderr)
+    if world != a.gpus:
+        print(f"[bench] --gpus {a.gpus} but WORLD_SIZE={world}: refusing to report a mislabelled run", file=sys.stderr)
+        sys.exit(2)
+    if a.plumbing:
+        return plumbing(a, world, rank)
     torch.cuda.set_device(local)
     dev = torch.device("cuda", local)
     if world > 1:
         dist.init_process_group("nccl", device_id=dev)
 
     from core.model import YOLO11Model
+    from yolomi.dist import broadcast_blob, enable_global_rule
     from yolomi.plan import pack_model
     from yolomi.synth import synth_weights
 
@@ -190,19 +320,13 @@ def main():
         qp = calibrate(ce, [synthetic_batch(a.batch, a.size, 500 + i, dev) for i in range(a.calib_batches)],
                        a.backend)
         del ce
-    if rank == 0:
-        blob = pack_model(a.model, a.task, synth_weights(a.model, a.task, 0), a.dtype, qp)
-        nbytes = torch.tensor([len(blob)], dtype=torch.int64, device=dev)
-    else:
-        blob, nbytes = None, torch.zeros(1, dtype=torch.int64, device=dev)
+    blob = pack_model(a.model, a.task, synth_weights(a.model, a.task, 0), a.dtype, qp) if rank == 0 else None
     if world > 1:
-        dist.broadcast(nbytes, 0)
-        buf = (torch.frombuffer(bytearray(blob), dtype=torch.uint8).to(dev) if rank == 0
-               else torch.empty(int(nbytes.item()), dtype=torch.uint8, device=dev))
-        dist.broadcast(buf, 0)
-        blob = bytes(buf.cpu().numpy())
+        blob = broadcast_blob(blob, dev)
     model = YOLO11Model(task=a.task, size=a.model, device=f"cuda:{local}", dtype=a.dtype, weights_blob=blob)
     model.model.engine.lanes = a.lanes
+    if world > 1:  # LoadTensor's /255 rule over the global batch: one fp32 all-reduce per step
+        enable_global_rule(model)
     init_s = time.perf_counter() - t_init
 
     B = a.batch
@@ -240,8 +364,10 @@ def main():
         "warmup": a.warmup, "ms_per_step": round(elapsed / a.steps * 1e3, 4), "higher_is_better": True,
         "scaling": "weak", "vs_baseline": None, "dtype": a.dtype, "data": "synthetic",
         "config": {"workload": f"yolo11{a.model} {a.task} {a.size}x{a.size} batch {B}/GPU {a.dtype}, predict() loop",
+                   "model": f"yolo11{a.model}{'-seg' if a.task == 'segment' else ''}",
                    "batch_per_gpu": B, "global_batch": B * world, "image_size": a.size,
-                   "parallelism": f"dp{world} (batch-sharded, RCCL weight broadcast)"},
+                   "parallelism": f"dp{world} (batch-sharded, RCCL weight broadcast"
+                                  f"{', global /255 rule: 1-float all-reduce per step' if world > 1 else ''})"},
         "device_images_per_s": round(dev_ips * world, 2),
         "init_s": round(init_s, 3),
     }
@@ -250,6 +376,7 @@ def main():
     out["config"]["conv_tiles"] = model.model.engine.tune_source.get((Bl, a.size, a.size), "heuristic")
     if rank == 0 and not a.no_roofline:
         out["roofline"] = conv_roofline(model, x, a.dtype, out["config"]["workload"])
+        out["kernels"] = kernel_table(model, x, a.dtype, out["config"]["workload"])
     if rank == 0 and world == 1 and not a.no_cpu:
         gdets = [r.boxes.data.cpu().numpy() for r in res]
         base, acc = cpu_baseline(a.model, a.task, gdets, x, a.cpu_seconds, qp)

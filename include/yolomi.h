@@ -29,13 +29,31 @@ extern "C" {
 
 typedef struct ym_ctx ym_ctx;
 
-/* Capacity hints (0 = grow on demand). */
+/* What the caller expects the context to run (family / scale / task / dtype / max_B / S).  Capacity
+ * fields are hints (0 = grow on demand); scale, task and dtype, when non-zero, are checked against every blob
+ * ym_load_weights receives (YM_EBLOB on a mismatch) — the reference resolves them from the model name
+ * (core/model.py:37-45, 106-107); here the packed plan carries them. */
 typedef struct {
   int max_batch;
   int max_h;
   int max_w;
-  int reserved[5];
+  int scale;  /* 0 = any, else 'n', 's', 'm', 'l' or 'x' */
+  int task;   /* 0 = any, YM_TASK_DETECT, YM_TASK_SEGMENT */
+  int dtype;  /* 0 = any, YM_DTYPE_F16, YM_DTYPE_F32, YM_DTYPE_I8, YM_DTYPE_F8 */
+  int reserved[2];
 } ym_model_desc;
+
+#define YM_TASK_DETECT 1
+#define YM_TASK_SEGMENT 2
+#define YM_DTYPE_F16 1 /* fp16 storage, fp32 MFMA accumulation (throughput plan) */
+#define YM_DTYPE_F32 2 /* exact-f32 MFMA (parity plan) */
+#define YM_DTYPE_I8 3  /* PTQ int8 (torch.ao qconfig of optimization/quantization/quantizers.py:124-131) */
+#define YM_DTYPE_F8 4  /* PTQ fp8 e4m3 (OCP) operands, fp32 accumulation */
+
+/* An RCCL unique id (ncclUniqueId: 128 opaque bytes). */
+typedef struct {
+  char internal[128];
+} ym_rccl_id;
 
 /* Per-call predict arguments: the Ultralytics predict kwargs that reach the hot path
  * (conf, iou, classes, agnostic_nms, max_det; NMS constants max_nms=30000, max_wh=7680;
@@ -53,7 +71,11 @@ typedef struct {
   int use_graph;       /* 1: capture/replay a HIP graph per (shape, pointers, args); 0: eager launches */
   int lanes;           /* 1..4 image slices run as concurrent graph branches (0 = 1); conv tile tables are looked
                           up at the slice batch ceil(B / lanes) */
-  int reserved[6];
+  int reserved0;
+  const float* d_batch_max; /* NULL: LoadTensor's /255 rule reduces over d_input (the whole batch).  Else a device
+                               pointer to ONE float, the max over the GLOBAL batch (batch-sharded multi-GPU: every
+                               rank's ym_input_max, all-reduced MAX), read by the forward instead of its shard */
+  int reserved[4];
 } ym_infer_args;
 
 /* Replaces `YOLO(model_path)` construction (core/model.py:100-116): create a context on `device`. */
@@ -66,12 +88,29 @@ int ym_load_weights(ym_ctx* ctx, const void* blob, size_t bytes);
  *  yolomi.plan.pack_graph(..., dtype="i8", qparams=...) — the runtime of PostTrainingQuantizer.optimize,
  *  /root/reference/optimization/quantization/quantizers.py:48-91.) */
 
+/* Multi-GPU initialisation (one process per GPU, batch-sharded): replaces the per-process
+ * `YOLO(model_path)` load of core/model.py:100-116 on every rank by ONE load on `root` and an RCCL broadcast over
+ * xGMI.  `comm` is an ncclComm_t of the RCCL library the process has loaded (e.g. from ym_rccl_comm_init).  On
+ * `root` the context must hold weights (ym_load_weights); every other rank's context receives the root's blob and
+ * loads it.  Collective: every rank of `comm` calls it.  Synchronous. */
+int ym_broadcast_weights(ym_ctx* ctx, void* comm, int root, void* stream);
+/* Minimal RCCL bootstrap for C hosts without their own communicator: rank 0 creates the id, the host ships the 128
+ * bytes to the other ranks (any channel), every rank creates its communicator on `device`. */
+int ym_rccl_get_unique_id(ym_rccl_id* id);
+int ym_rccl_comm_init(int device, int nranks, const ym_rccl_id* id, int rank, void** comm);
+int ym_rccl_comm_destroy(void* comm);
+
 /* Replaces `YOLO11Model.predict(tensor)` (core/model.py:118-133) for tensor sources: asynchronous on `stream`
  * (a hipStream_t, NULL = default).  d_input: B×3×H×W fp32 NCHW device tensor (H, W multiples of 32).
  * d_dets: B×max_det×(6+nm) fp32 [x1,y1,x2,y2,conf,cls,(mask coeffs)], rows ordered by NMS keep order;
  * d_counts: B int32 kept counts.  d_dets / d_counts must be device pointers. */
 int ym_infer(ym_ctx* ctx, const float* d_input, int B, int H, int W, const ym_infer_args* args, float* d_dets,
              int* d_counts, void* stream);
+
+/* LoadTensor statistics of a device batch: *d_max = max over the n fp32 elements of d_input (asynchronous on
+ * `stream`).  Each rank of a batch-sharded run computes its shard's max, the ranks all-reduce it (MAX), and pass the
+ * result as ym_infer_args.d_batch_max, so the /255 decision is the whole batch's, as in the reference. */
+int ym_input_max(ym_ctx* ctx, const float* d_input, size_t n, float* d_max, void* stream);
 
 /* PTQ calibration support (f32 plans only): one eager forward in which op i also writes its pre-activation output
  * to d_raw[i] (device pointer or NULL; fp32 row-major (pixels, channels): conv / depthwise ops their conv output, the

@@ -13,6 +13,9 @@ Fixtures (tests/golden/*.json):
   det_n_randn.json      : yolo11n, 1 x N(0,1) 640x640 (seed 2001) → LoadTensor /255 rule, conf 0.25
   det_n_320_lowconf.json: yolo11n, 1 x U[0,1) 320x320 (seed 3001), conf 0.05 (many candidates)
   det_s_uniform.json    : yolo11s, 1 x U[0,1) 640x640 (seed 4001)
+  seg_s_uniform.json    : yolo11s-seg (BASELINE config 5), 4 x U[0,1) 640x640 (seeds 6001-6004), conf 0.25 iou 0.7:
+                          per-image NMS rows with the 32 mask coefficients, proto checksums/samples, and per kept
+                          mask its pixel count and row/column sums (the full 640x640 masks are recomputed live)
   det_n_i8_qnnpack.json : yolo11n PTQ int8 (oracle/quant.py, qnnpack qconfig): calibrated on 2 x U[0,1) 640x640
                           (seeds 5001, 5002); the qparams + int8-oracle detections of 2 other images (5101, 5102)
   det_n_i8_fbgemm_320.json: same with the fbgemm qconfig (per-channel weights, reduce_range), 320x320 (5201 / 5301)
@@ -75,6 +78,33 @@ def det_fixture(scale, kind, seeds, S, conf=0.25, iou=0.7):
     }
 
 
+def seg_fixture(scale, seeds, S, conf=0.25, iou=0.7):
+    from oracle import postprocess as pp
+    sd = synth_weights(scale, "segment", 0)
+    om = OracleModel(scale, "segment", sd)
+    x = make_input("uniform", seeds, S)
+    im, y, ex = om.raw(x)
+    nms = pp.non_max_suppression(y, conf, iou, nc=80)
+    rows = []
+    for d in nms:
+        d = d.clone()
+        d[:, :4] = pp.clip_boxes(d[:, :4], (S, S))
+        rows.append(d.tolist())
+    res = om.predict(x, conf=conf, iou=iou)
+    masks = []
+    for r in res:
+        m = r["masks"]
+        masks.append([] if m is None else [[int(k.sum()), k.sum(1).nonzero().min().item(), k.sum(1).nonzero().max().item(),
+                                            k.sum(0).nonzero().min().item(), k.sum(0).nonzero().max().item()]
+                                           for k in m.to(torch.int64)])
+    return {
+        "scale": scale, "task": "segment", "weights_seed": 0, "input": {"kind": "uniform", "seeds": list(seeds), "size": S},
+        "conf": conf, "iou": iou, "max_det": 300, "proto": layer_stats(ex["proto"].permute(0, 2, 3, 1)),
+        "nms_rows": rows, "dets": [r["boxes"].tolist() for r in res],
+        "masks": masks, "masks_note": "per kept mask: [pixels set, first row, last row, first col, last col]",
+    }
+
+
 def weight_fixture(scale):
     sd = synth_weights(scale, "detect", 0)
     out = {"scale": scale, "seed": 0, "tensors": {}}
@@ -119,6 +149,12 @@ I8_FIXTURES = {
 }
 
 
+def main_seg():
+    d = seg_fixture("s", (6001, 6002, 6003, 6004), 640)
+    json.dump(d, open(os.path.join(HERE, "seg_s_uniform.json"), "w"))
+    print("seg_s_uniform", [len(x) for x in d["dets"]])
+
+
 def main_i8():
     for name, (scale, backend, cs, seeds, S) in I8_FIXTURES.items():
         d = det_i8_fixture(scale, backend, cs, seeds, S)
@@ -143,9 +179,10 @@ def main():
 
 
 if __name__ == "__main__":
-    if len(sys.argv) > 1 and sys.argv[1] == "i8":
+    if len(sys.argv) > 1 and sys.argv[1] in ("i8", "seg"):
         torch.set_num_threads(min(8, os.cpu_count() or 1))
-        main_i8()
+        main_i8() if sys.argv[1] == "i8" else main_seg()
     else:
         main()
+        main_seg()
         main_i8()

@@ -36,6 +36,7 @@ class MatchReport:
     max_dxy: float = 0.0
     max_dscore: float = 0.0
     failures: List[str] = field(default_factory=list)
+    pairs: List[tuple] = field(default_factory=list)  # (ref row, build row) of every match, in the callers' order
 
     @property
     def ok(self) -> bool:
@@ -60,13 +61,16 @@ def _exempt(d: np.ndarray, same: np.ndarray, conf: float, iou_thr: float, conf_m
 
 
 def match_image(ref: np.ndarray, got: np.ndarray, conf: float, iou_thr: float, tol_xy: float, tol_score: float,
-                conf_margin: float = 2e-3, iou_margin: float = 2e-2, rep: MatchReport = None,
+                conf_margin: float = 2e-3, iou_margin: float = 1e-3, rep: MatchReport = None,
                 max_det: int = 300) -> MatchReport:
     """When a list is truncated at max_det, detections scoring within conf_margin of the last kept score are
-    exempt too (which of several near-equal candidates make the cut is an ulp-level decision)."""
+    exempt too (which of several near-equal candidates make the cut is an ulp-level decision).  iou_margin is
+    SURVEY §8(c)'s 1e-3."""
     rep = rep or MatchReport()
-    ref = ref[np.argsort(-ref[:, 4], kind="stable")] if len(ref) else ref.reshape(0, 6)
-    got = got[np.argsort(-got[:, 4], kind="stable")] if len(got) else got.reshape(0, 6)
+    oref = np.argsort(-ref[:, 4], kind="stable") if len(ref) else np.zeros(0, np.int64)
+    ogot = np.argsort(-got[:, 4], kind="stable") if len(got) else np.zeros(0, np.int64)
+    ref = ref[oref] if len(ref) else ref.reshape(0, ref.shape[1] if ref.ndim == 2 else 6)
+    got = got[ogot] if len(got) else got.reshape(0, got.shape[1] if got.ndim == 2 else 6)
     cut = -np.inf
     for d in (ref, got):
         if len(d) >= max_det:
@@ -90,6 +94,7 @@ def match_image(ref: np.ndarray, got: np.ndarray, conf: float, iou_thr: float, t
             if dxy <= tol_xy and ds <= tol_score:
                 used[j] = True
                 rep.matched += 1
+                rep.pairs.append((int(oref[i]), int(ogot[j])))
                 rep.max_dxy = max(rep.max_dxy, dxy)
                 rep.max_dscore = max(rep.max_dscore, ds)
                 ok = True

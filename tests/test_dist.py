@@ -66,3 +66,33 @@ def test_shard_ranges():
         assert max(e - s for s, e in spans) - min(e - s for s, e in spans) <= 1
     with pytest.raises(ValueError):
         shard(8, 2, 2)
+
+
+@pytest.mark.timeout(300)
+def test_bench_spawns_its_own_ranks_plumbing_world2():
+    """`bench.py --gpus 2` without a launcher starts the two ranks itself (torch.distributed.run as a child); the
+    CPU/gloo rehearsal of its protocol reports n_gpus = 2, identical blobs on every rank and the /255 statistic
+    all-reduced over the global batch (only the last rank holds a 0-255 image)."""
+    import json
+    import subprocess
+    import sys
+    root = os.path.dirname(os.path.dirname(os.path.abspath(__file__)))
+    env = {k: v for k, v in os.environ.items() if k not in ("WORLD_SIZE", "RANK", "LOCAL_RANK")}
+    p = subprocess.run([sys.executable, os.path.join(root, "bench.py"), "--gpus", "2", "--plumbing", "--model", "n",
+                        "--steps", "5", "--warmup", "1"], capture_output=True, text=True, timeout=280, env=env)
+    assert p.returncode == 0, p.stderr[-2000:]
+    line = [ln for ln in p.stdout.splitlines() if ln.startswith("{")]
+    assert len(line) == 1, p.stdout
+    d = json.loads(line[0])
+    assert d["n_gpus"] == 2 and d["blob_equal_on_all_ranks"] and d["blob_bytes"] > 1_000_000
+    assert d["global_batch_max"] > 200.0
+
+
+def test_bench_refuses_mislabelled_world():
+    import subprocess
+    import sys
+    root = os.path.dirname(os.path.dirname(os.path.abspath(__file__)))
+    env = dict(os.environ, WORLD_SIZE="1", RANK="0", LOCAL_RANK="0")
+    p = subprocess.run([sys.executable, os.path.join(root, "bench.py"), "--gpus", "2", "--plumbing"],
+                       capture_output=True, text=True, timeout=120, env=env)
+    assert p.returncode == 2 and "WORLD_SIZE=1" in p.stderr

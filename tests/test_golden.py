@@ -45,6 +45,33 @@ def test_oracle_reproduces_golden(name):
 def test_golden_files_are_small_and_complete():
     total = sum(os.path.getsize(os.path.join(GOLD, f)) for f in os.listdir(GOLD))
     assert total < 2_000_000
-    for name in ("det_n_uniform", "det_n_randn", "det_n_320_lowconf", "det_s_uniform"):
+    for name in ("det_n_uniform", "det_n_randn", "det_n_320_lowconf", "det_s_uniform", "seg_s_uniform"):
         g = load(name)
         assert len(g["dets"]) == len(g["input"]["seeds"]) and all(len(d) > 0 for d in g["dets"])
+
+
+def test_oracle_reproduces_segment_golden():
+    """yolo11s-seg B=4 (BASELINE config 5): NMS rows incl. the 32 mask coefficients, proto, and per-mask extents."""
+    from oracle import postprocess as pp
+    g = load("seg_s_uniform")
+    torch.set_num_threads(min(8, os.cpu_count() or 1))
+    om = OracleModel("s", "segment", synth_weights("s", "segment", 0))
+    x = make_input("uniform", g["input"]["seeds"], 640)
+    im, y, ex = om.raw(x)
+    t = ex["proto"].permute(0, 2, 3, 1).double()
+    assert float(t.abs().sum()) == pytest.approx(g["proto"]["abs_sum"], rel=1e-5)
+    np.testing.assert_allclose(t.reshape(-1)[g["proto"]["samples_idx"]].numpy(), g["proto"]["samples"], rtol=1e-4,
+                               atol=1e-5)
+    nms = pp.non_max_suppression(y, g["conf"], g["iou"], nc=80)
+    for d, rows in zip(nms, g["nms_rows"]):
+        d = d.clone()
+        d[:, :4] = pp.clip_boxes(d[:, :4], (640, 640))
+        r = torch.tensor(rows)
+        assert d.shape == r.shape
+        np.testing.assert_allclose(d.numpy(), r.numpy(), rtol=1e-4, atol=1e-4)
+    res = om.predict(x, conf=g["conf"], iou=g["iou"])
+    for rr, ms in zip(res, g["masks"]):
+        got = [[int(k.sum())] for k in rr["masks"].to(torch.int64)]
+        assert len(got) == len(ms)
+        for a, b in zip(got, ms):
+            assert abs(a[0] - b[0]) <= max(2, 1e-3 * b[0])

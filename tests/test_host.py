@@ -239,3 +239,26 @@ def test_fused_pairs(scale, task):
     assert saved == mids + xs  # each intermediate was written and read once, each merged input read once, at 2 B
     with pytest.raises(ValueError):
         GraphBuilder(scale, task, quant=True, fuse=True)
+
+
+def test_checkpoint_architecture_is_inferred_and_mismatches_rejected():
+    """a checkpoint decides the plan (reference YOLO(model_path), core/model.py:100-110); packing a
+    state dict into a graph of another scale or class count fails loudly instead of writing past buffers."""
+    from yolomi.arch import infer_arch
+    from yolomi.plan import pack_graph
+    sd_s = synth_weights("s", "detect", 0)
+    assert infer_arch(sd_s) == ("s", "detect", 80)
+    assert infer_arch(synth_weights("n", "segment", 0)) == ("n", "segment", 80)
+    with pytest.raises(ValueError, match="shape"):
+        pack_graph(GraphBuilder("n", "detect"), sd_s, "f16")
+    # a 20-class checkpoint: the cls branch width c3 = max(ch0, min(nc, 100)) changes with nc too
+    rng = np.random.default_rng(0)
+    g20 = GraphBuilder("n", "detect", nc=20)
+    sd20 = {p.name: (rng.standard_normal(p.shape).astype(np.float32) * 0.1 if p.kind not in ("bn_var", "count")
+                     else np.ones(p.shape, np.float32)) for p in g20.params}
+    assert infer_arch(sd20) == ("n", "detect", 20)
+    pack_graph(g20, sd20, "f16")
+    with pytest.raises(ValueError, match="shape"):
+        pack_graph(GraphBuilder("n", "detect"), sd20, "f16")
+    blob = pack_model("s", "detect", sd_s, "f16")
+    assert struct.unpack("<32i", blob[:128])[19] == ord("s")  # ym_model_desc.scale is checked against this

@@ -120,6 +120,8 @@ class YOLO11Model:
         self._qparams = qparams
         self._sd = state_dict
         self.optimization_history: List[Dict[str, Any]] = []
+        # batch-sharded multi-GPU (yolomi.dist.enable_global_rule): callable x -> (1,) device max of the GLOBAL batch
+        self.global_batch_max = None
         self._validate_inputs()
         self.model = self._load_model()
         self.original_model = None
@@ -152,11 +154,20 @@ class YOLO11Model:
                 sd = _load_state_dict(Path(self.model_path))
             else:  # the reference fetches yolo11{size}.pt by name; offline we synthesise weights of that graph
                 sd = synth_weights(self.size, self.task, self.seed)
-            engine = Engine(self.size, self.task, sd, dev, self.dtype, blob=self._blob, qparams=self._qparams)
+            nc = 80
+            if sd and self._blob is None:  # the checkpoint decides the architecture, as YOLO(model_path) does
+                from yolomi.arch import infer_arch
+                scale, task, nc = infer_arch(sd)
+                if (scale, task) != (self.size, self.task):
+                    logger.warning(f"{self.model_path or 'state_dict'} holds a yolo11{scale} {task} model "
+                                   f"(nc={nc}); using it instead of size={self.size!r} task={self.task!r}")
+                    self.size, self.task = scale, task
+            engine = Engine(self.size, self.task, sd, dev, self.dtype, blob=self._blob, qparams=self._qparams, nc=nc)
+            names = COCO_NAMES if nc == 80 else {i: f"class{i}" for i in range(nc)}
         except Exception as e:
             logger.error(f"Failed to load model: {e}")
             raise
-        return _ModelHandle(sd, engine, COCO_NAMES)
+        return _ModelHandle(sd, engine, names)
 
     # ------------------------------------------------------------------ hot path
     def _as_batch(self, source, imgsz: int = 640):
@@ -197,8 +208,9 @@ class YOLO11Model:
         im, eps, imsrc = self._as_batch(source, int(kwargs.get("imgsz", 640)))
         t1 = time.perf_counter()
         eng = self.model.engine
+        bm = self.global_batch_max(im) if self.global_batch_max is not None and imsrc is None else None
         dets, counts = eng.run(im, conf=conf, iou=iou, max_det=max_det, classes=classes, agnostic=agnostic,
-                               in_eps=eps)
+                               in_eps=eps, batch_max=bm)
         B = im.shape[0]
         out = dets[:B].clone()
         n = counts[:B].tolist()  # the device→host sync of a predict call

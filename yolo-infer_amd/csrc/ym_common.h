@@ -215,6 +215,7 @@ struct PrepArgs {
   int* cnt; int cnt_len;       // split-K arrival counters, zeroed at the start of every forward
   int B, C, H, W;
   float eps;                   // LoadTensor rule: /255 when max > 1 + eps
+  const float* batch_max;      // non-null: the (global) batch max is given, skip the reduction
 };
 
 struct MaskArgs {
@@ -235,6 +236,7 @@ hipError_t ym_launch_dwconv(int dtype, const DwArgs& a, hipStream_t st);
 hipError_t ym_launch_sppf(int dtype, const PoolArgs& a, hipStream_t st);
 hipError_t ym_launch_attn(int dtype, const AttnArgs& a, hipStream_t st);
 hipError_t ym_launch_prep(int dtype, const PrepArgs& a, int* counts, int B, hipStream_t st);
+hipError_t ym_launch_input_max(const float* x, long n, float* ctl, float* out, hipStream_t st);
 hipError_t ym_launch_decode(const DecodeArgs& a, hipStream_t st);
 hipError_t ym_launch_nms(const NmsArgs& a, hipStream_t st);
 hipError_t ym_launch_stem(int dtype, const ConvArgs& a, hipStream_t st);

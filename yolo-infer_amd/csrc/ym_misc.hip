@@ -49,6 +49,20 @@ __global__ __launch_bounds__(256) void max_reduce(const float* __restrict__ x, l
   }
 }
 
+// The batch-sharded multi-GPU path: LoadTensor's rule is over the GLOBAL batch, whose max the ranks agree on with
+// one all-reduce (yolomi/dist.py); the forward then takes its /255 decision from that float instead of its shard.
+__global__ void ctl_from_max(float* ctl, const float* m) {
+  const int t = threadIdx.x;
+  if (t < YM_CTL_SLOTS) reinterpret_cast<int*>(ctl)[t * YM_CTL_STRIDE] = t == 0 ? f2ord(*m) : f2ord(-INFINITY);
+}
+__global__ void ctl_reset(float* ctl) {
+  const int t = threadIdx.x;
+  if (t < YM_CTL_SLOTS) reinterpret_cast<int*>(ctl)[t * YM_CTL_STRIDE] = f2ord(-INFINITY);
+}
+__global__ void ctl_to_max(const float* ctl, float* out) {
+  if (threadIdx.x == 0) *out = ym_input_max(ctl);
+}
+
 // ------------------------------------------------------------------------------------------------- depthwise 3x3
 // DWConv(c, c, 3) = Conv(g=c): 3x3, stride 1, pad 1, BN folded, SiLU.  One thread = 8 channels of one pixel.
 // Every load a thread needs (9 taps x 16 B of activations, 9 x 2 float4 of weights + 2 of bias, the weights L1/L2-
@@ -941,12 +955,26 @@ hipError_t ym_launch_prep(int dtype, const PrepArgs& a, int* counts, int B, hipS
   const int ib = (a.cnt_len / 4 + 255) / 256;
   hipLaunchKernelGGL(init_ctl, dim3(ib < 1 ? 1 : (ib > 64 ? 64 : ib)), dim3(256), 0, st, a.ctl, counts, B, a.cnt,
                      a.cnt_len);
+  if (a.batch_max) {  // the global batch max is given (multi-GPU shard): no reduction over this rank's images
+    hipLaunchKernelGGL(ctl_from_max, dim3(1), dim3(64), 0, st, a.ctl, a.batch_max);
+    return hipGetLastError();
+  }
   // one atomic per block: a few hundred same-address atomics, not thousands (one word takes ~90 per us)
   const long n = (long)a.B * a.C * a.H * a.W;
   long blocks = (n / 4 + 255) / 256;
   if (blocks > 2048) blocks = 2048;
   if (blocks < 1) blocks = 1;
   hipLaunchKernelGGL(max_reduce, dim3(blocks), dim3(256), 0, st, a.in, n, a.ctl);
+  return hipGetLastError();
+}
+
+hipError_t ym_launch_input_max(const float* x, long n, float* ctl, float* out, hipStream_t st) {
+  hipLaunchKernelGGL(ctl_reset, dim3(1), dim3(64), 0, st, ctl);
+  long blocks = (n / 4 + 255) / 256;
+  if (blocks > 2048) blocks = 2048;
+  if (blocks < 1) blocks = 1;
+  hipLaunchKernelGGL(max_reduce, dim3(blocks), dim3(256), 0, st, x, n, ctl);
+  hipLaunchKernelGGL(ctl_to_max, dim3(1), dim3(64), 0, st, ctl, out);
   return hipGetLastError();
 }
 

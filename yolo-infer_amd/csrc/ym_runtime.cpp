@@ -5,6 +5,8 @@
 // (input /255 rule → 80+ fused conv launches → attention → decode → NMS), so the Python host issues one call.
 #include <hip/hip_runtime.h>
 
+#include <dlfcn.h>
+
 #include <algorithm>
 #include <cstdarg>
 #include <cstdio>
@@ -78,10 +80,12 @@ struct ym_ctx {
   int strides[4] = {8, 16, 32, 0};
   int input_buf = -1, anchor_buf = -1, proto_buf = -1, no = 0;
   float* d_lowres = nullptr;  // Segment mask assembly scratch (ym_masks)
+  char* d_misc = nullptr;     // ym_input_max statistics slots
   size_t lowres_bytes = 0;
   std::vector<BufDesc> bufs;
   std::vector<Op> ops;
   char* d_weights = nullptr;
+  std::vector<char> blob_host;  // the loaded blob as received (what ym_broadcast_weights sends from the root)
   size_t off_wstem = 0;  // stem weights re-laid out as fp32 [27][N] behind the blob's weights (ym_stem.hip)
   // branch schedule of a one-lane forward (ops of independent DAG branches on up to kMaxLanes streams)
   int nbr = 1;
@@ -140,6 +144,7 @@ struct ym_ctx {
     if (d_arena) (void)hipFree(d_arena);
     if (d_weights) (void)hipFree(d_weights);
     if (d_lowres) (void)hipFree(d_lowres);
+    if (d_misc) (void)hipFree(d_misc);
     if (cap_stream) (void)hipStreamDestroy(cap_stream);
     for (int l = 0; l < kMaxLanes; ++l) {
       if (lane_streams[l]) (void)hipStreamDestroy(lane_streams[l]);
@@ -356,6 +361,7 @@ int launch_op(ym_ctx* c, const Op& op, int B, const float* d_in, const ym_infer_
       a.ctl = reinterpret_cast<float*>(c->d_arena + c->off_ctl);
       a.B = B; a.C = 3; a.H = c->cH; a.W = c->cW;
       a.eps = args->in_eps;
+      a.batch_max = args->d_batch_max;
       a.cnt = reinterpret_cast<int*>(c->d_arena + c->off_cnt);
       a.cnt_len = kMaxLanes * kSplitCounters;
       e = ym_launch_prep(dt, a, reinterpret_cast<int*>(c->d_arena + c->off_counts), B, st);
@@ -595,37 +601,113 @@ static void build_schedule(ym_ctx* c) {
   c->nbr = used;
 }
 
+// Structural check of a parsed plan before it is committed to a context: buffer ids of every op record in range,
+// every weight / bias / quantisation record inside the weight section.  The kernels index device memory with these
+// values, so a malformed blob must fail here (YM_EBLOB), never inside a launch.
+static int validate_plan(const std::vector<BufDesc>& bufs, const std::vector<Op>& ops, int dtype, size_t wbytes) {
+  const int nbuf = (int)bufs.size();
+  for (int i = 0; i < nbuf; ++i)
+    if (bufs[i].C <= 0 || bufs[i].C > (1 << 16) || bufs[i].f < 0 || bufs[i].f > 64)
+      return fail(YM_EBLOB, "buffer %d: bad geometry (C %d, f %d)", i, bufs[i].C, bufs[i].f);
+  const size_t esz = dtype == YM_DT_F32 ? 4 : (dtype == YM_DT_F16 ? 2 : 1);
+  for (const Op& o : ops) {
+    const int32_t* r = o.r;
+    auto buf_ok = [&](int b, bool opt) { return (opt && b == -1) || (b >= 0 && b < nbuf); };
+    auto w_ok = [&](int32_t off, size_t n) { return (size_t)(uint32_t)off + n <= wbytes; };
+    bool ok = true;
+    const size_t qrec = sizeof(QRec);
+    switch (r[0]) {
+      case OP_INPUT: case OP_DECODE: case OP_NMS: break;
+      case OP_CONV: {
+        const int N = r[4], Kpad = r[21];
+        ok = N > 0 && Kpad > 0 && Kpad <= (1 << 16) && buf_ok(r[6], false) && buf_ok(r[10], true) &&
+             buf_ok(r[13], false) && buf_ok(r[17], true) && w_ok(r[19], (size_t)N * Kpad * esz) &&
+             w_ok(r[20], (size_t)N * 4);
+        if (ok && dtype == YM_DT_I8) ok = w_ok(r[22], qrec) && w_ok(r[23], (size_t)N * 4) && w_ok(r[24], (size_t)N * 4);
+        if (ok && r[30]) {
+          const int N2 = r[27], K2 = r[29];
+          ok = N2 > 0 && K2 > 0 && K2 <= (1 << 16) && buf_ok(r[31], false) && w_ok(r[25], (size_t)N2 * K2 * 2) &&
+               w_ok(r[26], (size_t)N2 * 4);
+        }
+        break;
+      }
+      case OP_DW: case OP_ATTN: {
+        const int C = r[3];
+        ok = C > 0 && buf_ok(r[6], false) && buf_ok(r[13], false) &&
+             w_ok(r[19], (size_t)9 * C * (dtype == YM_DT_I8 ? 1 : 4)) && w_ok(r[20], (size_t)C * 4);
+        if (ok && dtype == YM_DT_I8) ok = w_ok(r[22], qrec) && w_ok(r[23], (size_t)C * 4);
+        break;
+      }
+      case OP_SPPF: ok = r[3] > 0 && buf_ok(r[13], false); break;
+      case OP_REQ: ok = r[3] > 0 && buf_ok(r[6], false) && buf_ok(r[13], false) && w_ok(r[22], qrec); break;
+      default: return fail(YM_EBLOB, "op %s: unknown op kind %d", o.name, r[0]);
+    }
+    if (!ok) return fail(YM_EBLOB, "op %s: buffer id or weight range out of bounds", o.name);
+  }
+  return YM_OK;
+}
+
 int ym_load_weights(ym_ctx* c, const void* blob, size_t bytes) {
   if (!c || !blob) return fail(YM_EINVAL, "null argument");
   HIPCK(hipSetDevice(c->device));
   const int32_t* h = static_cast<const int32_t*>(blob);
   if (bytes < kHdr * 4 || h[0] != kMagic || h[1] != 1) return fail(YM_EBLOB, "bad blob magic/version");
+  // everything is parsed into locals and validated; the context changes only once the whole blob checks out
   const int nbuf = h[11], nop = h[12];
+  if (nbuf < 1 || nbuf > 4096 || nop < 1 || nop > 4096) return fail(YM_EBLOB, "bad buffer/op counts (%d, %d)", nbuf, nop);
   const size_t wbytes = (size_t)(uint32_t)h[13] | ((size_t)(uint32_t)h[14] << 32);
   const size_t need = (size_t)kHdr * 4 + (size_t)nbuf * kBufRec * 4 + (size_t)nop * (kOpRec * 4 + kNameLen);
   const size_t woff = align_up(need, 256);
-  if (bytes < woff + wbytes) return fail(YM_EBLOB, "blob truncated (%zu < %zu)", bytes, woff + wbytes);
-  c->dtype = h[2];
-  if (c->dtype != YM_DT_F16 && c->dtype != YM_DT_F32 && c->dtype != YM_DT_I8)
-    return fail(YM_EBLOB, "unknown dtype %d", c->dtype);
-  c->task = h[3]; c->nc = h[4]; c->nm = h[5]; c->reg_max = h[6]; c->nl = h[7];
-  if (c->nl < 1 || c->nl > 4) return fail(YM_EBLOB, "bad level count");
-  for (int l = 0; l < c->nl; ++l) c->strides[l] = h[8 + l];
-  c->input_buf = h[15]; c->anchor_buf = h[16]; c->proto_buf = h[17]; c->no = h[18];
-  if (c->task == 1 && (c->proto_buf < 0 || c->proto_buf >= nbuf)) return fail(YM_EBLOB, "segment plan without proto buffer");
+  if (wbytes > bytes || bytes < woff + wbytes) return fail(YM_EBLOB, "blob truncated (%zu < %zu)", bytes, woff + wbytes);
+  const int dtype = h[2];
+  if (dtype != YM_DT_F16 && dtype != YM_DT_F32 && dtype != YM_DT_I8) return fail(YM_EBLOB, "unknown dtype %d", dtype);
+  const int task = h[3], nc = h[4], nm = h[5], reg_max = h[6], nl = h[7];
+  if (nl < 1 || nl > 4) return fail(YM_EBLOB, "bad level count");
+  if (nc < 1 || nc > 128 || nm < 0 || nm > 64 || reg_max < 1 || reg_max > 64)
+    return fail(YM_EBLOB, "bad head geometry (nc %d, nm %d, reg_max %d)", nc, nm, reg_max);
+  for (int l = 0; l < nl; ++l)
+    if (h[8 + l] < 1 || h[8 + l] > 64) return fail(YM_EBLOB, "bad stride %d", h[8 + l]);
+  const ym_model_desc& want = c->desc;  // what the creator expects (0 = any)
+  if (want.task && want.task != task + 1)
+    return fail(YM_EBLOB, "blob task %s, context created for %s", task ? "segment" : "detect",
+                want.task == YM_TASK_SEGMENT ? "segment" : "detect");
+  if (want.dtype && want.dtype != dtype + 1) return fail(YM_EBLOB, "blob dtype %d, context created for %d", dtype + 1, want.dtype);
+  if (want.scale && h[19] && want.scale != h[19])
+    return fail(YM_EBLOB, "blob scale '%c', context created for '%c'", (char)h[19], (char)want.scale);
+  const int input_buf = h[15], anchor_buf = h[16], proto_buf = h[17];
+  if (input_buf < 0 || input_buf >= nbuf || anchor_buf < 0 || anchor_buf >= nbuf)
+    return fail(YM_EBLOB, "bad input/anchor buffer ids");
+  if (task == 1 && (proto_buf < 0 || proto_buf >= nbuf)) return fail(YM_EBLOB, "segment plan without proto buffer");
   const int32_t* bp = h + kHdr;
-  c->bufs.resize(nbuf);
-  for (int i = 0; i < nbuf; ++i) c->bufs[i] = BufDesc{bp[i * kBufRec], bp[i * kBufRec + 1], bp[i * kBufRec + 2]};
+  std::vector<BufDesc> bufs(nbuf);
+  for (int i = 0; i < nbuf; ++i) bufs[i] = BufDesc{bp[i * kBufRec], bp[i * kBufRec + 1], bp[i * kBufRec + 2]};
   const int32_t* op = bp + (size_t)nbuf * kBufRec;
   const char* names = reinterpret_cast<const char*>(op + (size_t)nop * kOpRec);
-  c->ops.resize(nop);
+  std::vector<Op> ops(nop);
   for (int i = 0; i < nop; ++i) {
-    memcpy(c->ops[i].r, op + (size_t)i * kOpRec, kOpRec * 4);
-    memcpy(c->ops[i].name, names + (size_t)i * kNameLen, kNameLen);
-    c->ops[i].name[kNameLen - 1] = 0;
+    memcpy(ops[i].r, op + (size_t)i * kOpRec, kOpRec * 4);
+    memcpy(ops[i].name, names + (size_t)i * kNameLen, kNameLen);
+    ops[i].name[kNameLen - 1] = 0;
   }
-  if (c->input_buf < 0 || c->input_buf >= nbuf || c->anchor_buf < 0 || c->anchor_buf >= nbuf)
-    return fail(YM_EBLOB, "bad input/anchor buffer ids");
+  int rc = validate_plan(bufs, ops, dtype, wbytes);
+  if (rc) return rc;
+  // commit: a reload drops the previous plan's workspace, graphs and per-shape tile tables (they index its ops and
+  // buffers); the weights are replaced below
+  c->loaded = false;
+  c->clear_graphs();
+  if (c->d_arena) HIPCK(hipFree(c->d_arena));
+  c->d_arena = nullptr;
+  c->arena_bytes = 0;
+  c->cB = c->cH = c->cW = 0;
+  c->buf_off.clear();
+  c->cfgs.clear();
+  c->dtype = dtype;
+  c->task = task; c->nc = nc; c->nm = nm; c->reg_max = reg_max; c->nl = nl;
+  for (int l = 0; l < nl; ++l) c->strides[l] = h[8 + l];
+  c->input_buf = input_buf; c->anchor_buf = anchor_buf; c->proto_buf = proto_buf; c->no = h[18];
+  c->bufs = std::move(bufs);
+  c->ops = std::move(ops);
+  c->blob_host.assign(static_cast<const char*>(blob), static_cast<const char*>(blob) + bytes);  // ym_broadcast_weights
   build_schedule(c);
   while (c->op_ev.size() < c->ops.size()) {
     hipEvent_t ev;
@@ -769,6 +851,16 @@ int ym_infer(ym_ctx* c, const float* d_in, int B, int H, int W, const ym_infer_a
   HIPCK(hipGraphInstantiate(&ge.exec, ge.graph, nullptr, nullptr, 0));
   c->graphs.push_back(ge);
   HIPCK(hipGraphLaunch(ge.exec, st));
+  return YM_OK;
+}
+
+int ym_input_max(ym_ctx* c, const float* d_in, size_t n, float* d_max, void* stream) {
+  if (!c || !d_in || !d_max || n == 0) return fail(YM_EINVAL, "bad ym_input_max arguments");
+  HIPCK(hipSetDevice(c->device));
+  if (!c->d_misc) HIPCK(hipMalloc(&c->d_misc, 4096));
+  const hipError_t e = ym_launch_input_max(d_in, (long)n, reinterpret_cast<float*>(c->d_misc), d_max,
+                                           static_cast<hipStream_t>(stream));
+  if (e != hipSuccess) return fail(YM_EHIP, "input max: %s", hipGetErrorString(e));
   return YM_OK;
 }
 
@@ -1040,6 +1132,132 @@ int ym_masks(ym_ctx* c, const float* d_dets, int B, int max_det, const int* d_of
   const hipError_t e = ym_launch_masks(a, static_cast<hipStream_t>(stream));
   if (e != hipSuccess) return fail(YM_EHIP, "mask kernels: %s", hipGetErrorString(e));
   return YM_OK;
+}
+
+// ---------------------------------------------------------------------------------------------- RCCL (xGMI)
+// The init-time weight broadcast of the batch-sharded multi-GPU path: RCCL is resolved at run time
+// (dlopen of the process's already-loaded librccl — torch's, when the host is Python — else the ROCm one), so
+// libyolomi.so itself has no link-time dependency on it.  Only the four entry points below are used.
+namespace {
+struct Rccl {
+  typedef int (*GetUniqueId)(void*);
+  typedef int (*CommInitRank)(void**, int, ym_rccl_id, int);
+  typedef int (*CommDestroy)(void*);
+  typedef int (*CommUserRank)(void*, int*);
+  typedef int (*CommCount)(void*, int*);
+  typedef int (*Broadcast)(const void*, void*, size_t, int, int, void*, hipStream_t);
+  typedef const char* (*ErrStr)(int);
+  GetUniqueId get_id = nullptr;
+  CommInitRank init = nullptr;
+  CommDestroy destroy = nullptr;
+  CommUserRank user_rank = nullptr;
+  CommCount count = nullptr;
+  Broadcast bcast = nullptr;
+  ErrStr err = nullptr;
+  bool ok = false;
+};
+
+const Rccl* rccl() {
+  static Rccl r = [] {
+    Rccl x;
+    void* h = nullptr;
+    for (const char* n : {"librccl.so.1", "librccl.so"})
+      if (!h) h = dlopen(n, RTLD_NOW | RTLD_NOLOAD);
+    for (const char* n : {"librccl.so.1", "librccl.so", "/opt/rocm/lib/librccl.so.1"})
+      if (!h) h = dlopen(n, RTLD_NOW | RTLD_LOCAL);
+    if (!h) return x;
+    x.get_id = (Rccl::GetUniqueId)dlsym(h, "ncclGetUniqueId");
+    x.init = (Rccl::CommInitRank)dlsym(h, "ncclCommInitRank");
+    x.destroy = (Rccl::CommDestroy)dlsym(h, "ncclCommDestroy");
+    x.user_rank = (Rccl::CommUserRank)dlsym(h, "ncclCommUserRank");
+    x.count = (Rccl::CommCount)dlsym(h, "ncclCommCount");
+    x.bcast = (Rccl::Broadcast)dlsym(h, "ncclBroadcast");
+    x.err = (Rccl::ErrStr)dlsym(h, "ncclGetErrorString");
+    x.ok = x.get_id && x.init && x.destroy && x.user_rank && x.count && x.bcast && x.err;
+    return x;
+  }();
+  return r.ok ? &r : nullptr;
+}
+
+#define RCCLCK(x)                                                                                       \
+  do {                                                                                                  \
+    const int r_ = (x);                                                                                 \
+    if (r_ != 0) return fail(YM_EHIP, "%s: RCCL error %d (%s)", #x, r_, R->err ? R->err(r_) : "?");     \
+  } while (0)
+constexpr int kNcclUint8 = 1;  // ncclDataType_t ncclUint8
+}  // namespace
+
+int ym_rccl_get_unique_id(ym_rccl_id* id) {
+  if (!id) return fail(YM_EINVAL, "null id");
+  const Rccl* R = rccl();
+  if (!R) return fail(YM_ESTATE, "RCCL (librccl.so) is not available in this process");
+  RCCLCK(R->get_id(id));
+  return YM_OK;
+}
+
+int ym_rccl_comm_init(int device, int nranks, const ym_rccl_id* id, int rank, void** comm) {
+  if (!id || !comm || nranks < 1 || rank < 0 || rank >= nranks) return fail(YM_EINVAL, "bad ym_rccl_comm_init arguments");
+  const Rccl* R = rccl();
+  if (!R) return fail(YM_ESTATE, "RCCL (librccl.so) is not available in this process");
+  HIPCK(hipSetDevice(device));
+  *comm = nullptr;
+  RCCLCK(R->init(comm, nranks, *id, rank));
+  return YM_OK;
+}
+
+int ym_rccl_comm_destroy(void* comm) {
+  if (!comm) return YM_OK;
+  const Rccl* R = rccl();
+  if (!R) return fail(YM_ESTATE, "RCCL (librccl.so) is not available in this process");
+  RCCLCK(R->destroy(comm));
+  return YM_OK;
+}
+
+// The root rank's loaded blob (plan + weights, exactly the bytes its ym_load_weights received) goes to every rank
+// of `comm` as two RCCL broadcasts over xGMI — its size, then the bytes — and each non-root rank loads it into `c`
+// (ym_load_weights), so every rank ends with an identical model without touching the file system.  Synchronous.
+int ym_broadcast_weights(ym_ctx* c, void* comm, int root, void* stream) {
+  if (!c || !comm) return fail(YM_EINVAL, "null argument");
+  const Rccl* R = rccl();
+  if (!R) return fail(YM_ESTATE, "RCCL (librccl.so) is not available in this process");
+  int rank = -1, n = 0;
+  RCCLCK(R->user_rank(comm, &rank));
+  RCCLCK(R->count(comm, &n));
+  if (root < 0 || root >= n) return fail(YM_EINVAL, "root %d out of range (%d ranks)", root, n);
+  if (rank == root && !c->loaded) return fail(YM_ESTATE, "the root context has no weights to broadcast");
+  HIPCK(hipSetDevice(c->device));
+  hipStream_t st = static_cast<hipStream_t>(stream);
+  unsigned long long nbytes = rank == root ? (unsigned long long)c->blob_host.size() : 0ull;
+  char* d = nullptr;
+  HIPCK(hipMalloc(&d, 256));
+  int rc = YM_OK;
+  auto done = [&](int code) {
+    (void)hipFree(d);
+    return code;
+  };
+  if (hipMemcpyAsync(d, &nbytes, 8, hipMemcpyHostToDevice, st) != hipSuccess) return done(fail(YM_EHIP, "size copy"));
+  int r = R->bcast(d, d, 8, kNcclUint8, root, comm, st);
+  if (r) return done(fail(YM_EHIP, "ncclBroadcast(size): %s", R->err(r)));
+  if (hipMemcpyAsync(&nbytes, d, 8, hipMemcpyDeviceToHost, st) != hipSuccess || hipStreamSynchronize(st) != hipSuccess)
+    return done(fail(YM_EHIP, "size read-back"));
+  (void)hipFree(d);
+  d = nullptr;
+  if (nbytes < kHdr * 4 || nbytes > (1ull << 34)) return fail(YM_EBLOB, "broadcast blob size %llu", nbytes);
+  HIPCK(hipMalloc(&d, nbytes));
+  if (rank == root && hipMemcpyAsync(d, c->blob_host.data(), nbytes, hipMemcpyHostToDevice, st) != hipSuccess)
+    return done(fail(YM_EHIP, "blob upload"));
+  r = R->bcast(d, d, nbytes, kNcclUint8, root, comm, st);
+  if (r) return done(fail(YM_EHIP, "ncclBroadcast(blob): %s", R->err(r)));
+  if (rank != root) {
+    std::vector<char> h(nbytes);
+    if (hipMemcpyAsync(h.data(), d, nbytes, hipMemcpyDeviceToHost, st) != hipSuccess ||
+        hipStreamSynchronize(st) != hipSuccess)
+      return done(fail(YM_EHIP, "blob read-back"));
+    rc = ym_load_weights(c, h.data(), nbytes);
+  } else if (hipStreamSynchronize(st) != hipSuccess) {
+    return done(fail(YM_EHIP, "stream sync"));
+  }
+  return done(rc);
 }
 
 int ym_sync(ym_ctx* c) {

@@ -505,6 +505,25 @@ def _cls_shift(scale: str) -> float:
     return CLS_BIAS_SHIFT[scale]
 
 
+def infer_arch(sd) -> Tuple[str, str, int]:
+    """(scale, task, nc) of an Ultralytics-key state dict: the reference takes the architecture from the checkpoint
+    (`YOLO(model_path)`, core/model.py:100-110), so a loaded file decides the plan, not the `size` argument.  The
+    task comes from the Proto keys, nc from the last cls conv, the scale from the graph whose every parameter shape
+    matches."""
+    import numpy as np
+    task = "segment" if any(k.startswith("model.23.proto.") for k in sd) else "detect"
+    key = "model.23.cv3.0.2.bias"
+    if key not in sd:
+        raise ValueError(f"not a YOLO11 detect/segment state dict (no {key!r})")
+    nc = int(np.shape(sd[key])[0])
+    for scale in SCALES:
+        g = GraphBuilder(scale, task, nc=nc)
+        if all(p.kind in ("count", "dfl") or (p.name in sd and tuple(np.shape(sd[p.name])) == tuple(p.shape))
+               for p in g.params):
+            return scale, task, nc
+    raise ValueError(f"state dict matches no YOLO11 scale ({'/'.join(SCALES)}) for task {task}, nc={nc}")
+
+
 def param_specs(scale: str = "n", task: str = "detect"):
     g = GraphBuilder(scale, task)
     return [(p.name, p.shape, p.kind, p.extra) for p in g.params]

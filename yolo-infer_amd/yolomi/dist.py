@@ -1,9 +1,10 @@
 """Multi-GPU plumbing for batch-sharded inference.
 
-One process per GPU.  The only collective on the path is at init: rank 0 packs the model blob (BN-folded, NHWC
-packed weights + plan) and broadcasts it as ONE uint8 tensor (RCCL over xGMI on MI355X when the process group is
-`nccl`; gloo on CPU for tests).  Per batch there is no exchange: rank r runs images [r*B_local, (r+1)*B_local) of
-the global batch on its own stream/graph.  The reference itself is single-device for inference
+One process per GPU.  At init rank 0 packs the model blob (BN-folded, NHWC packed weights + plan) and broadcasts it
+as ONE uint8 tensor (RCCL over xGMI on MI355X when the process group is `nccl`; gloo on CPU for tests).  Per batch,
+rank r runs images [r*B_local, (r+1)*B_local) of the global batch on its own stream/graph; the only exchange is one
+fp32 all-reduce (MAX) so that LoadTensor's /255 rule — a whole-batch decision in the reference — is taken over the
+global batch, not per shard (`GlobalBatchMax`).  The reference itself is single-device for inference
 (/root/reference/core/model.py:111-112).
 """
 from __future__ import annotations
@@ -40,6 +41,35 @@ def shard(global_batch: int, rank: int, world: int) -> Tuple[int, int]:
     base, extra = divmod(global_batch, world)
     start = rank * base + min(rank, extra)
     return start, start + base + (1 if rank < extra else 0)
+
+
+class GlobalBatchMax:
+    """LoadTensor's statistic over the GLOBAL batch for a batch-sharded rank: the shard's max (the engine's
+    `ym_input_max` kernel) all-reduced with MAX over the process group, left in one persistent device float that
+    `Engine.run(batch_max=...)` hands to the forward (stream-ordered: no host synchronisation).  `local_max` may be
+    replaced (tests drive it on CPU with gloo)."""
+
+    def __init__(self, engine=None, device: Optional[torch.device] = None, group=None):
+        self.engine = engine
+        self.group = group
+        dev = device if device is not None else (engine.device if engine is not None else torch.device("cpu"))
+        self.buf = torch.empty((1,), dtype=torch.float32, device=dev)
+
+    def local_max(self, x: torch.Tensor) -> torch.Tensor:
+        return self.engine.input_max(x, out=self.buf)
+
+    def __call__(self, x: torch.Tensor) -> torch.Tensor:
+        self.local_max(x)
+        if dist.is_initialized() and dist.get_world_size(self.group) > 1:
+            dist.all_reduce(self.buf, op=dist.ReduceOp.MAX, group=self.group)
+        return self.buf
+
+
+def enable_global_rule(model, group=None) -> GlobalBatchMax:
+    """Make `model.predict` take the /255 decision over the global batch of this process group."""
+    rule = GlobalBatchMax(model.model.engine, group=group)
+    model.global_batch_max = rule
+    return rule
 
 
 def digest(blob: bytes) -> str:

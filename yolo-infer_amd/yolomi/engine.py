@@ -27,7 +27,7 @@ def tune_cache_dir() -> str:
 
 class Engine:
     def __init__(self, scale: str, task: str, state_dict: Dict[str, np.ndarray], device: torch.device,
-                 dtype: str = "f16", blob: Optional[bytes] = None, qparams: Optional[Dict] = None):
+                 dtype: str = "f16", blob: Optional[bytes] = None, qparams: Optional[Dict] = None, nc: int = 80):
         """dtype: 'f16' (throughput), 'f32' (exact parity mode) or 'i8' (PTQ int8; needs `qparams` from
         yolomi.quant.calibrate, or an int8 `blob`)."""
         if device.type != "cuda":
@@ -35,9 +35,10 @@ class Engine:
         self.scale, self.task, self.dtype = scale, task, dtype
         self.device = device
         self.qparams = qparams
-        self.graph = GraphBuilder(scale, task, quant=dtype == "i8", fuse=fuse_default(dtype))
+        self.graph = GraphBuilder(scale, task, nc=nc, quant=dtype == "i8", fuse=fuse_default(dtype))
         self.blob = blob if blob is not None else pack_graph(self.graph, state_dict, dtype, qparams)
-        self.rt = Runtime(device.index if device.index is not None else torch.cuda.current_device(), self.blob)
+        self.rt = Runtime(device.index if device.index is not None else torch.cuda.current_device(), self.blob,
+                          scale=scale, task=task, dtype=dtype)
         self.nm = self.graph.nm
         self._out: Dict[int, tuple] = {}
         # Per-shape conv tile tables: on the first call of each (B, H, W) a table is taken from the writable tune
@@ -56,14 +57,20 @@ class Engine:
         return f"{self.scale}-{self.task}-{self.dtype}-b{B}-{H}x{W}.json"
 
     def _load_table(self, B, H, W):
+        """The committed table first (the one the tests and the bench pin), then this machine's tune cache.  A table
+        is used only when its version, op-name list and device architecture all match this engine."""
         name = self._table_name(B, H, W)
-        for tag, d in (("cache", tune_cache_dir()), ("committed", TUNED_DIR)):
+        arch = torch.cuda.get_device_properties(self.device).gcnArchName
+        ops = [op.name for op in self.graph.ops]
+        for tag, d in (("committed", TUNED_DIR), ("cache", tune_cache_dir())):
             p = os.path.join(d, name)
             try:
                 t = json.load(open(p))
             except (OSError, ValueError):
                 continue
-            if t.get("version") == TUNE_VERSION and len(t.get("cfg", [])) == self.rt.n_ops:
+            dev = t.get("device")
+            if (t.get("version") == TUNE_VERSION and t.get("ops") == ops and len(t.get("cfg", [])) == self.rt.n_ops
+                    and (dev is None or dev.split(":")[0] == arch.split(":")[0])):
                 self.rt.set_op_cfg(B, H, W, t["cfg"])
                 return f"{tag} table {name}"
         return None
@@ -104,22 +111,29 @@ class Engine:
         return -(-B // L)
 
     def run(self, x: torch.Tensor, conf=0.25, iou=0.7, max_det=300, classes: Optional[Sequence[int]] = None,
-            agnostic=False, in_eps=None, use_graph=True, max_nms=30000, max_wh=7680.0, lanes=None):
-        """x: (B,3,H,W) float32 contiguous on this device. Returns the engine-owned (dets, counts) tensors."""
+            agnostic=False, in_eps=None, use_graph=True, max_nms=30000, max_wh=7680.0, lanes=None,
+            batch_max: Optional[torch.Tensor] = None):
+        """x: (B,3,H,W) float32 contiguous on this device. Returns the engine-owned (dets, counts) tensors.
+        batch_max: optional (1,) fp32 device tensor, the max over the GLOBAL batch (yolomi.dist: a batch-sharded
+        rank takes LoadTensor's /255 decision from it instead of from its own shard)."""
         assert x.is_cuda and x.dtype == torch.float32 and x.is_contiguous() and x.dim() == 4 and x.shape[1] == 3
         B, _, H, W = x.shape
         if in_eps is None:
             in_eps = torch.finfo(torch.float32).eps
         lanes = self.lanes if lanes is None else lanes
         # the ctypes argument block of a repeated call is reused (predict loops pass the same thresholds)
+        bm = 0
+        if batch_max is not None:
+            assert batch_max.is_cuda and batch_max.dtype == torch.float32 and batch_max.numel() >= 1
+            bm = batch_max.data_ptr()
         akey = (conf, iou, max_det, max_nms, agnostic, max_wh, in_eps, tuple(classes) if classes is not None else None,
-                use_graph, lanes)
+                use_graph, lanes, bm)
         args = self._args_cache.get(akey)
         if args is None:
             if len(self._args_cache) > 64:
                 self._args_cache.clear()
             args = self._args_cache[akey] = Runtime.make_args(conf, iou, max_det, max_nms, agnostic, max_wh, in_eps,
-                                                              classes, use_graph, lanes)
+                                                              classes, use_graph, lanes, bm)
         dets, counts = self.outputs(B, max_det)
         stream = torch.cuda.current_stream(self.device).cuda_stream
         Bl = self.lane_batch(B, lanes)
@@ -127,6 +141,14 @@ class Engine:
             self._prepare_shape(x[:Bl], Bl, H, W, args, dets, counts, stream)
         self.rt.infer(x.data_ptr(), B, H, W, args, dets.data_ptr(), counts.data_ptr(), stream)
         return dets, counts
+
+    def input_max(self, x: torch.Tensor, out: Optional[torch.Tensor] = None) -> torch.Tensor:
+        """(1,) fp32 device tensor: max over x (LoadTensor's statistic; asynchronous on the current stream)."""
+        assert x.is_cuda and x.dtype == torch.float32 and x.is_contiguous()
+        if out is None:
+            out = torch.empty((1,), dtype=torch.float32, device=self.device)
+        self.rt.input_max(x.data_ptr(), x.numel(), out.data_ptr(), torch.cuda.current_stream(self.device).cuda_stream)
+        return out
 
     def profile(self, x: torch.Tensor, **kw):
         B, _, H, W = x.shape

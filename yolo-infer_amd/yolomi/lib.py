@@ -18,14 +18,23 @@ class YMError(RuntimeError):
 
 
 class ModelDesc(C.Structure):
-    _fields_ = [("max_batch", C.c_int), ("max_h", C.c_int), ("max_w", C.c_int), ("reserved", C.c_int * 5)]
+    _fields_ = [("max_batch", C.c_int), ("max_h", C.c_int), ("max_w", C.c_int), ("scale", C.c_int), ("task", C.c_int),
+                ("dtype", C.c_int), ("reserved", C.c_int * 2)]
+
+
+TASK_CODES = {"detect": 1, "segment": 2}
+DTYPE_CODES = {"f16": 1, "f32": 2, "i8": 3, "f8": 4}
+
+
+class RcclId(C.Structure):
+    _fields_ = [("internal", C.c_char * 128)]
 
 
 class InferArgs(C.Structure):
     _fields_ = [("conf", C.c_float), ("max_wh", C.c_float), ("iou", C.c_double), ("max_det", C.c_int),
                 ("max_nms", C.c_int), ("agnostic", C.c_int), ("in_eps", C.c_float), ("has_classes", C.c_int),
-                ("classes", C.c_uint32 * 4), ("use_graph", C.c_int), ("lanes", C.c_int),
-                ("reserved", C.c_int * 6)]
+                ("classes", C.c_uint32 * 4), ("use_graph", C.c_int), ("lanes", C.c_int), ("reserved0", C.c_int),
+                ("d_batch_max", C.c_void_p), ("reserved", C.c_int * 4)]
 
 
 _lib = None
@@ -59,6 +68,11 @@ def load_library(path: os.PathLike = LIB_PATH):
         "ym_num_buffers": (I, [P]),
         "ym_buffer_info": (I, [P, I, C.POINTER(P), C.POINTER(I), C.POINTER(I), C.POINTER(I), C.POINTER(I)]),
         "ym_read_buffer": (I, [P, I, P, C.c_size_t]),
+        "ym_input_max": (I, [P, P, C.c_size_t, P, P]),
+        "ym_broadcast_weights": (I, [P, P, I, P]),
+        "ym_rccl_get_unique_id": (I, [C.POINTER(RcclId)]),
+        "ym_rccl_comm_init": (I, [I, I, C.POINTER(RcclId), I, C.POINTER(P)]),
+        "ym_rccl_comm_destroy": (I, [P]),
         "ym_sync": (I, [P]),
         "ym_last_error": (C.c_char_p, []),
         "ym_destroy": (None, [P]),
@@ -72,9 +86,11 @@ def load_library(path: os.PathLike = LIB_PATH):
     return lib
 
 
-EXPORTED = ("ym_create", "ym_load_weights", "ym_infer", "ym_calibrate", "ym_masks", "ym_letterbox", "ym_profile", "ym_profile_replay", "ym_tune", "ym_get_op_cfg", "ym_set_op_cfg",
-            "ym_num_ops", "ym_op_name", "ym_num_buffers",
-            "ym_buffer_info", "ym_read_buffer", "ym_sync", "ym_last_error", "ym_destroy", "ym_version")
+EXPORTED = ("ym_create", "ym_load_weights", "ym_broadcast_weights", "ym_rccl_get_unique_id", "ym_rccl_comm_init",
+            "ym_rccl_comm_destroy", "ym_infer", "ym_input_max", "ym_calibrate", "ym_masks", "ym_letterbox",
+            "ym_profile", "ym_profile_replay", "ym_tune", "ym_get_op_cfg", "ym_set_op_cfg", "ym_num_ops", "ym_op_name",
+            "ym_num_buffers", "ym_buffer_info", "ym_read_buffer", "ym_sync", "ym_last_error", "ym_destroy",
+            "ym_version")
 
 
 def _check(rc: int):
@@ -83,23 +99,62 @@ def _check(rc: int):
         raise YMError(f"yolomi {YM_ERRORS.get(rc, rc)}: {msg}")
 
 
+def rccl_unique_id() -> bytes:
+    lib = load_library()
+    rid = RcclId()
+    _check(lib.ym_rccl_get_unique_id(C.byref(rid)))
+    return C.string_at(C.addressof(rid), 128)  # all 128 bytes (a c_char array would stop at the first NUL)
+
+
+def rccl_comm_init(device: int, nranks: int, uid: bytes, rank: int) -> int:
+    lib = load_library()
+    if len(uid) != 128:
+        raise ValueError("an RCCL unique id is 128 bytes")
+    rid = RcclId()
+    C.memmove(C.addressof(rid), uid, 128)
+    comm = C.c_void_p()
+    _check(lib.ym_rccl_comm_init(device, nranks, C.byref(rid), rank, C.byref(comm)))
+    return comm.value
+
+
+def rccl_comm_destroy(comm: int):
+    _check(load_library().ym_rccl_comm_destroy(C.c_void_p(comm)))
+
+
 class Runtime:
     """One ym_ctx on one device holding one packed model."""
 
-    def __init__(self, device_index: int, blob: bytes):
+    def __init__(self, device_index: int, blob: bytes, scale: str = None, task: str = None, dtype: str = None):
+        """scale / task / dtype (optional): what the blob must be (ym_model_desc; a mismatch raises YMError)."""
         self.lib = load_library()
         self.ctx = C.c_void_p()
+        self.device_index = device_index
         desc = ModelDesc()
+        desc.scale = ord(scale) if scale else 0
+        desc.task = TASK_CODES.get(task, 0)
+        desc.dtype = DTYPE_CODES.get(dtype, 0)
         _check(self.lib.ym_create(device_index, C.byref(desc), C.byref(self.ctx)))
+        self.load(blob)
+
+    def load(self, blob: bytes):
         buf = C.create_string_buffer(blob, len(blob))
         _check(self.lib.ym_load_weights(self.ctx, C.cast(buf, C.c_void_p), len(blob)))
         self.n_ops = self.lib.ym_num_ops(self.ctx)
         self.op_names = [self.lib.ym_op_name(self.ctx, i).decode() for i in range(self.n_ops)]
 
+    def input_max(self, x_ptr: int, n: int, out_ptr: int, stream: int):
+        _check(self.lib.ym_input_max(self.ctx, C.c_void_p(x_ptr), n, C.c_void_p(out_ptr), C.c_void_p(stream)))
+
+    def broadcast_weights(self, comm: int, root: int, stream: int):
+        _check(self.lib.ym_broadcast_weights(self.ctx, C.c_void_p(comm), root, C.c_void_p(stream)))
+        self.n_ops = self.lib.ym_num_ops(self.ctx)
+        self.op_names = [self.lib.ym_op_name(self.ctx, i).decode() for i in range(self.n_ops)]
+
     @staticmethod
     def make_args(conf=0.25, iou=0.7, max_det=300, max_nms=30000, agnostic=False, max_wh=7680.0, in_eps=1.1920929e-07,
-                  classes=None, use_graph=True, lanes=1) -> InferArgs:
+                  classes=None, use_graph=True, lanes=1, batch_max_ptr=0) -> InferArgs:
         a = InferArgs()
+        a.d_batch_max = batch_max_ptr or None
         a.conf, a.iou, a.max_det, a.max_nms = float(conf), float(iou), int(max_det), int(max_nms)
         a.agnostic, a.max_wh, a.in_eps, a.use_graph = int(bool(agnostic)), float(max_wh), float(in_eps), int(use_graph)
         a.lanes = int(lanes)

@@ -102,6 +102,20 @@ def fuse_default(dtype: str) -> bool:
     return dtype == "f16" and os.environ.get("YM_FUSE", "1") != "0"
 
 
+def check_state_dict(g: GraphBuilder, sd: Dict[str, np.ndarray]) -> None:
+    """Every parameter the plan reads must exist with exactly the shape the graph declares: a checkpoint of another
+    scale, task or class count is rejected here instead of being packed with the wrong K pitch / channel count."""
+    for p in g.params:
+        if p.kind in ("count", "dfl"):
+            continue
+        if p.name not in sd:
+            raise ValueError(f"state dict has no {p.name!r} (plan yolo11{g.scale} {g.task}, nc={g.nc})")
+        shape = tuple(np.shape(sd[p.name]))
+        if shape != tuple(p.shape):
+            raise ValueError(f"{p.name}: checkpoint shape {shape} != plan shape {tuple(p.shape)} "
+                             f"(plan yolo11{g.scale} {g.task}, nc={g.nc}: scale/task/class-count mismatch)")
+
+
 def pack_model(scale: str, task: str, sd: Dict[str, np.ndarray], dtype: str = "f16", qparams: Dict = None) -> bytes:
     g = GraphBuilder(scale, task, quant=dtype == "i8", fuse=fuse_default(dtype))
     return pack_graph(g, sd, dtype, qparams)
@@ -113,6 +127,7 @@ def pack_graph(g: GraphBuilder, sd: Dict[str, np.ndarray], dtype: str = "f16", q
     quant = dtype == "i8"
     if quant != bool(g.quant):
         raise ValueError("int8 blobs need GraphBuilder(quant=True), float blobs quant=False")
+    check_state_dict(g, sd)
     if quant:
         from .quant import BACKENDS, inv32, post_table, qrange, quantize_weight
         if not qparams or qparams.get("backend") not in BACKENDS:
@@ -253,6 +268,7 @@ def pack_graph(g: GraphBuilder, sd: Dict[str, np.ndarray], dtype: str = "f16", q
     hdr[15], hdr[16] = g.input.id, g.anchor_buf.id
     hdr[17] = g.proto_buf.id if g.task == "segment" else -1
     hdr[18] = g.no
+    hdr[19] = ord(g.scale)  # checked against ym_model_desc.scale
     head = struct.pack("<32i", *hdr)
     bufs = b"".join(struct.pack("<8i", b.Cs or b.C, b.f, int(b.f32), 0, 0, 0, 0, 0) for b in g.buffers)
     ops = b"".join(struct.pack("<32i", *rr) for rr in op_recs)
