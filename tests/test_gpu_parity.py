@@ -308,7 +308,11 @@ def _force_cfg(eng, x, cfg):
     eng.rt.set_op_cfg(B, H, W, [cfg if op.kind == "conv" else -1 for op in eng.graph.ops])
 
 
-@pytest.mark.parametrize("cfg", list(range(DMA_FIRST, STREAM_FIRST + 32)))
+HALO_FIRST = STREAM_FIRST + 32  # then csrc/ym_conv_halo.hip: 12 halo-tile 3x3 configs
+HALO_CFGS = list(range(HALO_FIRST, HALO_FIRST + 12))
+
+
+@pytest.mark.parametrize("cfg", list(range(DMA_FIRST, STREAM_FIRST + 32)) + HALO_CFGS)
 def test_dma_conv_configs_match_oracle(cfg):
     """Every conv of yolo11n (1x1 two-source/upsampled, 3x3 s1/s2, residual, fp32 Detect rows) on one DMA or
     streaming config (ops a config does not apply to fall back to the heuristic choice)."""
@@ -650,3 +654,30 @@ def test_rccl_broadcast_weights_single_rank():
         L.rccl_comm_destroy(comm)
     d2, c2 = _runtime_infer(rt, x)
     assert torch.equal(c1, c2) and torch.equal(d1[0, :int(c1[0])], d2[0, :int(c2[0])])
+
+
+@pytest.mark.parametrize("cfg", HALO_CFGS)
+def test_halo_conv_configs_yolo11s_b8(cfg):
+    """csrc/ym_conv_halo.hip on every applicable 3x3 conv of yolo11s at B=8 (stride 1/2, Cin 16..512, N up to 512,
+    residual epilogues, tiles of 1..16 rows): layer outputs and head rows vs the oracle."""
+    from core.model import YOLO11Model
+    x = make_input("uniform", tuple(range(7401, 7409)), 640)
+    _, y, ex = oracle("s").raw(x, keep=(2, 4, 6, 8, 9, 10, 13, 16, 19, 22))
+    m = model("s", "f16")
+    eng = m.model.engine
+    xd = x.to(DEV)
+    try:
+        _force_cfg(eng, xd, cfg)
+        eng.run(xd, use_graph=False)
+        for b in eng.graph.buffers:
+            if b.name.startswith("L") and b.name[1:].isdigit() and int(b.name[1:]) in ex["saved"]:
+                ref = ex["saved"][int(b.name[1:])].permute(0, 2, 3, 1)
+                got = eng.read_buffer(b.id, 8)
+                rel = (got - ref).abs().max().item() / ref.abs().max().item()
+                assert rel < 1e-2, (cfg, b.name, rel)
+        no = eng.graph.no
+        ref_h = torch.cat([f.view(8, no, -1) for f in ex["feats"]], 2).transpose(1, 2)
+        got_h = eng.read_buffer(eng.graph.anchor_buf.id, 8).reshape(8, -1, eng.graph.anchor_buf.C)[..., :no]
+        assert (got_h - ref_h).abs().max().item() / ref_h.abs().max().item() < 1e-2
+    finally:
+        eng._tuned.discard((8, 640, 640))

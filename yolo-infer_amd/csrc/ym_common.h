@@ -246,6 +246,8 @@ hipError_t ym_launch_conv_dma(int out_f32, const ConvArgs& a, int i, hipStream_t
 int ym_conv_dma_num_cfgs();
 hipError_t ym_launch_conv_stream(int out_f32, const ConvArgs& a, int i, hipStream_t st);  // f16 1x1 only
 int ym_conv_stream_num_cfgs();
+hipError_t ym_launch_conv_halo(int out_f32, const ConvArgs& a, int i, hipStream_t st);  // f16 3x3 halo tiles
+int ym_conv_halo_num_cfgs();
 hipError_t ym_launch_masks(const MaskArgs& a, hipStream_t st);  // Segment: process_mask(upsample=True)
 // int8 (PTQ) plans: csrc/ym_conv_i8.hip
 hipError_t ym_launch_conv_i8(const ConvArgs& a, int cfg, hipStream_t st, bool strict);

@@ -618,8 +618,11 @@ int choose_cfg(const ConvArgs& a) {
 }  // namespace
 
 // ids [0, 17): first-generation kernels above; [17, 17 + ym_conv_dma_num_cfgs()): LDS-DMA / split-K kernels;
-// then ym_conv_stream_num_cfgs() streaming 1x1 kernels (csrc/ym_conv_stream.hip)
-int ym_conv_num_cfgs() { return kNumAllCfg + ym_conv_dma_num_cfgs() + ym_conv_stream_num_cfgs(); }
+// then ym_conv_stream_num_cfgs() streaming / small-M kernels (csrc/ym_conv_stream.hip), then
+// ym_conv_halo_num_cfgs() halo-tile 3x3 kernels (csrc/ym_conv_halo.hip)
+int ym_conv_num_cfgs() {
+  return kNumAllCfg + ym_conv_dma_num_cfgs() + ym_conv_stream_num_cfgs() + ym_conv_halo_num_cfgs();
+}
 
 hipError_t ym_launch_conv(int dtype, int out_f32, const ConvArgs& a, int cfg, hipStream_t st, bool strict) {
   int kind;
@@ -649,11 +652,14 @@ hipError_t ym_launch_conv(int dtype, int out_f32, const ConvArgs& a, int cfg, hi
   if (cfg >= kNumAllCfg) {
     // a DMA config that does not apply to this op (checked before anything is launched): the tuner skips the
     // candidate (strict); a pinned table falls back to the heuristic
-    const int ndma = ym_conv_dma_num_cfgs();
+    const int ndma = ym_conv_dma_num_cfgs(), nstr = ym_conv_stream_num_cfgs();
     hipError_t e = hipErrorInvalidValue;
-    if (dtype == YM_DT_F16)
-      e = cfg - kNumAllCfg < ndma ? ym_launch_conv_dma(out_f32, a, cfg - kNumAllCfg, st)
-                                  : ym_launch_conv_stream(out_f32, a, cfg - kNumAllCfg - ndma, st);
+    if (dtype == YM_DT_F16) {
+      const int i = cfg - kNumAllCfg;
+      e = i < ndma ? ym_launch_conv_dma(out_f32, a, i, st)
+                   : (i < ndma + nstr ? ym_launch_conv_stream(out_f32, a, i - ndma, st)
+                                      : ym_launch_conv_halo(out_f32, a, i - ndma - nstr, st));
+    }
     if (e != hipErrorInvalidValue || strict) return e;
     cfg = -1;
   }

@@ -974,6 +974,8 @@ int ym_tune(ym_ctx* c, const float* d_in, int B, int H, int W, const ym_infer_ar
   HIPCK(hipEventCreate(&e0));
   HIPCK(hipEventCreate(&e1));
   const int ncfg = c->dtype == YM_DT_I8 ? ym_conv_i8_num_cfgs() : ym_conv_num_cfgs();
+  const char* tl = getenv("YM_TUNE_LOG");  // per-candidate timings to stderr (tools/)
+  const bool tune_log = tl && *tl && *tl != '0';
   for (size_t i = 0; i < c->ops.size(); ++i) {
     const Op& op = c->ops[i];
     if (op.r[0] != OP_CONV) continue;
@@ -1008,6 +1010,7 @@ int ym_tune(ym_ctx* c, const float* d_in, int B, int H, int W, const ym_infer_ar
         HIPCK(hipEventElapsedTime(&ms, e0, e1));
         (void)hipGraphExecDestroy(ge);
         (void)hipGraphDestroy(g);
+        if (tune_log) fprintf(stderr, "[ym_tune] %s%s cfg %d: %.2f us\n", op.name, of32 < 0 ? "" : "", cf, ms * 1e3f / (2 * reps));
         if (ms < bt) { bt = ms; bcf = cf; }
       }
       return bt;

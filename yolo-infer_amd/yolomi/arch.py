@@ -464,8 +464,8 @@ class GraphBuilder:
                 f = d_.buf.f
                 npx = B * (H // f) * (W // f)
                 by = 2 * npx * d_.C * act_bytes
-            elif op.kind == "input":
-                by = B * H * W * (3 * 4 * 2 + 8 * act_bytes)
+            elif op.kind == "input":  # LoadTensor statistic: the fp32 NCHW batch read once (the stem reads it again)
+                by = B * H * W * 3 * 4
             elif op.kind == "decode":
                 A = sum((H // s) * (W // s) for s in STRIDES)
                 by = B * A * (a["anchor"].C * 4 + 24)
