@@ -681,3 +681,28 @@ def test_halo_conv_configs_yolo11s_b8(cfg):
         assert (got_h - ref_h).abs().max().item() / ref_h.abs().max().item() < 1e-2
     finally:
         eng._tuned.discard((8, 640, 640))
+
+
+def test_decode_staged_variant_bitwise_equals_register_variant():
+    """the LDS-staged decode_anchors<false> (any nc / reg_max; forced with YM_DECODE_STAGED=1 in a child
+    process, the switch is read once per process) and the register-direct decode_anchors<true> that every
+    nc=80 / reg_max=16 plan takes produce the same detections bit for bit."""
+    import subprocess
+    import sys
+    root = os.path.dirname(os.path.dirname(os.path.abspath(__file__)))
+    code = ("import sys, torch, numpy as np; sys.path[:0] = [%r, %r];"
+            "from tests.golden.make_golden import make_input; from core.model import YOLO11Model;"
+            "m = YOLO11Model(size='n', device='cuda:0', dtype='f16');"
+            "x = make_input('uniform', (7501, 7502, 7503), 640).cuda();"
+            "d, c = m.model.engine.run(x, conf=0.05);"
+            "np.save(sys.argv[1], np.concatenate([d[b, :int(c[b])].cpu().numpy() for b in range(3)]))"
+            % (os.path.join(root, "yolo-infer_amd"), root))
+    outs = []
+    for staged in ("0", "1"):
+        path = os.path.join(root, "gpurun_out", f"decode_{staged}.npy") if os.path.isdir(
+            os.path.join(root, "gpurun_out")) else f"/tmp/decode_{staged}.npy"
+        env = dict(os.environ, YM_DECODE_STAGED=staged)
+        subprocess.run([sys.executable, "-c", code, path], check=True, env=env, timeout=240)
+        outs.append(np.load(path))
+    assert outs[0].shape == outs[1].shape and outs[0].shape[0] > 100
+    assert np.array_equal(outs[0], outs[1])

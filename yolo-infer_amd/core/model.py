@@ -234,11 +234,15 @@ class YOLO11Model:
             return [Results.from_image(imsrc[0][b], imsrc[1][b], names, out[b, : n[b], :6], speed=speed)
                     for b in range(B)]
         res = []  # Segment: the predictor keeps only non-empty masks
+        mb = masks.view(torch.bool)  # the kernel writes 0/1 bytes: a bool view, no copy
         for b in range(B):
-            idx = [i for i in range(n[b]) if keep[offs[b] + i]]
-            sel = torch.tensor(idx, dtype=torch.long, device=out.device)
-            bx = out[b].index_select(0, sel)[:, :6]
-            mk = masks[offs[b]:offs[b + 1]].index_select(0, sel).bool()
+            kb = keep[offs[b]:offs[b + 1]]
+            if all(kb):  # the common case: every kept detection has a mask pixel — views, no gathers
+                bx, mk = out[b, :n[b], :6], mb[offs[b]:offs[b + 1]]
+            else:
+                sel = torch.tensor([i for i, k in enumerate(kb) if k], dtype=torch.long, device=out.device)
+                bx = out[b].index_select(0, sel)[:, :6]
+                mk = mb[offs[b]:offs[b + 1]].index_select(0, sel)
             if imsrc is None:
                 res.append(Results(im[b], names, bx, path=f"image{b}.jpg", speed=speed, masks=mk))
             else:

@@ -43,6 +43,7 @@ constexpr int kMaxFusedBytes = 112 * 1024;  // fused pairs: both weight matrices
 // nb, so the following 1x1 conv runs from registers: no LDS round trip, no HBM write/read of the intermediate, one
 // launch fewer.  The intermediate is rounded to fp16 like the stored tensor of the unfused pair.
 constexpr int kFuseMaxN = 128;  // first conv's N (= second conv's K) held in registers: 8 blocks of 16
+constexpr int RB = 8;           // output-channel blocks of 16 whose residuals are prefetched with the fragments
 
 template <typename OutT, int KIND, int KS, int PX, bool FUSE>
 __global__ __launch_bounds__(256) void conv_stream(const ConvArgs a) {
@@ -95,8 +96,12 @@ __global__ __launch_bounds__(256) void conv_stream(const ConvArgs a) {
   const int K = a.C0 + a.C1;
   const unsigned c8m = (0x1000000u + a.Cin8 - 1) / a.Cin8;  // 3x3: tap = (chunk * c8m) >> 24 (chunk < 9 Cin8)
 
-  // B fragments of the iteration starting at group gb: [PX][KS]
-  auto load = [&](int gb, h8 (&bf)[PX][KS]) {
+  // B fragments of the iteration starting at group gb: [PX][KS]; with a residual also the residual values of the
+  // first RB output-channel blocks of its pixels, one iteration ahead like the fragments (a residual load placed
+  // after the previous block's stores would make the compiler drain every outstanding load, the prefetch included)
+  const f16* res = static_cast<const f16*>(a.res);
+  const int NR = FUSE ? a.N2 : a.N;
+  auto load = [&](int gb, h8 (&bf)[PX][KS], f16x4 (&rr)[PX][RB]) {
 #pragma unroll
     for (int p = 0; p < PX; ++p) {
       const int m = (gb + p) * 16 + col;
@@ -104,6 +109,12 @@ __global__ __launch_bounds__(256) void conv_stream(const ConvArgs a) {
       const int mm = ok ? m : 0;
       const int b = ym_div(mm, a.fd_hw), rem = mm - b * HW;
       const int y = ym_div(rem, a.fd_w), x = rem - y * a.Wo;
+      if (res) {
+        const f16* rp = res + (size_t)(b * a.r_P + y * a.Wo + x) * a.r_ctot + a.r_coff + 4 * g;
+#pragma unroll
+        for (int j = 0; j < RB; ++j)
+          rr[p][j] = (ok && 16 * j + 4 * g < NR) ? *reinterpret_cast<const f16x4*>(rp + 16 * j) : f16x4{0, 0, 0, 0};
+      }
       if constexpr (KIND == 1) {
         const size_t p0 = a.up0 ? (size_t)b * a.s0_P + (y >> 1) * a.s0_W + (x >> 1) : (size_t)b * a.s0_P + y * a.s0_W + x;
         const size_t p1 = (size_t)b * a.s1_P + y * a.Win + x;
@@ -136,12 +147,12 @@ __global__ __launch_bounds__(256) void conv_stream(const ConvArgs a) {
 
   int gb = (blockIdx.x * 4 + wave) * PX;
   h8 cur[PX][KS], nxt[PX][KS];
-  load(gb, cur);
+  f16x4 rcur[PX][RB], rnxt[PX][RB];
+  load(gb, cur, rcur);
   __syncthreads();
   OutT* dst = static_cast<OutT*>(a.dst);
-  const f16* res = static_cast<const f16*>(a.res);
   for (; gb < G; gb += nw * PX) {
-    if (gb + nw * PX < G) load(gb + nw * PX, nxt);
+    if (gb + nw * PX < G) load(gb + nw * PX, nxt, rnxt);
     int ob[PX], rb[PX];  // output / residual pixel index of this lane's pixel in group p (ob -1: none)
 #pragma unroll
     for (int p = 0; p < PX; ++p) {
@@ -173,7 +184,11 @@ __global__ __launch_bounds__(256) void conv_stream(const ConvArgs a) {
           }
         }
       }
-      for (int nb2 = 0; nb2 < NB2; ++nb2) {
+      for (int nb20 = 0; nb20 < NB2; nb20 += RB)
+#pragma unroll
+      for (int j = 0; j < RB; ++j) {
+        const int nb2 = nb20 + j;
+        if (nb2 >= NB2) break;
         f16x4 a2[NBF];
 #pragma unroll
         for (int nb = 0; nb < NBF; ++nb)
@@ -194,7 +209,8 @@ __global__ __launch_bounds__(256) void conv_stream(const ConvArgs a) {
             v[r] = a.act2 ? ym_silu_fast(xv) : xv;
           }
           if (res) {
-            const f16x4 rv = *reinterpret_cast<const f16x4*>(res + (size_t)rb[p] * a.r_ctot + a.r_coff + n0);
+            const f16x4 rv = nb20 == 0 ? rcur[p][j]
+                                       : *reinterpret_cast<const f16x4*>(res + (size_t)rb[p] * a.r_ctot + a.r_coff + n0);
 #pragma unroll
             for (int r = 0; r < 4; ++r) v[r] += (float)rv[r];
           }
@@ -204,7 +220,11 @@ __global__ __launch_bounds__(256) void conv_stream(const ConvArgs a) {
         }
       }
     } else
-    for (int nb = 0; nb < NP / 16; ++nb) {
+    for (int nb0 = 0; nb0 < NP / 16; nb0 += RB)
+#pragma unroll
+    for (int j = 0; j < RB; ++j) {
+      const int nb = nb0 + j;
+      if (nb >= NP / 16) break;
       h8 af[KS];
 #pragma unroll
       for (int ks = 0; ks < KS; ++ks)
@@ -224,7 +244,8 @@ __global__ __launch_bounds__(256) void conv_stream(const ConvArgs a) {
           v[r] = a.act ? ym_silu_fast(xv) : xv;
         }
         if (res) {
-          const f16x4 rv = *reinterpret_cast<const f16x4*>(res + (size_t)rb[p] * a.r_ctot + a.r_coff + n0);
+          const f16x4 rv = nb0 == 0 ? rcur[p][j]
+                                    : *reinterpret_cast<const f16x4*>(res + (size_t)rb[p] * a.r_ctot + a.r_coff + n0);
 #pragma unroll
           for (int r = 0; r < 4; ++r) v[r] += (float)rv[r];
         }
@@ -234,9 +255,12 @@ __global__ __launch_bounds__(256) void conv_stream(const ConvArgs a) {
       }
     }
 #pragma unroll
-    for (int p = 0; p < PX; ++p)
+    for (int p = 0; p < PX; ++p) {
 #pragma unroll
       for (int ks = 0; ks < KS; ++ks) cur[p][ks] = nxt[p][ks];
+#pragma unroll
+      for (int j = 0; j < RB; ++j) rcur[p][j] = rnxt[p][j];
+    }
   }
 }
 

@@ -3,6 +3,8 @@
 //   attention (+ fused positional depthwise conv), anchor-free DFL decode, class-offset greedy NMS.
 // Each replaces an upstream Ultralytics/ATen/torchvision op reached from `YOLO11Model.predict`
 // (/root/reference/core/model.py:133) — SURVEY §2.2 and §8a rows a2, a8, a9, a11-a14.
+#include <stdlib.h>
+
 #include "ym_common.h"
 
 namespace {
@@ -1056,7 +1058,12 @@ hipError_t ym_launch_attn(int dtype, const AttnArgs& a, hipStream_t st) {
 hipError_t ym_launch_decode(const DecodeArgs& a, hipStream_t st) {
   const long total = (long)a.B * a.A;
   if (a.no_tot % 4) return hipErrorInvalidValue;
-  if (a.reg_max == 16 && a.nc == 80) {
+  // YM_DECODE_STAGED=1 forces the general LDS-staged variant (tests: both variants agree bit for bit)
+  static const bool staged = [] {
+    const char* e = getenv("YM_DECODE_STAGED");
+    return e && *e == '1';
+  }();
+  if (a.reg_max == 16 && a.nc == 80 && !staged) {
     hipLaunchKernelGGL(decode_anchors<true>, dim3((total + 63) / 64), dim3(256), 0, st, a);
     return hipGetLastError();
   }
