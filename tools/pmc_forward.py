@@ -32,12 +32,16 @@ def main():
     m = YOLO11Model(task=a.task, size=a.model, device="cuda:0", dtype=a.dtype)
     x = synthetic_batch(a.batch, a.size, 1000, torch.device("cuda", 0))
     eng = m.model.engine
-    if a.ops_out:
-        with open(a.ops_out, "w") as f:
-            for op in eng.graph.ops:
-                f.write(f"{op.name}\t{op.kind}\n")
     eng.run(x, use_graph=False)  # table lookup (or tuning) happens here
     torch.cuda.synchronize()
+    if a.ops_out:
+        # name, kind, kernel launches of the op (a split pair launches two), algorithmic FLOPs and bytes
+        cfg = eng.rt.get_op_cfg(a.batch, a.size, a.size) or [0] * len(eng.graph.ops)
+        costs = eng.graph.op_costs(a.batch, a.size, a.size, 1 if a.dtype == "i8" else 4 if a.dtype == "f32" else 2)
+        with open(a.ops_out, "w") as f:
+            for op, c, (fl, by) in zip(eng.graph.ops, cfg, costs):
+                n = 2 if op.kind == "input" or (op.kind == "conv" and c >= (1 << 20)) else 1
+                f.write(f"{op.name}\t{op.kind}\t{n}\t{int(fl)}\t{int(by)}\n")
     for _ in range(a.reps):
         eng.run(x, use_graph=False)
     torch.cuda.synchronize()

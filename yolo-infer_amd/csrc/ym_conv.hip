@@ -84,13 +84,14 @@ constexpr int KSTEP = 64;
 constexpr int KS = KSTEP / 16;
 
 // XCD-aware tile map: workgroups are dealt round-robin over the 8 XCDs (bid % 8), so give every N tile of one pixel
-// tile the same bid % 8: the pixel rows they all read then sit in ONE XCD's L2.  The grid is padded to a multiple
-// of 8 pixel tiles; padding workgroups exit immediately.  (Placement only affects speed, never results.)
+// tile the same bid % 8 (the pixel rows they all read then sit in ONE XCD's L2), and give each XCD one contiguous run
+// of pixel tiles (the rows a 3x3 tile shares with its neighbours too).  The grid is padded to a multiple of 8 pixel
+// tiles; padding workgroups exit immediately.  (Placement only affects speed, never results.)
 __device__ __forceinline__ bool xcd_tile(const ConvArgs& a, int BM, int& tm, int& tn) {
   const int bid = blockIdx.x;
   const int rest = bid >> 3;
   tn = rest % a.tiles_n;
-  tm = (rest / a.tiles_n) * 8 + (bid & 7);
+  tm = (bid & 7) * (int)(gridDim.x / (8u * a.tiles_n)) + rest / a.tiles_n;
   return tm * BM < a.M;
 }
 

@@ -95,13 +95,14 @@ __global__ __launch_bounds__(256 * KG) void conv_dma(const ConvArgs a) {
   const int wm = wq & 1, wn = wq >> 1;
   const int l32 = lane & 31, h = lane >> 5;
   // tile map: every N tile and every K split of pixel tile tm share bid % 8 = one XCD (its L2 holds the pixels and
-  // the split's slabs); padding workgroups (tm beyond M) exit before touching a counter
+  // the split's slabs), and each XCD owns one contiguous run of pixel tiles, so the image rows a 3x3 tile shares with
+  // its neighbours are fetched into one L2; padding workgroups (tm beyond M) exit before touching a counter
   const int bid = blockIdx.x;
   int rest = bid >> 3;
   const int sp = rest % SPLIT;
   rest /= SPLIT;
   const int tn = rest % a.tiles_n;
-  const int tm = (rest / a.tiles_n) * 8 + (bid & 7);
+  const int tm = (bid & 7) * (int)(gridDim.x / (8u * SPLIT * a.tiles_n)) + rest / a.tiles_n;
   if (tm * BM >= a.M) return;
 
   // ---- epilogue operands first (bias, residual; wave group 0 runs the epilogue): their latency hides behind the

@@ -105,8 +105,9 @@ __global__ __launch_bounds__(256) void conv_halo(const ConvArgs a, const HaloGeo
   const int tid = threadIdx.x, lane = tid & 63, wave = tid >> 6;
   const int wm = wave % WM, wn = wave / WM;
   const int l32 = lane & 31, hl = lane >> 5;
-  const int tn = blockIdx.x % a.tiles_n;
-  const int rest = blockIdx.x / a.tiles_n;
+  const int vb = ym_xcd_block(blockIdx.x, gridDim.x);  // neighbouring row tiles (shared halo rows) on one XCD
+  const int tn = vb % a.tiles_n;
+  const int rest = vb / a.tiles_n;
   const int ty = rest % g.tiles_y, b = rest / g.tiles_y;
   const int r0 = ty * g.TH;
   const int Cin = a.C0;

@@ -34,7 +34,7 @@ __device__ __forceinline__ bool xcd_tile(const ConvArgs& a, int BM, int& tm, int
   const int bid = blockIdx.x;
   const int rest = bid >> 3;
   tn = rest % a.tiles_n;
-  tm = (rest / a.tiles_n) * 8 + (bid & 7);
+  tm = (bid & 7) * (int)(gridDim.x / (8u * a.tiles_n)) + rest / a.tiles_n;  // one contiguous run per XCD
   return tm * BM < a.M;
 }
 
@@ -314,7 +314,8 @@ __global__ __launch_bounds__(256) void dwconv3x3_i8(const DwArgs a) {
   post[threadIdx.x] = Q->post[threadIdx.x];
   __syncthreads();
   const int C8 = a.C >> 3;
-  const int idx = blockIdx.x * blockDim.x + threadIdx.x;  // 32-bit index math (checked < 2^31 on the host)
+  // 32-bit index math (checked < 2^31 on the host); one contiguous run of blocks per XCD (shared tap rows)
+  const int idx = ym_xcd_block(blockIdx.x, gridDim.x) * blockDim.x + threadIdx.x;
   const int total = a.B * a.H * a.W * C8;
   if (idx >= total) return;
   const int pix = idx / C8;
@@ -375,8 +376,9 @@ __global__ __launch_bounds__(256) void attn_psa_i8(const AttnArgs a) {
   const int N = a.N;
   float* Qs = reinterpret_cast<float*>(S + (size_t)QB * N);
   const int nqb = (N + QB - 1) / QB;
-  const int qb = blockIdx.x % nqb;
-  const int bh = blockIdx.x / nqb;
+  const int vb = ym_xcd_block(blockIdx.x, gridDim.x);  // the query blocks of one (image, head) on one XCD
+  const int qb = vb % nqb;
+  const int bh = vb / nqb;
   const int h = bh % a.nh;
   const int b = bh / a.nh;
   const int tid = threadIdx.x;

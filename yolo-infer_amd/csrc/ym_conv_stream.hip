@@ -90,7 +90,6 @@ __global__ __launch_bounds__(256) void conv_stream(const ConvArgs a) {
 
   const int HW = a.Ho * a.Wo;
   const int G = (a.M + 15) >> 4;  // 16-pixel groups
-  const int nw = gridDim.x * 4;
   const f16* s0 = static_cast<const f16*>(a.src0);
   const f16* s1 = static_cast<const f16*>(a.src1);
   const int K = a.C0 + a.C1;
@@ -101,11 +100,19 @@ __global__ __launch_bounds__(256) void conv_stream(const ConvArgs a) {
   // after the previous block's stores would make the compiler drain every outstanding load, the prefetch included)
   const f16* res = static_cast<const f16*>(a.res);
   const int NR = FUSE ? a.N2 : a.N;
+  // XCD-contiguous group ranges: workgroup bid runs on XCD bid % 8 (round-robin dispatch), and each XCD sweeps one
+  // contiguous range of 16-pixel groups with all of its workgroups, so the neighbouring image rows a 3x3 tap reads
+  // (and a C2f residual) are fetched into that XCD's L2 once instead of once per XCD (speed only: any mapping gives
+  // the same results)
+  const int nwg = gridDim.x, xcd = blockIdx.x & 7, slot = blockIdx.x >> 3;
+  const int nwx = (nwg >> 3) + (xcd < (nwg & 7));                   // workgroups on this XCD
+  const int v0 = xcd * (nwg >> 3) + (xcd < (nwg & 7) ? xcd : (nwg & 7));  // workgroups on lower XCDs
+  const int gend = (int)((long)G * (v0 + nwx) / nwg);
   auto load = [&](int gb, h8 (&bf)[PX][KS], f16x4 (&rr)[PX][RB]) {
 #pragma unroll
     for (int p = 0; p < PX; ++p) {
       const int m = (gb + p) * 16 + col;
-      const bool ok = gb + p < G && m < a.M;
+      const bool ok = gb + p < gend && m < a.M;
       const int mm = ok ? m : 0;
       const int b = ym_div(mm, a.fd_hw), rem = mm - b * HW;
       const int y = ym_div(rem, a.fd_w), x = rem - y * a.Wo;
@@ -145,21 +152,22 @@ __global__ __launch_bounds__(256) void conv_stream(const ConvArgs a) {
     }
   };
 
-  int gb = (blockIdx.x * 4 + wave) * PX;
+  const int step = nwx * 4 * PX;
+  int gb = (int)((long)G * v0 / nwg) + (slot * 4 + wave) * PX;
   h8 cur[PX][KS], nxt[PX][KS];
   f16x4 rcur[PX][RB], rnxt[PX][RB];
   load(gb, cur, rcur);
   __syncthreads();
   OutT* dst = static_cast<OutT*>(a.dst);
-  for (; gb < G; gb += nw * PX) {
-    if (gb + nw * PX < G) load(gb + nw * PX, nxt, rnxt);
+  for (; gb < gend; gb += step) {
+    if (gb + step < gend) load(gb + step, nxt, rnxt);
     int ob[PX], rb[PX];  // output / residual pixel index of this lane's pixel in group p (ob -1: none)
 #pragma unroll
     for (int p = 0; p < PX; ++p) {
       const int m = (gb + p) * 16 + col;
       const int b = ym_div(m, a.fd_hw), rem = m - b * HW;
       const int y = ym_div(rem, a.fd_w), x = rem - y * a.Wo;
-      ob[p] = (gb + p < G && m < a.M) ? b * a.d_P + a.d_pixoff + y * a.d_W + x : -1;
+      ob[p] = (gb + p < gend && m < a.M) ? b * a.d_P + a.d_pixoff + y * a.d_W + x : -1;
       rb[p] = b * a.r_P + y * a.Wo + x;
     }
     if constexpr (FUSE) {
@@ -289,7 +297,8 @@ __global__ __launch_bounds__(256) void conv_small(const ConvArgs a) {
   const int tid = threadIdx.x, lane = tid & 63, wave = tid >> 6;
   const int g = lane >> 4, col = lane & 15;
   const int ntn = (a.N + 15) >> 4;
-  const int tn = blockIdx.x % ntn, tm = blockIdx.x / ntn;
+  const int vb = ym_xcd_block(blockIdx.x, gridDim.x);  // each XCD owns one contiguous run of pixel blocks
+  const int tn = vb % ntn, tm = vb / ntn;
   const int KS = a.Kpad >> 5;
   const int HW = a.Ho * a.Wo;
   const f16* s0 = static_cast<const f16*>(a.src0);

@@ -73,7 +73,8 @@ __global__ void ctl_to_max(const float* ctl, float* out) {
 template <typename T>
 __global__ __launch_bounds__(256) void dwconv3x3(const DwArgs a) {
   const int C8 = a.C >> 3;
-  const int idx = blockIdx.x * blockDim.x + threadIdx.x;  // 32-bit index math (checked < 2^31 on the host)
+  // 32-bit index math (checked < 2^31 on the host); each XCD owns one contiguous run of blocks (shared tap rows)
+  const int idx = ym_xcd_block(blockIdx.x, gridDim.x) * blockDim.x + threadIdx.x;
   const int total = a.B * a.H * a.W * C8;
   if (idx >= total) return;
   const int pix = idx / C8;
@@ -125,7 +126,7 @@ template <typename T, int PXT>
 __global__ __launch_bounds__(256) void dwconv3x3_row(const DwArgs a) {
   const int C8 = a.C >> 3;
   const int Wq = a.W / PXT;
-  const int idx = blockIdx.x * blockDim.x + threadIdx.x;
+  const int idx = ym_xcd_block(blockIdx.x, gridDim.x) * blockDim.x + threadIdx.x;  // contiguous run per XCD
   const int total = a.B * a.H * Wq * C8;
   if (idx >= total) return;
   const int q = idx / C8;
@@ -192,8 +193,9 @@ __global__ __launch_bounds__(256) void sppf_pool(const PoolArgs a) {
   const int HW = a.H * a.W;
   V* hr = in + HW;                      // [3][HW] row maxima, radius 2, 4, 6
   const int ng = a.C / 8;
-  const int b = blockIdx.x / ng;
-  const int c0 = (blockIdx.x % ng) * 8;
+  const int vb = ym_xcd_block(blockIdx.x, gridDim.x);  // an image's channel groups share cache lines: one XCD
+  const int b = vb / ng;
+  const int c0 = (vb % ng) * 8;
   T* buf = static_cast<T*>(a.buf);
   {  // all loads in flight before the first LDS store (HW <= 1024 on the separable path's maps)
     V v[4];
@@ -269,8 +271,9 @@ __global__ __launch_bounds__(256) void attn_psa(const AttnArgs a) {
   const int N = a.N;
   float* Qs = S + (size_t)QB * N;
   const int nqb = (N + QB - 1) / QB;
-  const int qb = blockIdx.x % nqb;
-  const int bh = blockIdx.x / nqb;
+  const int vb = ym_xcd_block(blockIdx.x, gridDim.x);  // the query blocks of one (image, head) on one XCD
+  const int qb = vb % nqb;
+  const int bh = vb / nqb;
   const int h = bh % a.nh;
   const int b = bh / a.nh;
   const int tid = threadIdx.x;
@@ -401,7 +404,8 @@ __global__ __launch_bounds__(256) void attn_psa_mfma(const AttnArgs a) {
   float* pw = reinterpret_cast<float*>(kl + 16 * NKT * LDK);
   const int N = a.N;
   const int nqb = (N + 63) / 64;
-  const int qb = blockIdx.x % nqb, bh = blockIdx.x / nqb;
+  const int vb = ym_xcd_block(blockIdx.x, gridDim.x);  // the query blocks of one (image, head) on one XCD
+  const int qb = vb % nqb, bh = vb / nqb;
   const int h = bh % a.nh, b = bh / a.nh;
   const int tid = threadIdx.x, lane = tid & 63, wave = tid >> 6;
   const int g = lane >> 4, c = lane & 15;
