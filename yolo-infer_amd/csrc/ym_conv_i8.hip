@@ -362,133 +362,166 @@ __global__ __launch_bounds__(256) void dwconv3x3_i8(const DwArgs a) {
 
 // ------------------------------------------------------------------------------------------------- attention
 // C2PSA Attention on the int8 qkv tensor (stored in the qkv conv's own output quantisation): q, k, v dequantised to
-// fp32; S = q·kᵀ·scale, softmax and O = P·V evaluated in float64 and rounded to fp32 once (the oracle's definition of
-// the int8 model's float island: order-independent, so the int8 outputs are bit-reproducible); + pe(v) as a quantized
-// depthwise conv (int MACs on the stored v bytes, requantised, dequantised); the sum is quantized into attn.x.
+// fp32 ((q - z)·s), then S = q·kᵀ·scale, softmax and O = P·V evaluated in float64 and rounded to fp32 once (the
+// oracle's definition of the int8 model's float island, oracle/quant.py:_psablock: f64 results agree far below one
+// fp32 ulp whatever the summation order, so the int8 outputs are bit-reproducible); + pe(v) as a quantized depthwise
+// conv (int MACs on the stored v bytes, requantised, dequantised); the sum is quantized into attn.x.
+//
+// One workgroup = 16 queries of one (image, head); its 4 waves each take every 4th 16-key block and run a flash-style
+// pass on v_mfma_f64_16x16x4_f64 (A/B one f64 per lane: A[l&15][k=l>>4], B[k=l>>4][l&15]; D col l&15, row
+// (l>>4)+4r): Sᵀ = K·Qᵀ (8 MFMAs over kd = 32), running max / sum per query column, and Oᵀ += Vᵀ·Pᵀ (4 d-blocks x 4
+// MFMAs) — the Pᵀ operand of key step s is exactly D register r = s of Sᵀ, so P never leaves registers.  The four
+// partial (max, sum, Oᵀ) meet in LDS.
 constexpr int AKD = 32, AHD = 64;
+typedef double f64x4 __attribute__((ext_vector_type(4)));
 
-template <int QB>
 __global__ __launch_bounds__(256) void attn_psa_i8(const AttnArgs a) {
-  extern __shared__ double S[];  // [QB][N] doubles, then Q [QB][AKD] floats, then a V chunk [64][AHD] floats
   __shared__ float post[256];
+  __shared__ double cm[4][16], cl[4][16];
+  __shared__ double co[4][AHD][17];  // Oᵀ partials [wave][d][q] (odd pitch: the column reads below)
   const QRec* Qr = a.q;
   post[threadIdx.x] = Qr->post[threadIdx.x];
-  const int N = a.N;
-  float* Qs = reinterpret_cast<float*>(S + (size_t)QB * N);
-  const int nqb = (N + QB - 1) / QB;
+  const int N = a.N, nqb = (N + 15) >> 4, nkb = nqb;
   const int vb = ym_xcd_block(blockIdx.x, gridDim.x);  // the query blocks of one (image, head) on one XCD
-  const int qb = vb % nqb;
-  const int bh = vb / nqb;
-  const int h = bh % a.nh;
-  const int b = bh / a.nh;
-  const int tid = threadIdx.x;
-  const int per = 2 * a.kd + a.hd;
+  const int qb = vb % nqb, bh = vb / nqb;
+  const int h = bh % a.nh, b = bh / a.nh;
+  const int tid = threadIdx.x, lane = tid & 63, w = tid >> 6;
+  const int lc = lane & 15, lg = lane >> 4;
   const i8* qkv = static_cast<const i8*>(a.qkv);
   const size_t img = (size_t)b * a.q_P;
-  const int hq = a.q_coff + h * per;
+  const int hq = a.q_coff + h * (2 * AKD + AHD);
   const float s_in = Qr->s_in;
   const int z_in = Qr->z_in;
   const double scale = (double)a.scale;
-  for (int i = tid; i < QB * AKD; i += 256) {
-    const int r = i / AKD, c = i % AKD;
-    const int n = qb * QB + r;
-    Qs[i] = (n < N && c < a.kd) ? deq((int)qkv[(img + n) * a.q_ctot + hq + c] + 128, z_in, s_in) : 0.f;
-  }
-  __syncthreads();
-  for (int key = tid; key < N; key += 256) {
-    double k[AKD];
-    const i8* kp = qkv + (img + key) * a.q_ctot + hq + a.kd;
-#pragma unroll
-    for (int c8 = 0; c8 < AKD / 8; ++c8) {
-      const Vec8<i8>::type v = Vec8<i8>::load(kp + c8 * 8);
-#pragma unroll
-      for (int e = 0; e < 8; ++e)
-        k[c8 * 8 + e] = (c8 * 8 + e < a.kd) ? (double)deq((int)v[e] + 128, z_in, s_in) : 0.0;
-    }
-#pragma unroll 2
-    for (int q = 0; q < QB; ++q) {
-      double s = 0.0;
-#pragma unroll
-      for (int c = 0; c < AKD; ++c) s = fma((double)Qs[q * AKD + c], k[c], s);
-      S[q * N + key] = s * scale;
-    }
-  }
-  __syncthreads();
+  auto dq = [&](unsigned word, int byte) {  // stored byte (q - 128) of a little-endian word -> f64 of deq(q)
+    return (double)deq((int)((word >> (8 * byte)) & 0xFFu) ^ 0x80, z_in, s_in);
+  };
+  // Qᵀ operand: Qᵀ[c = 4s + lg][q = lc]
+  double qf[8];
   {
-    constexpr int TPR = 256 / QB;
-    const int q = tid / TPR, sub = tid % TPR;
-    double* row = S + (size_t)q * N;
-    double m = -INFINITY;
-    for (int j = sub; j < N; j += TPR) m = fmax(m, row[j]);
+    const int qn = qb * 16 + lc;
+    const i32x4* qp = reinterpret_cast<const i32x4*>(qkv + (img + (qn < N ? qn : 0)) * a.q_ctot + hq);
+    const i32x4 u0 = qp[0], u1 = qp[1];
 #pragma unroll
-    for (int o = TPR / 2; o > 0; o >>= 1) m = fmax(m, __shfl_xor(m, o));
-    double sum = 0.0;
-    for (int j = sub; j < N; j += TPR) {
-      const double e = exp(row[j] - m);
-      row[j] = e;
-      sum += e;
-    }
-#pragma unroll
-    for (int o = TPR / 2; o > 0; o >>= 1) sum += __shfl_xor(sum, o);
-    for (int j = sub; j < N; j += TPR) row[j] = row[j] / sum;
+    for (int s = 0; s < 8; ++s) qf[s] = qn < N ? dq((unsigned)(s < 4 ? u0[s] : u1[s - 4]), lg) : 0.0;
   }
+  double m = -INFINITY, l = 0.0;
+  f64x4 o[4];
+#pragma unroll
+  for (int db = 0; db < 4; ++db) o[db] = f64x4{0.0, 0.0, 0.0, 0.0};
+  // the K row and V words of key block kb, one block ahead (each block's loads would otherwise be a full L2 round
+  // trip on the wave's serial path)
+  auto fetch = [&](int kb, i32x4& k0, i32x4& k1, unsigned (&vw)[4][4]) {
+    // Sᵀ = K·Qᵀ: A = K[key = 16 kb + lc][c = 4s + lg]
+    const int key = kb * 16 + lc;
+    const i32x4* kp = reinterpret_cast<const i32x4*>(qkv + (img + (key < N ? key : 0)) * a.q_ctot + hq + AKD);
+    k0 = kp[0];
+    k1 = kp[1];
+    // Vᵀ operand words: V[16 kb + 4s + lg][16 db + lc] is byte lc & 3 of word (lc >> 2) + 4 db of that key's v row
+#pragma unroll
+    for (int s = 0; s < 4; ++s) {
+      const int vk = kb * 16 + 4 * s + lg;
+      const unsigned* vp = reinterpret_cast<const unsigned*>(qkv + (img + (vk < N ? vk : 0)) * a.q_ctot + hq + 2 * AKD);
+#pragma unroll
+      for (int db = 0; db < 4; ++db) vw[s][db] = vp[(lc >> 2) + 4 * db];
+    }
+  };
+  i32x4 k0, k1, nk0, nk1;
+  unsigned vw[4][4], nvw[4][4];
+  if (w < nkb) fetch(w, k0, k1, vw);
+  for (int kb = w; kb < nkb; kb += 4) {
+    if (kb + 4 < nkb) fetch(kb + 4, nk0, nk1, nvw);
+    const int key = kb * 16 + lc;
+    f64x4 st = {0.0, 0.0, 0.0, 0.0};
+#pragma unroll
+    for (int s = 0; s < 8; ++s)
+      st = __builtin_amdgcn_mfma_f64_16x16x4f64(key < N ? dq((unsigned)(s < 4 ? k0[s] : k1[s - 4]), lg) : 0.0, qf[s],
+                                                st, 0, 0, 0);
+    double sv[4], mb = -INFINITY;
+#pragma unroll
+    for (int r = 0; r < 4; ++r) {  // row = key 16 kb + lg + 4 r, column = query lc
+      sv[r] = kb * 16 + lg + 4 * r < N ? st[r] * scale : -INFINITY;
+      mb = fmax(mb, sv[r]);
+    }
+    mb = fmax(mb, __shfl_xor(mb, 16));
+    mb = fmax(mb, __shfl_xor(mb, 32));
+    const double mn = fmax(m, mb);
+    const double alpha = exp(m - mn);  // m = -inf on the first block: 0
+    double p[4], ps = 0.0;
+#pragma unroll
+    for (int r = 0; r < 4; ++r) {
+      p[r] = exp(sv[r] - mn);
+      ps += p[r];
+    }
+    ps += __shfl_xor(ps, 16);
+    ps += __shfl_xor(ps, 32);
+    l = l * alpha + ps;
+    m = mn;
+#pragma unroll
+    for (int db = 0; db < 4; ++db) {
+      o[db] *= alpha;
+#pragma unroll
+      for (int s = 0; s < 4; ++s)
+        o[db] = __builtin_amdgcn_mfma_f64_16x16x4f64(dq(vw[s][db], lc & 3), p[s], o[db], 0, 0, 0);
+    }
+    k0 = nk0;
+    k1 = nk1;
+#pragma unroll
+    for (int s = 0; s < 4; ++s)
+#pragma unroll
+      for (int db = 0; db < 4; ++db) vw[s][db] = nvw[s][db];
+  }
+  if (lg == 0) {
+    cm[w][lc] = m;
+    cl[w][lc] = l;
+  }
+#pragma unroll
+  for (int db = 0; db < 4; ++db)
+#pragma unroll
+    for (int r = 0; r < 4; ++r) co[w][16 * db + lg + 4 * r][lc] = o[db][r];
   __syncthreads();
-  constexpr int QPG = QB / 4;
-  const int d = tid & 63, qg = tid >> 6;
-  double o[QPG];
+
+  // combine the four partials; + pe(v); quantize into attn.x
+  const int q = tid & 15, n = qb * 16 + q;
+  if (n >= N) return;
+  double M = -INFINITY;
 #pragma unroll
-  for (int i = 0; i < QPG; ++i) o[i] = 0.0;
-  float* Vs = Qs + QB * AKD;
-  for (int k0 = 0; k0 < N; k0 += 64) {
-    __syncthreads();
-    {
-      const int kk = tid >> 2, part = tid & 3;
-      const int key = k0 + kk;
+  for (int i = 0; i < 4; ++i) M = fmax(M, cm[i][q]);
+  double f[4], L = 0.0;
 #pragma unroll
-      for (int h8 = 0; h8 < 2; ++h8) {
-        const int d0 = part * 16 + h8 * 8;
-        Vec8<i8>::type v = Vec8<i8>::zero();
-        const bool okv = key < N && d0 < a.hd;
-        if (okv) v = Vec8<i8>::load(qkv + (img + key) * a.q_ctot + hq + 2 * a.kd + d0);
-#pragma unroll
-        for (int e = 0; e < 8; ++e) Vs[kk * AHD + d0 + e] = okv ? deq((int)v[e] + 128, z_in, s_in) : 0.f;
-      }
-    }
-    __syncthreads();
-    const int kn = N - k0 < 64 ? N - k0 : 64;
-    for (int kj = 0; kj < kn; ++kj) {
-      const double v = (double)Vs[kj * AHD + d];
-#pragma unroll
-      for (int i = 0; i < QPG; ++i) o[i] = fma(S[(qg + 4 * i) * N + k0 + kj], v, o[i]);
-    }
+  for (int i = 0; i < 4; ++i) {
+    f[i] = exp(cm[i][q] - M);  // a wave without keys: exp(-inf) = 0
+    L += cl[i][q] * f[i];
   }
-  if (d >= a.hd) return;
-  const int ch = h * a.hd + d;
-  const i8* vp = qkv + img * a.q_ctot + hq + 2 * a.kd + d;
-  i8* dst = static_cast<i8*>(a.dst);
-  int wv[9];
+  // thread = (query q, 4 consecutive channels 4 dg .. 4 dg + 3): pe's 3x3 taps are 9 dword loads of v bytes and 9 of
+  // weight bytes, all issued before any arithmetic (borders: clamped address, zero weight)
+  const int y = n / a.W, x = n - y * a.W;
+  const int dg = tid >> 4, ch0 = h * AHD + 4 * dg;
+  const i8* vimg = qkv + img * a.q_ctot + hq + 2 * AKD + 4 * dg;
+  unsigned vt[9], wt[9];
 #pragma unroll
-  for (int t = 0; t < 9; ++t) wv[t] = (int)a.pe_wq[t * a.C + ch];
-  const float sa = a.pe_sasw[ch], pb = a.pe_b[ch];
+  for (int t = 0; t < 9; ++t) {
+    const int iy = y + t / 3 - 1, ix = x + t % 3 - 1;
+    const bool ok = (unsigned)iy < (unsigned)a.H && (unsigned)ix < (unsigned)a.W;
+    vt[t] = *reinterpret_cast<const unsigned*>(vimg + (size_t)(ok ? iy * a.W + ix : n) * a.q_ctot);
+    wt[t] = ok ? *reinterpret_cast<const unsigned*>(a.pe_wq + t * a.C + ch0) : 0u;
+  }
+  const f32x4 sa4 = *reinterpret_cast<const f32x4*>(a.pe_sasw + ch0), pb4 = *reinterpret_cast<const f32x4*>(a.pe_b + ch0);
+  int ov[4];
 #pragma unroll
-  for (int i = 0; i < QPG; ++i) {
-    const int n = qb * QB + qg + 4 * i;
-    if (n >= N) continue;
-    const int y = n / a.W, x = n - (n / a.W) * a.W;
+  for (int e = 0; e < 4; ++e) {
+    const int d = 4 * dg + e;
+    double od = 0.0;
+#pragma unroll
+    for (int i = 0; i < 4; ++i) od += co[i][d][q] * f[i];
     int acc = 0;
-    for (int ky = 0; ky < 3; ++ky) {
-      const int iy = y + ky - 1;
-      if ((unsigned)iy >= (unsigned)a.H) continue;
-      for (int kx = 0; kx < 3; ++kx) {
-        const int ix = x + kx - 1;
-        if ((unsigned)ix >= (unsigned)a.W) continue;
-        acc += ((int)vp[(size_t)(iy * a.W + ix) * a.q_ctot] + 128 - z_in) * wv[ky * 3 + kx];
-      }
-    }
-    const float pe = post[requant_out(acc, sa, pb, Qr)];
-    dst[((size_t)b * a.d_P + n) * a.d_ctot + a.d_coff + ch] =
-        (i8)quant_store((float)o[i] + pe, Qr->inv_so, Qr->zo, Qr->qlo, Qr->qhi);
+#pragma unroll
+    for (int t = 0; t < 9; ++t)
+      acc += (((int)((vt[t] >> (8 * e)) & 0xFFu) ^ 0x80) - z_in) * (int)(signed char)(wt[t] >> (8 * e));
+    const float pe = post[requant_out(acc, sa4[e], pb4[e], Qr)];
+    ov[e] = quant_store(__fadd_rn((float)(od / L), pe), Qr->inv_so, Qr->zo, Qr->qlo, Qr->qhi);
   }
+  *reinterpret_cast<int*>(static_cast<i8*>(a.dst) + ((size_t)b * a.d_P + n) * a.d_ctot + a.d_coff + ch0) = pack4(ov);
 }
 
 // ------------------------------------------------------------------------------------------------- requant
@@ -544,20 +577,11 @@ hipError_t ym_launch_dwconv_i8(const DwArgs& a, hipStream_t st) {
 }
 
 hipError_t ym_launch_attn_i8(const AttnArgs& a, hipStream_t st) {
-  if (a.kd > AKD || a.hd > AHD || !a.q || !a.pe_wq) return hipErrorInvalidValue;
-  const size_t budget = 150 * 1024;
-  auto lds = [&](int qb) { return (size_t)qb * a.N * sizeof(double) + ((size_t)qb * AKD + 64 * AHD) * sizeof(float); };
-  auto wgs = [&](int qb) { return (long)a.B * a.nh * ((a.N + qb - 1) / qb); };
-  if (lds(32) <= budget && wgs(32) >= 512)
-    hipLaunchKernelGGL((attn_psa_i8<32>), dim3(a.B * a.nh * ((a.N + 31) / 32)), dim3(256), lds(32), st, a);
-  else if (lds(16) <= budget && (wgs(16) >= 512 || lds(8) > budget))
-    hipLaunchKernelGGL((attn_psa_i8<16>), dim3(a.B * a.nh * ((a.N + 15) / 16)), dim3(256), lds(16), st, a);
-  else if (lds(8) <= budget)
-    hipLaunchKernelGGL((attn_psa_i8<8>), dim3(a.B * a.nh * ((a.N + 7) / 8)), dim3(256), lds(8), st, a);
-  else if (lds(4) <= budget)
-    hipLaunchKernelGGL((attn_psa_i8<4>), dim3(a.B * a.nh * ((a.N + 3) / 4)), dim3(256), lds(4), st, a);
-  else
+  // the f64 MFMA kernel's fixed head geometry (YOLO11 C2PSA: head_dim 64, key_dim 32) and 16-byte q/k rows
+  if (a.kd != AKD || a.hd != AHD || !a.q || !a.pe_wq || (a.q_ctot & 15) || (a.q_coff & 15) || a.N < 1 ||
+      (a.d_ctot & 3) || (a.d_coff & 3) || (a.C & 3))
     return hipErrorInvalidValue;
+  hipLaunchKernelGGL(attn_psa_i8, dim3(a.B * a.nh * ((a.N + 15) / 16)), dim3(256), 0, st, a);
   return hipGetLastError();
 }
 
