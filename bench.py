@@ -37,8 +37,10 @@ import torch  # noqa: E402
 import torch.distributed as dist  # noqa: E402
 
 METRIC = "images/sec @640×640 (1/2/4/8 MI355X) + mAP50-95 vs CPU ref"
-PEAK_TFLOPS = {"f16": 2500.0, "f32": 157.3, "i8": 5000.0}  # dense MFMA peaks (MI355X_MICROARCH.md; i8 = TOP/s)
-ACT_BYTES = {"f16": 2, "f32": 4, "i8": 1}
+# dense MFMA peaks (MI355X_MICROARCH.md; i8 = TOP/s; f8 = the dense fp8 peak, although the non-scaled
+# v_mfma_f32_*_fp8_fp8 the fp8 plan issues runs at the bf16 rate)
+PEAK_TFLOPS = {"f16": 2500.0, "f32": 157.3, "i8": 5000.0, "f8": 5000.0}
+ACT_BYTES = {"f16": 2, "f32": 4, "i8": 1, "f8": 1}
 PEAK_HBM_GBS = 8000.0
 
 
@@ -99,7 +101,8 @@ def conv_roofline(model, x, dtype, workload, reps=20):
         "traffic_note": (f"HBM-side bytes per forward of all conv launches (PMC FETCH_SIZE x2 + WRITE_SIZE, {tsrc}); "
                          f"algorithmic bytes per forward {int(by)}") if traffic else "no PMC summary for this workload",
         "kernel": "conv implicit GEMM (%s): all %d conv launches of one lane's forward (%d images), aggregated%s"
-                  % ("conv_i8, v_mfma_i32_32x32x32_i8" if dtype == "i8" else "conv_stream/conv_small/conv_dma/conv_halo/conv_igemm", len(conv),
+                  % ({"i8": "conv_i8, v_mfma_i32_32x32x32_i8", "f8": "conv_i8<fp8>, v_mfma_f32_32x32x16_fp8_fp8"}.get(
+                      dtype, "conv_stream/conv_small/conv_dma/conv_halo/conv_igemm"), len(conv),
                      Bl, "; int8 ops counted as FLOPs" if dtype == "i8" else ""),
         "timing": f"HIP events around a graph of {reps} back-to-back launches per op, on the launch stream",
         "launches": len(conv), "avg_launch_us": round(t_conv / len(conv) * 1e6, 2),
@@ -198,7 +201,9 @@ def cpu_baseline(scale, task, x_gpu_dets, xs, seconds, qparams=None):
                         "unknown")
     except OSError:
         cpu_name = "unknown"
-    what = "int8 oracle (oracle/quant.py: integer convs as exact float64 convs)" if qparams else "oracle"
+    fp8 = bool(qparams) and qparams.get("backend") == "fp8"
+    what = ("fp8 oracle (oracle/quant.py backend fp8: e4m3 via torch.float8_e4m3fn, exact float64 convs)" if fp8 else
+            "int8 oracle (oracle/quant.py: integer convs as exact float64 convs)" if qparams else "oracle")
     bmax = max(rates)
     n8, dt8 = rates[bmax]
     n1, dt1 = rates[1]
@@ -208,7 +213,7 @@ def cpu_baseline(scale, task, x_gpu_dets, xs, seconds, qparams=None):
                       f"{os.cpu_count()}): B={bmax}: {n8} images in {dt8:.1f}s (value); B=1: {n1} images in "
                       f"{dt1:.1f}s (value_b1)"}
     acc = {"map50_95": round(m["map"], 4), "map50": round(m["map50"], 4), "images": len(gts),
-           "gt": ("int8 oracle (CPU) detections, same qparams, as pseudo ground truth" if qparams else
+           "gt": (f"{'fp8' if fp8 else 'int8'} oracle (CPU) detections, same qparams, as pseudo ground truth" if qparams else
                   "oracle (CPU fp32) detections as pseudo ground truth"),
            "dets_gpu": int(sum(len(d) for d in x_gpu_dets)), "dets_oracle": int(sum(len(g) for g in gts))}
     if qparams is not None:  # quantisation loss: int8 GPU detections vs the float oracle's
@@ -278,7 +283,7 @@ def main():
     ap.add_argument("--task", default="detect")
     ap.add_argument("--batch", type=int, default=8, help="images per GPU per step")
     ap.add_argument("--size", type=int, default=640)
-    ap.add_argument("--dtype", default="f16", choices=["f16", "f32", "i8"])
+    ap.add_argument("--dtype", default="f16", choices=["f16", "f32", "i8", "f8"])
     ap.add_argument("--backend", default="qnnpack", choices=["qnnpack", "fbgemm"], help="i8: PTQ qconfig")
     ap.add_argument("--calib-batches", type=int, default=4, help="i8: calibration batches (B images each)")
     ap.add_argument("--cpu-seconds", type=float, default=16.0)
@@ -313,12 +318,12 @@ def main():
     # calibration (exact-f32 plan + torch.ao observers, yolomi.quant) on synthetic batches disjoint from the timed one
     t_init = time.perf_counter()
     qp = None
-    if rank == 0 and a.dtype == "i8":
+    if rank == 0 and a.dtype in ("i8", "f8"):
         from yolomi.engine import Engine
         from yolomi.quant import calibrate
         ce = Engine(a.model, a.task, synth_weights(a.model, a.task, 0), dev, "f32")
         qp = calibrate(ce, [synthetic_batch(a.batch, a.size, 500 + i, dev) for i in range(a.calib_batches)],
-                       a.backend)
+                       "fp8" if a.dtype == "f8" else a.backend)
         del ce
     blob = pack_model(a.model, a.task, synth_weights(a.model, a.task, 0), a.dtype, qp) if rank == 0 else None
     if world > 1:

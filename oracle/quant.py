@@ -36,6 +36,14 @@ the build's explicit restatement of that qconfig on the BN-fused YOLO11 graph (A
     diag-matrix BLAS product.
 Tensor names are Ultralytics module paths (act:model.2.cat, act:model.12 = layer 12's Concat, out:model.2.cv1).
 Agreement with torch.ao's own quantized kernels is checked in tests/test_quant_oracle.py (quantized::conv2d).
+
+Backend "fp8" is the fp8 variant BASELINE config 4 names ("PTQ int8 ... fp8 MFMA"; SURVEY §8(c): e4m3 emulated by
+torch.float8_e4m3fn casts): the same quantisation points and structure, with every quantized tensor an OCP e4m3
+value (the gfx950 fp8 format) times a per-tensor scale s = amax / 448 from a min/max observer (zero point 0), code
+= e4m3(clamp(v * (1/s), +-448)) rounded to nearest even; weights e4m3 per output channel (s[n] = max|w[n]| / 448).
+A QT then holds the decoded e4m3 values in `q` (z = 0), so (q - z) * s is the dequantised tensor exactly as for
+int8, and a conv's float64 accumulation of e4m3 products is exact (8-bit significands).  Parity of the GPU fp8 plan
+is a tolerance, not bit-exactness: its MFMA accumulates in fp32, and an e4m3 rounding of a near-tie can differ.
 """
 from __future__ import annotations
 
@@ -50,8 +58,10 @@ from torch.ao.quantization.observer import HistogramObserver, MinMaxObserver, Pe
 from . import postprocess as pp
 from .yolo11 import C3k, Conv, YOLO11, build
 
-BACKENDS = {"qnnpack": (False, False), "fbgemm": (True, True)}  # backend -> (activation reduce_range, per-channel w)
+# backend -> (activation reduce_range, per-channel w)
+BACKENDS = {"qnnpack": (False, False), "fbgemm": (True, True), "fp8": (False, True)}
 F32 = np.float32
+E4M3_MAX = 448.0
 
 
 def silu64(x: torch.Tensor) -> torch.Tensor:
@@ -85,6 +95,26 @@ class QT:
 
 def quantize(v: torch.Tensor, s: float, z: int, qmin: int, qmax: int) -> torch.Tensor:
     return torch.clamp(torch.round(v * _t32(inv32(s))) + z, qmin, qmax)
+
+
+def fp8_scale(amax: float) -> float:
+    """e4m3 scale of an observed range: amax / 448 in fp32 (1 / 448 for an all-zero tensor)."""
+    amax = float(amax)
+    return float(F32(amax) / F32(E4M3_MAX)) if amax > 0 else float(F32(1.0) / F32(E4M3_MAX))
+
+
+def quantize_fp8(v: torch.Tensor, s: float) -> torch.Tensor:
+    """e4m3 VALUES (as fp32) of v * (1/s): clamp to +-448, then torch's round-to-nearest-even float8_e4m3fn cast."""
+    return torch.clamp(v.float() * _t32(inv32(s)), -E4M3_MAX, E4M3_MAX).to(torch.float8_e4m3fn).float()
+
+
+def quantize_weight_fp8(w: torch.Tensor) -> Tuple[torch.Tensor, np.ndarray]:
+    """Per-output-channel e4m3 weights over axis 0: (e4m3 values as fp32, fp32 scale per channel)."""
+    w = w.detach().float().contiguous()
+    amax = w.abs().reshape(w.shape[0], -1).amax(1)
+    s = np.array([fp8_scale(float(a)) for a in amax], F32)
+    inv = torch.from_numpy((F32(1.0) / s).astype(F32)).view(-1, *([1] * (w.dim() - 1)))
+    return torch.clamp(w * inv, -E4M3_MAX, E4M3_MAX).to(torch.float8_e4m3fn).float(), s
 
 
 def quantize_weight(w: torch.Tensor, per_channel: bool) -> Tuple[torch.Tensor, np.ndarray]:
@@ -136,6 +166,7 @@ class _Ctx:
         if backend not in BACKENDS:
             raise ValueError(f"backend {backend!r} not in {list(BACKENDS)}")
         self.backend, self.mode = backend, mode
+        self.fp8 = backend == "fp8"
         self.reduce_range, self.per_channel = BACKENDS[backend]
         self.qmin, self.qmax = 0, (127 if self.reduce_range else 255)
         self.obs: Dict[str, HistogramObserver] = {}
@@ -152,9 +183,13 @@ class _Ctx:
             return
         o = self.obs.get(key)
         if o is None:
-            o = self.obs[key] = HistogramObserver(dtype=torch.quint8, qscheme=torch.per_tensor_affine,
-                                                  reduce_range=self.reduce_range)
+            o = self.obs[key] = (MinMaxObserver(dtype=torch.quint8, qscheme=torch.per_tensor_affine) if self.fp8 else
+                                 HistogramObserver(dtype=torch.quint8, qscheme=torch.per_tensor_affine,
+                                                   reduce_range=self.reduce_range))
         o(t.detach().float())
+
+    def _quantize(self, v: torch.Tensor, s: float, z: int) -> torch.Tensor:
+        return quantize_fp8(v, s) if self.fp8 else quantize(v, s, z, self.qmin, self.qmax)
 
     # ---- tensors
     def store(self, name: str, v: torch.Tensor):
@@ -170,7 +205,7 @@ class _Ctx:
         if not self.quant:
             return v
         s, z = self.qp["act:" + name]
-        return QT(quantize(v, s, z, self.qmin, self.qmax), s, z)
+        return QT(self._quantize(v, s, z), s, z)
 
     def cat(self, name: str, parts: List):
         if not self.quant:
@@ -198,6 +233,11 @@ class _Ctx:
     def weights(self, name: str, mod: nn.Module):
         if name not in self.wcache:
             convT = isinstance(mod, nn.ConvTranspose2d)
+            if self.fp8:
+                if convT:
+                    raise ValueError("the fp8 plan covers detect models (no ConvTranspose2d)")
+                self.wcache[name] = quantize_weight_fp8(mod.weight)
+                return self.wcache[name]
             wq, sw = quantize_weight(mod.weight, self.per_channel and not convT)
             if convT:  # (in, out, kh, kw): one per-tensor scale, broadcast over the output channels
                 sw = np.full(mod.weight.shape[1], sw[0], F32)
@@ -222,7 +262,7 @@ class _Ctx:
         y = acc.float() * sasw.view(1, -1, 1, 1)
         y = y + mod.bias.detach().float().view(1, -1, 1, 1)
         so, zo = self.qp["out:" + name]
-        stored = QT(quantize(y, so, zo, self.qmin, self.qmax), so, zo)
+        stored = QT(self._quantize(y, so, zo), so, zo)
         if self.trace is not None:
             self.trace["out:" + name] = stored
             self.trace["y:" + name] = y
@@ -407,6 +447,9 @@ def calibrate(net: YOLO11, batches: Sequence[torch.Tensor], backend: str = "qnnp
         forward(ctx, net, pp.load_tensor_check(im.float()).float())
     qp = {"backend": backend}
     for k, o in ctx.obs.items():
+        if backend == "fp8":
+            qp[k] = (fp8_scale(max(abs(float(o.min_val)), abs(float(o.max_val)))), 0)
+            continue
         s, z = o.calculate_qparams()
         qp[k] = (float(F32(float(s))), int(z))
     return qp

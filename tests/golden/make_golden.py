@@ -149,6 +149,19 @@ I8_FIXTURES = {
 }
 
 
+# fp8 e4m3 PTQ plan (oracle/quant.py backend "fp8"): qparams from min/max observers, fp8-oracle detections
+F8_FIXTURES = {
+    "det_n_f8": ("n", "fp8", (5401, 5402), (5501, 5502), 640),
+}
+
+
+def main_f8():
+    for name, (scale, backend, cs, seeds, S) in F8_FIXTURES.items():
+        d = det_i8_fixture(scale, backend, cs, seeds, S)
+        json.dump(d, open(os.path.join(HERE, f"{name}.json"), "w"))
+        print(name, [len(x) for x in d["dets"]])
+
+
 def main_seg():
     d = seg_fixture("s", (6001, 6002, 6003, 6004), 640)
     json.dump(d, open(os.path.join(HERE, "seg_s_uniform.json"), "w"))
@@ -179,10 +192,11 @@ def main():
 
 
 if __name__ == "__main__":
-    if len(sys.argv) > 1 and sys.argv[1] in ("i8", "seg"):
+    if len(sys.argv) > 1 and sys.argv[1] in ("i8", "seg", "f8"):
         torch.set_num_threads(min(8, os.cpu_count() or 1))
-        main_i8() if sys.argv[1] == "i8" else main_seg()
+        {"i8": main_i8, "seg": main_seg, "f8": main_f8}[sys.argv[1]]()
     else:
         main()
         main_seg()
         main_i8()
+        main_f8()

@@ -1,0 +1,144 @@
+"""GPU tests of the fp8 (e4m3) PTQ plan through the C-ABI (csrc/ym_quant.h Q8<true>: v_mfma_f32_*_fp8_fp8 convs,
+e4m3 storage) against the fp8 oracle (oracle/quant.py backend "fp8") and its committed fixture.
+
+Parity bar (a tolerance, written here).  The oracle sums e4m3 products exactly (float64); the fp8 MFMA accumulates
+in fp32 with its own internal precision, and on gfx950 a conv's output code differs from the exact one in ~0.1 % of
+the elements (measured layer-locally, tools/f8_diag.py: the same rate whether the reference sums in float64 or in
+sequential fp32, so it is the instruction's accumulation, not the order).  One such flip moves a value by an e4m3
+step (6-12 %), and through 20+ quantized layers the flips cascade (an e4m3 network is chaotic under perturbations of
+that size), so end-to-end codes cannot be compared.  The bar is therefore:
+  * the stem (image quantisation + f16 MFMA on exact e4m3 values + the e4m3 epilogue): every code exact;
+  * every plain Conv layer fed the GPU's own stored input: >= 99.8 % of the output codes exact, none more than two
+    e4m3 steps away (the requantisation to the conv's observer, then the stored tensor's: one flip, two roundings);
+  * detections: the GPU plan's quality against the float oracle within 0.7x of the fp8 oracle's own (mAP50-95 on
+    the fixture images), i.e. the quantisation loss is the fp8 scheme's, not a kernel defect.
+The e4m3 codec itself (clamp, round to nearest even) is pinned on the CPU against an independent restatement of the
+format (tests/test_fp8_oracle.py).
+"""
+import json
+import os
+
+import numpy as np
+import pytest
+import torch
+
+from oracle import quant as Q
+from tests.golden.make_golden import F8_FIXTURES, make_input
+from tests.matching import MatchReport, match_image
+from yolomi.synth import synth_weights
+
+pytestmark = pytest.mark.gpu
+GOLD = os.path.join(os.path.dirname(os.path.abspath(__file__)), "golden")
+DEV = torch.device("cuda", 0)
+_cache = {}
+
+
+def fixture(name):
+    return json.load(open(os.path.join(GOLD, name + ".json")))
+
+
+def f8_model(name):
+    if name not in _cache:
+        from core.model import YOLO11Model
+        g = fixture(name)
+        _cache[name] = YOLO11Model(task="detect", size=g["scale"], device="cuda:0", dtype="f8",
+                                   qparams=Q.qparams_from_json(g["qparams"]))
+    return _cache[name]
+
+
+def oracle_f8(name):
+    k = ("o", name)
+    if k not in _cache:
+        torch.set_num_threads(min(16, os.cpu_count() or 1))
+        g = fixture(name)
+        _cache[k] = Q.Int8OracleModel(g["scale"], "detect", synth_weights(g["scale"], "detect", 0),
+                                      Q.qparams_from_json(g["qparams"]))
+    return _cache[k]
+
+
+def decode(codes: torch.Tensor) -> torch.Tensor:
+    return codes.to(torch.uint8).view(torch.float8_e4m3fn).float()
+
+
+def _layer_local(name, layers):
+    """(layer, fraction of exact codes, max distance in e4m3 steps): the oracle's conv + SiLU + store on the GPU's
+    own stored input of that layer."""
+    import torch.nn.functional as F
+    g = fixture(name)
+    qp = Q.qparams_from_json(g["qparams"])
+    x = make_input("uniform", g["input"]["seeds"], g["input"]["size"])
+    B = x.shape[0]
+    eng = f8_model(name).model.engine
+    eng.run(x.to(DEV), use_graph=False)
+    bufs = {b.name: b for b in eng.graph.buffers}
+    mods = dict(oracle_f8(name).net.named_modules())
+    grid = torch.unique(torch.arange(256).to(torch.uint8).view(torch.float8_e4m3fn).float().nan_to_num(0.0))
+    out = []
+    for i in layers:
+        bi, bo = bufs[f"L{i - 1}"], bufs[f"L{i}"]
+        src = eng.read_buffer(bi.id, B)[..., :bi.C].permute(0, 3, 1, 2).contiguous()
+        got = eng.read_buffer(bo.id, B)[..., :bo.C].permute(0, 3, 1, 2).contiguous()
+        conv = mods[f"model.{i}"].conv
+        wq, sw = Q.quantize_weight_fp8(conv.weight)
+        sasw = (Q._t32(qp[f"act:model.{i - 1}"][0]) * torch.from_numpy(sw)).view(1, -1, 1, 1)
+        acc = F.conv2d(src.double(), wq.double(), None, conv.stride, conv.padding).float()
+        y = acc * sasw + conv.bias.detach().float().view(1, -1, 1, 1)
+        so = qp[f"out:model.{i}"][0]
+        ref = Q.quantize_fp8(Q.silu64(Q.quantize_fp8(y, so) * Q._t32(so)), qp[f"act:model.{i}"][0])
+        dist = (torch.searchsorted(grid, ref.flatten()) - torch.searchsorted(grid, got.flatten())).abs()
+        out.append((i, float((ref == got).float().mean()), int(dist.max())))
+    return out
+
+
+@pytest.mark.parametrize("name", list(F8_FIXTURES))
+def test_f8_stem_codes_exact(name):
+    g = fixture(name)
+    x = make_input("uniform", g["input"]["seeds"], g["input"]["size"])
+    _, _, ex = oracle_f8(name).raw(x)
+    eng = f8_model(name).model.engine
+    eng.run(x.to(DEV), use_graph=False)
+    b0 = next(b for b in eng.graph.buffers if b.name == "L0")
+    got = decode(eng.read_buffer(b0.id, x.shape[0], raw=True)[..., :b0.C])
+    assert torch.equal(got, ex["stored"][0].q.permute(0, 2, 3, 1))
+
+
+@pytest.mark.parametrize("name", list(F8_FIXTURES))
+def test_f8_conv_layers_match_oracle_locally(name):
+    rep = _layer_local(name, (1, 3, 5, 7, 17, 20))
+    print("fp8 layer-local (layer, exact codes, max step distance):", rep)
+    for i, same, dmax in rep:
+        assert same >= 0.998 and dmax <= 2, rep
+
+
+@pytest.mark.parametrize("name", list(F8_FIXTURES))
+def test_f8_detection_quality_is_the_schemes(name):
+    from oracle.predict import OracleModel
+    from yolomi.metrics import evaluate
+    g = fixture(name)
+    x = make_input("uniform", g["input"]["seeds"], g["input"]["size"])
+    fl = [r["boxes"].numpy() for r in OracleModel(g["scale"], "detect", synth_weights(g["scale"], "detect", 0)).predict(x)]
+    o8 = [np.array(d, np.float32).reshape(-1, 6) for d in g["dets"]]
+    g8 = [r.boxes.data.cpu().numpy() for r in f8_model(name).predict(x.to(DEV), conf=g["conf"], iou=g["iou"])]
+    m_o8, m_g8 = evaluate(o8, fl)["map"], evaluate(g8, fl)["map"]
+    print(f"fp8 mAP50-95 vs float oracle: fp8 oracle {m_o8:.3f}, GPU fp8 plan {m_g8:.3f}; GPU vs fp8 oracle "
+          f"{evaluate(g8, o8)['map']:.3f}")
+    assert m_g8 >= 0.7 * m_o8
+
+
+def test_f8_graph_replay_bitwise_equals_eager():
+    name = next(iter(F8_FIXTURES))
+    g = fixture(name)
+    eng = f8_model(name).model.engine
+    x = make_input("uniform", g["input"]["seeds"], g["input"]["size"]).to(DEV)
+    d0, c0 = (t.clone() for t in eng.run(x, use_graph=False))
+    d1, c1 = (t.clone() for t in eng.run(x, use_graph=True))
+    assert torch.equal(c0, c1) and torch.equal(d0, d1)
+
+
+def test_f8_plan_is_distinct_from_int8():
+    """The fp8 blob is dtype 3 and its convs carry e4m3 codes: the same weights packed as int8 differ."""
+    from yolomi.plan import DTYPES
+    name = next(iter(F8_FIXTURES))
+    eng = f8_model(name).model.engine
+    assert np.frombuffer(eng.blob[:12], np.int32)[2] == DTYPES["f8"]
+    assert eng.rt.n_ops == len(eng.graph.ops)

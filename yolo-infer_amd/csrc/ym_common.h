@@ -13,7 +13,9 @@ typedef float f32x8 __attribute__((ext_vector_type(8)));
 
 // Activation storage precision of a plan: f16 (MFMA 32x32x16 f16), f32 (exact-f32 MFMA 32x32x2, parity mode) or
 // i8 (PTQ int8: activations stored as q - 128 in int8, weights int8, MFMA 32x32x32 i8 with int32 accumulation).
-enum { YM_DT_F16 = 0, YM_DT_F32 = 1, YM_DT_I8 = 2 };
+enum { YM_DT_F16 = 0, YM_DT_F32 = 1, YM_DT_I8 = 2, YM_DT_F8 = 3 };
+// one-byte quantized plans (int8 affine / fp8 e4m3): same graph, storage and kernels (csrc/ym_quant.h Q8)
+inline bool ym_dt_q8(int dt) { return dt == YM_DT_I8 || dt == YM_DT_F8; }
 
 typedef signed char i8;
 
@@ -250,10 +252,11 @@ hipError_t ym_launch_conv_halo(int out_f32, const ConvArgs& a, int i, hipStream_
 int ym_conv_halo_num_cfgs();
 hipError_t ym_launch_masks(const MaskArgs& a, hipStream_t st);  // Segment: process_mask(upsample=True)
 // int8 (PTQ) plans: csrc/ym_conv_i8.hip
-hipError_t ym_launch_conv_i8(const ConvArgs& a, int cfg, hipStream_t st, bool strict);
+// (f8: the fp8 e4m3 PTQ plan on the same kernels, csrc/ym_quant.h Q8<true>)
+hipError_t ym_launch_conv_i8(const ConvArgs& a, int cfg, hipStream_t st, bool strict, bool f8);
 int ym_conv_i8_num_cfgs();
-hipError_t ym_launch_conv_i8_stream(const ConvArgs& a, int i, hipStream_t st);
+hipError_t ym_launch_conv_i8_stream(const ConvArgs& a, int i, hipStream_t st, bool f8);
 int ym_conv_i8_stream_num_cfgs();
-hipError_t ym_launch_dwconv_i8(const DwArgs& a, hipStream_t st);
-hipError_t ym_launch_attn_i8(const AttnArgs& a, hipStream_t st);
-hipError_t ym_launch_requant(const ReqArgs& a, hipStream_t st);
+hipError_t ym_launch_dwconv_i8(const DwArgs& a, hipStream_t st, bool f8);
+hipError_t ym_launch_attn_i8(const AttnArgs& a, hipStream_t st, bool f8);
+hipError_t ym_launch_requant(const ReqArgs& a, hipStream_t st, bool f8);

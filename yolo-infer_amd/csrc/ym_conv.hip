@@ -632,7 +632,7 @@ hipError_t ym_launch_conv(int dtype, int out_f32, const ConvArgs& a, int cfg, hi
   else if (a.k == 3 && !a.src1 && !a.up0) kind = 3;
   else kind = -1;
   if (kind < 0) return hipErrorInvalidValue;
-  if (dtype == YM_DT_I8) return ym_launch_conv_i8(a, cfg, st, strict);  // csrc/ym_conv_i8.hip
+  if (ym_dt_q8(dtype)) return ym_launch_conv_i8(a, cfg, st, strict, dtype == YM_DT_F8);  // csrc/ym_conv_i8.hip
   // (concat/upsample sources only feed 1x1 convs; YOLO11 has k in {1, 3})
   if (a.Kpad % KSTEP) return hipErrorInvalidValue;
   if (a.w2) {  // fused pair: only the streaming kernels hold a whole N in one wave (csrc/ym_conv_stream.hip)

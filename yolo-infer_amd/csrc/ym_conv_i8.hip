@@ -21,7 +21,7 @@
 #include "ym_common.h"
 #include "ym_quant.h"
 
-typedef int i32x16 __attribute__((ext_vector_type(16)));
+
 
 namespace {
 
@@ -41,8 +41,9 @@ __device__ __forceinline__ bool xcd_tile(const ConvArgs& a, int BM, int& tm, int
 // WTM x WTN 32x32 blocks per wave; WM x WN x WK waves (WK: intra-workgroup split-K, partial tiles summed through LDS
 // — integer sums, so the result does not depend on the split).  KIND 1: 1x1 stride 1; KIND 3: 3x3 (stride a.s).
 // a.Cin8 holds the number of 16-channel blocks per tap in int8 plans.
-template <int WTM, int WTN, int WM, int WN, int WK, int KIND>
+template <int WTM, int WTN, int WM, int WN, int WK, int KIND, bool F8>
 __global__ __launch_bounds__(WM * WN * WK * 64) void conv_i8(const ConvArgs a) {
+  typedef Q8<F8> QS;
   constexpr int BM = WM * WTM * 32, BN = WN * WTN * 32, NT = WM * WN * WK * 64;
   __shared__ float post[256];
   const int lane = threadIdx.x & 63;
@@ -95,7 +96,7 @@ __global__ __launch_bounds__(WM * WN * WK * 64) void conv_i8(const ConvArgs a) {
     tap0 = c / a.Cin8;
     cb0 = c - tap0 * a.Cin8;
   }
-  const int fb = (Q->z_in - 128) & 0xFF;
+  const int fb = QS::pad_byte(Q);
   const int f4 = fb | (fb << 8) | (fb << 16) | (fb << 24);
   const i8x16 FILL = __builtin_bit_cast(i8x16, i32x4{f4, f4, f4, f4});
   const i8x16 ZERO = __builtin_bit_cast(i8x16, i32x4{0, 0, 0, 0});
@@ -121,7 +122,7 @@ __global__ __launch_bounds__(WM * WN * WK * 64) void conv_i8(const ConvArgs a) {
     }
   };
 
-  i32x16 acc[WTM][WTN];
+  typename QS::acc16 acc[WTM][WTN];
 #pragma unroll
   for (int i = 0; i < WTM; ++i)
 #pragma unroll
@@ -146,7 +147,7 @@ __global__ __launch_bounds__(WM * WN * WK * 64) void conv_i8(const ConvArgs a) {
       for (int i = 0; i < WTM; ++i)
 #pragma unroll
         for (int j = 0; j < WTN; ++j)
-          acc[i][j] = __builtin_amdgcn_mfma_i32_32x32x32_i8(fa[s][j], fbv[s][i], acc[i][j], 0, 0, 0);
+          acc[i][j] = mfma32(fa[s][j], fbv[s][i], acc[i][j]);
   };
 
   if (g < nsteps) load_step(fa0, fb0);
@@ -159,11 +160,12 @@ __global__ __launch_bounds__(WM * WN * WK * 64) void conv_i8(const ConvArgs a) {
   }
 
   if constexpr (WK > 1) {
-    extern __shared__ int red[];  // [(WK-1)][WM*WN][WTM*WTN*16][64]
+    extern __shared__ int red_raw[];  // [(WK-1)][WM*WN][WTM*WTN*16][64]
+    typename QS::acc_t* red = reinterpret_cast<typename QS::acc_t*>(red_raw);
     constexpr int PER = WTM * WTN * 16;
     const int grp = wid / WK;
     if (wk > 0) {
-      int* dst = red + ((size_t)((wk - 1) * (WM * WN) + grp) * PER) * 64 + lane;
+      typename QS::acc_t* dst = red + ((size_t)((wk - 1) * (WM * WN) + grp) * PER) * 64 + lane;
 #pragma unroll
       for (int i = 0; i < WTM; ++i)
 #pragma unroll
@@ -175,7 +177,7 @@ __global__ __launch_bounds__(WM * WN * WK * 64) void conv_i8(const ConvArgs a) {
     if (wk > 0) return;
 #pragma unroll 1
     for (int q = 1; q < WK; ++q) {
-      const int* src = red + ((size_t)((q - 1) * (WM * WN) + grp) * PER) * 64 + lane;
+      const typename QS::acc_t* src = red + ((size_t)((q - 1) * (WM * WN) + grp) * PER) * 64 + lane;
 #pragma unroll
       for (int i = 0; i < WTM; ++i)
 #pragma unroll
@@ -201,7 +203,7 @@ __global__ __launch_bounds__(WM * WN * WK * 64) void conv_i8(const ConvArgs a) {
       for (int q = 0; q < 4; ++q) {
         const int n = nbase + j * 32 + 8 * q + 4 * h;
         if (n >= a.N) continue;
-        const i32x4 bi = *reinterpret_cast<const i32x4*>(a.biasi + n);
+        const i32x4 bi = F8 ? i32x4{0, 0, 0, 0} : *reinterpret_cast<const i32x4*>(a.biasi + n);
         const f32x4 sa = *reinterpret_cast<const f32x4*>(a.sasw + n);
         const f32x4 bf = *reinterpret_cast<const f32x4*>(a.bias + n);
         const int r4 = res ? *reinterpret_cast<const int*>(res + rbase + n) : 0;
@@ -209,15 +211,15 @@ __global__ __launch_bounds__(WM * WN * WK * 64) void conv_i8(const ConvArgs a) {
         float fv[4];
 #pragma unroll
         for (int e = 0; e < 4; ++e) {
-          const int qc = requant_out(acc[i][j][4 * q + e] + bi[e], sa[e], bf[e], Q);
+          const int qc = QS::code(acc[i][j][4 * q + e], bi[e], sa[e], bf[e], Q);
           if (mode == 1) {
-            ov[e] = qc - 128;
+            ov[e] = QS::raw_byte(qc);
             continue;
           }
           float v = post[qc];
-          if (res) v = __fadd_rn(v, deq(((r4 >> (8 * e)) & 0xFF) ^ 0x80, Q->z_r, Q->s_r));
+          if (res) v = __fadd_rn(v, QS::dec(r4 >> (8 * e), Q->z_r, Q->s_r));
           fv[e] = v;
-          ov[e] = quant_store(v, Q->inv_so, Q->zo, Q->qlo, Q->qhi);
+          ov[e] = QS::store(v, Q);
         }
         size_t off = obase + n;
         if (a.shuffle) {
@@ -232,7 +234,7 @@ __global__ __launch_bounds__(WM * WN * WK * 64) void conv_i8(const ConvArgs a) {
   }
 }
 
-template <int WTM, int WTN, int WM, int WN, int WK>
+template <int WTM, int WTN, int WM, int WN, int WK, bool F8>
 hipError_t launch_cfg(ConvArgs a, int kind, hipStream_t st) {
   constexpr int BM = WM * WTM * 32, BN = WN * WTN * 32, NT = WM * WN * WK * 64;
   const int tiles_m8 = ((a.M + BM - 1) / BM + 7) / 8 * 8;
@@ -240,9 +242,9 @@ hipError_t launch_cfg(ConvArgs a, int kind, hipStream_t st) {
   const size_t lds = WK > 1 ? (size_t)(WK - 1) * WM * WN * WTM * WTN * 16 * 64 * sizeof(int) : 0;
   const dim3 grid(tiles_m8 * a.tiles_n);
   if (kind == 1)
-    hipLaunchKernelGGL((conv_i8<WTM, WTN, WM, WN, WK, 1>), grid, dim3(NT), lds, st, a);
+    hipLaunchKernelGGL((conv_i8<WTM, WTN, WM, WN, WK, 1, F8>), grid, dim3(NT), lds, st, a);
   else
-    hipLaunchKernelGGL((conv_i8<WTM, WTN, WM, WN, WK, 3>), grid, dim3(NT), lds, st, a);
+    hipLaunchKernelGGL((conv_i8<WTM, WTN, WM, WN, WK, 3, F8>), grid, dim3(NT), lds, st, a);
   return hipGetLastError();
 }
 
@@ -271,10 +273,10 @@ constexpr Cfg kCfgs[] = {
 };
 constexpr int kNumCfg = sizeof(kCfgs) / sizeof(kCfgs[0]);
 
-hipError_t launch_id(int id, const ConvArgs& a, int kind, hipStream_t st) {
+hipError_t launch_id(int id, const ConvArgs& a, int kind, hipStream_t st, bool f8) {
   switch (id) {
 #define YM_X(cid, A, B, C, D, E) \
-  case cid: return launch_cfg<A, B, C, D, E>(a, kind, st);
+  case cid: return f8 ? launch_cfg<A, B, C, D, E, true>(a, kind, st) : launch_cfg<A, B, C, D, E, false>(a, kind, st);
     YM_I8_CFGS(YM_X)
 #undef YM_X
   }
@@ -307,8 +309,11 @@ int choose_cfg(const ConvArgs& a) {
 
 // ------------------------------------------------------------------------------------------------- depthwise
 // DWConv 3x3 (Detect cv3): one thread = 8 channels of one pixel; acc = Σ over in-image taps (q - z_in)·w, then the
-// quantized-conv epilogue (mode 0).
+// quantized-conv epilogue (mode 0).  fp8: the 9 products of e4m3 values are summed in float64 (exact: 8-bit
+// significands) and rounded to fp32 once, as the oracle's float64 conv does.
+template <bool F8>
 __global__ __launch_bounds__(256) void dwconv3x3_i8(const DwArgs a) {
+  typedef Q8<F8> QS;
   __shared__ float post[256];
   const QRec* Q = a.q;
   post[threadIdx.x] = Q->post[threadIdx.x];
@@ -342,20 +347,31 @@ __global__ __launch_bounds__(256) void dwconv3x3_i8(const DwArgs a) {
   const f32x4 bb0 = *reinterpret_cast<const f32x4*>(a.bias + c0), bb1 = *reinterpret_cast<const f32x4*>(a.bias + c0 + 4);
   const float sav[8] = {sa0[0], sa0[1], sa0[2], sa0[3], sa1[0], sa1[1], sa1[2], sa1[3]};
   const float bbv[8] = {bb0[0], bb0[1], bb0[2], bb0[3], bb1[0], bb1[1], bb1[2], bb1[3]};
-  int acc[8];
-#pragma unroll
-  for (int e = 0; e < 8; ++e) acc[e] = 0;
-#pragma unroll
-  for (int t = 0; t < 9; ++t)
-    if (ok[t]) {
-#pragma unroll
-      for (int e = 0; e < 8; ++e) acc[e] += ((int)v[t][e] + 128 - zi) * (int)w[t][e];
-    }
   V o;
+  if constexpr (F8) {
+    double acc[8];
 #pragma unroll
-  for (int e = 0; e < 8; ++e) {
-    const int qc = requant_out(acc[e], sav[e], bbv[e], Q);
-    o[e] = (i8)quant_store(post[qc], Q->inv_so, Q->zo, Q->qlo, Q->qhi);
+    for (int e = 0; e < 8; ++e) acc[e] = 0.0;
+#pragma unroll
+    for (int t = 0; t < 9; ++t)
+      if (ok[t]) {
+#pragma unroll
+        for (int e = 0; e < 8; ++e) acc[e] = fma((double)f8_dec(v[t][e]), (double)f8_dec(w[t][e]), acc[e]);
+      }
+#pragma unroll
+    for (int e = 0; e < 8; ++e) o[e] = (i8)QS::store(post[QS::code((float)acc[e], 0, sav[e], bbv[e], Q)], Q);
+  } else {
+    int acc[8];
+#pragma unroll
+    for (int e = 0; e < 8; ++e) acc[e] = 0;
+#pragma unroll
+    for (int t = 0; t < 9; ++t)
+      if (ok[t]) {
+#pragma unroll
+        for (int e = 0; e < 8; ++e) acc[e] += ((int)v[t][e] + 128 - zi) * (int)w[t][e];
+      }
+#pragma unroll
+    for (int e = 0; e < 8; ++e) o[e] = (i8)QS::store(post[QS::code(acc[e], 0, sav[e], bbv[e], Q)], Q);
   }
   Vec8<i8>::store(static_cast<i8*>(a.dst) + (size_t)(b * a.d_P + p) * a.d_ctot + a.d_coff + c0, o);
 }
@@ -375,7 +391,9 @@ __global__ __launch_bounds__(256) void dwconv3x3_i8(const DwArgs a) {
 constexpr int AKD = 32, AHD = 64;
 typedef double f64x4 __attribute__((ext_vector_type(4)));
 
+template <bool F8>
 __global__ __launch_bounds__(256) void attn_psa_i8(const AttnArgs a) {
+  typedef Q8<F8> QS;
   __shared__ float post[256];
   __shared__ double cm[4][16], cl[4][16];
   __shared__ double co[4][AHD][17];  // Oᵀ partials [wave][d][q] (odd pitch: the column reads below)
@@ -393,8 +411,8 @@ __global__ __launch_bounds__(256) void attn_psa_i8(const AttnArgs a) {
   const float s_in = Qr->s_in;
   const int z_in = Qr->z_in;
   const double scale = (double)a.scale;
-  auto dq = [&](unsigned word, int byte) {  // stored byte (q - 128) of a little-endian word -> f64 of deq(q)
-    return (double)deq((int)((word >> (8 * byte)) & 0xFFu) ^ 0x80, z_in, s_in);
+  auto dq = [&](unsigned word, int byte) {  // stored byte of a little-endian word -> f64 of its dequantised value
+    return (double)QS::dec((int)(word >> (8 * byte)), z_in, s_in);
   };
   // Qᵀ operand: Qᵀ[c = 4s + lg][q = lc]
   double qf[8];
@@ -514,19 +532,30 @@ __global__ __launch_bounds__(256) void attn_psa_i8(const AttnArgs a) {
     double od = 0.0;
 #pragma unroll
     for (int i = 0; i < 4; ++i) od += co[i][d][q] * f[i];
-    int acc = 0;
+    int qc;
+    if constexpr (F8) {  // pe on e4m3 values: float64 sum of exact products, one rounding (as dwconv3x3_i8)
+      double acc = 0.0;
 #pragma unroll
-    for (int t = 0; t < 9; ++t)
-      acc += (((int)((vt[t] >> (8 * e)) & 0xFFu) ^ 0x80) - z_in) * (int)(signed char)(wt[t] >> (8 * e));
-    const float pe = post[requant_out(acc, sa4[e], pb4[e], Qr)];
-    ov[e] = quant_store(__fadd_rn((float)(od / L), pe), Qr->inv_so, Qr->zo, Qr->qlo, Qr->qhi);
+      for (int t = 0; t < 9; ++t)
+        acc = fma((double)f8_dec((int)(vt[t] >> (8 * e))), (double)f8_dec((int)(wt[t] >> (8 * e))), acc);
+      qc = QS::code((float)acc, 0, sa4[e], pb4[e], Qr);
+    } else {
+      int acc = 0;
+#pragma unroll
+      for (int t = 0; t < 9; ++t)
+        acc += (((int)((vt[t] >> (8 * e)) & 0xFFu) ^ 0x80) - z_in) * (int)(signed char)(wt[t] >> (8 * e));
+      qc = QS::code(acc, 0, sa4[e], pb4[e], Qr);
+    }
+    ov[e] = QS::store(__fadd_rn((float)(od / L), post[qc]), Qr);
   }
   *reinterpret_cast<int*>(static_cast<i8*>(a.dst) + ((size_t)b * a.d_P + n) * a.d_ctot + a.d_coff + ch0) = pack4(ov);
 }
 
 // ------------------------------------------------------------------------------------------------- requant
 // dst[p, coff + c] = quantize(dequantize(src[p' , c])) with p' = p or (y/2, x/2): 16 channels per thread.
+template <bool F8>
 __global__ __launch_bounds__(256) void requant_copy(const ReqArgs a) {
+  typedef Q8<F8> QS;
   const int C16 = a.C >> 4;
   const long idx = blockIdx.x * (long)blockDim.x + threadIdx.x;
   const long total = (long)a.B * a.H * a.W * C16;
@@ -543,7 +572,7 @@ __global__ __launch_bounds__(256) void requant_copy(const ReqArgs a) {
   int ov[16];
 #pragma unroll
   for (int e = 0; e < 16; ++e)
-    ov[e] = quant_store(deq((int)v[e] + 128, Q->z_in, Q->s_in), Q->inv_so, Q->zo, Q->qlo, Q->qhi);
+    ov[e] = QS::store(QS::dec(v[e], Q->z_in, Q->s_in), Q);
   const i32x4 o{pack4(ov), pack4(ov + 4), pack4(ov + 8), pack4(ov + 12)};
   *reinterpret_cast<i32x4*>(a.dst + (size_t)(b * a.d_P + p) * a.d_ctot + a.d_coff + cg * 16) = o;
 }
@@ -553,7 +582,7 @@ __global__ __launch_bounds__(256) void requant_copy(const ReqArgs a) {
 // ids [0, kNumCfg): conv_i8 above; then the streaming / small-M int8 kernels (csrc/ym_conv_i8_stream.hip)
 int ym_conv_i8_num_cfgs() { return kNumCfg + ym_conv_i8_stream_num_cfgs(); }
 
-hipError_t ym_launch_conv_i8(const ConvArgs& a, int cfg, hipStream_t st, bool strict) {
+hipError_t ym_launch_conv_i8(const ConvArgs& a, int cfg, hipStream_t st, bool strict, bool f8) {
   int kind;
   if (a.k == 1 && a.s == 1 && !a.src1 && !a.up0) kind = 1;
   else if (a.k == 3 && !a.src1 && !a.up0) kind = 3;
@@ -561,33 +590,37 @@ hipError_t ym_launch_conv_i8(const ConvArgs& a, int cfg, hipStream_t st, bool st
   if (a.Kpad % KSTEP || !a.q || !a.sasw || !a.biasi || (a.N & 3) || (a.s0_ctot & 15) || (a.s0_coff & 15))
     return hipErrorInvalidValue;
   if (cfg >= kNumCfg) {
-    const hipError_t e = ym_launch_conv_i8_stream(a, cfg - kNumCfg, st);
+    const hipError_t e = ym_launch_conv_i8_stream(a, cfg - kNumCfg, st, f8);
     if (e != hipErrorInvalidValue || strict) return e;
     cfg = -1;  // a pinned table entry that does not apply: the heuristic
   }
-  return launch_id(cfg >= 0 ? cfg : choose_cfg(a), a, kind, st);
+  return launch_id(cfg >= 0 ? cfg : choose_cfg(a), a, kind, st, f8);
 }
 
-hipError_t ym_launch_dwconv_i8(const DwArgs& a, hipStream_t st) {
+hipError_t ym_launch_dwconv_i8(const DwArgs& a, hipStream_t st, bool f8) {
   if (a.C % 8 || !a.q || !a.wq) return hipErrorInvalidValue;
   const long total = (long)a.B * a.H * a.W * (a.C / 8);
   if (total >= 0x7FFFFFFFL - 256) return hipErrorInvalidValue;  // the kernel indexes in 32 bits
-  hipLaunchKernelGGL(dwconv3x3_i8, dim3((total + 255) / 256), dim3(256), 0, st, a);
+  if (f8) hipLaunchKernelGGL(dwconv3x3_i8<true>, dim3((total + 255) / 256), dim3(256), 0, st, a);
+  else hipLaunchKernelGGL(dwconv3x3_i8<false>, dim3((total + 255) / 256), dim3(256), 0, st, a);
   return hipGetLastError();
 }
 
-hipError_t ym_launch_attn_i8(const AttnArgs& a, hipStream_t st) {
+hipError_t ym_launch_attn_i8(const AttnArgs& a, hipStream_t st, bool f8) {
   // the f64 MFMA kernel's fixed head geometry (YOLO11 C2PSA: head_dim 64, key_dim 32) and 16-byte q/k rows
   if (a.kd != AKD || a.hd != AHD || !a.q || !a.pe_wq || (a.q_ctot & 15) || (a.q_coff & 15) || a.N < 1 ||
       (a.d_ctot & 3) || (a.d_coff & 3) || (a.C & 3))
     return hipErrorInvalidValue;
-  hipLaunchKernelGGL(attn_psa_i8, dim3(a.B * a.nh * ((a.N + 15) / 16)), dim3(256), 0, st, a);
+  const dim3 grid(a.B * a.nh * ((a.N + 15) / 16));
+  if (f8) hipLaunchKernelGGL(attn_psa_i8<true>, grid, dim3(256), 0, st, a);
+  else hipLaunchKernelGGL(attn_psa_i8<false>, grid, dim3(256), 0, st, a);
   return hipGetLastError();
 }
 
-hipError_t ym_launch_requant(const ReqArgs& a, hipStream_t st) {
+hipError_t ym_launch_requant(const ReqArgs& a, hipStream_t st, bool f8) {
   if (a.C % 16 || a.s_coff % 16 || a.d_coff % 16 || a.s_ctot % 16 || a.d_ctot % 16 || !a.q) return hipErrorInvalidValue;
   const long total = (long)a.B * a.H * a.W * (a.C / 16);
-  hipLaunchKernelGGL(requant_copy, dim3((total + 255) / 256), dim3(256), 0, st, a);
+  if (f8) hipLaunchKernelGGL(requant_copy<true>, dim3((total + 255) / 256), dim3(256), 0, st, a);
+  else hipLaunchKernelGGL(requant_copy<false>, dim3((total + 255) / 256), dim3(256), 0, st, a);
   return hipGetLastError();
 }

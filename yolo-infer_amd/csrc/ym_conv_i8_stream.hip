@@ -59,32 +59,34 @@ __device__ __forceinline__ i8x16 gather(const ConvArgs& a, const i8* img, bool o
 }
 
 // the quantized-conv epilogue of 4 consecutive channels n0.. of one pixel (csrc/ym_conv_i8.hip conv_i8)
+template <bool F8>
 __device__ __forceinline__ void epilogue4(const ConvArgs& a, const QRec* Q, int mode, const float* post,
-                                          const i32x4 acc, const int* bi, const float* sa, const float* bf, int n0,
-                                          size_t obase, size_t rbase) {
+                                          const typename Q8<F8>::acc4 acc, const int* bi, const float* sa,
+                                          const float* bf, int n0, size_t obase, size_t rbase) {
+  typedef Q8<F8> QS;
   const i8* res = static_cast<const i8*>(a.res);
   const int r4 = res ? *reinterpret_cast<const int*>(res + rbase + n0) : 0;
   int ov[4];
   float fv[4];
 #pragma unroll
   for (int e = 0; e < 4; ++e) {
-    const int qc = requant_out(acc[e] + bi[e], sa[e], bf[e], Q);
+    const int qc = QS::code(acc[e], F8 ? 0 : bi[e], sa[e], bf[e], Q);
     if (mode == 1) {
-      ov[e] = qc - 128;
+      ov[e] = QS::raw_byte(qc);
       fv[e] = 0.f;
       continue;
     }
     float v = post[qc];
-    if (res) v = __fadd_rn(v, deq(((r4 >> (8 * e)) & 0xFF) ^ 0x80, Q->z_r, Q->s_r));
+    if (res) v = __fadd_rn(v, QS::dec(r4 >> (8 * e), Q->z_r, Q->s_r));
     fv[e] = v;
-    ov[e] = quant_store(v, Q->inv_so, Q->zo, Q->qlo, Q->qhi);
+    ov[e] = QS::store(v, Q);
   }
   if (mode == 2) *reinterpret_cast<f32x4*>(static_cast<float*>(a.dst) + obase + n0) = f32x4{fv[0], fv[1], fv[2], fv[3]};
   else *reinterpret_cast<int*>(static_cast<i8*>(a.dst) + obase + n0) = pack4(ov);
 }
 
 // ------------------------------------------------------------------------------------------------ streaming
-template <int KIND, int KS, int PX>
+template <int KIND, int KS, int PX, bool F8>
 __global__ __launch_bounds__(256) void conv_stream_i8(const ConvArgs a) {
   constexpr int KP = KS * 64;   // Kpad (bytes per weight row)
   constexpr int LDW = KP + 16;  // LDS row pitch: +16 bytes spreads the 16-row fragment reads over the banks
@@ -122,9 +124,14 @@ __global__ __launch_bounds__(256) void conv_stream_i8(const ConvArgs a) {
   }
   const int HW = a.Ho * a.Wo;
   const int G = (a.M + 15) >> 4;
-  const int nw = gridDim.x * 4;
+  // XCD-contiguous group ranges (as csrc/ym_conv_stream.hip conv_stream)
+  const int nwg = gridDim.x, xcd = blockIdx.x & 7, slot = blockIdx.x >> 3;
+  const int nwx = (nwg >> 3) + (xcd < (nwg & 7));
+  const int v0 = xcd * (nwg >> 3) + (xcd < (nwg & 7) ? xcd : (nwg & 7));
+  const int gend = (int)((long)G * (v0 + nwx) / nwg);
+  const int step = nwx * 4 * PX;
   const unsigned c16m = (0x1000000u + a.Cin8 - 1) / a.Cin8;
-  const int fb = (Q->z_in - 128) & 0xFF;
+  const int fb = Q8<F8>::pad_byte(Q);
   const int f4 = fb | (fb << 8) | (fb << 16) | (fb << 24);
   const i8x16 fill = __builtin_bit_cast(i8x16, i32x4{f4, f4, f4, f4});
   const i8* s0 = static_cast<const i8*>(a.src0) + a.s0_coff;
@@ -132,7 +139,7 @@ __global__ __launch_bounds__(256) void conv_stream_i8(const ConvArgs a) {
 #pragma unroll
     for (int p = 0; p < PX; ++p) {
       const int m = (gb + p) * 16 + col;
-      const bool ok = gb + p < G && m < a.M;
+      const bool ok = gb + p < gend && m < a.M;
       const int mm = ok ? m : 0;
       const int b = ym_div(mm, a.fd_hw), rem = mm - b * HW;
       const int y = ym_div(rem, a.fd_w), x = rem - y * a.Wo;
@@ -141,13 +148,13 @@ __global__ __launch_bounds__(256) void conv_stream_i8(const ConvArgs a) {
       for (int ks = 0; ks < KS; ++ks) bf[p][ks] = gather<KIND>(a, img, ok, y, x, ks, g, c16m, fill);
     }
   };
-  int gb = (blockIdx.x * 4 + wave) * PX;
+  int gb = (int)((long)G * v0 / nwg) + (slot * 4 + wave) * PX;
   i8x16 cur[PX][KS], nxt[PX][KS];
   load(gb, cur);
   __syncthreads();
   const int mode = Q->mode;
-  for (; gb < G; gb += nw * PX) {
-    if (gb + nw * PX < G) load(gb + nw * PX, nxt);
+  for (; gb < gend; gb += step) {
+    if (gb + step < gend) load(gb + step, nxt);
     size_t ob[PX], rb[PX];
     bool okp[PX];
 #pragma unroll
@@ -155,7 +162,7 @@ __global__ __launch_bounds__(256) void conv_stream_i8(const ConvArgs a) {
       const int m = (gb + p) * 16 + col;
       const int b = ym_div(m, a.fd_hw), rem = m - b * HW;
       const int y = ym_div(rem, a.fd_w), x = rem - y * a.Wo;
-      okp[p] = gb + p < G && m < a.M;
+      okp[p] = gb + p < gend && m < a.M;
       ob[p] = (size_t)(b * a.d_P + a.d_pixoff + y * a.d_W + x) * a.d_ctot + a.d_coff;
       rb[p] = (size_t)(b * a.r_P + y * a.Wo + x) * a.r_ctot + a.r_coff;
     }
@@ -166,11 +173,11 @@ __global__ __launch_bounds__(256) void conv_stream_i8(const ConvArgs a) {
       const int n0 = 16 * nb + 4 * g;
 #pragma unroll
       for (int p = 0; p < PX; ++p) {
-        i32x4 acc = {0, 0, 0, 0};
+        typename Q8<F8>::acc4 acc = {0, 0, 0, 0};
 #pragma unroll
-        for (int ks = 0; ks < KS; ++ks) acc = __builtin_amdgcn_mfma_i32_16x16x64_i8(af[ks], cur[p][ks], acc, 0, 0, 0);
+        for (int ks = 0; ks < KS; ++ks) acc = mfma16(af[ks], cur[p][ks], acc);
         if (!okp[p] || n0 >= a.N) continue;
-        epilogue4(a, Q, mode, post, acc, sbi + n0, ssa + n0, sbf + n0, n0, ob[p], rb[p]);
+        epilogue4<F8>(a, Q, mode, post, acc, sbi + n0, ssa + n0, sbf + n0, n0, ob[p], rb[p]);
       }
     }
 #pragma unroll
@@ -180,7 +187,7 @@ __global__ __launch_bounds__(256) void conv_stream_i8(const ConvArgs a) {
   }
 }
 
-template <int KIND, int KS, int PX, int CAP>
+template <int KIND, int KS, int PX, int CAP, bool F8>
 hipError_t launch_stream(const ConvArgs& a, hipStream_t st) {
   if (a.Kpad != KS * 64 || a.k != KIND) return hipErrorInvalidValue;
   const int G = (a.M + 15) / 16;
@@ -189,25 +196,27 @@ hipError_t launch_stream(const ConvArgs& a, hipStream_t st) {
   const int NP = (a.N + 15) & ~15;
   const size_t lds = 256 * 4 + (size_t)NP * 12 + (size_t)NP * (KS * 64 + 16);
   if (lds > kMaxLds) return hipErrorInvalidValue;
-  hipLaunchKernelGGL((conv_stream_i8<KIND, KS, PX>), dim3(wgs), dim3(256), lds, st, a);
+  hipLaunchKernelGGL((conv_stream_i8<KIND, KS, PX, F8>), dim3(wgs), dim3(256), lds, st, a);
   return hipGetLastError();
 }
 
 // ------------------------------------------------------------------------------------------------ small M
-template <int KIND, int KSW, int PXG>
+template <int KIND, int KSW, int PXG, bool F8>
 __global__ __launch_bounds__(256) void conv_small_i8(const ConvArgs a) {
-  __shared__ i32x4 red[3][PXG][64];
+  typedef typename Q8<F8>::acc4 A4;
+  __shared__ A4 red[3][PXG][64];
   __shared__ float post[256];
   const int tid = threadIdx.x, lane = tid & 63, wave = tid >> 6;
   const int g = lane >> 4, col = lane & 15;
   const QRec* Q = a.q;
   post[tid] = Q->post[tid];
   const int ntn = (a.N + 15) >> 4;
-  const int tn = blockIdx.x % ntn, tm = blockIdx.x / ntn;
+  const int vb = ym_xcd_block(blockIdx.x, gridDim.x);  // each XCD owns one contiguous run of pixel blocks
+  const int tn = vb % ntn, tm = vb / ntn;
   const int KS = a.Kpad >> 6;
   const int HW = a.Ho * a.Wo;
   const unsigned c16m = (0x1000000u + a.Cin8 - 1) / a.Cin8;
-  const int fb = (Q->z_in - 128) & 0xFF;
+  const int fb = Q8<F8>::pad_byte(Q);
   const int f4 = fb | (fb << 8) | (fb << 16) | (fb << 24);
   const i8x16 fill = __builtin_bit_cast(i8x16, i32x4{f4, f4, f4, f4});
   const i8x16 zero = __builtin_bit_cast(i8x16, i32x4{0, 0, 0, 0});
@@ -243,12 +252,12 @@ __global__ __launch_bounds__(256) void conv_small_i8(const ConvArgs a) {
       bfr[p][j] = ks < KS ? gather<KIND>(a, img, ok[p], y[p], x[p], ks, g, c16m, fill) : zero;
     }
   }
-  i32x4 acc[PXG];
+  A4 acc[PXG];
 #pragma unroll
   for (int p = 0; p < PXG; ++p) {
-    acc[p] = i32x4{0, 0, 0, 0};
+    acc[p] = A4{0, 0, 0, 0};
 #pragma unroll
-    for (int j = 0; j < KSW; ++j) acc[p] = __builtin_amdgcn_mfma_i32_16x16x64_i8(af[j], bfr[p][j], acc[p], 0, 0, 0);
+    for (int j = 0; j < KSW; ++j) acc[p] = mfma16(af[j], bfr[p][j], acc[p]);
     if (wave > 0) red[wave - 1][p][lane] = acc[p];
   }
   __syncthreads();
@@ -261,18 +270,18 @@ __global__ __launch_bounds__(256) void conv_small_i8(const ConvArgs a) {
 #pragma unroll
   for (int p = 0; p < PXG; ++p) {
     if (!ok[p]) continue;
-    const i32x4 r = acc[p] + red[0][p][lane] + red[1][p][lane] + red[2][p][lane];
+    const A4 r = acc[p] + red[0][p][lane] + red[1][p][lane] + red[2][p][lane];
     const size_t ob = (size_t)(b[p] * a.d_P + a.d_pixoff + y[p] * a.d_W + x[p]) * a.d_ctot + a.d_coff;
     const size_t rb = (size_t)(b[p] * a.r_P + y[p] * a.Wo + x[p]) * a.r_ctot + a.r_coff;
-    epilogue4(a, Q, mode, post, r, biv, sav, bfv, n0, ob, rb);
+    epilogue4<F8>(a, Q, mode, post, r, biv, sav, bfv, n0, ob, rb);
   }
 }
 
-template <int KIND, int KSW, int PXG>
+template <int KIND, int KSW, int PXG, bool F8>
 hipError_t launch_small(const ConvArgs& a, hipStream_t st) {
   if (a.k != KIND || a.Kpad > 256 * KSW) return hipErrorInvalidValue;
   const long wgs = (long)((a.M + 16 * PXG - 1) / (16 * PXG)) * ((a.N + 15) / 16);
-  hipLaunchKernelGGL((conv_small_i8<KIND, KSW, PXG>), dim3(wgs), dim3(256), 0, st, a);
+  hipLaunchKernelGGL((conv_small_i8<KIND, KSW, PXG, F8>), dim3(wgs), dim3(256), 0, st, a);
   return hipGetLastError();
 }
 
@@ -282,7 +291,7 @@ int ym_conv_i8_stream_num_cfgs() { return kNumStream + kNumSmall; }
 
 // Host-side applicability: one plain source (int8 plans materialise concats and upsamples), no pixel shuffle,
 // N % 4 == 0, 16-aligned channel slices, 1x1 stride 1 or 3x3 pad 1, LDS within 80 KB.
-hipError_t ym_launch_conv_i8_stream(const ConvArgs& a, int i, hipStream_t st) {
+hipError_t ym_launch_conv_i8_stream(const ConvArgs& a, int i, hipStream_t st, bool f8) {
   if (i < 0 || i >= kNumStream + kNumSmall) return hipErrorInvalidValue;
   if (a.shuffle || a.src1 || a.up0 || !a.src0 || !a.q || !a.sasw || !a.biasi || (a.N & 3) || a.Kpad % 64)
     return hipErrorInvalidValue;
@@ -291,13 +300,13 @@ hipError_t ym_launch_conv_i8_stream(const ConvArgs& a, int i, hipStream_t st) {
   if (a.k == 1 ? (a.s != 1) : (a.k != 3 || a.pad != 1 || a.Cin8 > 1024)) return hipErrorInvalidValue;
   switch (i) {
 #define YM_X(id, kind, ks, px, cap) \
-  case id: return launch_stream<kind, ks, px, cap>(a, st);
+  case id: return f8 ? launch_stream<kind, ks, px, cap, true>(a, st) : launch_stream<kind, ks, px, cap, false>(a, st);
     YM_I8S_CFGS(YM_X)
 #undef YM_X
   }
   switch (i - kNumStream) {
 #define YM_X(id, kind, ksw, pxg) \
-  case id: return launch_small<kind, ksw, pxg>(a, st);
+  case id: return f8 ? launch_small<kind, ksw, pxg, true>(a, st) : launch_small<kind, ksw, pxg, false>(a, st);
     YM_I8M_CFGS(YM_X)
 #undef YM_X
   }

@@ -185,9 +185,26 @@ __global__ __launch_bounds__(256) void dwconv3x3_row(const DwArgs a) {
 template <typename V>
 __device__ __forceinline__ V vmax(V x, V y) { return __builtin_elementwise_max(x, y); }  // v_pk_max_f16 for fp16
 
-template <typename T>
+// fp8 e4m3 codes (sign-magnitude bytes) are max-pooled as order keys: key = sign ? -magnitude : magnitude, an int8
+// whose order is the values' order (both zeros -> 0, stored back as +0: the same value)
+template <typename V>
+__device__ __forceinline__ V f8_key(V v) {
+#pragma unroll
+  for (int e = 0; e < 8; ++e) v[e] = (v[e] & 0x80) ? (signed char)(-(v[e] & 0x7F)) : v[e];
+  return v;
+}
+template <typename V>
+__device__ __forceinline__ V f8_unkey(V v) {
+#pragma unroll
+  for (int e = 0; e < 8; ++e) v[e] = v[e] < 0 ? (signed char)(0x80 | -v[e]) : v[e];
+  return v;
+}
+
+template <typename T, bool F8 = false>
 __global__ __launch_bounds__(256) void sppf_pool(const PoolArgs a) {
   typedef typename Vec8<T>::type V;
+  auto ld = [&](const T* p) { V v = Vec8<T>::load(p); if constexpr (F8) v = f8_key(v); return v; };
+  auto st = [&](T* p, V v) { if constexpr (F8) v = f8_unkey(v); Vec8<T>::store(p, v); };
   extern __shared__ __attribute__((aligned(16))) unsigned char smraw[];
   V* in = reinterpret_cast<V*>(smraw);  // [HW]
   const int HW = a.H * a.W;
@@ -202,7 +219,7 @@ __global__ __launch_bounds__(256) void sppf_pool(const PoolArgs a) {
 #pragma unroll
     for (int it = 0; it < 4; ++it) {
       const int p = threadIdx.x + 256 * it;
-      if (p < HW) v[it] = Vec8<T>::load(buf + (size_t)(b * a.P + p) * a.ctot + a.coff + c0);
+      if (p < HW) v[it] = ld(buf + (size_t)(b * a.P + p) * a.ctot + a.coff + c0);
     }
 #pragma unroll
     for (int it = 0; it < 4; ++it) {
@@ -210,7 +227,7 @@ __global__ __launch_bounds__(256) void sppf_pool(const PoolArgs a) {
       if (p < HW) in[p] = v[it];
     }
     for (int p = threadIdx.x + 1024; p < HW; p += 256)
-      in[p] = Vec8<T>::load(buf + (size_t)(b * a.P + p) * a.ctot + a.coff + c0);
+      in[p] = ld(buf + (size_t)(b * a.P + p) * a.ctot + a.coff + c0);
   }
   __syncthreads();
   if (!a.sep) {  // LDS holds only the input image (large maps in f32): direct 2-D windows
@@ -221,7 +238,7 @@ __global__ __launch_bounds__(256) void sppf_pool(const PoolArgs a) {
       V m = in[p];
       for (int yy = y - r < 0 ? 0 : y - r; yy <= y + r && yy < a.H; ++yy)
         for (int xx = x - r < 0 ? 0 : x - r; xx <= x + r && xx < a.W; ++xx) m = vmax(m, in[yy * a.W + xx]);
-      Vec8<T>::store(buf + (size_t)(b * a.P + p) * a.ctot + a.coff + (j + 1) * a.C + c0, m);
+      st(buf + (size_t)(b * a.P + p) * a.ctot + a.coff + (j + 1) * a.C + c0, m);
     }
     return;
   }
@@ -253,7 +270,7 @@ __global__ __launch_bounds__(256) void sppf_pool(const PoolArgs a) {
       if (dy == 0 || (unsigned)yy >= (unsigned)a.H) continue;
       m = vmax(m, h[yy * a.W + x]);
     }
-    Vec8<T>::store(buf + (size_t)(b * a.P + p) * a.ctot + a.coff + (j + 1) * a.C + c0, m);
+    st(buf + (size_t)(b * a.P + p) * a.ctot + a.coff + (j + 1) * a.C + c0, m);
   }
 }
 
@@ -985,7 +1002,7 @@ hipError_t ym_launch_input_max(const float* x, long n, float* ctl, float* out, h
 }
 
 hipError_t ym_launch_dwconv(int dtype, const DwArgs& a, hipStream_t st) {
-  if (dtype == YM_DT_I8) return ym_launch_dwconv_i8(a, st);
+  if (ym_dt_q8(dtype)) return ym_launch_dwconv_i8(a, st, dtype == YM_DT_F8);
   const long total = (long)a.B * a.H * a.W * (a.C / 8);
   if (total >= 0x7FFFFFFFL - 256) return hipErrorInvalidValue;  // the kernel indexes in 32 bits
   const dim3 g((total + 255) / 256);
@@ -1006,7 +1023,7 @@ hipError_t ym_launch_dwconv(int dtype, const DwArgs& a, hipStream_t st) {
 
 hipError_t ym_launch_sppf(int dtype, const PoolArgs& a, hipStream_t st) {
   const size_t HW = (size_t)a.H * a.W;
-  const size_t img = HW * 8 * (dtype == YM_DT_F16 ? 2 : (dtype == YM_DT_I8 ? 1 : 4));
+  const size_t img = HW * 8 * (dtype == YM_DT_F16 ? 2 : (ym_dt_q8(dtype) ? 1 : 4));
   PoolArgs b = a;
   b.sep = 4 * img <= 128 * 1024;  // input + 3 row-max images, 8 channels
   const size_t lds = b.sep ? 4 * img : img;
@@ -1014,6 +1031,7 @@ hipError_t ym_launch_sppf(int dtype, const PoolArgs& a, hipStream_t st) {
   const dim3 g(a.B * (a.C / 8));
   if (dtype == YM_DT_F16) hipLaunchKernelGGL(sppf_pool<f16>, g, dim3(256), lds, st, b);
   else if (dtype == YM_DT_I8) hipLaunchKernelGGL(sppf_pool<i8>, g, dim3(256), lds, st, b);  // max on q - 128: exact
+  else if (dtype == YM_DT_F8) hipLaunchKernelGGL((sppf_pool<i8, true>), g, dim3(256), lds, st, b);
   else hipLaunchKernelGGL(sppf_pool<float>, g, dim3(256), lds, st, b);
   return hipGetLastError();
 }
@@ -1046,7 +1064,7 @@ hipError_t launch_attn_mfma(const AttnArgs& a, hipStream_t st) {
 }
 
 hipError_t ym_launch_attn(int dtype, const AttnArgs& a, hipStream_t st) {
-  if (dtype == YM_DT_I8) return ym_launch_attn_i8(a, st);
+  if (ym_dt_q8(dtype)) return ym_launch_attn_i8(a, st, dtype == YM_DT_F8);
   if (dtype == YM_DT_F16 && a.kd == 32 && a.hd == 64 && !a.raw && a.nh * 128 <= a.q_ctot && a.d_ctot % 4 == 0 &&
       a.d_coff % 4 == 0 && a.q_ctot % 8 == 0 && a.q_coff % 8 == 0) {
     const int nkt = (a.N + 15) / 16;

@@ -22,3 +22,72 @@ __device__ __forceinline__ float deq(int q, int z, float s) { return ym_opaque((
 __device__ __forceinline__ int pack4(const int* v) {
   return (v[0] & 0xFF) | ((v[1] & 0xFF) << 8) | ((v[2] & 0xFF) << 16) | ((unsigned)(v[3] & 0xFF) << 24);
 }
+
+// ---------------------------------------------------------------------------------------------- fp8 (e4m3) plans
+// The fp8 PTQ plan (oracle/quant.py backend "fp8") stores every quantized tensor as OCP e4m3 codes (gfx950's fp8
+// format) with a per-tensor scale and zero point 0: code = e4m3(clamp(v·(1/s), ±448)), round to nearest even, and
+// its value is e4m3(code)·s.  Weights are e4m3 with per-output-channel scales; convs accumulate on the fp8 MFMA in
+// fp32.  Everything else — requantising the conv output to its observer, the 256-entry post table indexed by that
+// code, residual adds, the stored tensor's code — is the int8 plan's structure with this codec in place of the affine
+// uint8 one (the post table still has exactly 256 entries: a code is one byte).
+typedef float f32x16 __attribute__((ext_vector_type(16)));
+typedef int i32x16 __attribute__((ext_vector_type(16)));
+
+__device__ __forceinline__ int f8_enc(float v, float inv) {
+  float x = __fmul_rn(v, inv);
+  x = fminf(fmaxf(x, -448.f), 448.f);
+  return __builtin_amdgcn_cvt_pk_fp8_f32(x, x, 0, false) & 0xFF;
+}
+__device__ __forceinline__ float f8_dec(int code) { return __builtin_amdgcn_cvt_f32_fp8(code & 0xFF, 0); }
+
+// The two quantisation schemes behind one interface (F8 = false: int8 storage q - 128, affine uint8 observers)
+template <bool F8> struct Q8;
+template <> struct Q8<false> {
+  typedef int acc_t;
+  typedef i32x4 acc4;
+  typedef i32x16 acc16;
+  // conv output requantised to its own observer: the post-table index
+  static __device__ __forceinline__ int code(int acc, int bi, float sa, float bf, const QRec* Q) {
+    return requant_out(acc + bi, sa, bf, Q);
+  }
+  static __device__ __forceinline__ int raw_byte(int c) { return c - 128; }  // mode 1: the code stored as is
+  static __device__ __forceinline__ float dec(int byte, int z, float s) { return deq((byte & 0xFF) ^ 0x80, z, s); }
+  static __device__ __forceinline__ int store(float v, const QRec* Q) {
+    return quant_store(v, Q->inv_so, Q->zo, Q->qlo, Q->qhi);
+  }
+  static __device__ __forceinline__ int pad_byte(const QRec* Q) { return (Q->z_in - 128) & 0xFF; }  // real zero
+};
+template <> struct Q8<true> {
+  typedef float acc_t;
+  typedef f32x4 acc4;
+  typedef f32x16 acc16;
+  static __device__ __forceinline__ int code(float acc, int, float sa, float bf, const QRec* Q) {
+    const float y = ym_opaque(acc * sa) + bf;
+    return f8_enc(y, Q->inv_sc);
+  }
+  static __device__ __forceinline__ int raw_byte(int c) { return c; }
+  static __device__ __forceinline__ float dec(int byte, int, float s) { return ym_opaque(f8_dec(byte) * s); }
+  static __device__ __forceinline__ int store(float v, const QRec* Q) { return f8_enc(v, Q->inv_so); }
+  static __device__ __forceinline__ int pad_byte(const QRec*) { return 0; }
+};
+
+// one 16-byte K chunk per lane: int8 = one MFMA, fp8 = two (bytes 0-7, 8-15; A and B split alike, so the pairs of
+// k indices the hardware multiplies are the same as in the int8 instruction)
+__device__ __forceinline__ i32x4 mfma16(i8x16 a, i8x16 b, i32x4 c) {
+  return __builtin_amdgcn_mfma_i32_16x16x64_i8(a, b, c, 0, 0, 0);
+}
+__device__ __forceinline__ f32x4 mfma16(i8x16 a, i8x16 b, f32x4 c) {
+  typedef long l2 __attribute__((ext_vector_type(2)));
+  const l2 la = __builtin_bit_cast(l2, a), lb = __builtin_bit_cast(l2, b);
+  c = __builtin_amdgcn_mfma_f32_16x16x32_fp8_fp8(la[0], lb[0], c, 0, 0, 0);
+  return __builtin_amdgcn_mfma_f32_16x16x32_fp8_fp8(la[1], lb[1], c, 0, 0, 0);
+}
+__device__ __forceinline__ i32x16 mfma32(i8x16 a, i8x16 b, i32x16 c) {
+  return __builtin_amdgcn_mfma_i32_32x32x32_i8(a, b, c, 0, 0, 0);
+}
+__device__ __forceinline__ f32x16 mfma32(i8x16 a, i8x16 b, f32x16 c) {
+  typedef long l2 __attribute__((ext_vector_type(2)));
+  const l2 la = __builtin_bit_cast(l2, a), lb = __builtin_bit_cast(l2, b);
+  c = __builtin_amdgcn_mfma_f32_32x32x16_fp8_fp8(la[0], lb[0], c, 0, 0, 0);
+  return __builtin_amdgcn_mfma_f32_32x32x16_fp8_fp8(la[1], lb[1], c, 0, 0, 0);
+}

@@ -167,7 +167,7 @@ struct ym_ctx {
   }
   int buf_H(int b) const { return bufs[b].f == 0 ? 1 : cH / bufs[b].f; }
   int buf_Wd(int b) const { return bufs[b].f == 0 ? A : cW / bufs[b].f; }
-  int elem(int b) const { return (bufs[b].f32 || dtype == YM_DT_F32) ? 4 : (dtype == YM_DT_I8 ? 1 : 2); }
+  int elem(int b) const { return (bufs[b].f32 || dtype == YM_DT_F32) ? 4 : (ym_dt_q8(dtype) ? 1 : 2); }
   template <typename T> const T* wptr(int32_t off) const {
     return reinterpret_cast<const T*>(d_weights + (size_t)(uint32_t)off);
   }
@@ -264,7 +264,7 @@ int conv_args(ym_ctx* c, const Op& op, int B, const float* d_in, float in_eps, C
       a.Wo = (a.Win + 2 * a.pad - k) / s + 1;
       if (cin % 8 || (a.C0 + a.C1) != cin) return fail(YM_EBLOB, "op %s: cin %d not a multiple of 8", op.name, cin);
       a.Cin8 = cin / 8;
-      if (c->dtype == YM_DT_I8) {  // int8 plans: K chunks of 16 channels (the stem keeps its 8-padded taps)
+      if (ym_dt_q8(c->dtype)) {  // int8 / fp8 plans: K chunks of 16 channels (the stem keeps its 8-padded taps)
         if (b0 != c->input_buf) {
           if (cin % 16) return fail(YM_EBLOB, "op %s: int8 cin %d not a multiple of 16", op.name, cin);
           a.Cin8 = cin / 16;
@@ -385,7 +385,7 @@ int launch_op(ym_ctx* c, const Op& op, int B, const float* d_in, const ym_infer_
       a.w = reinterpret_cast<const float*>(c->d_weights + (size_t)(uint32_t)r[19]);
       a.bias = reinterpret_cast<const float*>(c->d_weights + (size_t)(uint32_t)r[20]);
       a.C = r[3]; a.act = r[5]; a.H = c->buf_H(bs); a.W = c->buf_Wd(bs); a.B = B;
-      if (dt == YM_DT_I8) {
+      if (ym_dt_q8(dt)) {
         a.w = nullptr;
         a.wq = c->wptr<i8>(r[19]);
         a.q = c->wptr<QRec>(r[22]);
@@ -413,7 +413,7 @@ int launch_op(ym_ctx* c, const Op& op, int B, const float* d_in, const ym_infer_
       a.C = r[3]; a.nh = r[4]; a.kd = r[5]; a.hd = r[9];
       a.H = c->buf_H(bq); a.W = c->buf_Wd(bq); a.N = a.H * a.W; a.B = B;
       memcpy(&a.scale, &r[21], 4);
-      if (dt == YM_DT_I8) {
+      if (ym_dt_q8(dt)) {
         a.pe_w = nullptr;
         a.pe_wq = c->wptr<i8>(r[19]);
         a.q = c->wptr<QRec>(r[22]);
@@ -424,7 +424,7 @@ int launch_op(ym_ctx* c, const Op& op, int B, const float* d_in, const ym_infer_
       break;
     }
     case OP_REQ: {
-      if (dt != YM_DT_I8) return fail(YM_EBLOB, "op %s: requant in a non-int8 plan", op.name);
+      if (!ym_dt_q8(dt)) return fail(YM_EBLOB, "op %s: requant in a non-quantized plan", op.name);
       ReqArgs a{};
       const int bs = r[6], bd = r[13];
       a.src = static_cast<const i8*>(c->bptr(bs)); a.s_ctot = c->bufs[bs].C; a.s_coff = r[7]; a.s_P = c->buf_P(bs);
@@ -435,7 +435,7 @@ int launch_op(ym_ctx* c, const Op& op, int B, const float* d_in, const ym_infer_
       if (c->buf_H(bs) * (a.up ? 2 : 1) != a.H || a.s_W * (a.up ? 2 : 1) != a.W)
         return fail(YM_EBLOB, "op %s: requant source/destination shapes disagree", op.name);
       a.q = c->wptr<QRec>(r[22]);
-      e = ym_launch_requant(a, st);
+      e = ym_launch_requant(a, st, dt == YM_DT_F8);
       break;
     }
     case OP_DECODE: {
@@ -604,6 +604,13 @@ static void build_schedule(ym_ctx* c) {
 // Structural check of a parsed plan before it is committed to a context: buffer ids of every op record in range,
 // every weight / bias / quantisation record inside the weight section.  The kernels index device memory with these
 // values, so a malformed blob must fail here (YM_EBLOB), never inside a launch.
+// OCP e4m3 (gfx950 fp8) code -> value: the fp8 plan's stem weights, re-laid out as fp32 (exact)
+static float e4m3_value(uint8_t b) {
+  const int e = (b >> 3) & 15, m = b & 7;
+  const float v = e == 0 ? ldexpf((float)m, -9) : ((e == 15 && m == 7) ? NAN : ldexpf((float)(8 + m), e - 10));
+  return (b & 0x80) ? -v : v;
+}
+
 static int validate_plan(const std::vector<BufDesc>& bufs, const std::vector<Op>& ops, int dtype, size_t wbytes) {
   const int nbuf = (int)bufs.size();
   for (int i = 0; i < nbuf; ++i)
@@ -623,7 +630,7 @@ static int validate_plan(const std::vector<BufDesc>& bufs, const std::vector<Op>
         ok = N > 0 && Kpad > 0 && Kpad <= (1 << 16) && buf_ok(r[6], false) && buf_ok(r[10], true) &&
              buf_ok(r[13], false) && buf_ok(r[17], true) && w_ok(r[19], (size_t)N * Kpad * esz) &&
              w_ok(r[20], (size_t)N * 4);
-        if (ok && dtype == YM_DT_I8) ok = w_ok(r[22], qrec) && w_ok(r[23], (size_t)N * 4) && w_ok(r[24], (size_t)N * 4);
+        if (ok && ym_dt_q8(dtype)) ok = w_ok(r[22], qrec) && w_ok(r[23], (size_t)N * 4) && w_ok(r[24], (size_t)N * 4);
         if (ok && r[30]) {
           const int N2 = r[27], K2 = r[29];
           ok = N2 > 0 && K2 > 0 && K2 <= (1 << 16) && buf_ok(r[31], false) && w_ok(r[25], (size_t)N2 * K2 * 2) &&
@@ -634,8 +641,8 @@ static int validate_plan(const std::vector<BufDesc>& bufs, const std::vector<Op>
       case OP_DW: case OP_ATTN: {
         const int C = r[3];
         ok = C > 0 && buf_ok(r[6], false) && buf_ok(r[13], false) &&
-             w_ok(r[19], (size_t)9 * C * (dtype == YM_DT_I8 ? 1 : 4)) && w_ok(r[20], (size_t)C * 4);
-        if (ok && dtype == YM_DT_I8) ok = w_ok(r[22], qrec) && w_ok(r[23], (size_t)C * 4);
+             w_ok(r[19], (size_t)9 * C * (ym_dt_q8(dtype) ? 1 : 4)) && w_ok(r[20], (size_t)C * 4);
+        if (ok && ym_dt_q8(dtype)) ok = w_ok(r[22], qrec) && w_ok(r[23], (size_t)C * 4);
         break;
       }
       case OP_SPPF: ok = r[3] > 0 && buf_ok(r[13], false); break;
@@ -660,7 +667,7 @@ int ym_load_weights(ym_ctx* c, const void* blob, size_t bytes) {
   const size_t woff = align_up(need, 256);
   if (wbytes > bytes || bytes < woff + wbytes) return fail(YM_EBLOB, "blob truncated (%zu < %zu)", bytes, woff + wbytes);
   const int dtype = h[2];
-  if (dtype != YM_DT_F16 && dtype != YM_DT_F32 && dtype != YM_DT_I8) return fail(YM_EBLOB, "unknown dtype %d", dtype);
+  if (dtype != YM_DT_F16 && dtype != YM_DT_F32 && !ym_dt_q8(dtype)) return fail(YM_EBLOB, "unknown dtype %d", dtype);
   const int task = h[3], nc = h[4], nm = h[5], reg_max = h[6], nl = h[7];
   if (nl < 1 || nl > 4) return fail(YM_EBLOB, "bad level count");
   if (nc < 1 || nc > 128 || nm < 0 || nm > 64 || reg_max < 1 || reg_max > 64)
@@ -719,7 +726,8 @@ int ym_load_weights(ym_ctx* c, const void* blob, size_t bytes) {
   c->d_weights = nullptr;
   // The stem conv's weights, re-laid out on the host as fp32 [27][N] (tap-major: (ky, kx, c), N contiguous) so the
   // stem kernel reads them with wave-uniform (scalar) loads; the blob packs them as [N][Kpad] GEMM rows with the
-  // 3 input channels padded to 8 per tap.  int8 plans keep the integer weight values (exact in fp32).
+  // 3 input channels padded to 8 per tap.  int8 plans keep the integer weight values, fp8 plans the e4m3 values
+  // (both exact in fp32).
   std::vector<float> wstem;
   for (const Op& o : c->ops) {
     if (o.r[0] != OP_CONV || o.r[6] != c->input_buf) continue;
@@ -735,6 +743,7 @@ int ym_load_weights(ym_ctx* c, const void* blob, size_t bytes) {
         float v;
         if (c->dtype == YM_DT_F32) memcpy(&v, w + 4 * i, 4);
         else if (c->dtype == YM_DT_F16) { _Float16 h16; memcpy(&h16, w + 2 * i, 2); v = (float)h16; }
+        else if (c->dtype == YM_DT_F8) v = e4m3_value(reinterpret_cast<const uint8_t*>(w)[i]);
         else v = (float)reinterpret_cast<const int8_t*>(w)[i];
         wstem[(size_t)t * N + n] = v;
       }
@@ -973,7 +982,7 @@ int ym_tune(ym_ctx* c, const float* d_in, int B, int H, int W, const ym_infer_ar
   hipEvent_t e0, e1;
   HIPCK(hipEventCreate(&e0));
   HIPCK(hipEventCreate(&e1));
-  const int ncfg = c->dtype == YM_DT_I8 ? ym_conv_i8_num_cfgs() : ym_conv_num_cfgs();
+  const int ncfg = ym_dt_q8(c->dtype) ? ym_conv_i8_num_cfgs() : ym_conv_num_cfgs();
   const char* tl = getenv("YM_TUNE_LOG");  // per-candidate timings to stderr (tools/)
   const bool tune_log = tl && *tl && *tl != '0';
   for (size_t i = 0; i < c->ops.size(); ++i) {

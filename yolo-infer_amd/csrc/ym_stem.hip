@@ -18,6 +18,7 @@
 // f32 parity plan — stem_valu: one thread per output pixel, fp32 FMAs, weights read with wave-uniform addresses;
 // optionally the pre-activation output for the calibration runs.
 #include "ym_common.h"
+#include "ym_quant.h"
 
 namespace {
 
@@ -44,7 +45,8 @@ typedef _Float16 h8 __attribute__((ext_vector_type(8)));
 
 constexpr int MTH = 16;  // MFMA path: 16 output rows per workgroup (32 groups of 16 pixels, 8 per wave)
 
-template <typename T, int NT>  // NT = Cout / 16 channel tiles
+// NT = Cout / 16 channel tiles; F8 (T = i8 storage): the fp8 e4m3 PTQ plan (csrc/ym_quant.h)
+template <typename T, int NT, bool F8 = false>
 __global__ __launch_bounds__(256) void stem_mfma(const ConvArgs a) {
   constexpr bool QUANT = sizeof(T) == 1;
   constexpr int TH = MTH, PH = 2 * TH + 1;
@@ -114,7 +116,8 @@ __global__ __launch_bounds__(256) void stem_mfma(const ConvArgs a) {
       for (int e = 0; e < 4; ++e) {
         float x = v[it][e];
         if (div) x = x / 255.0f;
-        if constexpr (QUANT) h[e] = (f16)(float)(clampi((int)rintf(__fmul_rn(x, inv)) + zi, lo, hi) - zi);
+        if constexpr (F8) h[e] = (f16)f8_dec(f8_enc(x, inv));  // e4m3 values are exact in f16
+        else if constexpr (QUANT) h[e] = (f16)(float)(clampi((int)rintf(__fmul_rn(x, inv)) + zi, lo, hi) - zi);
         else h[e] = (f16)x;  // the activation storage precision, as the NHWC input of the MFMA path
       }
     }
@@ -147,8 +150,12 @@ __global__ __launch_bounds__(256) void stem_mfma(const ConvArgs a) {
 #pragma unroll
         for (int r = 0; r < 4; ++r) {
           const float y = ym_opaque(acc[r] * sasw[t][r]) + bias[t][r];  // two roundings, as the oracle's mul + add
-          const int qc = clampi((int)rintf(__fmul_rn(y, Q->inv_sc)) + Q->zc, lo, hi);
-          ov[r] = clampi((int)rintf(__fmul_rn(post[qc], Q->inv_so)) + Q->zo, lo, hi) - 128;
+          if constexpr (F8) {
+            ov[r] = f8_enc(post[f8_enc(y, Q->inv_sc)], Q->inv_so);
+          } else {
+            const int qc = clampi((int)rintf(__fmul_rn(y, Q->inv_sc)) + Q->zc, lo, hi);
+            ov[r] = clampi((int)rintf(__fmul_rn(post[qc], Q->inv_so)) + Q->zo, lo, hi) - 128;
+          }
         }
         *reinterpret_cast<int*>(dst + 16 * t) =
             (ov[0] & 0xFF) | ((ov[1] & 0xFF) << 8) | ((ov[2] & 0xFF) << 16) | ((unsigned)(ov[3] & 0xFF) << 24);
@@ -230,13 +237,13 @@ dim3 grid_of(const ConvArgs& a, int TH) {
   return dim3(B * ((a.Ho + TH - 1) / TH) * ((a.Wo + TW - 1) / TW));
 }
 
-template <typename T>
+template <typename T, bool F8 = false>
 hipError_t launch_mfma(const ConvArgs& a, hipStream_t st) {
   switch (a.N / 16) {
-    case 1: hipLaunchKernelGGL((stem_mfma<T, 1>), grid_of(a, MTH), dim3(256), 0, st, a); break;
-    case 2: hipLaunchKernelGGL((stem_mfma<T, 2>), grid_of(a, MTH), dim3(256), 0, st, a); break;
-    case 4: hipLaunchKernelGGL((stem_mfma<T, 4>), grid_of(a, MTH), dim3(256), 0, st, a); break;
-    case 6: hipLaunchKernelGGL((stem_mfma<T, 6>), grid_of(a, MTH), dim3(256), 0, st, a); break;
+    case 1: hipLaunchKernelGGL((stem_mfma<T, 1, F8>), grid_of(a, MTH), dim3(256), 0, st, a); break;
+    case 2: hipLaunchKernelGGL((stem_mfma<T, 2, F8>), grid_of(a, MTH), dim3(256), 0, st, a); break;
+    case 4: hipLaunchKernelGGL((stem_mfma<T, 4, F8>), grid_of(a, MTH), dim3(256), 0, st, a); break;
+    case 6: hipLaunchKernelGGL((stem_mfma<T, 6, F8>), grid_of(a, MTH), dim3(256), 0, st, a); break;
     default: return hipErrorInvalidValue;
   }
   return hipGetLastError();
@@ -249,6 +256,7 @@ hipError_t ym_launch_stem(int dtype, const ConvArgs& a, hipStream_t st) {
       a.M % (a.Ho * a.Wo))
     return hipErrorInvalidValue;
   if (dtype == YM_DT_I8) return a.q && a.sasw ? launch_mfma<i8>(a, st) : hipErrorInvalidValue;
+  if (dtype == YM_DT_F8) return a.q && a.sasw ? launch_mfma<i8, true>(a, st) : hipErrorInvalidValue;
   if (dtype == YM_DT_F16) return a.raw ? hipErrorInvalidValue : launch_mfma<f16>(a, st);
   hipLaunchKernelGGL(stem_valu, grid_of(a, 8), dim3(256), 0, st, a);
   return hipGetLastError();

@@ -14,7 +14,7 @@ import torch
 
 from .arch import GraphBuilder
 from .lib import Runtime
-from .plan import fuse_default, pack_graph
+from .plan import QUANT_DTYPES, fuse_default, pack_graph
 
 # Bump when the meaning of a conv config index (csrc/ym_conv.hip kCfgs) changes: stale tables are then ignored.
 TUNE_VERSION = 9
@@ -28,14 +28,15 @@ def tune_cache_dir() -> str:
 class Engine:
     def __init__(self, scale: str, task: str, state_dict: Dict[str, np.ndarray], device: torch.device,
                  dtype: str = "f16", blob: Optional[bytes] = None, qparams: Optional[Dict] = None, nc: int = 80):
-        """dtype: 'f16' (throughput), 'f32' (exact parity mode) or 'i8' (PTQ int8; needs `qparams` from
-        yolomi.quant.calibrate, or an int8 `blob`)."""
+        """dtype: 'f16' (throughput), 'f32' (exact parity mode), 'i8' (PTQ int8) or 'f8' (PTQ fp8 e4m3); the
+        quantized plans need `qparams` from yolomi.quant.calibrate (backend 'fp8' for 'f8'), or a packed `blob`."""
         if device.type != "cuda":
             raise RuntimeError(f"the yolomi engine runs on a gfx950 GPU (got device {device}); there is no CPU path")
         self.scale, self.task, self.dtype = scale, task, dtype
         self.device = device
         self.qparams = qparams
-        self.graph = GraphBuilder(scale, task, nc=nc, quant=dtype == "i8", fuse=fuse_default(dtype))
+        self.graph = GraphBuilder(scale, task, nc=nc, quant=dtype in QUANT_DTYPES,
+                                  fuse=fuse_default(dtype))
         self.blob = blob if blob is not None else pack_graph(self.graph, state_dict, dtype, qparams)
         self.rt = Runtime(device.index if device.index is not None else torch.cuda.current_device(), self.blob,
                           scale=scale, task=task, dtype=dtype)
@@ -186,15 +187,20 @@ class Engine:
                           nonempty.data_ptr(), stream)
         return masks, nonempty, offs
 
-    def read_buffer(self, buf_id: int, B: int) -> torch.Tensor:
+    def read_buffer(self, buf_id: int, B: int, raw: bool = False) -> torch.Tensor:
         """NHWC contents of plan buffer `buf_id` for the first B images (after run/profile), as a CPU float32 tensor
-        (int8 plans: the quantized values q = stored byte + 128, over the storage channels)."""
+        (int8 plans: the quantized values q = stored byte + 128; fp8 plans: the e4m3 values of the stored codes;
+        over the storage channels).  raw=True: the stored elements as they are (int8 / fp16 / fp32 tensor)."""
         _, C, H, W, eb = self.rt.buffer_info(buf_id)
         dt = {1: torch.int8, 2: torch.float16, 4: torch.float32}[eb]
         out = torch.empty((B, H, W, C), dtype=dt)
         torch.cuda.synchronize(self.device)
         self.rt.read_buffer(buf_id, out.data_ptr(), out.numel() * out.element_size())
-        return out.float() + 128.0 if eb == 1 else out.float()
+        if raw or eb != 1:
+            return out if raw else out.float()
+        if self.dtype == "f8":
+            return out.view(torch.uint8).view(torch.float8_e4m3fn).float()
+        return out.float() + 128.0
 
     def raw_shapes(self, B: int, H: int, W: int) -> Dict[int, tuple]:
         """(rows, cols) of every op's pre-activation output in a calibration run (ym_calibrate)."""

@@ -31,7 +31,8 @@ from .arch import REG_MAX, STRIDES, GraphBuilder
 MAGIC = 0x4C504D59
 VERSION = 1
 OP_IDS = {"input": 1, "conv": 2, "dwconv": 3, "sppf": 4, "attn": 5, "decode": 6, "nms": 7, "requant": 8}
-DTYPES = {"f16": 0, "f32": 1, "i8": 2}
+DTYPES = {"f16": 0, "f32": 1, "i8": 2, "f8": 3}
+QUANT_DTYPES = ("i8", "f8")  # one-byte PTQ plans: int8 affine (torch.ao qconfig) and fp8 e4m3 (yolomi/quant.py)
 BK = 64  # conv K is padded to the kernel K step (csrc/ym_conv.hip KSTEP)
 
 
@@ -117,23 +118,37 @@ def check_state_dict(g: GraphBuilder, sd: Dict[str, np.ndarray]) -> None:
 
 
 def pack_model(scale: str, task: str, sd: Dict[str, np.ndarray], dtype: str = "f16", qparams: Dict = None) -> bytes:
-    g = GraphBuilder(scale, task, quant=dtype == "i8", fuse=fuse_default(dtype))
+    g = GraphBuilder(scale, task, quant=dtype in QUANT_DTYPES, fuse=fuse_default(dtype))
     return pack_graph(g, sd, dtype, qparams)
 
 
 def pack_graph(g: GraphBuilder, sd: Dict[str, np.ndarray], dtype: str = "f16", qparams: Dict = None) -> bytes:
     if dtype not in DTYPES:
         raise ValueError(f"dtype {dtype!r} not in {list(DTYPES)}")
-    quant = dtype == "i8"
+    quant = dtype in QUANT_DTYPES
+    f8 = dtype == "f8"
     if quant != bool(g.quant):
-        raise ValueError("int8 blobs need GraphBuilder(quant=True), float blobs quant=False")
+        raise ValueError("int8/fp8 blobs need GraphBuilder(quant=True), float blobs quant=False")
     check_state_dict(g, sd)
     if quant:
-        from .quant import BACKENDS, inv32, post_table, qrange, quantize_weight
-        if not qparams or qparams.get("backend") not in BACKENDS:
-            raise ValueError("dtype 'i8' needs calibrated qparams (yolomi.quant.calibrate) with a known backend")
+        from .quant import (BACKENDS, inv32, post_table, post_table_fp8, qrange, quantize_weight,
+                            quantize_weight_fp8)
+        if not qparams or qparams.get("backend") not in BACKENDS or (qparams["backend"] == "fp8") != f8:
+            raise ValueError(f"dtype {dtype!r} needs calibrated qparams (yolomi.quant.calibrate) of backend "
+                             f"{'fp8' if f8 else 'qnnpack / fbgemm'}")
+        if f8 and g.task != "detect":
+            raise ValueError("the fp8 plan covers detect models")
         per_channel = BACKENDS[qparams["backend"]][1]
         qlo, qhi = qrange(qparams["backend"])
+
+        def qweight(w, pc):  # (codes as int8 bytes, fp32 scale per output channel)
+            if f8:
+                c, sw_ = quantize_weight_fp8(w)
+                return c.view(np.int8), sw_
+            return quantize_weight(w, pc)
+
+        def post(s_, z_, act):
+            return post_table_fp8(s_, act) if f8 else post_table(s_, z_, act)
 
         def qp(key):
             if key not in qparams:
@@ -154,7 +169,7 @@ def pack_graph(g: GraphBuilder, sd: Dict[str, np.ndarray], dtype: str = "f16", q
             C0 = src0.C
             stem = src0.buf is g.input
             if quant:
-                w, sw = quantize_weight(w, per_channel and not a.get("convT"))  # int8 (N, k, k, cin), fp32 (N,)
+                w, sw = qweight(w, per_channel and not a.get("convT"))  # int8 / e4m3 (N, k, k, cin), fp32 (N,)
             if stem:  # stem: RGB padded to 8 channels
                 pad = 8 - C0
                 w = np.concatenate([w, np.zeros(w.shape[:3] + (pad,), w.dtype)], axis=3)
@@ -198,9 +213,9 @@ def pack_graph(g: GraphBuilder, sd: Dict[str, np.ndarray], dtype: str = "f16", q
                 mode = 2 if d.f32 else (1 if d.qkind == "out" else 0)
                 s_b, z_b = (1.0, 0) if mode else qp(d.qkey)
                 s_r, z_r = qp(res.buf.qkey) if res is not None else (0.0, 0)
-                rec = _qrec(inv32(so), zo, qlo, qhi, mode, post_table(so, zo, bool(a["act"])), inv32(s_b), z_b, s_r,
+                rec = _qrec(inv32(so), zo, qlo, qhi, mode, post(so, zo, bool(a["act"])), inv32(s_b), z_b, s_r,
                             z_r, s_in, z_in, inv32(s_in))
-                biasi = np.zeros(N, np.int64) if stem else (128 - z_in) * wp.astype(np.int64).sum(1)
+                biasi = np.zeros(N, np.int64) if (stem or f8) else (128 - z_in) * wp.astype(np.int64).sum(1)
                 assert np.abs(biasi).max() < 2 ** 31
                 r[22] = arena.add(np.frombuffer(rec, np.uint8))
                 r[23] = arena.add((np.float32(s_in) * sw).astype(np.float32))
@@ -211,11 +226,11 @@ def pack_graph(g: GraphBuilder, sd: Dict[str, np.ndarray], dtype: str = "f16", q
             r[6], r[7] = a["src"].buf.id, a["src"].coff
             r[13], r[14] = a["dst"].buf.id, a["dst"].coff
             if quant:
-                wq, sw = quantize_weight(np.ascontiguousarray(w9.T), per_channel)  # (C, 9): per output channel
+                wq, sw = qweight(np.ascontiguousarray(w9.T), per_channel)  # (C, 9): per output channel
                 s_in, z_in = qp(a["src"].buf.qkey)
                 so, zo = qp("out:" + a["wkey"])
                 s_b, z_b = qp(a["dst"].buf.qkey)
-                rec = _qrec(inv32(so), zo, qlo, qhi, 0, post_table(so, zo, bool(a["act"])), inv32(s_b), z_b,
+                rec = _qrec(inv32(so), zo, qlo, qhi, 0, post(so, zo, bool(a["act"])), inv32(s_b), z_b,
                             s_in=s_in, z_in=z_in)
                 r[19], r[20] = arena.add(np.ascontiguousarray(wq.T)), arena.add(b)
                 r[22] = arena.add(np.frombuffer(rec, np.uint8))
@@ -233,11 +248,11 @@ def pack_graph(g: GraphBuilder, sd: Dict[str, np.ndarray], dtype: str = "f16", q
             r[13], r[14] = a["dst"].buf.id, a["dst"].coff
             r[21] = struct.unpack("<i", struct.pack("<f", float(np.float32(a["kd"] ** -0.5))))[0]
             if quant:
-                wq, sw = quantize_weight(np.ascontiguousarray(w9.T), per_channel)
+                wq, sw = qweight(np.ascontiguousarray(w9.T), per_channel)
                 s_in, z_in = qp(a["qkv"].buf.qkey)
                 so, zo = qp("out:" + a["wkey"])
                 s_b, z_b = qp(a["dst"].buf.qkey)
-                rec = _qrec(inv32(so), zo, qlo, qhi, 0, post_table(so, zo, False), inv32(s_b), z_b, s_in=s_in,
+                rec = _qrec(inv32(so), zo, qlo, qhi, 0, post(so, zo, False), inv32(s_b), z_b, s_in=s_in,
                             z_in=z_in)
                 r[19], r[20] = arena.add(np.ascontiguousarray(wq.T)), arena.add(b)
                 r[22] = arena.add(np.frombuffer(rec, np.uint8))

@@ -17,8 +17,10 @@ from typing import Dict, Iterable, Optional, Tuple
 import numpy as np
 import torch
 
-BACKENDS = {"qnnpack": (False, False), "fbgemm": (True, True)}  # backend -> (activation reduce_range, per-channel w)
+# backend -> (activation reduce_range, per-channel w); "fp8" is the e4m3 PTQ plan (dtype "f8", below)
+BACKENDS = {"qnnpack": (False, False), "fbgemm": (True, True), "fp8": (False, True)}
 F32 = np.float32
+E4M3_MAX = 448.0
 
 
 def qrange(backend: str) -> Tuple[int, int]:
@@ -26,8 +28,50 @@ def qrange(backend: str) -> Tuple[int, int]:
 
 
 def act_observer(backend: str):
-    from torch.ao.quantization.observer import HistogramObserver
+    from torch.ao.quantization.observer import HistogramObserver, MinMaxObserver
+    if backend == "fp8":  # amax observer: s = max|x| / 448
+        return MinMaxObserver(dtype=torch.quint8, qscheme=torch.per_tensor_affine)
     return HistogramObserver(dtype=torch.quint8, qscheme=torch.per_tensor_affine, reduce_range=BACKENDS[backend][0])
+
+
+# ----------------------------------------------------------------------------------------- fp8 (e4m3) PTQ plan
+# The same quantisation points as the int8 plan, with OCP e4m3 codes (gfx950 fp8) in place of affine uint8: a tensor
+# has a per-tensor scale s = amax / 448 (zero point 0) and code = e4m3(clamp(v * (1/s), +-448)) (round to nearest
+# even), weights per-output-channel e4m3; convs accumulate on v_mfma_f32_*_fp8_fp8.  Restated in oracle/quant.py
+# (backend "fp8") with torch.float8_e4m3fn casts; kernels: csrc/ym_quant.h Q8<true>.
+def fp8_scale(amax: float) -> float:
+    amax = float(amax)
+    return float(F32(amax) / F32(E4M3_MAX)) if amax > 0 else float(F32(1.0) / F32(E4M3_MAX))
+
+
+def e4m3_codes(v: torch.Tensor) -> torch.Tensor:
+    """uint8 e4m3 codes of fp32 values already scaled: clamp to +-448, round to nearest even (torch's cast)."""
+    return torch.clamp(v.float(), -E4M3_MAX, E4M3_MAX).to(torch.float8_e4m3fn).view(torch.uint8)
+
+
+def e4m3_table() -> np.ndarray:
+    """value of every e4m3 code (0x7f / 0xff are NaN: never produced, read as 0)."""
+    t = torch.arange(256, dtype=torch.int32).to(torch.uint8).view(torch.float8_e4m3fn).float().numpy()
+    return np.nan_to_num(t, nan=0.0).astype(F32)
+
+
+def quantize_weight_fp8(w: np.ndarray) -> Tuple[np.ndarray, np.ndarray]:
+    """Per-output-channel e4m3 weights: s[n] = max|w[n]| / 448, code = e4m3(w * (1/s[n])) -> (uint8 codes, s)."""
+    w = np.ascontiguousarray(w, dtype=F32)
+    amax = np.abs(w.reshape(w.shape[0], -1)).max(1)
+    s = np.array([fp8_scale(a) for a in amax], F32)
+    inv = (F32(1.0) / s).astype(F32)
+    t = torch.from_numpy(w) * torch.from_numpy(inv).view(-1, *([1] * (w.ndim - 1)))
+    return e4m3_codes(t).numpy(), s
+
+
+def post_table_fp8(s: float, act: bool) -> np.ndarray:
+    """post[code] = act(e4m3(code) * s) for the 256 codes (SiLU in float64, rounded once, as post_table)."""
+    x = (e4m3_table() * F32(s)).astype(F32)
+    if act:
+        d = x.astype(np.float64)
+        x = (d / (1.0 + np.exp(-d))).astype(F32)
+    return x.astype(F32)
 
 
 def quantize_weight(w: np.ndarray, per_channel: bool) -> Tuple[np.ndarray, np.ndarray]:
@@ -75,6 +119,9 @@ class _Observers:
     def qparams(self) -> Dict:
         qp = {"backend": self.backend}
         for k, o in self.obs.items():
+            if self.backend == "fp8":
+                qp[k] = (fp8_scale(max(abs(float(o.min_val)), abs(float(o.max_val)))), 0)
+                continue
             s, z = o.calculate_qparams()
             qp[k] = (float(F32(float(s))), int(z))
         return qp
