@@ -160,6 +160,15 @@ int ym_read_buffer(ym_ctx* ctx, int buf, void* dst, size_t bytes);
 int ym_masks(ym_ctx* ctx, const float* d_dets, int B, int max_det, const int* d_offsets, int total, int H, int W,
              unsigned char* d_masks, int* d_nonempty, void* stream);
 
+/* Segment plans, single-sync form of ym_masks: the masks of the first min(counts[b], cap) detections of every image,
+ * taken from the DEVICE counts of the last ym_infer (d_counts, B ints), so the masks are enqueued right behind the
+ * forward with no host round trip in between.  d_masks: B x cap x H x W bytes, slot (b, i) = detection i of image b
+ * (unused slots are left unwritten); d_flags: B*cap + B ints = the non-empty flag of every slot (0 when unused),
+ * then a copy of the B counts, so ONE device->host read of d_flags returns both.  The caller checks counts[b] <= cap
+ * (else it calls ym_masks for that batch).  Same arithmetic as ym_masks.  Asynchronous on `stream`. */
+int ym_masks_slots(ym_ctx* ctx, const float* d_dets, int B, int max_det, const int* d_counts, int cap, int H, int W,
+                   unsigned char* d_masks, int* d_flags, void* stream);
+
 /* Image sources: Ultralytics `LetterBox` + predictor preprocessing of ONE HWC uint8 image already
  * in device memory (d_src, rows row_bytes apart, 3 channels; bgr = 1 for cv2.imread order).  The image is resized to
  * uh x uw with OpenCV's 8-bit INTER_LINEAR fixed-point arithmetic (skipped when the size does not change), placed at

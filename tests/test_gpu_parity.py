@@ -428,6 +428,21 @@ def test_segment_masks_match_oracle(dtype, agree, min_frac, scale, seeds):
     assert total > 0 and matched >= min_frac * total - 1, (matched, total)
 
 
+def test_segment_slot_masks_equal_exact_size_masks():
+    """predict()'s single-sync mask path (ym_masks_slots: masks enqueued behind the forward from the device counts)
+    and the two-read path it falls back to (ym_masks, exact-size; forced here with a slot cap of 1) give the same
+    boxes and the same masks, and the cap grows after a fallback."""
+    x = make_input("uniform", (6001, 6002, 6003, 6004), 640).to(DEV)
+    m = model("s", "f16", "segment")
+    a = m.predict(x, conf=0.25)
+    m._mask_cap = 1
+    b = m.predict(x, conf=0.25)
+    assert m._mask_cap >= max(len(r) for r in b) > 1
+    for ra, rb in zip(a, b):
+        assert torch.equal(ra.boxes.data, rb.boxes.data)
+        assert torch.equal(ra.masks.data, rb.masks.data)
+
+
 def test_ultralytics_pt_model_path(tmp_path):
     """YOLO11Model(model_path=<Ultralytics .pt>) runs the checkpoint's weights (yolomi/ptimport.py): the same
     detections as a model packed from those (fp16-rounded) weights directly."""

@@ -122,6 +122,7 @@ class YOLO11Model:
         self.optimization_history: List[Dict[str, Any]] = []
         # batch-sharded multi-GPU (yolomi.dist.enable_global_rule): callable x -> (1,) device max of the GLOBAL batch
         self.global_batch_max = None
+        self._mask_cap = 64  # segment: mask slots per image enqueued before the sync (grows on demand)
         self._validate_inputs()
         self.model = self._load_model()
         self.original_model = None
@@ -213,13 +214,27 @@ class YOLO11Model:
                                in_eps=eps, batch_max=bm)
         B = im.shape[0]
         out = dets[:B].clone()
-        n = counts[:B].tolist()  # the device→host sync of a predict call
         names = self.model.names
         masks = None
         if self.task == "segment":  # process_mask(upsample=True) on the GPU, in letterboxed coordinates
+            # the masks of the first `cap` detections per image are enqueued behind the forward, reading the device
+            # counts, so ONE device→host read returns counts and non-empty flags; a batch with more detections per
+            # image than `cap` takes the exact-size two-read path (and raises `cap` for the next call)
             H, W = im.shape[2:]
-            masks, nonempty, offs = eng.masks(out, n, H, W)
-            keep = nonempty.tolist()
+            cap = min(self._mask_cap, max_det)
+            mslots, flags = eng.masks_slots(out, counts[:B], cap, H, W)
+            fl = flags.tolist()  # the device→host sync of a segment predict call
+            n = fl[B * cap:]
+            if max(n) <= cap:
+                masks = mslots
+                keep = fl
+                offs = [b * cap for b in range(B + 1)]
+            else:
+                self._mask_cap = min(max_det, 1 << (max(n) - 1).bit_length())
+                masks, nonempty, offs = eng.masks(out, n, H, W)
+                keep = nonempty.tolist()
+        else:
+            n = counts[:B].tolist()  # the device→host sync of a predict call
         if imsrc is not None:  # ops.scale_boxes back to each original image
             from yolomi.preprocess import scale_boxes
             for b in range(B):
@@ -234,15 +249,15 @@ class YOLO11Model:
             return [Results.from_image(imsrc[0][b], imsrc[1][b], names, out[b, : n[b], :6], speed=speed)
                     for b in range(B)]
         res = []  # Segment: the predictor keeps only non-empty masks
-        mb = masks.view(torch.bool)  # the kernel writes 0/1 bytes: a bool view, no copy
+        mb = masks.view(torch.bool).reshape(-1, H, W)  # the kernel writes 0/1 bytes: a bool view, no copy
         for b in range(B):
-            kb = keep[offs[b]:offs[b + 1]]
+            kb = keep[offs[b]:offs[b] + n[b]]
             if all(kb):  # the common case: every kept detection has a mask pixel — views, no gathers
-                bx, mk = out[b, :n[b], :6], mb[offs[b]:offs[b + 1]]
+                bx, mk = out[b, :n[b], :6], mb[offs[b]:offs[b] + n[b]]
             else:
                 sel = torch.tensor([i for i, k in enumerate(kb) if k], dtype=torch.long, device=out.device)
                 bx = out[b].index_select(0, sel)[:, :6]
-                mk = mb[offs[b]:offs[b + 1]].index_select(0, sel)
+                mk = mb[offs[b]:offs[b] + n[b]].index_select(0, sel)
             if imsrc is None:
                 res.append(Results(im[b], names, bx, path=f"image{b}.jpg", speed=speed, masks=mk))
             else:

@@ -202,6 +202,7 @@ struct NmsArgs {
   int A, kstride, nm, max_det, max_nms, agnostic, B;
   float max_wh, img_h, img_w;
   double iou;
+  int dbg;  // phase ablation (YM_NMS_DBG, timing only): exit after phase dbg of the bit-matrix path
 };
 
 struct LetterboxArgs {
@@ -227,6 +228,8 @@ struct MaskArgs {
   float* lowres;                        // (total, MH, MW) cropped prototype-space masks
   unsigned char* masks; int H, W;       // (total, H, W) 0/1 masks at input resolution
   int* nonempty;                        // (total) 1 when any pixel of the mask is set
+  const int* counts; int cap;           // slot mode (counts != null): mask d = slot (d / cap, d % cap), used while
+                                        // d % cap < counts[d / cap]; total = B * cap; nonempty[B*cap + b] = counts[b]
 };
 
 // ------------------------------------------------------------------------------------------------------------
@@ -250,7 +253,8 @@ hipError_t ym_launch_conv_stream(int out_f32, const ConvArgs& a, int i, hipStrea
 int ym_conv_stream_num_cfgs();
 hipError_t ym_launch_conv_halo(int out_f32, const ConvArgs& a, int i, hipStream_t st);  // f16 3x3 halo tiles
 int ym_conv_halo_num_cfgs();
-hipError_t ym_launch_masks(const MaskArgs& a, hipStream_t st);  // Segment: process_mask(upsample=True)
+hipError_t ym_launch_masks(const MaskArgs& a, hipStream_t st);
+bool ym_masks_fused(const MaskArgs& a);  // the one-launch path (no (total, MH, MW) scratch)  // Segment: process_mask(upsample=True)
 // int8 (PTQ) plans: csrc/ym_conv_i8.hip
 // (f8: the fp8 e4m3 PTQ plan on the same kernels, csrc/ym_quant.h Q8<true>)
 hipError_t ym_launch_conv_i8(const ConvArgs& a, int cfg, hipStream_t st, bool strict, bool f8);

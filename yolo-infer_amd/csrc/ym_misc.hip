@@ -724,6 +724,38 @@ __device__ void bitonic_sort_desc(unsigned long long* k, int n2, int tid) {
   }
 }
 
+// one output row [x1 y1 x2 y2 conf cls coef_0 .. coef_nm-1]: box clipped to the image; a Segment head's nm mask
+// coefficients are fetched as float4s all issued before the first store (a scalar load-store loop waited one memory
+// latency per coefficient)
+__device__ __forceinline__ void write_det(const NmsArgs& a, float* r, size_t anc) {
+  const float4 v = a.boxes[anc];
+  const float sc = a.scores[anc];
+  const int cl = a.cls[anc];
+  if (a.nm > 0 && a.nm <= 64 && (a.nm & 3) == 0 && ((a.no_tot | a.mask_off) & 3) == 0) {
+    const float4* src = reinterpret_cast<const float4*>(a.anchors + anc * a.no_tot + a.mask_off);
+    float4 c[16];
+#pragma unroll
+    for (int i = 0; i < 16; ++i)
+      if (4 * i < a.nm) c[i] = src[i];
+#pragma unroll
+    for (int i = 0; i < 16; ++i)
+      if (4 * i < a.nm) {
+        r[6 + 4 * i] = c[i].x;
+        r[7 + 4 * i] = c[i].y;
+        r[8 + 4 * i] = c[i].z;
+        r[9 + 4 * i] = c[i].w;
+      }
+  } else {
+    for (int m = 0; m < a.nm; ++m) r[6 + m] = a.anchors[anc * a.no_tot + a.mask_off + m];
+  }
+  r[0] = fminf(fmaxf(v.x, 0.f), a.img_w);
+  r[1] = fminf(fmaxf(v.y, 0.f), a.img_h);
+  r[2] = fminf(fmaxf(v.z, 0.f), a.img_w);
+  r[3] = fminf(fmaxf(v.w, 0.f), a.img_h);
+  r[4] = sc;
+  r[5] = (float)cl;
+}
+
 __device__ __forceinline__ bool iou_gt(const float4 bi, float ai_area, const float4 bj, float aj_area, double thr) {
   const float xx1 = fmaxf(bi.x, bj.x), yy1 = fmaxf(bi.y, bj.y);
   const float xx2 = fminf(bi.z, bj.z), yy2 = fminf(bi.w, bj.w);
@@ -741,8 +773,10 @@ __global__ __launch_bounds__(NMS_T) void nms_image(const NmsArgs a) {
   __shared__ unsigned char ssup[NMS_LDS];
   const int b = blockIdx.x;
   const int tid = threadIdx.x;
+  if (a.dbg == 6) return;
   int n = a.counts[b];
   if (n > a.A) n = a.A;
+  if (a.dbg == 7) return;
   unsigned long long* gk = a.keys + (size_t)b * a.kstride;
   const size_t ib = (size_t)b * a.A;
   const int rowlen = 6 + a.nm;
@@ -789,15 +823,7 @@ __global__ __launch_bounds__(NMS_T) void nms_image(const NmsArgs a) {
     const unsigned long long km = __ballot(keep);
     if (keep) {
       const int pos = __popcll(km & ((1ull << lane) - 1ull));
-      const float4 v = a.boxes[ib + ai];
-      float* r = out + (size_t)pos * rowlen;
-      r[0] = fminf(fmaxf(v.x, 0.f), a.img_w);
-      r[1] = fminf(fmaxf(v.y, 0.f), a.img_h);
-      r[2] = fminf(fmaxf(v.z, 0.f), a.img_w);
-      r[3] = fminf(fmaxf(v.w, 0.f), a.img_h);
-      r[4] = a.scores[ib + ai];
-      r[5] = (float)a.cls[ib + ai];
-      for (int m = 0; m < a.nm; ++m) r[6 + m] = a.anchors[(ib + ai) * a.no_tot + a.mask_off + m];
+      write_det(a, out + (size_t)pos * rowlen, ib + ai);
     }
     if (lane == 0) a.out_counts[b] = kept;
     return;
@@ -812,6 +838,7 @@ __global__ __launch_bounds__(NMS_T) void nms_image(const NmsArgs a) {
     if (tid < n) sk[tid] = ki = gk[tid];
     if (tid == n) sk[n] = 0ull;  // pad to an even count (keys are > 0: the score bits of a candidate are)
     __syncthreads();
+    if (a.dbg == 1) return;
     if (tid < n) {
       int r = 0;
       const int n2 = (n + 1) >> 1;
@@ -823,6 +850,7 @@ __global__ __launch_bounds__(NMS_T) void nms_image(const NmsArgs a) {
       sorted[r] = ki;
     }
     __syncthreads();
+    if (a.dbg == 2) return;
     const int ne = n < a.max_nms ? n : a.max_nms;
     const int W = (ne + 63) >> 6;
     if (tid < ne) {
@@ -834,6 +862,7 @@ __global__ __launch_bounds__(NMS_T) void nms_image(const NmsArgs a) {
       sar[tid] = __fmul_rn(__fsub_rn(o.z, o.x), __fsub_rn(o.w, o.y));
     }
     __syncthreads();
+    if (a.dbg == 3) return;
     {  // one IoU per lane: wave item (i, w) has lane l test box j = 64 w + l against row i; the ballot IS word w
       const int wv = tid >> 6, ln = tid & 63;
       for (int pq = wv; pq < ne * W; pq += NMS_T / 64) {
@@ -845,54 +874,56 @@ __global__ __launch_bounds__(NMS_T) void nms_image(const NmsArgs a) {
       }
     }
     __syncthreads();
+    if (a.dbg == 4) return;
     __shared__ int keep_bm[NMS_BM], kept_bm;
     if (tid < 64) {
-      // greedy scan, 64 candidates per block: lane w holds removed-word w; within block k the rows' own word k
-      // (lane l: row 64k + l) decides sequentially from registers (readlane), then the block's kept rows are
-      // OR-reduced across the wave into the later words
+      // greedy scan, 64 candidates per block: lane w holds removed-word w.  Within block k the decisions are a
+      // wave-uniform chain on scalar registers: rem (the block's removed bits) and each row's own diagonal word are
+      // read into SGPRs (readfirstlane / readlane), so a row costs a few scalar instructions, no exec-mask branch;
+      // the block's kept rows are then written in parallel and OR-reduced across the wave into the later words.
       const int lane = tid, cap = a.max_det;
-      unsigned long long rem = 0;
+      // the removed words live in LDS: a kept row ORs its later mask words in with ds_or_b64 (one LDS atomic per
+      // word, no cross-lane reduction)
+      __shared__ unsigned long long rem_w[NMS_BM / 64];
+      if (lane < W) rem_w[lane] = 0ull;
       int kept = 0;
-      bool stop = false;
-      for (int k = 0; k < W && !stop; ++k) {
+      for (int k = 0; k < W && kept < cap; ++k) {
         const int row = 64 * k + lane;
         const unsigned long long diag = row < ne ? mask[row * W + k] : 0ull;
         const unsigned dlo = (unsigned)diag, dhi = (unsigned)(diag >> 32);
-        unsigned long long remk = __shfl(rem, k);
-        unsigned long long keepbits = 0;
+        const unsigned long long remv = rem_w[k];
+        unsigned long long remk =
+            ((unsigned long long)(unsigned)__builtin_amdgcn_readfirstlane((unsigned)(remv >> 32)) << 32) |
+            (unsigned long long)(unsigned)__builtin_amdgcn_readfirstlane((unsigned)remv);
         const int jn = ne - 64 * k < 64 ? ne - 64 * k : 64;
-        for (int j = 0; j < jn; ++j) {
-          if ((remk >> j) & 1ull) continue;
-          if (kept >= cap) { stop = true; break; }
+        // visit only the rows that are kept: the next one is the lowest bit of the block's not-yet-removed rows
+        // (a row's diagonal word only has bits above the row, so rows below it are final)
+        unsigned long long keepbits = 0;
+        int kk = kept;
+        unsigned long long avail = ~remk & (jn == 64 ? ~0ull : ((1ull << jn) - 1ull));
+        while (avail && kk < cap) {
+          const int j = __builtin_ctzll(avail);
           keepbits |= 1ull << j;
-          if (lane == 0) keep_bm[kept] = 64 * k + j;
-          ++kept;
-          remk |= ((unsigned long long)__builtin_amdgcn_readlane(dhi, j) << 32) |
+          ++kk;
+          remk |= ((unsigned long long)(unsigned)__builtin_amdgcn_readlane(dhi, j) << 32) |
                   (unsigned long long)(unsigned)__builtin_amdgcn_readlane(dlo, j);
+          avail &= ~remk & ~((2ull << j) - 1ull);
         }
         const bool mine = (keepbits >> lane) & 1ull;
-        for (int w = k + 1; w < W; ++w) {
-          unsigned long long v = (mine && row < ne) ? mask[row * W + w] : 0ull;
-#pragma unroll
-          for (int o = 32; o > 0; o >>= 1) v |= __shfl_xor(v, o);
-          if (lane == w) rem |= v;
+        if (mine) {
+          keep_bm[kept + __popcll(keepbits & ((1ull << lane) - 1ull))] = row;
+          for (int w = k + 1; w < W; ++w) atomicOr(&rem_w[w], mask[row * W + w]);
         }
+        kept = kk;
       }
       if (lane == 0) kept_bm = kept;
     }
     __syncthreads();
+    if (a.dbg == 5) return;
     const int kept = kept_bm;
     for (int q = tid; q < kept; q += NMS_T) {
       const unsigned ai = 0xFFFFFFFFu - (unsigned)(sorted[keep_bm[q]] & 0xFFFFFFFFull);
-      const float4 v = a.boxes[ib + ai];
-      float* r = out + (size_t)q * rowlen;
-      r[0] = fminf(fmaxf(v.x, 0.f), a.img_w);
-      r[1] = fminf(fmaxf(v.y, 0.f), a.img_h);
-      r[2] = fminf(fmaxf(v.z, 0.f), a.img_w);
-      r[3] = fminf(fmaxf(v.w, 0.f), a.img_h);
-      r[4] = a.scores[ib + ai];
-      r[5] = (float)a.cls[ib + ai];
-      for (int m = 0; m < a.nm; ++m) r[6 + m] = a.anchors[(ib + ai) * a.no_tot + a.mask_off + m];
+      write_det(a, out + (size_t)q * rowlen, ib + ai);
     }
     if (tid == 0) a.out_counts[b] = kept;
     return;
@@ -941,15 +972,7 @@ __global__ __launch_bounds__(NMS_T) void nms_image(const NmsArgs a) {
   for (int q = tid; q < kept; q += NMS_T) {
     const int i = keep_pos[q];
     const unsigned ai = 0xFFFFFFFFu - (unsigned)(k[i] & 0xFFFFFFFFull);
-    const float4 v = a.boxes[ib + ai];
-    float* r = out + (size_t)q * rowlen;
-    r[0] = fminf(fmaxf(v.x, 0.f), a.img_w);
-    r[1] = fminf(fmaxf(v.y, 0.f), a.img_h);
-    r[2] = fminf(fmaxf(v.z, 0.f), a.img_w);
-    r[3] = fminf(fmaxf(v.w, 0.f), a.img_h);
-    r[4] = a.scores[ib + ai];
-    r[5] = (float)a.cls[ib + ai];
-    for (int m = 0; m < a.nm; ++m) r[6 + m] = a.anchors[(ib + ai) * a.no_tot + a.mask_off + m];
+    write_det(a, out + (size_t)q * rowlen, ib + ai);
   }
   if (tid == 0) a.out_counts[b] = kept;
 }
@@ -1094,7 +1117,10 @@ hipError_t ym_launch_decode(const DecodeArgs& a, hipStream_t st) {
   return hipGetLastError();
 }
 
-hipError_t ym_launch_nms(const NmsArgs& a, hipStream_t st) {
+hipError_t ym_launch_nms(const NmsArgs& a0, hipStream_t st) {
+  static const int dbg = [] { const char* e = getenv("YM_NMS_DBG"); return e ? atoi(e) : 0; }();
+  NmsArgs a = a0;
+  a.dbg = dbg;
   hipLaunchKernelGGL(nms_image, dim3(a.B), dim3(NMS_T), 0, st, a);
   return hipGetLastError();
 }

@@ -1113,37 +1113,51 @@ int ym_letterbox(ym_ctx* c, const void* d_src, int h, int w, int row_bytes, int 
   return YM_OK;
 }
 
-int ym_masks(ym_ctx* c, const float* d_dets, int B, int max_det, const int* d_offsets, int total, int H, int W,
-             unsigned char* d_masks, int* d_nonempty, void* stream) {
+static int launch_masks(ym_ctx* c, MaskArgs& a, int B, int H, int W, void* stream) {
   if (!c) return fail(YM_EINVAL, "null context");
   if (c->task != 1 || c->proto_buf < 0) return fail(YM_ESTATE, "ym_masks needs a segment plan");
   if (!c->d_arena || B > c->cB || H != c->cH || W != c->cW)
     return fail(YM_ESTATE, "ym_masks must follow ym_infer of the same (B, H, W) (workspace %dx%dx%d)", c->cB, c->cH,
                 c->cW);
-  if (total < 0 || max_det < 1 || (total > 0 && (!d_dets || !d_offsets || !d_masks || !d_nonempty)))
-    return fail(YM_EINVAL, "bad ym_masks arguments");
-  if (total == 0) return YM_OK;
   HIPCK(hipSetDevice(c->device));
-  const int MH = c->buf_H(c->proto_buf), MW = c->buf_Wd(c->proto_buf);
-  const size_t need = (size_t)total * MH * MW * sizeof(float);
-  if (need > c->lowres_bytes) {
-    if (c->d_lowres) HIPCK(hipFree(c->d_lowres));
-    c->d_lowres = nullptr;
-    hipError_t e = hipMalloc(&c->d_lowres, need);
-    if (e != hipSuccess) return fail(YM_ENOMEM, "mask scratch hipMalloc(%zu): %s", need, hipGetErrorString(e));
-    c->lowres_bytes = need;
-  }
-  MaskArgs a{};
   a.proto = reinterpret_cast<const float*>(c->bptr(c->proto_buf));
-  a.MH = MH; a.MW = MW; a.nm = c->nm;
-  a.dets = d_dets; a.max_det = max_det; a.no = 6 + c->nm;
-  a.offsets = d_offsets; a.B = B; a.total = total;
-  a.lowres = c->d_lowres;
-  a.masks = d_masks; a.H = H; a.W = W;
-  a.nonempty = d_nonempty;
+  a.MH = c->buf_H(c->proto_buf); a.MW = c->buf_Wd(c->proto_buf); a.nm = c->nm;
+  a.no = 6 + c->nm; a.B = B; a.H = H; a.W = W;
+  if (a.total == 0) return YM_OK;
+  if (!ym_masks_fused(a)) {  // the two-kernel path: (total, MH, MW) prototype-resolution scratch
+    const size_t need = (size_t)a.total * a.MH * a.MW * sizeof(float);
+    if (need > c->lowres_bytes) {
+      if (c->d_lowres) HIPCK(hipFree(c->d_lowres));
+      c->d_lowres = nullptr;
+      hipError_t e = hipMalloc(&c->d_lowres, need);
+      if (e != hipSuccess) return fail(YM_ENOMEM, "mask scratch hipMalloc(%zu): %s", need, hipGetErrorString(e));
+      c->lowres_bytes = need;
+    }
+    a.lowres = c->d_lowres;
+  }
   const hipError_t e = ym_launch_masks(a, static_cast<hipStream_t>(stream));
   if (e != hipSuccess) return fail(YM_EHIP, "mask kernels: %s", hipGetErrorString(e));
   return YM_OK;
+}
+
+int ym_masks(ym_ctx* c, const float* d_dets, int B, int max_det, const int* d_offsets, int total, int H, int W,
+             unsigned char* d_masks, int* d_nonempty, void* stream) {
+  if (total < 0 || max_det < 1 || (total > 0 && (!d_dets || !d_offsets || !d_masks || !d_nonempty)))
+    return fail(YM_EINVAL, "bad ym_masks arguments");
+  MaskArgs a{};
+  a.dets = d_dets; a.max_det = max_det; a.offsets = d_offsets; a.total = total;
+  a.masks = d_masks; a.nonempty = d_nonempty;
+  return launch_masks(c, a, B, H, W, stream);
+}
+
+int ym_masks_slots(ym_ctx* c, const float* d_dets, int B, int max_det, const int* d_counts, int cap, int H, int W,
+                   unsigned char* d_masks, int* d_flags, void* stream) {
+  if (B < 1 || cap < 1 || max_det < 1 || cap > max_det || !d_dets || !d_counts || !d_masks || !d_flags)
+    return fail(YM_EINVAL, "bad ym_masks_slots arguments");
+  MaskArgs a{};
+  a.dets = d_dets; a.max_det = max_det; a.counts = d_counts; a.cap = cap; a.total = B * cap;
+  a.masks = d_masks; a.nonempty = d_flags;
+  return launch_masks(c, a, B, H, W, stream);
 }
 
 // ---------------------------------------------------------------------------------------------- RCCL (xGMI)

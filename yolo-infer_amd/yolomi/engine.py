@@ -179,13 +179,25 @@ class Engine:
             offs.append(offs[-1] + int(n))
         total = offs[-1]
         masks = torch.empty((total, H, W), dtype=torch.uint8, device=self.device)
-        nonempty = torch.zeros((total,), dtype=torch.int32, device=self.device)
+        nonempty = torch.empty((total,), dtype=torch.int32, device=self.device)  # zeroed by ym_masks
         if total:
             off_t = torch.tensor(offs, dtype=torch.int32).to(self.device, non_blocking=True)
             stream = torch.cuda.current_stream(self.device).cuda_stream
             self.rt.masks(dets.data_ptr(), B, dets.shape[1], off_t.data_ptr(), total, H, W, masks.data_ptr(),
                           nonempty.data_ptr(), stream)
         return masks, nonempty, offs
+
+    def masks_slots(self, dets: torch.Tensor, counts: torch.Tensor, cap: int, H: int, W: int):
+        """Single-sync form of masks(): enqueued behind the forward, reading the DEVICE counts.  Returns the
+        (B, cap, H, W) uint8 masks (slot (b, i) = detection i of image b, for i < min(count_b, cap)) and a (B*cap + B)
+        int32 tensor: the slots' non-empty flags, then the B counts (read both with one .tolist())."""
+        B = counts.shape[0]
+        masks = torch.empty((B, cap, H, W), dtype=torch.uint8, device=self.device)
+        flags = torch.empty((B * cap + B,), dtype=torch.int32, device=self.device)
+        stream = torch.cuda.current_stream(self.device).cuda_stream
+        self.rt.masks_slots(dets.data_ptr(), B, dets.shape[1], counts.data_ptr(), cap, H, W, masks.data_ptr(),
+                            flags.data_ptr(), stream)
+        return masks, flags
 
     def read_buffer(self, buf_id: int, B: int, raw: bool = False) -> torch.Tensor:
         """NHWC contents of plan buffer `buf_id` for the first B images (after run/profile), as a CPU float32 tensor

@@ -60,6 +60,7 @@ def load_library(path: os.PathLike = LIB_PATH):
         "ym_profile_replay": (I, [P, P, I, I, I, C.POINTER(InferArgs), P, P, P, I, F, I]),
         "ym_tune": (I, [P, P, I, I, I, C.POINTER(InferArgs), P, P, P, I]),
         "ym_masks": (I, [P, P, I, I, P, I, I, I, P, P, P]),
+        "ym_masks_slots": (I, [P, P, I, I, P, I, I, I, P, P, P]),
         "ym_letterbox": (I, [P, P, I, I, I, I, I, I, I, I, P, I, I, P]),
         "ym_get_op_cfg": (I, [P, I, I, I, C.POINTER(I), I]),
         "ym_set_op_cfg": (I, [P, I, I, I, C.POINTER(I), I]),
@@ -87,7 +88,7 @@ def load_library(path: os.PathLike = LIB_PATH):
 
 
 EXPORTED = ("ym_create", "ym_load_weights", "ym_broadcast_weights", "ym_rccl_get_unique_id", "ym_rccl_comm_init",
-            "ym_rccl_comm_destroy", "ym_infer", "ym_input_max", "ym_calibrate", "ym_masks", "ym_letterbox",
+            "ym_rccl_comm_destroy", "ym_infer", "ym_input_max", "ym_calibrate", "ym_masks", "ym_masks_slots", "ym_letterbox",
             "ym_profile", "ym_profile_replay", "ym_tune", "ym_get_op_cfg", "ym_set_op_cfg", "ym_num_ops", "ym_op_name",
             "ym_num_buffers", "ym_buffer_info", "ym_read_buffer", "ym_sync", "ym_last_error", "ym_destroy",
             "ym_version")
@@ -191,6 +192,10 @@ class Runtime:
     def masks(self, dets_ptr, B, max_det, offsets_ptr, total, H, W, masks_ptr, nonempty_ptr, stream):
         _check(self.lib.ym_masks(self.ctx, C.c_void_p(dets_ptr), B, max_det, C.c_void_p(offsets_ptr), total, H, W,
                                  C.c_void_p(masks_ptr), C.c_void_p(nonempty_ptr), C.c_void_p(stream)))
+
+    def masks_slots(self, dets_ptr, B, max_det, counts_ptr, cap, H, W, masks_ptr, flags_ptr, stream):
+        _check(self.lib.ym_masks_slots(self.ctx, C.c_void_p(dets_ptr), B, max_det, C.c_void_p(counts_ptr), cap, H, W,
+                                       C.c_void_p(masks_ptr), C.c_void_p(flags_ptr), C.c_void_p(stream)))
 
     def letterbox(self, src_ptr, h, w, row_bytes, bgr, uh, uw, top, left, dst_ptr, Hn, Wn, stream):
         _check(self.lib.ym_letterbox(self.ctx, C.c_void_p(src_ptr), h, w, row_bytes, int(bool(bgr)), uh, uw, top, left,
