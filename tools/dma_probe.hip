@@ -2,7 +2,7 @@
 // workgroup 0 / wave 0 around the prologue, every K stage's wait and compute, and the epilogue; plus the event time
 // of the launch.  Synthetic fp16 operands; NHWC input B x H x W x C, 3x3 (or 1x1) conv to N channels.
 //   hipcc -O3 -std=c++17 --offload-arch=gfx950 -DYM_DMA_STAMPS tools/dma_probe.hip -o tools/dma_probe
-//   ./tools/dma_probe B H W C N k cfg      (cfg = index into the DMA table, 0..11)
+//   ./tools/dma_probe B H W C N k cfg [stride]   (cfg = index into the DMA table)
 #include "../yolo-infer_amd/csrc/ym_conv_dma.hip"
 
 #include <cstdio>
@@ -22,8 +22,9 @@ int main(int argc, char** argv) {
   const int B = argc > 1 ? atoi(argv[1]) : 8, H = argc > 2 ? atoi(argv[2]) : 20, W = argc > 3 ? atoi(argv[3]) : 20;
   const int C = argc > 4 ? atoi(argv[4]) : 128, N = argc > 5 ? atoi(argv[5]) : 128, k = argc > 6 ? atoi(argv[6]) : 3;
   const int cfg = argc > 7 ? atoi(argv[7]) : 0;
+  const int S = argc > 8 ? atoi(argv[8]) : 1, CT = argc > 9 ? atoi(argv[9]) : C, Ho = (H + 2 * (k / 2) - k) / S + 1, Wo = (W + 2 * (k / 2) - k) / S + 1;
   const int K = k * k * C, Kpad = (K + 63) / 64 * 64;
-  const size_t nin = (size_t)B * H * W * C, nout = (size_t)B * H * W * N;
+  const size_t nin = (size_t)B * H * W * CT, nout = (size_t)B * Ho * Wo * N;
   std::vector<f16> hin(nin), hw((size_t)N * Kpad);
   for (size_t i = 0; i < nin; ++i) hin[i] = (f16)((int)(i * 2654435761u % 2001) * 0.001f - 1.f);
   for (size_t i = 0; i < hw.size(); ++i) hw[i] = (f16)((int)(i * 40503u % 2001) * 0.0005f - 0.5f);
@@ -47,13 +48,13 @@ int main(int argc, char** argv) {
   CK(hipMemcpyToSymbol(HIP_SYMBOL(ym_dma_stamps), &stamps, sizeof(stamps)));
 #endif
   ConvArgs a{};
-  a.src0 = din; a.s0_ctot = C; a.s0_coff = 0; a.C0 = C; a.s0_W = W; a.s0_P = H * W; a.up0 = 0;
+  a.src0 = din; a.s0_ctot = CT; a.s0_coff = 0; a.C0 = C; a.s0_W = W; a.s0_P = H * W; a.up0 = 0;
   a.w = dw; a.bias = dbias;
-  a.dst = dout; a.d_ctot = N; a.d_coff = 0; a.d_P = H * W; a.d_pixoff = 0; a.d_W = W;
-  a.Hin = H; a.Win = W; a.Ho = H; a.Wo = W; a.k = k; a.s = 1; a.pad = k / 2;
-  a.Cin8 = C / 8; a.Kc = K / 8; a.N = N; a.Kpad = Kpad; a.act = 1; a.npr = N; a.M = B * H * W;
+  a.dst = dout; a.d_ctot = N; a.d_coff = 0; a.d_P = Ho * Wo; a.d_pixoff = 0; a.d_W = Wo;
+  a.Hin = H; a.Win = W; a.Ho = Ho; a.Wo = Wo; a.k = k; a.s = S; a.pad = k / 2;
+  a.Cin8 = C / 8; a.Kc = K / 8; a.N = N; a.Kpad = Kpad; a.act = 1; a.npr = N; a.M = B * Ho * Wo;
   a.s0_elems = (long)nin; a.s1_elems = 0;
-  a.fd_hw = ym_fdiv(H * W); a.fd_w = ym_fdiv(W);
+  a.fd_hw = ym_fdiv(Ho * Wo); a.fd_w = ym_fdiv(Wo);
   a.slab = slab; a.slab_cap = 64 << 20; a.cnt = cnt; a.cnt_cap = 65536;
   hipStream_t st;
   CK(hipStreamCreate(&st));
@@ -62,7 +63,7 @@ int main(int argc, char** argv) {
   hipEvent_t e0, e1;
   CK(hipEventCreate(&e0));
   CK(hipEventCreate(&e1));
-  const int reps = 50;
+  const int reps = getenv("PROBE_REPS") ? atoi(getenv("PROBE_REPS")) : 50;
   CK(hipEventRecord(e0, st));
   for (int i = 0; i < reps; ++i) CK(ym_launch_conv_dma(0, a, cfg, st));
   CK(hipEventRecord(e1, st));
@@ -72,11 +73,12 @@ int main(int argc, char** argv) {
   std::vector<unsigned long long> hs(512);
   CK(hipMemcpy(hs.data(), stamps, 512 * 8, hipMemcpyDeviceToHost));
   const int nk = Kpad / 64;
-  printf("B=%d %dx%d C=%d N=%d k=%d cfg=%d (BM=%d BN=%d split=%d kg=%d): %d stages, %.2f us/launch (stream, eager)\n",
-         B, H, W, C, N, k, cfg, kDma[cfg].bm, kDma[cfg].bn, kDma[cfg].split, kDma[cfg].kg, nk, ms * 1e3 / reps);
+  const DmaCfg dc = cfg < kNumDma ? kDma[cfg] : DmaCfg{0, 0, 1, 0};  // deep-ring ids >= kNumDma: see YM_DMA_DEEP_CFGS
+  printf("B=%d %dx%d C=%d N=%d k=%d s=%d cfg=%d (BM=%d BN=%d split=%d kg=%d): %d stages, %.2f us/launch (stream, eager)\n",
+         B, H, W, C, N, k, S, cfg, dc.bm, dc.bn, dc.split, dc.kg, nk, ms * 1e3 / reps);
   const unsigned long long t0 = hs[0];
   printf("  prologue (indices + first stages issued): %llu cyc\n", hs[1] - t0);
-  const int per = nk / kDma[cfg].split;
+  const int per = nk / dc.split;
   for (int it = 0; it < per && it < 64; ++it) {
     const unsigned long long* q = &hs[8 + 4 * it];
     const unsigned long long prev = it ? hs[8 + 4 * (it - 1) + 3] : hs[1];
