@@ -503,6 +503,46 @@ def test_fused_pairs_split_equals_unfused_plan():
     assert rel(hs, hu) < 1e-2 and rel(hf, hu) < 1e-2
 
 
+BNECK_BASE = 17 + 18 + 32 + 12  # csrc/ym_conv.hip: first-gen + DMA + streaming + halo ids, then the Bottleneck kernels
+N_BNECK = 8
+
+
+@pytest.mark.parametrize("scale", ["n", "s"])
+def test_bneck_kernel_matches_split_pair(scale):
+    """csrc/ym_conv_bneck.hip: every Bottleneck variant (rows per band x pixel groups per item) on every fused
+    Bottleneck of the f16 plan — 160x160, 80x80 and (n) 40x40 maps, where 40 is not a multiple of the 16-pixel group
+    — equals the same pair run as two conv launches (fp16 mid tensor in HBM) within fp16 rounding of the output: the
+    fused kernel rounds the mid tensor to fp16 exactly as the stored tensor is, only fp32 summation order differs."""
+    m = model(scale, "f16")
+    e = m.model.engine
+    x = make_input("uniform", (5, 6), 640).to(DEV)
+    B, _, H, W = x.shape
+    e.run(x, use_graph=False)
+    tuned = e.rt.get_op_cfg(B, H, W)
+    ops = e.graph.ops
+    bn = [i for i, op in enumerate(ops) if op.args.get("pair") and op.args["pair"]["k"] == 3]
+    assert len(bn) >= 3
+
+    def outputs(cfg_bn):
+        e.rt.set_op_cfg(B, H, W, [cfg_bn if i in bn else -1 for i in range(len(ops))])
+        e.run(x, use_graph=False)
+        return [e.read_buffer(ops[i].args["dst"].buf.id, B)[..., ops[i].args["dst"].coff:
+                                                               ops[i].args["dst"].coff + ops[i].args["dst"].C]
+                for i in bn]
+
+    try:
+        ref = outputs(SPLIT_TAG + 128 * 29 + 29)  # the two convs as separate launches (LDS-DMA tiles)
+        for v in range(N_BNECK):
+            got = outputs(BNECK_BASE + v)
+            for i, r, g in zip(bn, ref, got):
+                err = (g - r).abs().max().item() / r.abs().max().item()
+                assert err < 5e-3, (ops[i].name, v, err)
+    finally:
+        if tuned is not None:
+            e.rt.set_op_cfg(B, H, W, tuned)
+        e._tuned.discard((B, H, W))
+
+
 # ------------------------------------------------------------------------------------------------ BASELINE configs
 def _coeff_check(ref_rows, got_rows, conf, iou, tol_xy, tol_s, tol_c, min_frac):
     """NMS rows with mask coefficients: boxes/scores by the matching protocol, then the 32 coefficients of every

@@ -209,8 +209,8 @@ def test_save_detection_results_formats(tmp_path):
 
 @pytest.mark.parametrize("scale,task", [("n", "detect"), ("s", "detect"), ("s", "segment")])
 def test_fused_pairs(scale, task):
-    """GraphBuilder.fuse_pairs: each fused op is a conv followed by a 1x1 conv that was the only reader of the
-    conv's output; the work (MACs) is unchanged, the intermediate tensor leaves the byte count and no op reads it."""
+    """GraphBuilder.fuse_pairs: each fused op is a conv followed by a 1x1 conv (or, for a Bottleneck, a 3x3 conv)
+    that was the only reader of the conv's output; the work (MACs) is unchanged, the intermediate tensor leaves the byte count and no op reads it."""
     g0, g = GraphBuilder(scale, task), GraphBuilder(scale, task, fuse=True)
     pairs = [op for op in g.ops if op.args.get("pair")]
     names0 = [op.name for op in g0.ops]
@@ -224,7 +224,10 @@ def test_fused_pairs(scale, task):
         first = op.name.split("+")[0]
         i = names0.index(first)
         nxt = g0.ops[i + 1]
-        assert nxt.args["k"] == 1 and nxt.args["src0"].buf.name == op.args["pair"]["mid"].buf.name
+        assert nxt.args["k"] == op.args["pair"]["k"] and nxt.args["src0"].buf.name == op.args["pair"]["mid"].buf.name
+        if op.args["pair"]["k"] == 3:  # a Bottleneck: both 3x3, the shortcut is the first conv's input
+            assert op.args["k"] == 3 and op.args["res"] is not None
+            assert (op.args["res"].buf.name, op.args["res"].coff) == (op.args["src0"].buf.name, op.args["src0"].coff)
         assert (op.args["dst"].buf.name, op.args["dst"].coff) == (nxt.args["dst"].buf.name, nxt.args["dst"].coff)
         mid = op.args["pair"]["mid"].buf
         for o in g.ops:

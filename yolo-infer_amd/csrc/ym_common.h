@@ -150,6 +150,9 @@ struct ConvArgs {
   // registers — out = act2(W2 · h + bias2) (+ res) with h = fp16(act(W · x + bias)); dst/res then describe the
   // second conv's output.  w2 [N2][Kpad2] (K = this conv's N output channels), null for a single conv.
   const void* w2; const float* bias2; int N2, Kpad2, act2;
+  // successor kernel size: 1 = the 1x1 above (streaming FUSE); 3 = a YOLO11 Bottleneck's second 3x3 conv, dst/res the
+  // Bottleneck output / shortcut (csrc/ym_conv_bneck.hip); w2 then [N2][Kpad2] with K = (ky, kx, mid channel)
+  int k2;
 };
 
 struct DwArgs {
@@ -249,6 +252,8 @@ hipError_t ym_launch_letterbox(const LetterboxArgs& a, hipStream_t st);
 hipError_t ym_launch_spin(int usec, hipStream_t st);  // profiling: park the stream for usec (wall clock)
 hipError_t ym_launch_conv_dma(int out_f32, const ConvArgs& a, int i, hipStream_t st);  // f16 plans only
 int ym_conv_dma_num_cfgs();
+hipError_t ym_launch_conv_bneck(int out_f32, const ConvArgs& a, int i, hipStream_t st);  // fused Bottleneck
+int ym_conv_bneck_num_cfgs();
 hipError_t ym_launch_conv_stream(int out_f32, const ConvArgs& a, int i, hipStream_t st);  // f16 1x1 only
 int ym_conv_stream_num_cfgs();
 hipError_t ym_launch_conv_halo(int out_f32, const ConvArgs& a, int i, hipStream_t st);  // f16 3x3 halo tiles

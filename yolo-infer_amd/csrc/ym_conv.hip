@@ -620,9 +620,12 @@ int choose_cfg(const ConvArgs& a) {
 
 // ids [0, 17): first-generation kernels above; [17, 17 + ym_conv_dma_num_cfgs()): LDS-DMA / split-K kernels;
 // then ym_conv_stream_num_cfgs() streaming / small-M kernels (csrc/ym_conv_stream.hip), then
-// ym_conv_halo_num_cfgs() halo-tile 3x3 kernels (csrc/ym_conv_halo.hip)
+// ym_conv_halo_num_cfgs() halo-tile 3x3 kernels (csrc/ym_conv_halo.hip), then ym_conv_bneck_num_cfgs() fused
+// Bottleneck kernels (csrc/ym_conv_bneck.hip; fused pairs with a 3x3 successor only) — appended last so the ids of
+// committed tables stay valid
 int ym_conv_num_cfgs() {
-  return kNumAllCfg + ym_conv_dma_num_cfgs() + ym_conv_stream_num_cfgs() + ym_conv_halo_num_cfgs();
+  return kNumAllCfg + ym_conv_dma_num_cfgs() + ym_conv_stream_num_cfgs() + ym_conv_halo_num_cfgs() +
+         ym_conv_bneck_num_cfgs();
 }
 
 hipError_t ym_launch_conv(int dtype, int out_f32, const ConvArgs& a, int cfg, hipStream_t st, bool strict) {
@@ -635,6 +638,22 @@ hipError_t ym_launch_conv(int dtype, int out_f32, const ConvArgs& a, int cfg, hi
   if (ym_dt_q8(dtype)) return ym_launch_conv_i8(a, cfg, st, strict, dtype == YM_DT_F8);  // csrc/ym_conv_i8.hip
   // (concat/upsample sources only feed 1x1 convs; YOLO11 has k in {1, 3})
   if (a.Kpad % KSTEP) return hipErrorInvalidValue;
+  if (a.w2 && a.k2 == 3) {  // fused Bottleneck (3x3 -> 3x3): csrc/ym_conv_bneck.hip
+    if (dtype != YM_DT_F16) return hipErrorInvalidValue;
+    const int bb = kNumAllCfg + ym_conv_dma_num_cfgs() + ym_conv_stream_num_cfgs() + ym_conv_halo_num_cfgs();
+    const int nb = ym_conv_bneck_num_cfgs();
+    if (cfg >= bb && cfg < bb + nb) {
+      const hipError_t e = ym_launch_conv_bneck(out_f32, a, cfg - bb, st);
+      if (e != hipErrorInvalidValue || strict) return e;
+    } else if (strict) {
+      return hipErrorInvalidValue;
+    }
+    for (int i = 0; i < nb; ++i) {  // untuned: the first variant that takes the shape
+      const hipError_t e = ym_launch_conv_bneck(out_f32, a, i, st);
+      if (e != hipErrorInvalidValue) return e;
+    }
+    return hipErrorInvalidValue;
+  }
   if (a.w2) {  // fused pair: only the streaming kernels hold a whole N in one wave (csrc/ym_conv_stream.hip)
     if (dtype != YM_DT_F16) return hipErrorInvalidValue;
     const int sbase = kNumAllCfg + ym_conv_dma_num_cfgs(), ns = ym_conv_stream_num_cfgs();

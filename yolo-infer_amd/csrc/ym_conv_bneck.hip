@@ -1,0 +1,330 @@
+// Fused YOLO11 Bottleneck for gfx950 (f16 plans): out = x + SiLU(BN2(conv3x3(SiLU(BN1(conv3x3(x)))))) in ONE launch
+// (the C3k2 `m` Bottlenecks, reference core/model.py:118-133 -> Ultralytics
+// nn/modules/block.py Bottleneck with k=(3,3), shortcut).  Planned by yolomi/arch.py fuse_pairs as a conv pair whose
+// successor is a 3x3 (ConvArgs::k2 == 3); the tuner also times the pair as two launches and keeps the faster.
+//
+// Why: at 160x160 / 80x80 the Bottleneck convs have few channels (C = 16..64 in, C/2 mid), so per output pixel they
+// move a few hundred bytes and do little math; the implicit-GEMM families gather every input pixel 9 times per conv
+// from L2 and pay two launches plus a round trip of the mid tensor through HBM (yolo11s B=8: 85 us for three
+// Bottlenecks whose HBM floor is ~15 us).  Here one workgroup owns a band of RB full output rows of one image:
+//   phase 0  the band's input rows + a 2-row / 1-column halo (RB+4 rows x W+2 px x C) are read from HBM ONCE into
+//            LDS, W1 and the biases are staged, W2 is prefetched into registers, the mid image is zeroed;
+//   phase 1  cv1 for the RB+2 mid rows the band needs (rows outside the image stay zero: cv2's padding), implicit
+//            im2col straight from the LDS image, v_mfma_f32_16x16x32_f16, bias + SiLU, rounded to fp16 (as the stored
+//            mid tensor of the unfused pair) into the LDS mid image (RB+2 rows x W+2 px x Cm);
+//   phase 2  W2 goes from registers into W1's LDS slot; cv2 from the mid image, bias + SiLU + the residual (the
+//            input pixels, still in LDS), 8-byte NHWC stores into the output channel slice.
+// Nothing but the input band, the weights and the output touches global memory.
+//
+// LDS images are pixel-major with C contiguous; a pixel's 16-byte chunk c sits at position c ^ f(p),
+// f(p) = (p / (16 / CH)) % CH for CH = C / 8 chunks per pixel, so the 16 lanes of an MFMA operand read (16
+// consecutive pixels, one chunk) hit 16 distinct 4-bank groups — for any 16 consecutive pixels, so every tap offset
+// is conflict-free.  Weight rows are pitched 2K + 16 bytes (16 rows, one chunk: distinct bank groups).
+// Results: fp32 accumulation of fp16 products with one fp16 rounding of the mid tensor and of the output, like the
+// unfused pair (only the summation order differs; f16-plan tolerance, tests/test_gpu_parity.py).
+#include <stdlib.h>
+
+#include "ym_common.h"
+
+namespace {
+
+template <int CH>
+__device__ __forceinline__ int swz(int p) {
+  if constexpr (CH == 1) return 0;
+  else return (p / (16 / CH)) % CH;
+}
+
+struct BneckGeom {
+  int RB;          // output rows per band
+  int nbands;      // ceil(H / RB)
+  int C, Cm, N2;   // input (= residual) channels, mid channels, output channels
+  int KS1, KS2;    // K steps of 32 per conv (9·C, 9·Cm rounded up)
+  int P1, P2;      // weight row pitches (bytes)
+  int offM, offW, offB;  // LDS byte offsets: mid image, weight slot, biases (input image at 0)
+  int lds;
+  int dbg;  // tools/bneck_ablate.py timing ablations (YM_BNECK_DBG): 1 no input loads, 2 no cv1, 4 no cv2, 8 no stores
+};
+
+// one lane's 16-byte B fragment: pixel p (LDS image index), K chunk c (8 channels) of a CH-chunk image
+template <int CH>
+__device__ __forceinline__ f16x8 ld_px(const char* img, int p, int c) {
+  return *reinterpret_cast<const f16x8*>(img + ((p * CH + (c ^ swz<CH>(p))) << 4));
+}
+
+template <int C, int CM, int N2, int PX, int NW>
+__global__ __launch_bounds__(64 * NW) void conv_bneck(const ConvArgs a, const BneckGeom g) {
+  constexpr int NT = 64 * NW;
+  constexpr int CH = C / 8, CHM = CM / 8;
+  constexpr int NB1 = (CM + 15) / 16, NB2 = N2 / 16;
+  constexpr int KS1 = (9 * C + 31) / 32, KS2 = (9 * CM + 31) / 32;
+  extern __shared__ __attribute__((aligned(16))) char smem[];
+  char* sX = smem;
+  char* sM = smem + g.offM;
+  char* sW = smem + g.offW;
+  float* sB1 = reinterpret_cast<float*>(smem + g.offB);
+  float* sB2 = sB1 + 16 * NB1;
+  const int tid = threadIdx.x, lane = tid & 63, wave = tid >> 6;
+  const int col = lane & 15, kg = lane >> 4;
+  const int W = a.Wo, H = a.Ho, WP = W + 2;
+  const int vb = ym_xcd_block(blockIdx.x, gridDim.x);  // neighbouring bands (shared halo rows) on one XCD
+  const int band = vb % g.nbands, b = vb / g.nbands;
+  const int RB = g.RB, r0 = band * RB;
+  const f16* src = static_cast<const f16*>(a.src0);
+  const f16* W1 = static_cast<const f16*>(a.w);
+  const f16* W2 = static_cast<const f16*>(a.w2);
+
+  // ---- phase 0: W2 prefetch (registers), W1 + biases, input band + halo, zeroed mid image
+  constexpr int W2CH = N2 * KS2 * 4;  // 16-byte chunks of W2 rows [N2][KS2 * 32]
+  constexpr int W2PT = (W2CH + NT - 1) / NT;
+  f16x8 w2r[W2PT];
+#pragma unroll
+  for (int u = 0; u < W2PT; ++u) {
+    const int i = tid + NT * u;
+    const int n = i / (KS2 * 4), c = i - n * (KS2 * 4);
+    w2r[u] = i < W2CH ? *reinterpret_cast<const f16x8*>(W2 + (size_t)n * a.Kpad2 + 8 * c) : Vec8<f16>::zero();
+  }
+  for (int i = tid; i < 16 * NB1 * KS1 * 4; i += NT) {
+    const int n = i / (KS1 * 4), c = i - n * (KS1 * 4);
+    const f16x8 v = n < CM ? *reinterpret_cast<const f16x8*>(W1 + (size_t)n * a.Kpad + 8 * c) : Vec8<f16>::zero();
+    *reinterpret_cast<f16x8*>(sW + n * g.P1 + 16 * c) = v;
+  }
+  for (int i = tid; i < 16 * NB1; i += NT) sB1[i] = i < CM ? a.bias[i] : 0.f;
+  for (int i = tid; i < N2; i += NT) sB2[i] = a.bias2[i];
+  {
+    const int nx = (RB + 4) * WP * CH;  // input image chunks
+    const size_t img = (size_t)b * a.s0_P;
+    for (int i0 = tid; i0 < nx; i0 += NT * 8) {
+      f16x8 v[8];
+#pragma unroll
+      for (int u = 0; u < 8; ++u) {
+        const int i = i0 + NT * u;
+        const int p = i / CH, c = i - p * CH;
+        const int row = p / WP, j = p - row * WP;
+        const int gy = r0 - 2 + row, gx = j - 1;
+        v[u] = (i < nx && !(g.dbg & 1) && (unsigned)gy < (unsigned)H && (unsigned)gx < (unsigned)W)
+                   ? *reinterpret_cast<const f16x8*>(src + (img + (size_t)gy * W + gx) * a.s0_ctot + a.s0_coff + 8 * c)
+                   : Vec8<f16>::zero();
+      }
+#pragma unroll
+      for (int u = 0; u < 8; ++u) {
+        const int i = i0 + NT * u;
+        if (i < nx) {
+          const int p = i / CH, c = i - p * CH;
+          *reinterpret_cast<f16x8*>(sX + ((p * CH + (c ^ swz<CH>(p))) << 4)) = v[u];
+        }
+      }
+    }
+    const int nm = (RB + 2) * WP * CHM;
+    for (int i = tid; i < nm; i += NT) *reinterpret_cast<f16x8*>(sM + (i << 4)) = Vec8<f16>::zero();
+  }
+  __syncthreads();
+
+  // ---- phase 1: cv1 over the RB+2 mid rows (image rows r0-1 .. r0+RB), PX 16-pixel groups per work item
+  const int gpr = (W + 15) / 16;  // 16-pixel groups per row (lanes past the row's end compute but never store)
+  {
+    const int ng = (g.dbg & 2) ? 0 : (RB + 2) * gpr;
+    for (int it = wave * PX; it < ng; it += NW * PX) {
+      int prow[PX], px0[PX];
+      bool ok[PX];
+#pragma unroll
+      for (int q = 0; q < PX; ++q) {
+        const int gi = it + q < ng ? it + q : ng - 1;  // a tail slot recomputes the last group, never stores it
+        prow[q] = gi / gpr;
+        px0[q] = (gi - prow[q] * gpr) * 16;
+        const int gm = r0 - 1 + prow[q];
+        ok[q] = it + q < ng && (unsigned)gm < (unsigned)H;
+      }
+      f32x4 acc[NB1][PX];
+#pragma unroll
+      for (int nb = 0; nb < NB1; ++nb)
+#pragma unroll
+        for (int q = 0; q < PX; ++q) acc[nb][q] = f32x4{0.f, 0.f, 0.f, 0.f};
+#pragma unroll 3
+      for (int s = 0; s < KS1; ++s) {
+        const int K = 32 * s + 8 * kg;
+        int tap = K / C;
+        const int ch = (K - tap * C) >> 3;
+        if (tap > 8) tap = 8;  // K padding: finite pixels times zero weights
+        const int ky = tap / 3, kx = tap - 3 * ky;
+        f16x8 wa[NB1], xb[PX];
+#pragma unroll
+        for (int nb = 0; nb < NB1; ++nb)
+          wa[nb] = *reinterpret_cast<const f16x8*>(sW + (16 * nb + col) * g.P1 + 2 * K);
+#pragma unroll
+        for (int q = 0; q < PX; ++q) xb[q] = ld_px<CH>(sX, (prow[q] + ky) * WP + px0[q] + col + kx, ch);
+#pragma unroll
+        for (int nb = 0; nb < NB1; ++nb)
+#pragma unroll
+          for (int q = 0; q < PX; ++q) acc[nb][q] = __builtin_amdgcn_mfma_f32_16x16x32_f16(wa[nb], xb[q], acc[nb][q], 0, 0, 0);
+      }
+      // lane: channels 16 nb + 4 kg .. + 3 of pixel px0 + col -> 8 bytes of the mid image
+#pragma unroll
+      for (int q = 0; q < PX; ++q) {
+        if (!ok[q] || px0[q] + col >= W) continue;
+        const int p = prow[q] * WP + px0[q] + col + 1;
+#pragma unroll
+        for (int nb = 0; nb < NB1; ++nb) {
+          const int n0 = 16 * nb + 4 * kg;
+          if (n0 >= CM) continue;
+          f16x4 h;
+#pragma unroll
+          for (int r = 0; r < 4; ++r) {
+            const float v = acc[nb][q][r] + sB1[n0 + r];
+            h[r] = (f16)(a.act ? ym_silu_fast(v) : v);
+          }
+          const int c = n0 >> 3;
+          *reinterpret_cast<f16x4*>(sM + ((p * CHM + (c ^ swz<CHM>(p))) << 4) + ((n0 & 4) << 1)) = h;
+        }
+      }
+    }
+  }
+  __syncthreads();  // mid image complete; every wave is done with W1
+#pragma unroll
+  for (int u = 0; u < W2PT; ++u) {
+    const int i = tid + NT * u;
+    if (i < W2CH) {
+      const int n = i / (KS2 * 4), c = i - n * (KS2 * 4);
+      *reinterpret_cast<f16x8*>(sW + n * g.P2 + 16 * c) = w2r[u];
+    }
+  }
+  __syncthreads();
+
+  // ---- phase 2: cv2 over the RB output rows, + residual from the LDS input image, stores
+  {
+    const int rows = H - r0 < RB ? H - r0 : RB;
+    const int ng = (g.dbg & 4) ? 0 : rows * gpr;
+    f16* dst = static_cast<f16*>(a.dst);
+    const bool res = a.res != nullptr;
+    for (int it = wave * PX; it < ng; it += NW * PX) {
+      int prow[PX], px0[PX];
+#pragma unroll
+      for (int q = 0; q < PX; ++q) {
+        const int gi = it + q < ng ? it + q : ng - 1;
+        prow[q] = gi / gpr;
+        px0[q] = (gi - prow[q] * gpr) * 16;
+      }
+      f32x4 acc[NB2][PX];
+#pragma unroll
+      for (int nb = 0; nb < NB2; ++nb)
+#pragma unroll
+        for (int q = 0; q < PX; ++q) acc[nb][q] = f32x4{0.f, 0.f, 0.f, 0.f};
+#pragma unroll 3
+      for (int s = 0; s < KS2; ++s) {
+        const int K = 32 * s + 8 * kg;
+        int tap = K / CM;
+        const int ch = (K - tap * CM) >> 3;
+        if (tap > 8) tap = 8;
+        const int ky = tap / 3, kx = tap - 3 * ky;
+        f16x8 wa[NB2], xb[PX];
+#pragma unroll
+        for (int nb = 0; nb < NB2; ++nb)
+          wa[nb] = *reinterpret_cast<const f16x8*>(sW + (16 * nb + col) * g.P2 + 2 * K);
+#pragma unroll
+        for (int q = 0; q < PX; ++q) xb[q] = ld_px<CHM>(sM, (prow[q] + ky) * WP + px0[q] + col + kx, ch);
+#pragma unroll
+        for (int nb = 0; nb < NB2; ++nb)
+#pragma unroll
+          for (int q = 0; q < PX; ++q) acc[nb][q] = __builtin_amdgcn_mfma_f32_16x16x32_f16(wa[nb], xb[q], acc[nb][q], 0, 0, 0);
+      }
+#pragma unroll
+      for (int q = 0; q < PX; ++q) {
+        if (it + q >= ng || px0[q] + col >= W) continue;
+        const int y = r0 + prow[q], x = px0[q] + col;
+        const int px = (prow[q] + 2) * WP + x + 1;  // the same pixel in the input image (residual)
+        const size_t obase = (size_t)(b * a.d_P + y * a.d_W + x) * a.d_ctot + a.d_coff;
+#pragma unroll
+        for (int nb = 0; nb < NB2; ++nb) {
+          const int n0 = 16 * nb + 4 * kg;
+          f16x4 rv = {0, 0, 0, 0};
+          if (res) {
+            const int c = n0 >> 3;
+            rv = *reinterpret_cast<const f16x4*>(sX + ((px * CH + (c ^ swz<CH>(px))) << 4) + ((n0 & 4) << 1));
+          }
+          f16x4 o;
+#pragma unroll
+          for (int r = 0; r < 4; ++r) {
+            const float v = acc[nb][q][r] + sB2[n0 + r];
+            o[r] = (f16)((a.act2 ? ym_silu_fast(v) : v) + (float)rv[r]);
+          }
+          if (!(g.dbg & 8)) *reinterpret_cast<f16x4*>(dst + obase + n0) = o;
+        }
+      }
+    }
+  }
+}
+
+// (id, RB, PX, NW): output rows per band, 16-pixel groups per work item, waves per workgroup (one workgroup per CU:
+// NW / 4 waves per SIMD hide each other's LDS-read latency)
+#define YM_BNECK_CFGS(X) \
+  X(0, 2, 4, 8) X(1, 4, 4, 8) X(2, 5, 4, 8) X(3, 8, 4, 8) X(4, 4, 2, 16) X(5, 5, 2, 16) X(6, 8, 2, 16) X(7, 2, 2, 16)
+constexpr int kNumBneck = 8;
+constexpr int kMaxLds = 160 * 1024;
+
+bool bneck_geom(const ConvArgs& a, int C, int CM, int N2, int RB, BneckGeom& g) {
+  g.RB = RB;
+  g.nbands = (a.Ho + RB - 1) / RB;
+  g.C = C; g.Cm = CM; g.N2 = N2;
+  g.KS1 = (9 * C + 31) / 32;
+  g.KS2 = (9 * CM + 31) / 32;
+  g.P1 = 2 * 32 * g.KS1 + 16;
+  g.P2 = 2 * 32 * g.KS2 + 16;
+  const int WP = a.Wo + 2;
+  const int sx = (RB + 4) * WP * C * 2, sm = (RB + 2) * WP * CM * 2;
+  const int nb1 = (CM + 15) / 16;
+  const int w1 = 16 * nb1 * g.P1, w2 = N2 * g.P2;
+  g.offM = sx;
+  g.offW = sx + sm;
+  g.offB = g.offW + (w1 > w2 ? w1 : w2);
+  g.lds = g.offB + (16 * nb1 + N2) * 4;
+  static const int dbg = [] {
+    const char* e = getenv("YM_BNECK_DBG");
+    return e ? atoi(e) : 0;
+  }();
+  g.dbg = dbg;
+  return g.lds <= kMaxLds;
+}
+
+template <int C, int CM, int N2, int RB, int PX, int NW>
+hipError_t launch(const ConvArgs& a, hipStream_t st) {
+  BneckGeom g;
+  if (!bneck_geom(a, C, CM, N2, RB, g)) return hipErrorInvalidValue;
+  const int B = a.M / (a.Ho * a.Wo);
+  hipLaunchKernelGGL((conv_bneck<C, CM, N2, PX, NW>), dim3(B * g.nbands), dim3(64 * NW), g.lds, st, a, g);
+  return hipGetLastError();
+}
+
+template <int C, int CM, int N2>
+hipError_t dispatch_cfg(const ConvArgs& a, int i, hipStream_t st) {
+  switch (i) {
+#define YM_X(id, rb, px, nw) \
+  case id: return launch<C, CM, N2, rb, px, nw>(a, st);
+    YM_BNECK_CFGS(YM_X)
+#undef YM_X
+  }
+  return hipErrorInvalidValue;
+}
+
+}  // namespace
+
+int ym_conv_bneck_num_cfgs() { return kNumBneck; }
+
+// Host-side applicability: a fused pair (w2) whose successor is a 3x3 (k2 == 3); both convs 3x3 / stride 1 / pad 1
+// on one plain source; (C, Cm, N2) one of the YOLO11 Bottleneck shapes instantiated below;
+// the residual, if any, IS the input view (Bottleneck shortcut); fp16 output into a 4-aligned channel slice.
+hipError_t ym_launch_conv_bneck(int out_f32, const ConvArgs& a, int i, hipStream_t st) {
+  if (i < 0 || i >= kNumBneck || out_f32) return hipErrorInvalidValue;
+  if (!a.w2 || a.k2 != 3 || a.k != 3 || a.s != 1 || a.pad != 1 || a.src1 || a.up0 || a.shuffle || a.raw || a.nchw)
+    return hipErrorInvalidValue;
+  if (a.Hin != a.Ho || a.Win != a.Wo || a.d_W != a.Wo || a.d_pixoff) return hipErrorInvalidValue;
+  if ((a.s0_ctot & 7) || (a.s0_coff & 7) || (a.d_ctot & 3) || (a.d_coff & 3)) return hipErrorInvalidValue;
+  if (a.res && (a.res != a.src0 || a.r_ctot != a.s0_ctot || a.r_coff != a.s0_coff || a.r_P != a.s0_P))
+    return hipErrorInvalidValue;
+  const int C = a.C0, CM = a.N, N2 = a.N2;
+  if (C != 8 * a.Cin8 || a.Kpad < 32 * ((9 * C + 31) / 32) || a.Kpad2 < 32 * ((9 * CM + 31) / 32))
+    return hipErrorInvalidValue;
+  if (C == 16 && CM == 8 && N2 == 16) return dispatch_cfg<16, 8, 16>(a, i, st);
+  if (C == 32 && CM == 16 && N2 == 32) return dispatch_cfg<32, 16, 32>(a, i, st);
+  if (C == 64 && CM == 32 && N2 == 64) return dispatch_cfg<64, 32, 64>(a, i, st);
+  if (C == 32 && CM == 32 && N2 == 32) return dispatch_cfg<32, 32, 32>(a, i, st);
+  return hipErrorInvalidValue;
+}

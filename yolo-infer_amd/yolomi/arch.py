@@ -383,7 +383,7 @@ class GraphBuilder:
                 a, b = op.args, nxt.args
                 args = dict(a)
                 args.update(dst=b["dst"], res=b["res"], anchor_level=b["anchor_level"],
-                            pair=dict(k=1, c1=b["c1"], c2=b["c2"], act=b["act"], bn=b["bn"], wkey=b["wkey"],
+                            pair=dict(k=b["k"], c1=b["c1"], c2=b["c2"], act=b["act"], bn=b["bn"], wkey=b["wkey"],
                                       dst=b["dst"], res=b["res"], mid=a["dst"]))
                 out.append(Op("conv", args, f"{op.name}+{nxt.name.rsplit('.', 1)[-1]}"))
                 i += 2
@@ -392,12 +392,24 @@ class GraphBuilder:
             i += 1
         self.ops = out
 
+    # csrc/ym_conv_bneck.hip: the (C, C_mid, C_out) Bottleneck shapes with a fused kernel
+    BNECK_SHAPES = {(16, 8, 16), (32, 16, 32), (64, 32, 64), (32, 32, 32)}
+
     def _fusable(self, A: Op, B: Op) -> bool:
         if A.kind != "conv" or B.kind != "conv":
             return False
         a, b = A.args, B.args
         if a.get("pair") or a.get("convT") or a["shuffle2x2"] or a["res"] is not None or a["anchor_level"] >= 0:
             return False
+        if b["k"] == 3:  # a Bottleneck (3x3 -> 3x3 + shortcut) on the fused kernel of csrc/ym_conv_bneck.hip
+            mid = a["dst"]
+            return (a["k"] == 3 and a["s"] == 1 and b["s"] == 1 and a["src1"] is None and not a["up0"]
+                    and b["src1"] is None and not b["up0"] and not b["shuffle2x2"] and b["anchor_level"] < 0
+                    and b["src0"].buf is mid.buf and mid.coff == 0 and mid.C == mid.buf.C
+                    and self._readers(mid.buf) == 1
+                    and (b["res"] is None or (b["res"].buf is a["src0"].buf and b["res"].coff == a["src0"].coff
+                                              and b["res"].C == a["src0"].C))
+                    and (a["c1"], a["c2"], b["c2"]) in self.BNECK_SHAPES)
         if b["k"] != 1 or b["s"] != 1 or b["src1"] is not None or b["up0"] or b["shuffle2x2"] or b.get("convT"):
             return False
         mid = a["dst"]
@@ -437,10 +449,10 @@ class GraphBuilder:
                     by += B * (H // f1) * (W // f1) * a["src1"].C * act_bytes
                 by += a["k"] * a["k"] * cin * a["c2"] * act_bytes + a["c2"] * 4
                 c_out = a["c2"]
-                if a.get("pair"):  # + the second 1x1 conv; its input (this conv's output) never reaches HBM
-                    c_out = a["pair"]["c2"]
-                    fl += 2 * npx * a["c2"] * c_out
-                    by += a["c2"] * c_out * act_bytes + c_out * 4
+                if a.get("pair"):  # + the second conv; its input (this conv's output) never reaches HBM
+                    c_out, k2 = a["pair"]["c2"], a["pair"]["k"]
+                    fl += 2 * npx * k2 * k2 * a["c2"] * c_out
+                    by += k2 * k2 * a["c2"] * c_out * act_bytes + c_out * 4
                 ob = 4 if a["dst"].buf.f32 else act_bytes
                 by += npx * c_out * ob
                 if a["res"] is not None:
@@ -482,7 +494,7 @@ class GraphBuilder:
                 npx = (H // fo) * (W // fo)
                 tot += npx * a["k"] * a["k"] * (a["c1"] if op.name != "model.0" else 3) * a["c2"]
                 if a.get("pair"):
-                    tot += npx * a["c2"] * a["pair"]["c2"]
+                    tot += npx * a["pair"]["k"] ** 2 * a["c2"] * a["pair"]["c2"]
             elif op.kind == "dwconv":
                 f = a["src"].buf.f
                 tot += (H // f) * (W // f) * 9 * a["C"]

@@ -16,8 +16,9 @@ Blob layout (int32 little-endian; parsed by `csrc/ym_runtime.cpp:ym_load_weights
   header[32] | buffers[nbuf][8] | ops[nop][32] | names[nop][48 bytes] | pad to 256 | weights
 Conv op record: [1..5] k, s, Cin, N, act | [6..9] src0 buf, coff, C, up0 | [10..12] src1 | [13..16] dst buf, coff,
 anchor level, pixel shuffle | [17..18] residual | [19..21] weight / bias offsets, Kpad | [22..24] int8 QRec, s_in·s_w,
-int32 bias | [25..31] fused 1x1 successor (f16 plans, GraphBuilder.fuse_pairs): W2 / bias2 offsets, N2, act2, Kpad2,
-flag, intermediate buffer (used when the tuner runs the pair as two launches).
+int32 bias | [25..31] fused successor conv (f16 plans, GraphBuilder.fuse_pairs): W2 / bias2 offsets, N2, act2, Kpad2,
+its kernel size k2 (1: streaming FUSE; 3: Bottleneck kernel), intermediate buffer (used when the tuner runs the pair as
+two launches).
 """
 from __future__ import annotations
 
@@ -195,17 +196,18 @@ def pack_graph(g: GraphBuilder, sd: Dict[str, np.ndarray], dtype: str = "f16", q
             r[20] = arena.add(b.astype(np.float32))
             r[21] = Kpad
             pair = a.get("pair")
-            if pair is not None:  # fused 1x1 successor (GraphBuilder.fuse_pairs): W2 [N2][Kpad2], K = this conv's N
+            if pair is not None:  # fused successor (GraphBuilder.fuse_pairs): W2 [N2][Kpad2], K = (ky, kx, this conv's N)
                 if dtype != "f16":
                     raise ValueError(f"op {op.name}: fused conv pairs are f16-only")
-                w2, b2 = _conv_weights(pair, sd)  # (N2, 1, 1, N)
-                N2 = w2.shape[0]
-                assert w2.shape[3] == N
-                Kpad2 = (N + BK - 1) // BK * BK
+                w2, b2 = _conv_weights(pair, sd)  # (N2, k2, k2, N)
+                N2, k2 = w2.shape[0], pair["k"]
+                assert w2.shape[1:] == (k2, k2, N)
+                K2 = k2 * k2 * N
+                Kpad2 = (K2 + BK - 1) // BK * BK
                 w2p = np.zeros((N2, Kpad2), np.float32)
-                w2p[:, :N] = w2.reshape(N2, N)
+                w2p[:, :K2] = w2.reshape(N2, K2)
                 r[25], r[26] = arena.add(w2p.astype(np.float16)), arena.add(b2.astype(np.float32))
-                r[27:32] = [N2, int(bool(pair["act"])), Kpad2, 1, pair["mid"].buf.id]
+                r[27:32] = [N2, int(bool(pair["act"])), Kpad2, k2, pair["mid"].buf.id]
             if quant:
                 s_in, z_in = qp("act:input" if stem else src0.buf.qkey)
                 so, zo = qp("out:" + a["wkey"])
