@@ -504,7 +504,7 @@ def test_fused_pairs_split_equals_unfused_plan():
 
 
 BNECK_BASE = 17 + 18 + 32 + 12  # csrc/ym_conv.hip: first-gen + DMA + streaming + halo ids, then the Bottleneck kernels
-N_BNECK = 8
+N_BNECK = 14
 
 
 @pytest.mark.parametrize("scale", ["n", "s"])
