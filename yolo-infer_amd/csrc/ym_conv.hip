@@ -358,7 +358,7 @@ hipError_t launch_cfg(ConvArgs a, int kind, hipStream_t st) {
 // ---------------------------------------------------------------------------------------------------------------
 // LDS-staged variant for the MFMA-dense layers (large K): one BM x BN tile per 256-thread workgroup (2x2 waves),
 // 64-deep K stages double-buffered in LDS.  Every operand byte is loaded from global ONCE per workgroup with
-// coalesced 16-byte row loads (8 lanes cover a 128-byte row), stored XOR-swizzled (chunk c of row r at c ^ (r&7))
+// coalesced 16-byte row loads (8 lanes cover a 128-byte row), stored XOR-swizzled (chunk c of row r at c ^ ((r >> 1) & 7): conflict-free for ds_read_b128's non-contiguous lane groups)
 // so the MFMA fragment reads (ds_read_b128, 32 rows at one K offset) do not pile onto one bank group; the next
 // stage's global loads are in flight while the current stage's MFMAs run; one barrier per stage.
 template <typename T, typename OutT, int BM, int BN, int KIND>
@@ -447,12 +447,12 @@ __global__ __launch_bounds__(256) void conv_lds(const ConvArgs a) {
 #pragma unroll
     for (int i = 0; i < RA; ++i) {
       const int r = (tid >> 3) + 32 * i;
-      *reinterpret_cast<V*>(&sA[buf][r * BK + ((kc ^ (r & 7)) * 8)]) = rw[i];
+      *reinterpret_cast<V*>(&sA[buf][r * BK + ((kc ^ ((r >> 1) & 7)) * 8)]) = rw[i];
     }
 #pragma unroll
     for (int i = 0; i < RB; ++i) {
       const int r = (tid >> 3) + 32 * i;
-      *reinterpret_cast<V*>(&sB[buf][r * BK + ((kc ^ (r & 7)) * 8)]) = ra[i];
+      *reinterpret_cast<V*>(&sB[buf][r * BK + ((kc ^ ((r >> 1) & 7)) * 8)]) = ra[i];
     }
   };
   f32x16 acc[TM][TN];
@@ -477,12 +477,12 @@ __global__ __launch_bounds__(256) void conv_lds(const ConvArgs a) {
 #pragma unroll
       for (int j = 0; j < TN; ++j) {
         const int r = wn * (BN / 2) + j * 32 + l32;
-        fa[j] = *reinterpret_cast<const V*>(&sA[cur][r * BK + ((cc ^ (r & 7)) * 8)]);
+        fa[j] = *reinterpret_cast<const V*>(&sA[cur][r * BK + ((cc ^ ((r >> 1) & 7)) * 8)]);
       }
 #pragma unroll
       for (int i = 0; i < TM; ++i) {
         const int r = wm * (BM / 2) + i * 32 + l32;
-        fb[i] = *reinterpret_cast<const V*>(&sB[cur][r * BK + ((cc ^ (r & 7)) * 8)]);
+        fb[i] = *reinterpret_cast<const V*>(&sB[cur][r * BK + ((cc ^ ((r >> 1) & 7)) * 8)]);
       }
 #pragma unroll
       for (int i = 0; i < TM; ++i)

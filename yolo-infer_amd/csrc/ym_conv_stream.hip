@@ -48,12 +48,16 @@ constexpr int RB = 8;           // output-channel blocks of 16 whose residuals a
 template <typename OutT, int KIND, int KS, int PX, bool FUSE>
 __global__ __launch_bounds__(256) void conv_stream(const ConvArgs a) {
   constexpr int KP = KS * 32;      // Kpad
-  constexpr int LDW = KP + 8;      // LDS row pitch (halves): +16 bytes
+  // LDS row pitch (halves) KP + 16 = 4·KS + 2 16-byte slots: the A-fragment reads (16 rows x one K chunk per lane
+  // group kg) hit distinct slots in each of ds_read_b128's non-contiguous lane groups (MI355X_MICROARCH §LDS);
+  // a +8 pitch is 2-way there
+  constexpr int LDW = KP + 16;
   constexpr int NBF = FUSE ? kFuseMaxN / 16 : 1;
   extern __shared__ __attribute__((aligned(16))) f16 ws[];  // [N][LDW], then bias [N] f32 (FUSE: then W2, bias2)
   float* bs = reinterpret_cast<float*>(ws + ((a.N + 15) & ~15) * LDW);
   const int NB = (a.N + 15) >> 4;
-  const int LDW2 = 16 * NB + 4;  // W2 row pitch (halves): the 8-byte A reads of 16 rows spread over the banks
+  const int LDW2 = 16 * NB + 8;  // W2 row pitch (halves): the 8-byte A reads of 16 rows x 2 lane groups hit 32
+                                 // distinct 8-byte slots of a ds_read_b64 half-wave (+4 was 2-way)
   f16* w2s = reinterpret_cast<f16*>(bs + 16 * NB);
   const int NB2 = FUSE ? (a.N2 + 15) >> 4 : 0;
   float* bs2 = reinterpret_cast<float*>(w2s + 16 * NB2 * LDW2);
@@ -409,11 +413,11 @@ hipError_t launch(const ConvArgs& a, hipStream_t st) {
   long wgs = (G + 4 * PX - 1) / (4 * PX);
   if (wgs > CAP) wgs = CAP;  // the persistent grid: CAP workgroups, the rest streams through them
   const int NP = (a.N + 15) & ~15;
-  size_t lds = (size_t)NP * (KS * 32 + 8) * sizeof(f16) + (size_t)NP * sizeof(float);
+  size_t lds = (size_t)NP * (KS * 32 + 16) * sizeof(f16) + (size_t)NP * sizeof(float);
   if (lds > kMaxWBytes) return hipErrorInvalidValue;
-  if (a.w2) {  // fused pair: + W2 [N2P][NP + 4] and bias2 (checked by ym_launch_conv_stream: N <= 128)
+  if (a.w2) {  // fused pair: + W2 [N2P][NP + 8] and bias2 (checked by ym_launch_conv_stream: N <= 128)
     const int N2P = (a.N2 + 15) & ~15;
-    lds += (size_t)N2P * (NP + 4) * sizeof(f16) + (size_t)N2P * sizeof(float);
+    lds += (size_t)N2P * (NP + 8) * sizeof(f16) + (size_t)N2P * sizeof(float);
     if (lds > kMaxFusedBytes) return hipErrorInvalidValue;
     hipLaunchKernelGGL((conv_stream<OutT, KIND, KS, PX, true>), dim3(wgs), dim3(256), lds, st, a);
   } else {

@@ -424,9 +424,9 @@ class GraphBuilder:
         if N > self.FUSE_MAX_N or N % 4 or N2 % 4 or kpad // 32 not in self.STREAM_KS[a["k"]]:
             return False
         NP, N2P = -(-N // 16) * 16, -(-N2 // 16) * 16
-        if NP * (kpad + 8) * 2 + NP * 4 > 80 * 1024:
+        if NP * (kpad + 16) * 2 + NP * 4 > 80 * 1024:  # csrc/ym_conv_stream.hip LDS: W [NP][Kpad + 16], W2 [N2P][NP + 8]
             return False
-        return NP * (kpad + 8) * 2 + NP * 4 + N2P * (NP + 4) * 2 + N2P * 4 <= self.FUSE_MAX_LDS
+        return NP * (kpad + 16) * 2 + NP * 4 + N2P * (NP + 8) * 2 + N2P * 4 <= self.FUSE_MAX_LDS
 
     # ------------------------------------------------------------------ accounting
     def op_costs(self, B: int, H: int, W: int, act_bytes: int = 2):
