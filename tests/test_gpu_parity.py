@@ -503,7 +503,7 @@ def test_fused_pairs_split_equals_unfused_plan():
     assert rel(hs, hu) < 1e-2 and rel(hf, hu) < 1e-2
 
 
-BNECK_BASE = 17 + 18 + 32 + 12  # csrc/ym_conv.hip: first-gen + DMA + streaming + halo ids, then the Bottleneck kernels
+BNECK_BASE = 17 + 18 + 35 + 12  # csrc/ym_conv.hip: first-gen + DMA + streaming + halo ids, then the Bottleneck kernels
 N_BNECK = 14
 
 

@@ -28,14 +28,15 @@ struct SCfg {
   X(0, 1, 2, 1, 1024) X(1, 1, 2, 2, 1024) X(2, 1, 2, 1, 4096) X(3, 1, 4, 1, 1024) X(4, 1, 4, 2, 1024)            \
   X(5, 1, 8, 1, 1024) X(6, 1, 4, 1, 4096) X(7, 3, 4, 1, 1024) X(8, 3, 6, 1, 1024) X(9, 3, 10, 1, 1024)          \
   X(10, 3, 18, 1, 1024) X(11, 3, 4, 1, 4096) X(12, 3, 6, 1, 4096) X(13, 3, 10, 1, 4096) X(14, 3, 18, 1, 4096)         \
-  X(15, 1, 2, 2, 4096) X(16, 1, 2, 4, 4096) X(17, 1, 4, 2, 4096) X(18, 3, 4, 2, 4096) X(19, 3, 6, 2, 4096)
+  X(15, 1, 2, 2, 4096) X(16, 1, 2, 4, 4096) X(17, 1, 4, 2, 4096) X(18, 3, 4, 2, 4096) X(19, 3, 6, 2, 4096)        \
+  X(20, 1, 6, 1, 4096) X(21, 1, 6, 2, 4096) X(22, 1, 6, 1, 1024)
 constexpr SCfg kStream[] = {
 #define YM_X(id, kind, ks, px, cap) {kind, ks, px, cap},
     YM_STREAM_CFGS(YM_X)
 #undef YM_X
 };
 constexpr int kNumStream = sizeof(kStream) / sizeof(kStream[0]);
-constexpr int kMaxWBytes = 80 * 1024;
+constexpr int kMaxWBytes = 144 * 1024;  // whole weight matrix in LDS (one workgroup per CU above ~75 KB: the KS 6 configs)
 constexpr int kMaxFusedBytes = 112 * 1024;  // fused pairs: both weight matrices
 
 // FUSE: the fused pair (ConvArgs::w2) — the first conv's activated output block nb (16 channels x 16 pixels, lane

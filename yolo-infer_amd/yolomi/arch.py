@@ -354,7 +354,7 @@ class GraphBuilder:
         # the stem reads 3 real channels out of the 8-channel padded input: pad its weights' Cin to 8 at pack time
 
     # ------------------------------------------------------------------ fused pairs (f16 plans)
-    STREAM_KS = {1: (2, 4, 8), 3: (4, 6, 10, 18)}  # csrc/ym_conv_stream.hip K steps of 32 per kind
+    STREAM_KS = {1: (2, 4, 6, 8), 3: (4, 6, 10, 18)}  # csrc/ym_conv_stream.hip K steps of 32 per kind
     FUSE_MAX_N = 128                                 # csrc/ym_conv_stream.hip kFuseMaxN
     FUSE_MAX_LDS = 112 * 1024                        # csrc/ym_conv_stream.hip kMaxFusedBytes
 
