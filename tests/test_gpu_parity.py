@@ -509,10 +509,11 @@ N_BNECK = 14
 
 @pytest.mark.parametrize("scale", ["n", "s"])
 def test_bneck_kernel_matches_split_pair(scale):
-    """csrc/ym_conv_bneck.hip: every Bottleneck variant (rows per band x pixel groups per item) on every fused
-    Bottleneck of the f16 plan — 160x160, 80x80 and (n) 40x40 maps, where 40 is not a multiple of the 16-pixel group
-    — equals the same pair run as two conv launches (fp16 mid tensor in HBM) within fp16 rounding of the output: the
-    fused kernel rounds the mid tensor to fp16 exactly as the stored tensor is, only fp32 summation order differs."""
+    """csrc/ym_conv_bneck.hip: every variant (rows x tile width x pixel groups x waves) on every fused Bottleneck of
+    the f16 plan — 160x160, 80x80 and (n) 40x40 maps, where 40 is not a multiple of the 16-pixel group — and on every
+    stride-2 3x3 -> 1x1 pair (even/odd column layout) equals the same pair run as two conv launches (fp16 mid tensor
+    in HBM) within fp16 rounding of the output: the fused kernel rounds the mid tensor to fp16 exactly as the stored
+    tensor is, only fp32 summation order differs."""
     m = model(scale, "f16")
     e = m.model.engine
     x = make_input("uniform", (5, 6), 640).to(DEV)
@@ -520,8 +521,8 @@ def test_bneck_kernel_matches_split_pair(scale):
     e.run(x, use_graph=False)
     tuned = e.rt.get_op_cfg(B, H, W)
     ops = e.graph.ops
-    bn = [i for i, op in enumerate(ops) if op.args.get("pair") and op.args["pair"]["k"] == 3]
-    assert len(bn) >= 3
+    bn = [i for i, op in enumerate(ops) if op.args.get("pair") and (op.args["pair"]["k"] == 3 or op.args["s"] == 2)]
+    assert len(bn) >= 4  # the Bottlenecks and the stride-2 3x3 -> 1x1 pairs (model.1+cv1, n: model.3+cv1)
 
     def outputs(cfg_bn):
         e.rt.set_op_cfg(B, H, W, [cfg_bn if i in bn else -1 for i in range(len(ops))])

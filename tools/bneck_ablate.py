@@ -24,7 +24,7 @@ def child(model, cfgs):
     x = synthetic_batch(8, 640, 1000, torch.device("cuda", 0))
     e.run(x)
     ops = e.graph.ops
-    bn = [i for i, op in enumerate(ops) if op.args.get("pair") and op.args["pair"]["k"] == 3]
+    bn = [i for i, op in enumerate(ops) if op.args.get("pair") and (op.args["pair"]["k"] == 3 or op.args["s"] == 2)]
     base = e.rt.get_op_cfg(8, 640, 640)
     for c in cfgs:
         e.rt.set_op_cfg(8, 640, 640, [c if i in bn else base[i] for i in range(len(ops))])

@@ -654,8 +654,14 @@ hipError_t ym_launch_conv(int dtype, int out_f32, const ConvArgs& a, int cfg, hi
     }
     return hipErrorInvalidValue;
   }
-  if (a.w2) {  // fused pair: only the streaming kernels hold a whole N in one wave (csrc/ym_conv_stream.hip)
+  if (a.w2) {  // fused pair: the streaming kernels hold a whole N in one wave (csrc/ym_conv_stream.hip); a stride-2
+    // 3x3 followed by a 1x1 can also take the band kernel of csrc/ym_conv_bneck.hip
     if (dtype != YM_DT_F16) return hipErrorInvalidValue;
+    const int bb = kNumAllCfg + ym_conv_dma_num_cfgs() + ym_conv_stream_num_cfgs() + ym_conv_halo_num_cfgs();
+    if (cfg >= bb && cfg < bb + ym_conv_bneck_num_cfgs()) {
+      const hipError_t e = ym_launch_conv_bneck(out_f32, a, cfg - bb, st);
+      if (e != hipErrorInvalidValue || strict) return e;
+    }
     const int sbase = kNumAllCfg + ym_conv_dma_num_cfgs(), ns = ym_conv_stream_num_cfgs();
     if (cfg >= sbase && cfg < sbase + ns) {
       const hipError_t e = ym_launch_conv_stream(out_f32, a, cfg - sbase, st);

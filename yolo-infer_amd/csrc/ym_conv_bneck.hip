@@ -39,12 +39,14 @@ __device__ __forceinline__ int swz(int p) {
 }
 
 struct BneckGeom {
-  int RB;          // output rows per band
+  int RB;          // output rows per tile
   int nbands;      // ceil(H / RB)
   int TW, ntx;     // tile width (pixels, a multiple of 16 or the map width) and tiles per row
   int C, Cm, N2;   // input (= residual) channels, mid channels, output channels
-  int KS1, KS2;    // K steps of 32 per conv (9·C, 9·Cm rounded up)
+  int KS1, KS2;    // K steps of 32 per conv
   int P1, P2;      // weight row pitches (bytes)
+  int MR, MC;      // mid tile rows / columns (K2 = 3: + 1-pixel halo)
+  int XR, XC, XE;  // input tile rows / columns; S1 = 2: even columns first (XE of them), then the odd ones
   int offM, offW, offB;  // LDS byte offsets: mid image, weight slot, biases (input image at 0)
   int lds;
   int dbg;  // tools/bneck_ablate.py timing ablations (YM_BNECK_DBG): 1 no input loads, 2 no cv1, 4 no cv2, 8 no stores
@@ -56,12 +58,23 @@ __device__ __forceinline__ f16x8 ld_px(const char* img, int p, int c) {
   return *reinterpret_cast<const f16x8*>(img + ((p * CH + (c ^ swz<CH>(p))) << 4));
 }
 
-template <int C, int CM, int N2, int PX, int NW>
+// LDS pixel index of input-tile pixel (row, column xc).  Stride 2 keeps even and odd columns in separate half-rows,
+// so the taps of 16 consecutive mid pixels (input columns 2j + kx) read 16 consecutive pixel slots.
+template <int S1>
+__device__ __forceinline__ int xpix(int row, int xc, int XC, int XE) {
+  if constexpr (S1 == 1) return row * XC + xc;
+  else return row * XC + ((xc & 1) ? XE + (xc >> 1) : (xc >> 1));
+}
+
+// S1: stride of the first 3x3 conv (1: Bottleneck, 2: a downsampling Conv); K2: kernel of the second conv (3: the
+// Bottleneck's cv2 with its 1-pixel halo on the mid image; 1: a following 1x1 such as C3k2.cv1, no halo).
+template <int C, int CM, int N2, int PX, int NW, int S1, int K2>
 __global__ __launch_bounds__(64 * NW) void conv_bneck(const ConvArgs a, const BneckGeom g) {
   constexpr int NT = 64 * NW;
   constexpr int CH = C / 8, CHM = CM / 8;
   constexpr int NB1 = (CM + 15) / 16, NB2 = N2 / 16;
-  constexpr int KS1 = (9 * C + 31) / 32, KS2 = (9 * CM + 31) / 32;
+  constexpr int KS1 = (9 * C + 31) / 32, KS2 = (K2 * K2 * CM + 31) / 32;
+  constexpr int HM = K2 / 2;  // mid-tile halo
   extern __shared__ __attribute__((aligned(16))) char smem[];
   char* sX = smem;
   char* sM = smem + g.offM;
@@ -70,18 +83,18 @@ __global__ __launch_bounds__(64 * NW) void conv_bneck(const ConvArgs a, const Bn
   float* sB2 = sB1 + 16 * NB1;
   const int tid = threadIdx.x, lane = tid & 63, wave = tid >> 6;
   const int col = lane & 15, kg = lane >> 4;
-  const int W = a.Wo, H = a.Ho, TW = g.TW;
-  const int WPX = TW + 4, WPM = TW + 2;  // input / mid image row pitches (pixels): 2- and 1-column halos
+  const int W = a.Wo, H = a.Ho, TW = g.TW;  // mid (= output) map
+  const int MR = g.MR, MC = g.MC, XR = g.XR, XC = g.XC, XE = g.XE;
   const int vb = ym_xcd_block(blockIdx.x, gridDim.x);  // neighbouring tiles (shared halo rows) on one XCD
   const int tx = vb % g.ntx, band = (vb / g.ntx) % g.nbands, b = vb / (g.ntx * g.nbands);
   const int RB = g.RB, r0 = band * RB, x0 = tx * TW;  // the tile: rows r0 .. r0+RB-1, columns x0 .. x0+TW-1
+  const int mr0 = r0 - HM, mc0 = x0 - HM;           // mid tile origin (map coordinates)
+  const int xr0 = mr0 * S1 - 1, xc0 = mc0 * S1 - 1;  // input tile origin (input map coordinates)
   const f16* src = static_cast<const f16*>(a.src0);
   const f16* W1 = static_cast<const f16*>(a.w);
   const f16* W2 = static_cast<const f16*>(a.w2);
 
-  // ---- phase 0: W2 prefetch (registers), W1 + biases, input tile + halo, zeroed mid image.  Input image: rows
-  // r0-2 .. r0+RB+1, columns x0-2 .. x0+TW+1 (zeros outside the map); mid image: rows r0-1 .. r0+RB, columns
-  // x0-1 .. x0+TW (zero where outside the map: cv2's padding)
+  // ---- phase 0: W2 prefetch (registers), W1 + biases, input tile (zeros outside the input map), zeroed mid image
   constexpr int W2CH = N2 * KS2 * 4;  // 16-byte chunks of W2 rows [N2][KS2 * 32]
   constexpr int W2PT = (W2CH + NT - 1) / NT;
   f16x8 w2r[W2PT];
@@ -99,50 +112,52 @@ __global__ __launch_bounds__(64 * NW) void conv_bneck(const ConvArgs a, const Bn
   for (int i = tid; i < 16 * NB1; i += NT) sB1[i] = i < CM ? a.bias[i] : 0.f;
   for (int i = tid; i < N2; i += NT) sB2[i] = a.bias2[i];
   {
-    const int nx = (RB + 4) * WPX * CH;  // input image chunks
+    const int nx = XR * XC * CH;  // input tile chunks, in input-map order
     const size_t img = (size_t)b * a.s0_P;
     for (int i0 = tid; i0 < nx; i0 += NT * 8) {
       f16x8 v[8];
 #pragma unroll
       for (int u = 0; u < 8; ++u) {
         const int i = i0 + NT * u;
-        const int p = i / CH, c = i - p * CH;
-        const int row = p / WPX, j = p - row * WPX;
-        const int gy = r0 - 2 + row, gx = x0 - 2 + j;
-        v[u] = (i < nx && !(g.dbg & 1) && (unsigned)gy < (unsigned)H && (unsigned)gx < (unsigned)W)
-                   ? *reinterpret_cast<const f16x8*>(src + (img + (size_t)gy * W + gx) * a.s0_ctot + a.s0_coff + 8 * c)
+        const int q = i / CH, c = i - q * CH;
+        const int row = q / XC, xc = q - row * XC;
+        const int gy = xr0 + row, gx = xc0 + xc;
+        v[u] = (i < nx && !(g.dbg & 1) && (unsigned)gy < (unsigned)a.Hin && (unsigned)gx < (unsigned)a.Win)
+                   ? *reinterpret_cast<const f16x8*>(src + (img + (size_t)gy * a.Win + gx) * a.s0_ctot + a.s0_coff + 8 * c)
                    : Vec8<f16>::zero();
       }
 #pragma unroll
       for (int u = 0; u < 8; ++u) {
         const int i = i0 + NT * u;
         if (i < nx) {
-          const int p = i / CH, c = i - p * CH;
+          const int q = i / CH, c = i - q * CH;
+          const int row = q / XC, xc = q - row * XC;
+          const int p = xpix<S1>(row, xc, XC, XE);
           *reinterpret_cast<f16x8*>(sX + ((p * CH + (c ^ swz<CH>(p))) << 4)) = v[u];
         }
       }
     }
-    const int nm = (RB + 2) * WPM * CHM;
+    const int nm = MR * MC * CHM;
     for (int i = tid; i < nm; i += NT) *reinterpret_cast<f16x8*>(sM + (i << 4)) = Vec8<f16>::zero();
   }
   __syncthreads();
 
-  // ---- phase 1: cv1 over the RB+2 mid rows x TW+2 mid columns, PX 16-pixel groups per work item (lanes past the
-  // row's end compute but never store)
+  // ---- phase 1: the first conv over the MR x MC mid tile, PX 16-pixel groups per work item (lanes past a row's end
+  // compute but never store)
   {
-    const int gpr = (WPM + 15) / 16;
-    const int ng = (g.dbg & 2) ? 0 : (RB + 2) * gpr;
+    const int gpr = (MC + 15) / 16;
+    const int ng = (g.dbg & 2) ? 0 : MR * gpr;
     for (int it = wave * PX; it < ng; it += NW * PX) {
-      int prow[PX], pm[PX];  // mid row, this lane's mid column
+      int prow[PX], pm[PX];  // mid row, this lane's mid column (tile coordinates)
       bool ok[PX];
 #pragma unroll
       for (int q = 0; q < PX; ++q) {
         const int gi = it + q < ng ? it + q : ng - 1;  // a tail slot recomputes the last group, never stores it
         prow[q] = gi / gpr;
         pm[q] = (gi - prow[q] * gpr) * 16 + col;
-        const int gm = r0 - 1 + prow[q], xm = x0 - 1 + pm[q];
-        ok[q] = it + q < ng && pm[q] < WPM && (unsigned)gm < (unsigned)H && (unsigned)xm < (unsigned)W;
-        if (pm[q] >= WPM) pm[q] = WPM - 1;  // keep the reads inside the image rows
+        const int gm = mr0 + prow[q], xm = mc0 + pm[q];
+        ok[q] = it + q < ng && pm[q] < MC && (unsigned)gm < (unsigned)H && (unsigned)xm < (unsigned)W;
+        if (pm[q] >= MC) pm[q] = MC - 1;  // keep the reads inside the image rows
       }
       f32x4 acc[NB1][PX];
 #pragma unroll
@@ -161,7 +176,8 @@ __global__ __launch_bounds__(64 * NW) void conv_bneck(const ConvArgs a, const Bn
         for (int nb = 0; nb < NB1; ++nb)
           wa[nb] = *reinterpret_cast<const f16x8*>(sW + (16 * nb + col) * g.P1 + 2 * K);
 #pragma unroll
-        for (int q = 0; q < PX; ++q) xb[q] = ld_px<CH>(sX, (prow[q] + ky) * WPX + pm[q] + kx, ch);
+        for (int q = 0; q < PX; ++q)
+          xb[q] = ld_px<CH>(sX, xpix<S1>(prow[q] * S1 + ky, pm[q] * S1 + kx, XC, XE), ch);
 #pragma unroll
         for (int nb = 0; nb < NB1; ++nb)
 #pragma unroll
@@ -171,7 +187,7 @@ __global__ __launch_bounds__(64 * NW) void conv_bneck(const ConvArgs a, const Bn
 #pragma unroll
       for (int q = 0; q < PX; ++q) {
         if (!ok[q]) continue;
-        const int p = prow[q] * WPM + pm[q];
+        const int p = prow[q] * MC + pm[q];
 #pragma unroll
         for (int nb = 0; nb < NB1; ++nb) {
           const int n0 = 16 * nb + 4 * kg;
@@ -199,14 +215,15 @@ __global__ __launch_bounds__(64 * NW) void conv_bneck(const ConvArgs a, const Bn
   }
   __syncthreads();
 
-  // ---- phase 2: cv2 over the RB output rows x TW columns, + residual from the LDS input image, stores
+  // ---- phase 2: the second conv over the RB x TW output tile, + residual (S1 = 1, K2 = 3: the input pixels, still in
+  // LDS), stores
   {
     const int rows = H - r0 < RB ? H - r0 : RB;
     const int xe = W - x0 < TW ? W - x0 : TW;  // tile columns inside the map
     const int gpr = (TW + 15) / 16;
     const int ng = (g.dbg & 4) ? 0 : rows * gpr;
     f16* dst = static_cast<f16*>(a.dst);
-    const bool res = a.res != nullptr;
+    const bool res = S1 == 1 && K2 == 3 && a.res != nullptr;
     for (int it = wave * PX; it < ng; it += NW * PX) {
       int prow[PX], pc[PX];  // output row, this lane's output column (both within the tile)
 #pragma unroll
@@ -214,6 +231,7 @@ __global__ __launch_bounds__(64 * NW) void conv_bneck(const ConvArgs a, const Bn
         const int gi = it + q < ng ? it + q : ng - 1;
         prow[q] = gi / gpr;
         pc[q] = (gi - prow[q] * gpr) * 16 + col;
+        if (K2 == 1 && pc[q] >= MC) pc[q] = MC - 1;
       }
       f32x4 acc[NB2][PX];
 #pragma unroll
@@ -225,14 +243,14 @@ __global__ __launch_bounds__(64 * NW) void conv_bneck(const ConvArgs a, const Bn
         const int K = 32 * s + 8 * kg;
         int tap = K / CM;
         const int ch = (K - tap * CM) >> 3;
-        if (tap > 8) tap = 8;
+        if (tap > K2 * K2 - 1) tap = K2 * K2 - 1;
         const int ky = tap / 3, kx = tap - 3 * ky;
         f16x8 wa[NB2], xb[PX];
 #pragma unroll
         for (int nb = 0; nb < NB2; ++nb)
           wa[nb] = *reinterpret_cast<const f16x8*>(sW + (16 * nb + col) * g.P2 + 2 * K);
 #pragma unroll
-        for (int q = 0; q < PX; ++q) xb[q] = ld_px<CHM>(sM, (prow[q] + ky) * WPM + pc[q] + kx, ch);
+        for (int q = 0; q < PX; ++q) xb[q] = ld_px<CHM>(sM, (prow[q] + ky) * MC + pc[q] + kx, ch);
 #pragma unroll
         for (int nb = 0; nb < NB2; ++nb)
 #pragma unroll
@@ -242,7 +260,7 @@ __global__ __launch_bounds__(64 * NW) void conv_bneck(const ConvArgs a, const Bn
       for (int q = 0; q < PX; ++q) {
         if (it + q >= ng || pc[q] >= xe) continue;
         const int y = r0 + prow[q], x = x0 + pc[q];
-        const int px = (prow[q] + 2) * WPX + pc[q] + 2;  // the same pixel in the input image (residual)
+        const int px = xpix<S1>(prow[q] + 2, pc[q] + 2, XC, XE);  // the same pixel in the input tile (residual)
         const size_t obase = (size_t)(b * a.d_P + y * a.d_W + x) * a.d_ctot + a.d_coff;
 #pragma unroll
         for (int nb = 0; nb < NB2; ++nb) {
@@ -275,7 +293,7 @@ __global__ __launch_bounds__(64 * NW) void conv_bneck(const ConvArgs a, const Bn
 constexpr int kNumBneck = 14;
 constexpr int kMaxLds = 160 * 1024;
 
-bool bneck_geom(const ConvArgs& a, int C, int CM, int N2, int RB, int TW, BneckGeom& g) {
+bool bneck_geom(const ConvArgs& a, int C, int CM, int N2, int S1, int K2, int RB, int TW, BneckGeom& g) {
   g.RB = RB;
   g.nbands = (a.Ho + RB - 1) / RB;
   if (TW >= a.Wo) TW = 0;
@@ -283,10 +301,16 @@ bool bneck_geom(const ConvArgs& a, int C, int CM, int N2, int RB, int TW, BneckG
   g.ntx = (a.Wo + g.TW - 1) / g.TW;
   g.C = C; g.Cm = CM; g.N2 = N2;
   g.KS1 = (9 * C + 31) / 32;
-  g.KS2 = (9 * CM + 31) / 32;
+  g.KS2 = (K2 * K2 * CM + 31) / 32;
   g.P1 = 64 * g.KS1 + 32;
   g.P2 = 64 * g.KS2 + 32;
-  const int sx = (RB + 4) * (g.TW + 4) * C * 2, sm = (RB + 2) * (g.TW + 2) * CM * 2;
+  const int hm = K2 / 2;
+  g.MR = RB + 2 * hm;
+  g.MC = g.TW + 2 * hm;
+  g.XR = (g.MR - 1) * S1 + 3;
+  g.XC = (g.MC - 1) * S1 + 3;
+  g.XE = (g.XC + 1) / 2;
+  const int sx = g.XR * g.XC * C * 2, sm = g.MR * g.MC * CM * 2;
   const int nb1 = (CM + 15) / 16;
   const int w1 = 16 * nb1 * g.P1, w2 = N2 * g.P2;
   g.offM = sx;
@@ -301,20 +325,20 @@ bool bneck_geom(const ConvArgs& a, int C, int CM, int N2, int RB, int TW, BneckG
   return g.lds <= kMaxLds;
 }
 
-template <int C, int CM, int N2, int RB, int TW, int PX, int NW>
+template <int C, int CM, int N2, int S1, int K2, int RB, int TW, int PX, int NW>
 hipError_t launch(const ConvArgs& a, hipStream_t st) {
   BneckGeom g;
-  if ((TW && TW >= a.Wo) || !bneck_geom(a, C, CM, N2, RB, TW, g)) return hipErrorInvalidValue;  // (TW: a real split)
+  if ((TW && TW >= a.Wo) || !bneck_geom(a, C, CM, N2, S1, K2, RB, TW, g)) return hipErrorInvalidValue;  // (TW: a real split)
   const int B = a.M / (a.Ho * a.Wo);
-  hipLaunchKernelGGL((conv_bneck<C, CM, N2, PX, NW>), dim3(B * g.nbands * g.ntx), dim3(64 * NW), g.lds, st, a, g);
+  hipLaunchKernelGGL((conv_bneck<C, CM, N2, PX, NW, S1, K2>), dim3(B * g.nbands * g.ntx), dim3(64 * NW), g.lds, st, a, g);
   return hipGetLastError();
 }
 
-template <int C, int CM, int N2>
+template <int C, int CM, int N2, int S1, int K2>
 hipError_t dispatch_cfg(const ConvArgs& a, int i, hipStream_t st) {
   switch (i) {
 #define YM_X(id, rb, tw, px, nw) \
-  case id: return launch<C, CM, N2, rb, tw, px, nw>(a, st);
+  case id: return launch<C, CM, N2, S1, K2, rb, tw, px, nw>(a, st);
     YM_BNECK_CFGS(YM_X)
 #undef YM_X
   }
@@ -325,23 +349,31 @@ hipError_t dispatch_cfg(const ConvArgs& a, int i, hipStream_t st) {
 
 int ym_conv_bneck_num_cfgs() { return kNumBneck; }
 
-// Host-side applicability: a fused pair (w2) whose successor is a 3x3 (k2 == 3); both convs 3x3 / stride 1 / pad 1
-// on one plain source; (C, Cm, N2) one of the YOLO11 Bottleneck shapes instantiated below;
-// the residual, if any, IS the input view (Bottleneck shortcut); fp16 output into a 4-aligned channel slice.
+// Host-side applicability: a fused pair (w2) of a 3x3 / pad 1 conv on one plain source followed by either
+//   * a 3x3 stride-1 conv (k2 == 3, first conv stride 1): a Bottleneck; the residual, if any, IS the input view, or
+//   * a 1x1 conv (k2 == 1, first conv stride 2): a downsampling Conv and the next C3k2's cv1, no residual;
+// (C, Cm, N2) one of the YOLO11 shapes instantiated below; fp16 output into a 4-aligned channel slice.
 hipError_t ym_launch_conv_bneck(int out_f32, const ConvArgs& a, int i, hipStream_t st) {
   if (i < 0 || i >= kNumBneck || out_f32) return hipErrorInvalidValue;
-  if (!a.w2 || a.k2 != 3 || a.k != 3 || a.s != 1 || a.pad != 1 || a.src1 || a.up0 || a.shuffle || a.raw || a.nchw)
+  if (!a.w2 || a.k != 3 || a.pad != 1 || a.src1 || a.up0 || a.shuffle || a.raw || a.nchw) return hipErrorInvalidValue;
+  const bool bneck = a.k2 == 3 && a.s == 1, down = a.k2 == 1 && a.s == 2;
+  if (!bneck && !down) return hipErrorInvalidValue;
+  if (a.Ho != (a.Hin - 1) / a.s + 1 || a.Wo != (a.Win - 1) / a.s + 1 || a.d_W != a.Wo || a.d_pixoff)
     return hipErrorInvalidValue;
-  if (a.Hin != a.Ho || a.Win != a.Wo || a.d_W != a.Wo || a.d_pixoff) return hipErrorInvalidValue;
   if ((a.s0_ctot & 7) || (a.s0_coff & 7) || (a.d_ctot & 3) || (a.d_coff & 3)) return hipErrorInvalidValue;
-  if (a.res && (a.res != a.src0 || a.r_ctot != a.s0_ctot || a.r_coff != a.s0_coff || a.r_P != a.s0_P))
+  if (a.res && (down || a.res != a.src0 || a.r_ctot != a.s0_ctot || a.r_coff != a.s0_coff || a.r_P != a.s0_P))
     return hipErrorInvalidValue;
-  const int C = a.C0, CM = a.N, N2 = a.N2;
-  if (C != 8 * a.Cin8 || a.Kpad < 32 * ((9 * C + 31) / 32) || a.Kpad2 < 32 * ((9 * CM + 31) / 32))
+  const int C = a.C0, CM = a.N, N2 = a.N2, K2 = a.k2;
+  if (C != 8 * a.Cin8 || a.Kpad < 32 * ((9 * C + 31) / 32) || a.Kpad2 < 32 * ((K2 * K2 * CM + 31) / 32))
     return hipErrorInvalidValue;
-  if (C == 16 && CM == 8 && N2 == 16) return dispatch_cfg<16, 8, 16>(a, i, st);
-  if (C == 32 && CM == 16 && N2 == 32) return dispatch_cfg<32, 16, 32>(a, i, st);
-  if (C == 64 && CM == 32 && N2 == 64) return dispatch_cfg<64, 32, 64>(a, i, st);
-  if (C == 32 && CM == 32 && N2 == 32) return dispatch_cfg<32, 32, 32>(a, i, st);
+  if (bneck) {
+    if (C == 16 && CM == 8 && N2 == 16) return dispatch_cfg<16, 8, 16, 1, 3>(a, i, st);
+    if (C == 32 && CM == 16 && N2 == 32) return dispatch_cfg<32, 16, 32, 1, 3>(a, i, st);
+    if (C == 64 && CM == 32 && N2 == 64) return dispatch_cfg<64, 32, 64, 1, 3>(a, i, st);
+    if (C == 32 && CM == 32 && N2 == 32) return dispatch_cfg<32, 32, 32, 1, 3>(a, i, st);
+  } else {
+    if (C == 32 && CM == 64 && N2 == 64) return dispatch_cfg<32, 64, 64, 2, 1>(a, i, st);  // s model.1, n model.3
+    if (C == 16 && CM == 32 && N2 == 32) return dispatch_cfg<16, 32, 32, 2, 1>(a, i, st);  // n model.1
+  }
   return hipErrorInvalidValue;
 }
