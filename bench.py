@@ -104,7 +104,7 @@ def conv_roofline(model, x, dtype, workload, reps=20):
                          f"algorithmic bytes per forward {int(by)}") if traffic else "no PMC summary for this workload",
         "kernel": "conv implicit GEMM (%s): all %d conv launches of one lane's forward (%d images), aggregated%s"
                   % ({"i8": "conv_i8, v_mfma_i32_32x32x32_i8", "f8": "conv_i8<fp8>, v_mfma_f32_32x32x16_fp8_fp8"}.get(
-                      dtype, "conv_stream/conv_small/conv_dma/conv_halo/conv_igemm"), len(conv),
+                      dtype, "conv_stream/conv_small/conv_dma/conv_lds/conv_bneck/conv_halo/conv_igemm"), len(conv),
                      Bl, "; int8 ops counted as FLOPs" if dtype == "i8" else ""),
         "timing": f"HIP events around a graph of {reps} back-to-back launches per op, on the launch stream",
         "launches": len(conv), "avg_launch_us": round(t_conv / len(conv) * 1e6, 2),
