@@ -371,6 +371,7 @@ hipError_t ym_launch_conv_bneck(int out_f32, const ConvArgs& a, int i, hipStream
     if (C == 32 && CM == 16 && N2 == 32) return dispatch_cfg<32, 16, 32, 1, 3>(a, i, st);
     if (C == 64 && CM == 32 && N2 == 64) return dispatch_cfg<64, 32, 64, 1, 3>(a, i, st);
     if (C == 32 && CM == 32 && N2 == 32) return dispatch_cfg<32, 32, 32, 1, 3>(a, i, st);
+    if (C == 64 && CM == 64 && N2 == 64) return dispatch_cfg<64, 64, 64, 1, 3>(a, i, st);  // s: C3k at 40x40
   } else {
     if (C == 32 && CM == 64 && N2 == 64) return dispatch_cfg<32, 64, 64, 2, 1>(a, i, st);  // s model.1, n model.3
     if (C == 16 && CM == 32 && N2 == 32) return dispatch_cfg<16, 32, 32, 2, 1>(a, i, st);  // n model.1

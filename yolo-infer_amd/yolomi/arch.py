@@ -393,7 +393,7 @@ class GraphBuilder:
         self.ops = out
 
     # csrc/ym_conv_bneck.hip: the (C, C_mid, C_out) Bottleneck shapes with a fused kernel
-    BNECK_SHAPES = {(16, 8, 16), (32, 16, 32), (64, 32, 64), (32, 32, 32)}
+    BNECK_SHAPES = {(16, 8, 16), (32, 16, 32), (64, 32, 64), (32, 32, 32), (64, 64, 64)}
 
     def _fusable(self, A: Op, B: Op) -> bool:
         if A.kind != "conv" or B.kind != "conv":
@@ -406,9 +406,9 @@ class GraphBuilder:
             return (a["k"] == 3 and a["s"] == 1 and b["s"] == 1 and a["src1"] is None and not a["up0"]
                     and b["src1"] is None and not b["up0"] and not b["shuffle2x2"] and b["anchor_level"] < 0
                     and b["src0"].buf is mid.buf and mid.coff == 0 and mid.C == mid.buf.C
-                    and self._readers(mid.buf) == 1
-                    and (b["res"] is None or (b["res"].buf is a["src0"].buf and b["res"].coff == a["src0"].coff
-                                              and b["res"].C == a["src0"].C))
+                    and self._readers(mid.buf) == 1  # a Bottleneck: the shortcut is the first conv's input
+                    and b["res"] is not None and b["res"].buf is a["src0"].buf and b["res"].coff == a["src0"].coff
+                    and b["res"].C == a["src0"].C
                     and (a["c1"], a["c2"], b["c2"]) in self.BNECK_SHAPES)
         if b["k"] != 1 or b["s"] != 1 or b["src1"] is not None or b["up0"] or b["shuffle2x2"] or b.get("convT"):
             return False
