@@ -161,7 +161,11 @@ def test_branch_schedule_bitwise_equals_serial(dtype, scale):
     beside the neck) computes exactly what the serial launch order computes: same kernels, so bit-equal outputs."""
     from core.model import YOLO11Model
     x = make_input("uniform", tuple(range(41, 49)), 640).to(DEV)
-    m = model(scale, dtype)  # the default (serial) order
+    os.environ["YM_BRANCHES"] = "1"  # the serial launch order
+    try:
+        m = YOLO11Model(size=scale, device="cuda:0", dtype=dtype, verbose=False)
+    finally:
+        del os.environ["YM_BRANCHES"]
     eng = m.model.engine
     d1, c1 = eng.run(x, use_graph=True)
     d1, c1 = d1.clone(), c1.clone()

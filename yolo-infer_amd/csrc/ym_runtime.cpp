@@ -565,10 +565,12 @@ static void build_schedule(ym_ctx* c) {
   std::vector<std::vector<int>> snap(nop);                          // known vector of an op's stream after it
   std::vector<int> rd, wr;
   int used = 1;
-  // opt-in (YM_BRANCHES=2..4): measured on MI355X, graph replays gain nothing (0.732 vs 0.734 ms per yolo11n B=8
-  // forward, tools/branch_check.py) and eager launches lose (0.774 vs 0.727 ms), so the serial order is the default
+  // YM_BRANCHES=1..4 (default 4).  Round 1 measured no gain for graph replays; with the round-2 kernels (fused
+  // Bottlenecks, conflict-free LDS layouts) the 4-stream schedule replays 6-10 % faster than the serial order on
+  // yolo11n/s B=8 (bench.py A/B on MI355X: s 7.93k -> 8.41-8.73k img/s, n 11.5k -> 12.1-12.4k): the Detect-head
+  // chains of one level now overlap the neck's 20x20 / 40x40 layers, whose launches leave most CUs idle.
   const char* env = getenv("YM_BRANCHES");
-  const int maxs = env && *env ? (atoi(env) < 1 ? 1 : (atoi(env) > S ? S : atoi(env))) : 1;
+  const int maxs = env && *env ? (atoi(env) < 1 ? 1 : (atoi(env) > S ? S : atoi(env))) : S;
   for (int i = 0; i < nop; ++i) {
     rw(c->ops[i], rd, wr);
     std::vector<int> deps;
