@@ -66,12 +66,14 @@ def test_i8_stored_tensors_match_oracle(name):
         diff = (got - ref).abs()
         frac = float((diff > 0).float().mean())
         report.append((i, frac, float(diff.max())))
-        assert frac <= 1e-5, (b.name, frac, float(diff.max()), report)
+        # exact: the fixture's inputs are fixed, so the ~1e-8-per-element float64 straddle above either occurs for
+        # them or not — it does not, and any differing element is a bug
+        assert frac == 0, (b.name, frac, float(diff.max()), report)
     no = eng.graph.no
     ref_h = torch.cat([f.reshape(B, no, -1) for f in ex["feats"]], 2).transpose(1, 2)
     got_h = eng.read_buffer(eng.graph.anchor_buf.id, B).reshape(B, -1, eng.graph.anchor_buf.C)[..., :no]
     hd = (got_h - ref_h).abs()
-    assert float((hd > 0).float().mean()) <= 1e-5, report
+    assert float(hd.max()) == 0, report
 
 
 @pytest.mark.parametrize("name", list(I8_FIXTURES))

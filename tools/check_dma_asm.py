@@ -1,8 +1,9 @@
 #!/usr/bin/env python3
 """Static check of the LDS-DMA conv kernels (csrc/ym_conv_dma.hip) in the gfx950 assembly.
 
-The K loop waits with a counted `s_waitcnt vmcnt(NL)` that assumes every stage issues exactly NL = BM/32 + BN/32
-`buffer_load_dwordx4 … lds` wave-instructions (NSTAGE-1 prologue stages + 1 in the loop body = NSTAGE·NL per kernel).  If the
+The K loop waits with a counted `s_waitcnt vmcnt(NL)` that assumes every stage issues exactly NL = SUB·(BM + BN)/(32·KG)
+`buffer_load_dwordx4 … lds` wave-instructions (NSTAGE-1 prologue stages + 1 in the loop body = NSTAGE·NL per kernel;
+NSTAGE and SUB are the kernel's last two template arguments).  If the
 compiler ever duplicates a DMA into divergent branches, the count is off and the wait no longer covers the stage —
 silently wrong results on the GPU.  This check compiles the file for gfx950 (device only, -S) and counts.
 
@@ -16,7 +17,6 @@ import tempfile
 
 ROOT = os.path.dirname(os.path.dirname(os.path.abspath(__file__)))
 SRC = os.path.join(ROOT, "yolo-infer_amd", "csrc", "ym_conv_dma.hip")
-NSTAGE = int(re.search(r"constexpr int NSTAGE = (\d+);", open(SRC).read()).group(1))  # (NSTAGE-1) prologue + 1 loop
 HIPCC = os.environ.get("HIPCC", "/opt/rocm/bin/hipcc")
 
 
@@ -26,10 +26,11 @@ def kernel_dma_counts(asm: str):
     for i, m in enumerate(labels):
         end = labels[i + 1].start() if i + 1 < len(labels) else len(asm)
         body = asm[m.end():end].split(".Lfunc_end")[0]
-        bm, bn, kind, split, kg = map(int, re.search(r"Li(\d+)ELi(\d+)ELi(\d)ELi(\d)ELi(\d)E", m.group(1)).groups())
-        nl = (bm // 8 + bn // 8) // (4 * kg)  # DMA instructions per wave per stage
+        bm, bn, kind, split, kg, nstage, sub = map(
+            int, re.search(r"Li(\d+)ELi(\d+)ELi(\d)ELi(\d)ELi(\d)ELi(\d)ELi(\d)E", m.group(1)).groups())
+        nl = sub * (bm // 8 + bn // 8) // (4 * kg)  # DMA instructions per wave per stage
         n = len(re.findall(r"buffer_load_dwordx4 .*\blds\b", body))
-        out.append((m.group(1), bm, bn, kind, split, n, NSTAGE * nl))
+        out.append((m.group(1), bm, bn, kind, split, n, nstage * nl))  # (NSTAGE-1) prologue + 1 loop stage
     return out
 
 

@@ -3,8 +3,9 @@
 Same protocol and result keys as the reference: `_benchmark_inference` (`speed_benchmark.py:307-350`) puts the
 model in eval mode, runs warm-up predicts, then times each `predict(test_input)` with wall clock and reports
 avg/min/max/stdev, `fps = 1/avg` and `throughput = B/avg`; `benchmark_model_sizes` (`:61-122`) sweeps sizes x
-image sizes x batch sizes; `benchmark_throughput` (`:211-305`) is the sustained loop.  The reference's quantization
-A/B (`:124-209`) and GPUtil resource monitor (NVIDIA-only) are not part of this path.
+image sizes x batch sizes; `benchmark_quantization` (`:124-209`) is the PTQ A/B (`speedup = t_original / t_quant`,
+`:191`); `benchmark_throughput` (`:211-305`) is the sustained loop.  The GPUtil resource monitor (NVIDIA-only) is not
+part of this path.
 """
 from __future__ import annotations
 
@@ -20,6 +21,7 @@ from typing import Any, Dict, List
 import torch
 
 from core.model import YOLO11Model
+from optimization.quantization.quantizers import create_quantizer
 
 logger = logging.getLogger(__name__)
 
@@ -57,6 +59,45 @@ class SpeedBenchmark:
                                                       "batch_size": batch_size, **metrics})
         results["summary"] = self._calculate_summary(results["configurations"])
         self._save_results(results, "model_sizes_benchmark.json")
+        return results
+
+    def benchmark_quantization(self, model_size: str = "n", task: str = "detect",
+                               quantization_methods: List[str] = ["dynamic", "ptq"], image_size: int = 640,
+                               batch_size: int = 1, original_dtype: str = "f16") -> Dict[str, Any]:
+        """The reference's quantization A/B (`speed_benchmark.py:124-209`): time the original model, then each
+        method's quantized model on the same randn input, `speedup = original avg / quantized avg`.  'ptq' calibrates
+        on ten copies of the test input (`:180-183`) with the quantizer's default config (qnnpack int8); 'ptq_fp8'
+        is the same flow on the fp8 e4m3 plan (BASELINE config 4).  A method that fails is recorded as
+        {'error': ...} like the reference's except path (`:196-201`): 'dynamic' is one (a no-op on this conv-only
+        graph, SURVEY §2.1).  `original_dtype` is the original model's plan ('f16' throughput plan by default;
+        'f32' = the exact parity plan, the reference's FP32 model)."""
+        logger.info(f"Benchmarking quantization methods: {quantization_methods}")
+        results = {"model_size": model_size, "task": task, "image_size": image_size, "batch_size": batch_size,
+                   "original_dtype": original_dtype, "system_info": self.system_info, "methods": {}}
+        original_model = YOLO11Model(task=task, size=model_size, dtype=original_dtype)
+        test_input = torch.randn(batch_size, 3, image_size, image_size)
+        if torch.cuda.is_available():
+            test_input = test_input.cuda()
+        original_metrics = self._benchmark_inference(original_model, test_input)
+        results["methods"]["original"] = original_metrics
+        for method in quantization_methods:
+            logger.info(f"Benchmarking quantization method: {method}")
+            try:
+                if method == "ptq_fp8":
+                    quantizer = create_quantizer("ptq", original_model, {"backend": "fp8"})
+                else:
+                    quantizer = create_quantizer(method, original_model)
+                quantizer.set_calibration_data([test_input for _ in range(10)])
+                quantized_model = quantizer.optimize()
+                quantized_metrics = self._benchmark_inference(quantized_model, test_input)
+                quantized_metrics.update({
+                    "speedup": original_metrics["avg_inference_time"] / quantized_metrics["avg_inference_time"],
+                    "optimization_info": quantizer.get_optimization_info()})
+                results["methods"][method] = quantized_metrics
+            except Exception as e:  # the reference records the failure and moves on (:196-201)
+                logger.error(f"Failed to benchmark quantization method {method}: {e}")
+                results["methods"][method] = {"error": str(e)}
+        self._save_results(results, "quantization_benchmark.json")
         return results
 
     def benchmark_throughput(self, model_size: str = "n", task: str = "detect", duration_seconds: float = 60,

@@ -40,7 +40,6 @@ __device__ unsigned long long* ym_dma_stamps;
 namespace {
 
 constexpr int DK = 64;                    // K per stage
-constexpr int NSTAGE = 4;                 // LDS ring depth (three stages of loads in flight)
 constexpr unsigned OOB = 0x80000000u;     // byte offset past num_records: the DMA deposits zeros
 
 template <int N>
@@ -76,14 +75,20 @@ template <> struct Store4<float> {
 // KIND 4: 3x3 with Cin % 64 == 0 — every 64-deep stage is ONE tap, so the tap, its pixel offset and the channel
 // block are wave-uniform scalars and a DMA address is one add onto a per-row base, validity one bit of a 9-bit
 // per-row tap mask.
-template <typename OutT, int BM, int BN, int KIND, int SPLIT, int KG>
+// NSTAGE: LDS ring depth (NSTAGE - 1 stages of loads in flight); 3 for the 256 x 128 tiles (48 KB per stage), 2
+// (double buffer) for the 256-deep stages.
+// SUB: 64-deep K sub-stages per stage (one barrier, one LDS-read latency and one wait per SUB x 64 of K): the small-M
+// layers' K loops are chains of per-stage fixed costs, which SUB 2 halves; launched only where every split's K range
+// is whole stages (no partial stage: every stage issues exactly NL DMA instructions, tools/check_dma_asm.py)
+template <typename OutT, int BM, int BN, int KIND, int SPLIT, int KG, int NSTAGE, int SUB>
 __global__ __launch_bounds__(256 * KG) void conv_dma(const ConvArgs a) {
   constexpr int NW = 4 * KG;
   constexpr int TM = BM / 64, TN = BN / 64;
   static_assert((BM / 8) % NW == 0 && (BN / 8) % NW == 0, "DMA groups must divide over the waves");
   constexpr int GB = BM / 8 / NW, GA = BN / 8 / NW;  // DMA wave-instructions per stage per wave (8 rows x 128 B)
-  constexpr int NL = GA + GB;
-  constexpr int SB = (BM + BN) * 128;                // bytes per stage
+  constexpr int NL = (GA + GB) * SUB;                // DMA wave-instructions per stage per wave
+  constexpr int SBS = (BM + BN) * 128;               // bytes per 64-deep sub-stage
+  constexpr int SB = SUB * SBS;                      // bytes per stage
   constexpr int NREG = TM * TN * 16;
   constexpr int SPW = 4 / KG;                        // 16-deep k sub-steps per wave per stage
   constexpr int NACC = TM * TN == 1 && SPW >= 2 ? 2 : 1;  // one 32x32 block per wave: alternate two accumulators
@@ -203,7 +208,7 @@ __global__ __launch_bounds__(256 * KG) void conv_dma(const ConvArgs a) {
 
   const int nst = a.Kpad / DK;
   const int k_lo = (nst * sp) / SPLIT, k_hi = (nst * (sp + 1)) / SPLIT;
-  const int nk = k_hi - k_lo;
+  const int nk = (k_hi - k_lo) / SUB;  // stages (launch_dma: a multiple of SUB sub-stages)
   // KIND 3: tap / channel block of this lane's chunk at stage k_lo (chunk index k*8 + c);
   // KIND 4: the stage's tap (ky, kx) and channel block cb (wave-uniform)
   int tap = 0, cb = 0, ky = 0, kx = 0;
@@ -219,8 +224,7 @@ __global__ __launch_bounds__(256 * KG) void conv_dma(const ConvArgs a) {
   }
   int kcur = k_lo;  // stage whose loads are issued next
 
-  auto issue = [&](int slot) {
-    char* sbase = smem + slot * SB;
+  auto issue_sub = [&](char* sbase) {
     const int chunk = kcur * 8 + c;
     // B: pixels
     if constexpr (KIND == 1) {
@@ -265,6 +269,10 @@ __global__ __launch_bounds__(256 * KG) void conv_dma(const ConvArgs a) {
     }
     ++kcur;
   };
+  auto issue = [&](int slot) {
+#pragma unroll
+    for (int u = 0; u < SUB; ++u) issue_sub(smem + slot * SB + u * SBS);
+  };
 
   f32x16 acc[NACC][TM][TN];
 #pragma unroll
@@ -279,41 +287,49 @@ __global__ __launch_bounds__(256 * KG) void conv_dma(const ConvArgs a) {
   const int key = (l32 >> 1) & 7;
   // this wave's k sub-steps of the stage: fragment reads first, then the MFMAs (one LDS latency per stage)
   auto compute = [&](int slot) {
-    const char* sb = smem + slot * SB;
-    const char* sa = sb + BM * 128;
-    f16x8 fb[SPW][TM], fa[SPW][TN];
+    f16x8 fb[SUB][SPW][TM], fa[SUB][SPW][TN];
 #pragma unroll
-    for (int u = 0; u < SPW; ++u) {
-      const int s = kg * SPW + u;
-      const int off = ((((2 * s + h) ^ key)) << 4) + l32 * 128;
+    for (int su = 0; su < SUB; ++su) {
+      const char* sb = smem + slot * SB + su * SBS;
+      const char* sa = sb + BM * 128;
 #pragma unroll
-      for (int i = 0; i < TM; ++i) fb[u][i] = *reinterpret_cast<const f16x8*>(sb + (wm * (BM / 2) + 32 * i) * 128 + off);
+      for (int u = 0; u < SPW; ++u) {
+        const int s = kg * SPW + u;
+        const int off = ((((2 * s + h) ^ key)) << 4) + l32 * 128;
 #pragma unroll
-      for (int j = 0; j < TN; ++j) fa[u][j] = *reinterpret_cast<const f16x8*>(sa + (wn * (BN / 2) + 32 * j) * 128 + off);
-    }
-#pragma unroll
-    for (int u = 0; u < SPW; ++u)
-#pragma unroll
-      for (int i = 0; i < TM; ++i)
+        for (int i = 0; i < TM; ++i)
+          fb[su][u][i] = *reinterpret_cast<const f16x8*>(sb + (wm * (BM / 2) + 32 * i) * 128 + off);
 #pragma unroll
         for (int j = 0; j < TN; ++j)
-          acc[u % NACC][i][j] = __builtin_amdgcn_mfma_f32_32x32x16_f16(fa[u][j], fb[u][i], acc[u % NACC][i][j], 0, 0, 0);
+          fa[su][u][j] = *reinterpret_cast<const f16x8*>(sa + (wn * (BN / 2) + 32 * j) * 128 + off);
+      }
+    }
+#pragma unroll
+    for (int su = 0; su < SUB; ++su)
+#pragma unroll
+      for (int u = 0; u < SPW; ++u)
+#pragma unroll
+        for (int i = 0; i < TM; ++i)
+#pragma unroll
+          for (int j = 0; j < TN; ++j)
+            acc[u % NACC][i][j] =
+                __builtin_amdgcn_mfma_f32_32x32x16_f16(fa[su][u][j], fb[su][u][i], acc[u % NACC][i][j], 0, 0, 0);
   };
 
-  static_assert(NSTAGE == 4, "the waits below assume three stages in flight");
-  if (nk > 0) issue(0);
-  if (nk > 1) issue(1);
-  if (nk > 2) issue(2);
+  static_assert(NSTAGE >= 2 && NSTAGE <= 4, "ring depth");
+#pragma unroll
+  for (int s0 = 0; s0 < NSTAGE - 1; ++s0)
+    if (nk > s0) issue(s0);
   YM_STAMP(1);
   for (int it = 0; it < nk; ++it) {
     // stage it is complete when at most the stages issued after it are outstanding (loads retire in order)
-    if (it + 2 < nk) wait_vm<2 * NL>();
-    else if (it + 1 < nk) wait_vm<NL>();
+    if (it + NSTAGE - 2 < nk) wait_vm<(NSTAGE - 2) * NL>();
+    else if (NSTAGE == 4 && it + 1 < nk) wait_vm<NL>();
     else wait_vm<0>();
     YM_STAMP(8 + 4 * (it & 63));
     raw_barrier();  // stage it is in LDS for every wave; every wave is done reading stage it-1's slot
     YM_STAMP(9 + 4 * (it & 63));
-    if (it + 3 < nk) issue((it + 3) % NSTAGE);
+    if (it + NSTAGE - 1 < nk) issue((it + NSTAGE - 1) % NSTAGE);
     YM_STAMP(10 + 4 * (it & 63));
     compute(it % NSTAGE);
     YM_STAMP(11 + 4 * (it & 63));
@@ -446,22 +462,28 @@ __global__ __launch_bounds__(256 * KG) void conv_dma(const ConvArgs a) {
 }
 
 struct DmaCfg {
-  int bm, bn, split, kg;
+  int bm, bn, split, kg, ns, sub;
 };
-// (ids 17 + i in the conv config space of csrc/ym_conv.hip)
-#define YM_DMA_CFGS(X)                                                                                   \
-  X(0, 64, 64, 1, 1) X(1, 64, 64, 2, 1) X(2, 64, 64, 4, 1) X(3, 64, 64, 8, 1) X(4, 128, 64, 1, 1)     \
-  X(5, 128, 64, 2, 1) X(6, 128, 64, 4, 1) X(7, 64, 128, 1, 1) X(8, 64, 128, 2, 1) X(9, 64, 128, 4, 1) \
-  X(10, 128, 128, 1, 1) X(11, 128, 128, 2, 1) X(12, 64, 64, 1, 2) X(13, 64, 64, 2, 2)                  \
-  X(14, 64, 64, 4, 2) X(15, 128, 64, 1, 2) X(16, 64, 128, 1, 2) X(17, 128, 128, 1, 2)
+// (ids 17 + i in the conv config space of csrc/ym_conv.hip).  18-20: the large tiles of the MFMA-dense 3x3 layers
+// (80² / 160² maps): 256 pixels x 128 channels per workgroup = 85 FLOP per staged byte (128 x 128: 64); 21-26:
+// 128- to 256-deep stages (SUB 2-4) for the K-chain-bound 20² / 40² layers
+#define YM_DMA_CFGS(X)                                                                                           \
+  X(0, 64, 64, 1, 1, 4, 1) X(1, 64, 64, 2, 1, 4, 1) X(2, 64, 64, 4, 1, 4, 1) X(3, 64, 64, 8, 1, 4, 1)             \
+  X(4, 128, 64, 1, 1, 4, 1) X(5, 128, 64, 2, 1, 4, 1) X(6, 128, 64, 4, 1, 4, 1) X(7, 64, 128, 1, 1, 4, 1)         \
+  X(8, 64, 128, 2, 1, 4, 1) X(9, 64, 128, 4, 1, 4, 1) X(10, 128, 128, 1, 1, 4, 1) X(11, 128, 128, 2, 1, 4, 1)     \
+  X(12, 64, 64, 1, 2, 4, 1) X(13, 64, 64, 2, 2, 4, 1) X(14, 64, 64, 4, 2, 4, 1) X(15, 128, 64, 1, 2, 4, 1)        \
+  X(16, 64, 128, 1, 2, 4, 1) X(17, 128, 128, 1, 2, 4, 1) X(18, 256, 128, 1, 1, 3, 1) X(19, 128, 256, 1, 1, 3, 1)  \
+  X(20, 256, 64, 1, 2, 3, 1) X(21, 64, 64, 1, 2, 4, 2) X(22, 64, 64, 1, 1, 4, 2) X(23, 64, 64, 2, 2, 4, 2)        \
+  X(24, 128, 64, 1, 2, 3, 2) X(25, 64, 128, 1, 2, 3, 2) X(26, 64, 64, 1, 2, 3, 2) X(27, 64, 64, 1, 2, 3, 3)        \
+  X(28, 64, 64, 1, 2, 2, 4) X(29, 64, 64, 2, 2, 3, 3) X(30, 64, 128, 1, 2, 2, 3)
 constexpr DmaCfg kDma[] = {
-#define YM_X(id, bm, bn, sp, kg) {bm, bn, sp, kg},
+#define YM_X(id, bm, bn, sp, kg, ns, sub) {bm, bn, sp, kg, ns, sub},
     YM_DMA_CFGS(YM_X)
 #undef YM_X
 };
 constexpr int kNumDma = sizeof(kDma) / sizeof(kDma[0]);
 
-template <typename OutT, int BM, int BN, int SPLIT, int KG>
+template <typename OutT, int BM, int BN, int SPLIT, int KG, int NS, int SUB>
 hipError_t launch_dma(ConvArgs a, int kind, hipStream_t st) {
   const int tiles_m8 = ((a.M + BM - 1) / BM + 7) / 8 * 8;
   a.tiles_n = (a.N + BN - 1) / BN;
@@ -470,14 +492,15 @@ hipError_t launch_dma(ConvArgs a, int kind, hipStream_t st) {
     if (tiles > a.cnt_cap || tiles * SPLIT * BM * BN * 4 > a.slab_cap) return hipErrorInvalidValue;
     if (a.Kpad / DK < SPLIT) return hipErrorInvalidValue;
   }
+  if (SUB > 1 && (a.Kpad / DK) % (SPLIT * SUB)) return hipErrorInvalidValue;  // whole stages in every split
   const dim3 grid(tiles_m8 * a.tiles_n * SPLIT), block(256 * KG);
   if (kind == 1) {
-    hipLaunchKernelGGL((conv_dma<OutT, BM, BN, 1, SPLIT, KG>), grid, block, 0, st, a);
+    hipLaunchKernelGGL((conv_dma<OutT, BM, BN, 1, SPLIT, KG, NS, SUB>), grid, block, 0, st, a);
   } else if constexpr (sizeof(OutT) == 2) {  // fp32 outputs exist only for the Detect head's 1x1 convs
     if (kind == 4)
-      hipLaunchKernelGGL((conv_dma<OutT, BM, BN, 4, SPLIT, KG>), grid, block, 0, st, a);
+      hipLaunchKernelGGL((conv_dma<OutT, BM, BN, 4, SPLIT, KG, NS, SUB>), grid, block, 0, st, a);
     else
-      hipLaunchKernelGGL((conv_dma<OutT, BM, BN, 3, SPLIT, KG>), grid, block, 0, st, a);
+      hipLaunchKernelGGL((conv_dma<OutT, BM, BN, 3, SPLIT, KG, NS, SUB>), grid, block, 0, st, a);
   } else {
     return hipErrorInvalidValue;
   }
@@ -487,8 +510,8 @@ hipError_t launch_dma(ConvArgs a, int kind, hipStream_t st) {
 template <typename OutT>
 hipError_t dispatch(const ConvArgs& a, int kind, int i, hipStream_t st) {
   switch (i) {
-#define YM_X(id, bm, bn, sp, kg) \
-  case id: return launch_dma<OutT, bm, bn, sp, kg>(a, kind, st);
+#define YM_X(id, bm, bn, sp, kg, ns, sub) \
+  case id: return launch_dma<OutT, bm, bn, sp, kg, ns, sub>(a, kind, st);
     YM_DMA_CFGS(YM_X)
 #undef YM_X
   }

@@ -22,16 +22,21 @@ namespace {
 typedef _Float16 h8 __attribute__((ext_vector_type(8)));
 
 struct SCfg {
-  int kind, ks, px, cap;  // kind 1 = 1x1 s1, 3 = 3x3; K steps of 32 (Kpad / 32); 16-pixel groups per wave
-};                        // iteration; workgroup cap of the persistent grid
-#define YM_STREAM_CFGS(X)                                                                                        \
-  X(0, 1, 2, 1, 1024) X(1, 1, 2, 2, 1024) X(2, 1, 2, 1, 4096) X(3, 1, 4, 1, 1024) X(4, 1, 4, 2, 1024)            \
-  X(5, 1, 8, 1, 1024) X(6, 1, 4, 1, 4096) X(7, 3, 4, 1, 1024) X(8, 3, 6, 1, 1024) X(9, 3, 10, 1, 1024)          \
-  X(10, 3, 18, 1, 1024) X(11, 3, 4, 1, 4096) X(12, 3, 6, 1, 4096) X(13, 3, 10, 1, 4096) X(14, 3, 18, 1, 4096)         \
-  X(15, 1, 2, 2, 4096) X(16, 1, 2, 4, 4096) X(17, 1, 4, 2, 4096) X(18, 3, 4, 2, 4096) X(19, 3, 6, 2, 4096)        \
-  X(20, 1, 6, 1, 4096) X(21, 1, 6, 2, 4096) X(22, 1, 6, 1, 1024)
+  int kind, ks, px, cap, nw;  // kind 1 = 1x1 s1, 3 = 3x3; K steps of 32 (Kpad / 32); 16-pixel groups per wave
+};                            // iteration; workgroup cap of the persistent grid; waves per workgroup
+// nw 8: two waves per SIMD share one LDS copy of the weights — for the matrices too large for two workgroups per CU
+// (N 256 x K 192: 106 KB), where one wave per SIMD leaves the SIMD idle while that wave waits for its next pixels
+#define YM_STREAM_CFGS(X)                                                                                          \
+  X(0, 1, 2, 1, 1024, 4) X(1, 1, 2, 2, 1024, 4) X(2, 1, 2, 1, 4096, 4) X(3, 1, 4, 1, 1024, 4)                      \
+  X(4, 1, 4, 2, 1024, 4) X(5, 1, 8, 1, 1024, 4) X(6, 1, 4, 1, 4096, 4) X(7, 3, 4, 1, 1024, 4)                      \
+  X(8, 3, 6, 1, 1024, 4) X(9, 3, 10, 1, 1024, 4) X(10, 3, 18, 1, 1024, 4) X(11, 3, 4, 1, 4096, 4)                  \
+  X(12, 3, 6, 1, 4096, 4) X(13, 3, 10, 1, 4096, 4) X(14, 3, 18, 1, 4096, 4) X(15, 1, 2, 2, 4096, 4)                \
+  X(16, 1, 2, 4, 4096, 4) X(17, 1, 4, 2, 4096, 4) X(18, 3, 4, 2, 4096, 4) X(19, 3, 6, 2, 4096, 4)                  \
+  X(20, 1, 6, 1, 4096, 4) X(21, 1, 6, 2, 4096, 4) X(22, 1, 6, 1, 1024, 4) X(23, 1, 4, 1, 4096, 8)                  \
+  X(24, 1, 4, 2, 4096, 8) X(25, 1, 6, 1, 4096, 8) X(26, 1, 6, 2, 4096, 8) X(27, 1, 8, 1, 4096, 8)                  \
+  X(28, 1, 2, 2, 4096, 8) X(29, 3, 10, 1, 4096, 8) X(30, 3, 4, 2, 4096, 8)
 constexpr SCfg kStream[] = {
-#define YM_X(id, kind, ks, px, cap) {kind, ks, px, cap},
+#define YM_X(id, kind, ks, px, cap, nw) {kind, ks, px, cap, nw},
     YM_STREAM_CFGS(YM_X)
 #undef YM_X
 };
@@ -46,8 +51,9 @@ constexpr int kMaxFusedBytes = 112 * 1024;  // fused pairs: both weight matrices
 constexpr int kFuseMaxN = 128;  // first conv's N (= second conv's K) held in registers: 8 blocks of 16
 constexpr int RB = 8;           // output-channel blocks of 16 whose residuals are prefetched with the fragments
 
-template <typename OutT, int KIND, int KS, int PX, bool FUSE>
-__global__ __launch_bounds__(256) void conv_stream(const ConvArgs a) {
+template <typename OutT, int KIND, int KS, int PX, bool FUSE, int NWV>
+__global__ __launch_bounds__(64 * NWV) void conv_stream(const ConvArgs a) {
+  constexpr int NT = 64 * NWV;     // threads per workgroup
   constexpr int KP = KS * 32;      // Kpad
   // LDS row pitch (halves) KP + 16 = 4·KS + 2 16-byte slots: the A-fragment reads (16 rows x one K chunk per lane
   // group kg) hit distinct slots in each of ds_read_b128's non-contiguous lane groups (MI355X_MICROARCH §LDS);
@@ -66,31 +72,31 @@ __global__ __launch_bounds__(256) void conv_stream(const ConvArgs a) {
   const int g = lane >> 4, col = lane & 15;
   const f16* W = static_cast<const f16*>(a.w);
   const int NP = (a.N + 15) & ~15;  // rows padded to the 16-row MFMA block (zero weights, outputs not stored)
-  for (int i0 = tid; i0 < NP * (KP / 8); i0 += 256 * 8) {  // 8 loads in flight per thread and round
+  for (int i0 = tid; i0 < NP * (KP / 8); i0 += NT * 8) {  // 8 loads in flight per thread and round
     f16x8 v[8];
 #pragma unroll
     for (int u = 0; u < 8; ++u) {
-      const int i = i0 + 256 * u, n = i / (KP / 8), c = i - n * (KP / 8);
+      const int i = i0 + NT * u, n = i / (KP / 8), c = i - n * (KP / 8);
       v[u] = (i < NP * (KP / 8) && n < a.N) ? *reinterpret_cast<const f16x8*>(W + (size_t)n * KP + 8 * c)
                                              : Vec8<f16>::zero();
     }
 #pragma unroll
     for (int u = 0; u < 8; ++u) {
-      const int i = i0 + 256 * u, n = i / (KP / 8), c = i - n * (KP / 8);
+      const int i = i0 + NT * u, n = i / (KP / 8), c = i - n * (KP / 8);
       if (i < NP * (KP / 8)) *reinterpret_cast<f16x8*>(ws + n * LDW + 8 * c) = v[u];
     }
   }
-  for (int i = tid; i < NP; i += 256) bs[i] = i < a.N ? a.bias[i] : 0.f;
+  for (int i = tid; i < NP; i += NT) bs[i] = i < a.N ? a.bias[i] : 0.f;
   if constexpr (FUSE) {  // W2 [16 NB2][LDW2]: row n2, K = first-conv channel (zero past N / N2)
     const f16* W2 = static_cast<const f16*>(a.w2);
     const int q4 = 4 * NB;  // 4-channel quads per row
-    for (int i = tid; i < 16 * NB2 * q4; i += 256) {
+    for (int i = tid; i < 16 * NB2 * q4; i += NT) {
       const int n = i / q4, c = 4 * (i - n * q4);
       f16x4 v = {0, 0, 0, 0};
       if (n < a.N2 && c < a.N) v = *reinterpret_cast<const f16x4*>(W2 + (size_t)n * a.Kpad2 + c);
       *reinterpret_cast<f16x4*>(w2s + n * LDW2 + c) = v;
     }
-    for (int i = tid; i < 16 * NB2; i += 256) bs2[i] = i < a.N2 ? a.bias2[i] : 0.f;
+    for (int i = tid; i < 16 * NB2; i += NT) bs2[i] = i < a.N2 ? a.bias2[i] : 0.f;
   }
 
   const int HW = a.Ho * a.Wo;
@@ -157,8 +163,8 @@ __global__ __launch_bounds__(256) void conv_stream(const ConvArgs a) {
     }
   };
 
-  const int step = nwx * 4 * PX;
-  int gb = (int)((long)G * v0 / nwg) + (slot * 4 + wave) * PX;
+  const int step = nwx * NWV * PX;
+  int gb = (int)((long)G * v0 / nwg) + (slot * NWV + wave) * PX;
   h8 cur[PX][KS], nxt[PX][KS];
   f16x4 rcur[PX][RB], rnxt[PX][RB];
   load(gb, cur, rcur);
@@ -407,11 +413,11 @@ hipError_t launch_small(const ConvArgs& a, hipStream_t st) {
   return hipGetLastError();
 }
 
-template <typename OutT, int KIND, int KS, int PX, int CAP>
+template <typename OutT, int KIND, int KS, int PX, int CAP, int NWV>
 hipError_t launch(const ConvArgs& a, hipStream_t st) {
   if (a.Kpad != KS * 32 || a.k != KIND) return hipErrorInvalidValue;
   const int G = (a.M + 15) / 16;
-  long wgs = (G + 4 * PX - 1) / (4 * PX);
+  long wgs = (G + NWV * PX - 1) / (NWV * PX);
   if (wgs > CAP) wgs = CAP;  // the persistent grid: CAP workgroups, the rest streams through them
   const int NP = (a.N + 15) & ~15;
   size_t lds = (size_t)NP * (KS * 32 + 16) * sizeof(f16) + (size_t)NP * sizeof(float);
@@ -420,9 +426,10 @@ hipError_t launch(const ConvArgs& a, hipStream_t st) {
     const int N2P = (a.N2 + 15) & ~15;
     lds += (size_t)N2P * (NP + 8) * sizeof(f16) + (size_t)N2P * sizeof(float);
     if (lds > kMaxFusedBytes) return hipErrorInvalidValue;
-    hipLaunchKernelGGL((conv_stream<OutT, KIND, KS, PX, true>), dim3(wgs), dim3(256), lds, st, a);
+    if constexpr (NWV == 8 && PX > 1) return hipErrorInvalidValue;  // 256 VGPRs per wave: the pair would spill
+    else hipLaunchKernelGGL((conv_stream<OutT, KIND, KS, PX, true, NWV>), dim3(wgs), dim3(64 * NWV), lds, st, a);
   } else {
-    hipLaunchKernelGGL((conv_stream<OutT, KIND, KS, PX, false>), dim3(wgs), dim3(256), lds, st, a);
+    hipLaunchKernelGGL((conv_stream<OutT, KIND, KS, PX, false, NWV>), dim3(wgs), dim3(64 * NWV), lds, st, a);
   }
   return hipGetLastError();
 }
@@ -430,8 +437,8 @@ hipError_t launch(const ConvArgs& a, hipStream_t st) {
 template <typename OutT>
 hipError_t dispatch(const ConvArgs& a, int i, hipStream_t st) {
   switch (i) {
-#define YM_X(id, kind, ks, px, cap) \
-  case id: return launch<OutT, kind, ks, px, cap>(a, st);
+#define YM_X(id, kind, ks, px, cap, nw) \
+  case id: return launch<OutT, kind, ks, px, cap, nw>(a, st);
     YM_STREAM_CFGS(YM_X)
 #undef YM_X
   }

@@ -1,7 +1,7 @@
 """PostTrainingQuantizer on MI355X — the reference's `optimization/quantization/quantizers.py:24-308` (PTQ) and
 `create_quantizer` (:860-889), with the same plugin surface (`set_calibration_data`, `optimize`,
-`get_optimization_info`, `evaluate`, config keys `backend` (default 'qnnpack', :42), `num_calibration_batches` (100,
-:41), `dtype`).
+`get_optimization_info`, `evaluate`, config keys `backend` (default 'qnnpack', :42; also 'fbgemm', and 'fp8' = the
+e4m3 plan of BASELINE config 4), `num_calibration_batches` (100, :41), `dtype`).
 
 `optimize()` follows the reference's prepare → calibrate → convert (:66-77), re-designed for the GPU runtime:
   * prepare: the exact-f32 plan of the model (the float model torch.ao would observe);
@@ -38,8 +38,9 @@ class PostTrainingQuantizer(QuantizationOptimizer):
         if calibration_loader is None and self.calibration_data is None:
             raise ValueError("Calibration data is required for post-training quantization")
         calibration_loader = calibration_loader or self.calibration_data
-        if self.quantization_backend not in ("qnnpack", "fbgemm"):
-            raise ValueError(f"backend {self.quantization_backend!r}: the int8 runtime restates qnnpack and fbgemm")
+        if self.quantization_backend not in ("qnnpack", "fbgemm", "fp8"):
+            raise ValueError(f"backend {self.quantization_backend!r}: the int8 runtime restates qnnpack and fbgemm "
+                             f"(and 'fp8', the e4m3 plan)")
         logger.info("Starting post-training quantization...")
         f32 = self._prepare_model_for_quantization()
         t0 = time.perf_counter()
@@ -77,7 +78,8 @@ class PostTrainingQuantizer(QuantizationOptimizer):
     def _convert(self) -> Any:
         from core.model import YOLO11Model
         src = self._source()
-        q = YOLO11Model(task=src.task, size=src.size, device=src.device, dtype="i8", qparams=self.qparams,
+        q = YOLO11Model(task=src.task, size=src.size, device=src.device,
+                        dtype="f8" if self.quantization_backend == "fp8" else "i8", qparams=self.qparams,
                         state_dict=src.model.state_dict_numpy())
         q.optimization_history = list(getattr(src, "optimization_history", [])) + [
             {"type": "post_training_quantization", "backend": self.quantization_backend}]
