@@ -183,6 +183,10 @@ int ym_sync(ym_ctx* ctx);
 const char* ym_last_error(void);
 void ym_destroy(ym_ctx* ctx);
 int ym_version(void);
+/* Size of the conv tile-configuration catalogue of a plan dtype (ym_model_desc codes: 1 f16, 2 f32, 3 i8, 4 f8;
+ * YM_EINVAL otherwise): the id space of the ym_get_op_cfg / ym_set_op_cfg tables, so a cached table is reused only
+ * by a library with the same catalogue. */
+int ym_num_conv_cfgs(int dtype);
 
 #ifdef __cplusplus
 }

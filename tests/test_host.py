@@ -87,6 +87,8 @@ def test_capi_exports_every_declared_symbol():
         assert hasattr(lib, name), name
     assert set(L.EXPORTED) == declared
     assert lib.ym_version() == 1
+    assert lib.ym_num_conv_cfgs(1) == lib.ym_num_conv_cfgs(2) > 100 and 0 < lib.ym_num_conv_cfgs(3) == lib.ym_num_conv_cfgs(4)
+    assert lib.ym_num_conv_cfgs(0) < 0
 
 
 def test_facade_contract_without_gpu():

@@ -475,7 +475,8 @@ struct DmaCfg {
   X(16, 64, 128, 1, 2, 4, 1) X(17, 128, 128, 1, 2, 4, 1) X(18, 256, 128, 1, 1, 3, 1) X(19, 128, 256, 1, 1, 3, 1)  \
   X(20, 256, 64, 1, 2, 3, 1) X(21, 64, 64, 1, 2, 4, 2) X(22, 64, 64, 1, 1, 4, 2) X(23, 64, 64, 2, 2, 4, 2)        \
   X(24, 128, 64, 1, 2, 3, 2) X(25, 64, 128, 1, 2, 3, 2) X(26, 64, 64, 1, 2, 3, 2) X(27, 64, 64, 1, 2, 3, 3)        \
-  X(28, 64, 64, 1, 2, 2, 4) X(29, 64, 64, 2, 2, 3, 3) X(30, 64, 128, 1, 2, 2, 3)
+  X(28, 64, 64, 1, 2, 2, 4) X(29, 64, 64, 2, 2, 3, 3) X(30, 64, 128, 1, 2, 2, 3) X(31, 128, 128, 1, 2, 2, 2)     \
+  X(32, 128, 64, 1, 2, 2, 3) X(33, 128, 128, 2, 2, 2, 2)
 constexpr DmaCfg kDma[] = {
 #define YM_X(id, bm, bn, sp, kg, ns, sub) {bm, bn, sp, kg, ns, sub},
     YM_DMA_CFGS(YM_X)

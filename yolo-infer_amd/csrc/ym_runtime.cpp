@@ -507,6 +507,10 @@ int check_call(ym_ctx* c, const float* d_in, int B, int H, int W, const ym_infer
 extern "C" {
 
 int ym_version(void) { return 1; }
+int ym_num_conv_cfgs(int dtype) {  // public dtype codes (ym_model_desc): 1 f16, 2 f32, 3 i8, 4 f8
+  if (dtype < 1 || dtype > 4) return YM_EINVAL;
+  return dtype >= 3 ? ym_conv_i8_num_cfgs() : ym_conv_num_cfgs();
+}
 
 const char* ym_last_error(void) { return g_err.c_str(); }
 

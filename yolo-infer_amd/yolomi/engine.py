@@ -59,7 +59,8 @@ class Engine:
 
     def _load_table(self, B, H, W):
         """The committed table first (the one the tests and the bench pin), then this machine's tune cache.  A table
-        is used only when its version, op-name list and device architecture all match this engine."""
+        is used only when its version, op-name list, device architecture and conv-config catalogue size
+        (ym_num_conv_cfgs: the id space its entries index) all match this engine."""
         name = self._table_name(B, H, W)
         arch = torch.cuda.get_device_properties(self.device).gcnArchName
         ops = [op.name for op in self.graph.ops]
@@ -71,10 +72,14 @@ class Engine:
                 continue
             dev = t.get("device")
             if (t.get("version") == TUNE_VERSION and t.get("ops") == ops and len(t.get("cfg", [])) == self.rt.n_ops
-                    and (dev is None or dev.split(":")[0] == arch.split(":")[0])):
+                    and t.get("ncfg") == self._ncfg() and (dev is None or dev.split(":")[0] == arch.split(":")[0])):
                 self.rt.set_op_cfg(B, H, W, t["cfg"])
                 return f"{tag} table {name}"
         return None
+
+    def _ncfg(self) -> int:
+        from yolomi.lib import DTYPE_CODES, load_library
+        return load_library().ym_num_conv_cfgs(DTYPE_CODES[self.dtype])
 
     def _save_table(self, B, H, W):
         cfg = self.rt.get_op_cfg(B, H, W)
@@ -85,7 +90,7 @@ class Engine:
             os.makedirs(d, exist_ok=True)
             with open(os.path.join(d, self._table_name(B, H, W)), "w") as f:
                 json.dump({"version": TUNE_VERSION, "device": torch.cuda.get_device_properties(self.device).gcnArchName,
-                           "ops": [op.name for op in self.graph.ops], "cfg": cfg}, f)
+                           "ncfg": self._ncfg(), "ops": [op.name for op in self.graph.ops], "cfg": cfg}, f)
         except OSError:
             pass  # a read-only home: the table lives for this process only
 

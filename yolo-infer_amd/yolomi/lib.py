@@ -78,6 +78,7 @@ def load_library(path: os.PathLike = LIB_PATH):
         "ym_last_error": (C.c_char_p, []),
         "ym_destroy": (None, [P]),
         "ym_version": (I, []),
+        "ym_num_conv_cfgs": (I, [I]),
     }
     for name, (res, args) in sig.items():
         fn = getattr(lib, name)
@@ -91,7 +92,7 @@ EXPORTED = ("ym_create", "ym_load_weights", "ym_broadcast_weights", "ym_rccl_get
             "ym_rccl_comm_destroy", "ym_infer", "ym_input_max", "ym_calibrate", "ym_masks", "ym_masks_slots", "ym_letterbox",
             "ym_profile", "ym_profile_replay", "ym_tune", "ym_get_op_cfg", "ym_set_op_cfg", "ym_num_ops", "ym_op_name",
             "ym_num_buffers", "ym_buffer_info", "ym_read_buffer", "ym_sync", "ym_last_error", "ym_destroy",
-            "ym_version")
+            "ym_version", "ym_num_conv_cfgs")
 
 
 def _check(rc: int):
