@@ -2,7 +2,7 @@
 """Turn rocprofv3 output into the per-round evidence committed under profiles/.
 
     python tools/rocprof_summary.py stats  <rocprof_dir> <tag>   # --kernel-trace --stats run of bench.py
-    python tools/rocprof_summary.py pmc    <fetch_dir> <write_dir> <tag> [--graph n] [--batch 8] [--size 640]
+    python tools/rocprof_summary.py pmc    <fetch_dir> <write_dir> <tag> [workload description]
 
 `stats`: copies kernel_stats.csv to profiles/<tag>_kernel_stats.csv and writes profiles/<tag>_summary.json with the
 conv implicit-GEMM family time per forward (forwards counted by stem-kernel dispatches) — the figure bench.py's

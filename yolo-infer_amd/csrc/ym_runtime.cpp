@@ -569,12 +569,14 @@ static void build_schedule(ym_ctx* c) {
   std::vector<std::vector<int>> snap(nop);                          // known vector of an op's stream after it
   std::vector<int> rd, wr;
   int used = 1;
-  // YM_BRANCHES=1..4 (default 4).  Round 1 measured no gain for graph replays; with the round-2 kernels (fused
-  // Bottlenecks, conflict-free LDS layouts) the 4-stream schedule replays 6-10 % faster than the serial order on
-  // yolo11n/s B=8 (bench.py A/B on MI355X: s 7.93k -> 8.41-8.73k img/s, n 11.5k -> 12.1-12.4k): the Detect-head
-  // chains of one level now overlap the neck's 20x20 / 40x40 layers, whose launches leave most CUs idle.
+  // YM_BRANCHES=1..4; default 4 streams for f16 detect plans, serial otherwise.  tools/branch_ab.sh on MI355X (one
+  // box, bench.py device img/s, serial -> 4 streams): yolo11s f16 B=8 8.06k -> 8.51k, yolo11n f16 12.1k -> 13.0k (the
+  // Detect-head chains of one level overlap the neck's 20x20 / 40x40 layers, whose launches leave most CUs idle), but
+  // yolo11s-seg f16 B=4 4.35k -> 3.84k, yolo11n int8 8.62k -> 7.39k and fp8 9.25k -> 7.87k (their head / requant /
+  // float-island kernels contend with the neck instead of filling idle CUs).
   const char* env = getenv("YM_BRANCHES");
-  const int maxs = env && *env ? (atoi(env) < 1 ? 1 : (atoi(env) > S ? S : atoi(env))) : S;
+  const int def = c->dtype == YM_DT_F16 && c->task == 0 ? S : 1;
+  const int maxs = env && *env ? (atoi(env) < 1 ? 1 : (atoi(env) > S ? S : atoi(env))) : def;
   for (int i = 0; i < nop; ++i) {
     rw(c->ops[i], rd, wr);
     std::vector<int> deps;
