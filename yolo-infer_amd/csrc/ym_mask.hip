@@ -89,16 +89,19 @@ __global__ __launch_bounds__(256) void mask_upsample(const MaskArgs a) {
   if (bal && (threadIdx.x & 63) == __builtin_ctzll(bal)) a.nonempty[d] = 1;
 }
 
-// 16 consecutive pixels of a row per thread (W % 16 == 0): one 16-byte store instead of 16 byte stores; the
+// 16 consecutive pixels of a row per thread and run (W % 16 == 0): one 16-byte store instead of 16 byte stores; the
 // prototype-resolution rows the workgroup's output rows read (at most LROWS) are staged in LDS once, so a pixel's four
 // bilinear taps are LDS reads; 16-pixel runs wholly outside the box (scaled to prototype resolution, plus the
 // bilinear reach) are all zero — crop_mask zeroes the prototype mask there — and are stored without evaluation.
-constexpr int LROWS = 8, LMW = 512;
+// A workgroup covers RPT x 256 runs (~26 rows at 640 px): its dependent chain (detection row -> coefficients ->
+// prototype rows -> masks) is paid once per 16 KB of mask instead of once per 4 KB (yolo11s-seg B=4: 25,600
+// workgroups of ~5 us chains made the masks ~130 us per predict, well above their ~12 us of stores).
+constexpr int LROWS = 12, LMW = 512, RPT = 4;
 __global__ __launch_bounds__(256) void mask_upsample16(const MaskArgs a) {
   __shared__ float tile[LROWS * LMW];
   const int d = blockIdx.y;
   const int runs = a.W >> 4;
-  const int q0 = blockIdx.x * 256, q = q0 + threadIdx.x;  // 16-pixel run
+  const int q0 = blockIdx.x * 256 * RPT;  // first 16-pixel run of the workgroup
   int b;
   const float* row = det_row(a, d, b);
   if (!row) return;  // unused slot (uniform per workgroup)
@@ -109,7 +112,7 @@ __global__ __launch_bounds__(256) void mask_upsample16(const MaskArgs a) {
   const float lo_x = (floorf(row[0] * rw) - 2.f) * sx, hi_x = (ceilf(row[2] * rw) + 2.f) * sx;
   const float lo_y = (floorf(row[1] * rh) - 2.f) * sy, hi_y = (ceilf(row[3] * rh) + 2.f) * sy;
   // source rows of this workgroup's output rows
-  const int oyA = q0 / runs, oyB = min((q0 + 255) / runs, a.H - 1);
+  const int oyA = q0 / runs, oyB = min((q0 + 256 * RPT - 1) / runs, a.H - 1);
   auto src_y = [&](int oy) { const float f = ((float)oy + 0.5f) * rh - 0.5f; return f < 0.f ? 0 : (int)f; };
   const int ya = src_y(oyA), yb = min(src_y(oyB) + 1, a.MH - 1);
   const bool rows_hit = (float)oyB >= lo_y && (float)oyA < hi_y;
@@ -139,7 +142,10 @@ __global__ __launch_bounds__(256) void mask_upsample16(const MaskArgs a) {
   }
   __syncthreads();
   bool on = false;
-  if (q < a.H * runs) {
+#pragma unroll 1
+  for (int r = 0; r < RPT; ++r) {
+    const int q = q0 + 256 * r + threadIdx.x;  // consecutive threads: consecutive runs (coalesced 16-byte stores)
+    if (q >= a.H * runs) break;
     const int oy = q / runs, ox0 = (q - oy * runs) * 16;
     unsigned w[4] = {0u, 0u, 0u, 0u};
     if (rows_hit && (float)oy >= lo_y && (float)oy < hi_y && (float)(ox0 + 16) > lo_x && (float)ox0 < hi_x) {
@@ -158,7 +164,7 @@ __global__ __launch_bounds__(256) void mask_upsample16(const MaskArgs a) {
         const float v = (1.f - ly) * ((1.f - lx) * t0[x0] + lx * t0[x1]) + ly * ((1.f - lx) * t1[x0] + lx * t1[x1]);
         if (v > 0.f) w[i >> 2] |= 1u << (8 * (i & 3));
       }
-      on = (w[0] | w[1] | w[2] | w[3]) != 0u;
+      on = on || (w[0] | w[1] | w[2] | w[3]) != 0u;
     }
     typedef unsigned u32x4 __attribute__((ext_vector_type(4)));
     *reinterpret_cast<u32x4*>(a.masks + (size_t)d * a.H * a.W + (size_t)oy * a.W + ox0) = u32x4{w[0], w[1], w[2], w[3]};
@@ -173,7 +179,7 @@ __global__ __launch_bounds__(256) void mask_upsample16(const MaskArgs a) {
 bool ym_masks_fused(const MaskArgs& a) {
   if (a.W % 16 || a.MW > LMW) return false;
   const int runs = a.W / 16;
-  const int rows_out = 256 / runs + 2;  // output rows one workgroup touches
+  const int rows_out = 256 * RPT / runs + 2;  // output rows one workgroup touches
   return (int)ceilf((float)rows_out * a.MH / a.H) + 2 <= LROWS;
 }
 
@@ -193,7 +199,8 @@ hipError_t ym_launch_masks(const MaskArgs& a, hipStream_t st) {
   else
     (void)hipMemsetAsync(a.nonempty, 0, (size_t)a.total * sizeof(int), st);
   if (ym_masks_fused(a)) {  // fused: prototype masks computed per workgroup in LDS
-    hipLaunchKernelGGL(mask_upsample16, dim3((a.H * (a.W / 16) + 255) / 256, a.total), dim3(256), 0, st, a);
+    hipLaunchKernelGGL(mask_upsample16, dim3((a.H * (a.W / 16) + 256 * RPT - 1) / (256 * RPT), a.total), dim3(256), 0,
+                       st, a);
   } else {
     hipLaunchKernelGGL(mask_lowres, dim3((a.MH * a.MW + 255) / 256, a.total), dim3(256), 0, st, a);
     hipLaunchKernelGGL(mask_upsample, dim3((a.H * a.W + 255) / 256, a.total), dim3(256), 0, st, a);
