@@ -123,21 +123,29 @@ __global__ __launch_bounds__(256) void mask_upsample16(const MaskArgs a) {
   __syncthreads();
   if (rows_hit) {
     const float bx1 = row[0] * rw, by1 = row[1] * rh, bx2 = row[2] * rw, by2 = row[3] * rh;
+    // crop_mask's integer ranges (x >= bx1 and x < bx2 in fp32 <=> ceil(bx1) <= x < ceil(bx2)), clipped to the tile:
+    // out-of-box entries are zeroed first, then only the in-box ones are computed — a narrow box's few pixels spread
+    // over all threads instead of one dependent prototype load round per 256 tile entries
+    const int cx0 = max(0, (int)ceilf(bx1)), cx1 = min(a.MW, (int)ceilf(bx2));
+    const int cy0 = max(ya, (int)ceilf(by1)), cy1 = min(yb + 1, (int)ceilf(by2));
     for (int i = threadIdx.x; i < (yb - ya + 1) * a.MW; i += 256) {
       const int y = ya + i / a.MW, x = i - (i / a.MW) * a.MW;
+      if (!(x >= cx0 && x < cx1 && y >= cy0 && y < cy1)) tile[i] = 0.f;
+    }
+    const int bw = cx1 - cx0, nin = cx1 > cx0 && cy1 > cy0 ? (cy1 - cy0) * bw : 0;
+    for (int j = threadIdx.x; j < nin; j += 256) {
+      const int y = cy0 + j / bw, x = cx0 + (j - (j / bw) * bw);
+      const f32x4* pr = reinterpret_cast<const f32x4*>(a.proto + ((size_t)b * a.MH * a.MW + (size_t)y * a.MW + x) * a.nm);
       float v = 0.f;
-      if ((float)x >= bx1 && (float)x < bx2 && (float)y >= by1 && (float)y < by2) {
-        const f32x4* pr = reinterpret_cast<const f32x4*>(a.proto + ((size_t)b * a.MH * a.MW + (size_t)y * a.MW + x) * a.nm);
 #pragma unroll 8
-        for (int c4 = 0; c4 < a.nm / 4; ++c4) {
-          const f32x4 p4 = pr[c4];
-          v = fmaf(coef[4 * c4], p4[0], v);
-          v = fmaf(coef[4 * c4 + 1], p4[1], v);
-          v = fmaf(coef[4 * c4 + 2], p4[2], v);
-          v = fmaf(coef[4 * c4 + 3], p4[3], v);
-        }
+      for (int c4 = 0; c4 < a.nm / 4; ++c4) {
+        const f32x4 p4 = pr[c4];
+        v = fmaf(coef[4 * c4], p4[0], v);
+        v = fmaf(coef[4 * c4 + 1], p4[1], v);
+        v = fmaf(coef[4 * c4 + 2], p4[2], v);
+        v = fmaf(coef[4 * c4 + 3], p4[3], v);
       }
-      tile[i] = v;
+      tile[(y - ya) * a.MW + x] = v;
     }
   }
   __syncthreads();
