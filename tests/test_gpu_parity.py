@@ -302,7 +302,7 @@ def test_results_contract_and_benchmark():
 
 # ------------------------------------------------------------------------------------------------ LDS-DMA conv configs
 DMA_FIRST = 17  # csrc/ym_conv.hip: ids >= 17 are the LDS-DMA / split-K kernels of csrc/ym_conv_dma.hip
-STREAM_FIRST = DMA_FIRST + 34  # then csrc/ym_conv_stream.hip: 31 streaming 1x1 / 3x3 configs, 12 small-M split-K ones
+STREAM_FIRST = DMA_FIRST + 30  # then csrc/ym_conv_stream.hip: 31 streaming 1x1 / 3x3 configs, 12 small-M split-K ones
 
 
 def _force_cfg(eng, x, cfg):
@@ -353,7 +353,7 @@ def test_dma_split_configs_on_segment_head():
     _, y, ex = oracle("n", "segment").raw(x)
     eng = model("n", "f16", "segment").model.engine
     xd = x.to(DEV)
-    for cfg in (DMA_FIRST + 2, DMA_FIRST + 5):
+    for cfg in (DMA_FIRST + 4, DMA_FIRST + 29):  # 64x64 split 4, 128x64 split 2
         _force_cfg(eng, xd, cfg)
         eng.run(xd, use_graph=False)
         proto = eng.read_buffer(eng.graph.proto_buf.id, 1)
@@ -507,7 +507,7 @@ def test_fused_pairs_split_equals_unfused_plan():
     assert rel(hs, hu) < 1e-2 and rel(hf, hu) < 1e-2
 
 
-BNECK_BASE = 17 + 34 + 43 + 12  # csrc/ym_conv.hip: first-gen + DMA + streaming + halo ids, then the Bottleneck kernels
+BNECK_BASE = 17 + 30 + 43 + 12  # csrc/ym_conv.hip: first-gen + DMA + streaming + halo ids, then the Bottleneck kernels
 N_BNECK = 14
 
 

@@ -43,7 +43,7 @@ def main():
     torch.cuda.synchronize()
     base = eng.rt.get_op_cfg(B, S, S)
     ops = eng.graph.ops
-    ncfg = 106  # csrc/ym_conv.hip ym_conv_num_cfgs() without the Bottleneck ids: 17 first-gen + 34 DMA + 43 stream + 12 halo
+    ncfg = 102  # csrc/ym_conv.hip ym_conv_num_cfgs() without the Bottleneck ids: 17 first-gen + 30 DMA + 43 stream + 12 halo
     print(f"source {eng.tune_source}, {ncfg} conv configs", flush=True)
     conv = [i for i, op in enumerate(ops) if op.kind == "conv" and i > 1 and base[i] >= 0 and base[i] < 1 << 20]
 
