@@ -103,7 +103,7 @@ def main():
     if t_new < t_old:
         os.makedirs(os.path.dirname(a.out), exist_ok=True)
         json.dump({"version": TUNE_VERSION, "device": torch.cuda.get_device_properties(dev).gcnArchName,
-                   "ops": [op.name for op in ops], "cfg": cur,
+                   "ncfg": eng._ncfg(), "ops": [op.name for op in ops], "cfg": cur,
                    "note": f"tools/ctx_tune.py refinement of the isolated ym_tune table ({t_old * 1e3:.1f} -> "
                            f"{t_new * 1e3:.1f} us per graph-replayed forward)"}, open(a.out, "w"))
         print(f"wrote {a.out}")
