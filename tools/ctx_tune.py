@@ -45,7 +45,8 @@ def main():
     ops = eng.graph.ops
     ncfg = 102  # csrc/ym_conv.hip ym_conv_num_cfgs() without the Bottleneck ids: 17 first-gen + 30 DMA + 43 stream + 12 halo
     print(f"source {eng.tune_source}, {ncfg} conv configs", flush=True)
-    conv = [i for i, op in enumerate(ops) if op.kind == "conv" and i > 1 and base[i] >= 0 and base[i] < 1 << 20]
+    # (ops on a fused Bottleneck id, base >= ncfg, keep it: the other families do not take a fused pair's shape)
+    conv = [i for i, op in enumerate(ops) if op.kind == "conv" and i > 1 and 0 <= base[i] < ncfg]
 
     # isolated per-op times of every config (graph of back-to-back launches per op, as ym_tune)
     iso = {}
