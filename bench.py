@@ -39,8 +39,10 @@ import torch.distributed as dist  # noqa: E402
 METRIC = "images/sec @640×640 (1/2/4/8 MI355X) + mAP50-95 vs CPU ref"
 # dense MFMA peaks (MI355X_MICROARCH.md; i8 = TOP/s; f8 = the dense fp8 peak, although the non-scaled
 # v_mfma_f32_*_fp8_fp8 the fp8 plan issues runs at the bf16 rate)
-PEAK_TFLOPS = {"f16": 2500.0, "f32": 157.3, "i8": 5000.0, "f8": 5000.0}
-ACT_BYTES = {"f16": 2, "f32": 4, "i8": 1, "f8": 1}
+# x3 (fp32 storage, split-f16 MFMA): the algorithmic FLOPs against the f16 peak, although each K chunk issues three
+# f16 MFMAs (so its MFMA-issue ceiling is a third of that)
+PEAK_TFLOPS = {"f16": 2500.0, "f32": 157.3, "i8": 5000.0, "f8": 5000.0, "x3": 2500.0}
+ACT_BYTES = {"f16": 2, "f32": 4, "i8": 1, "f8": 1, "x3": 4}
 PEAK_HBM_GBS = 8000.0
 
 
@@ -103,7 +105,8 @@ def conv_roofline(model, x, dtype, workload, reps=20):
         "traffic_note": (f"HBM-side bytes per forward of all conv launches (PMC FETCH_SIZE x2 + WRITE_SIZE, {tsrc}); "
                          f"algorithmic bytes per forward {int(by)}") if traffic else "no PMC summary for this workload",
         "kernel": "conv implicit GEMM (%s): all %d conv launches of one lane's forward (%d images), aggregated%s"
-                  % ({"i8": "conv_i8, v_mfma_i32_32x32x32_i8", "f8": "conv_i8<fp8>, v_mfma_f32_32x32x16_fp8_fp8"}.get(
+                  % ({"i8": "conv_i8, v_mfma_i32_32x32x32_i8", "f8": "conv_i8<fp8>, v_mfma_f32_32x32x16_fp8_fp8",
+                      "x3": "conv_igemm/conv_lds<x3>, 3x v_mfma_f32_32x32x16_f16 per K chunk"}.get(
                       dtype, "conv_stream/conv_small/conv_dma/conv_lds/conv_bneck/conv_halo/conv_igemm"), len(conv),
                      Bl, "; int8 ops counted as FLOPs" if dtype == "i8" else ""),
         "timing": f"HIP events around a graph of {reps} back-to-back launches per op, on the launch stream",
@@ -288,7 +291,7 @@ def main():
     ap.add_argument("--task", default="detect")
     ap.add_argument("--batch", type=int, default=8, help="images per GPU per step")
     ap.add_argument("--size", type=int, default=640)
-    ap.add_argument("--dtype", default="f16", choices=["f16", "f32", "i8", "f8"])
+    ap.add_argument("--dtype", default="f16", choices=["f16", "f32", "i8", "f8", "x3"])
     ap.add_argument("--backend", default="qnnpack", choices=["qnnpack", "fbgemm"], help="i8: PTQ qconfig")
     ap.add_argument("--calib-batches", type=int, default=4, help="i8: calibration batches (B images each)")
     ap.add_argument("--cpu-seconds", type=float, default=16.0)

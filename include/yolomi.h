@@ -39,7 +39,7 @@ typedef struct {
   int max_w;
   int scale;  /* 0 = any, else 'n', 's', 'm', 'l' or 'x' */
   int task;   /* 0 = any, YM_TASK_DETECT, YM_TASK_SEGMENT */
-  int dtype;  /* 0 = any, YM_DTYPE_F16, YM_DTYPE_F32, YM_DTYPE_I8, YM_DTYPE_F8 */
+  int dtype;  /* 0 = any, YM_DTYPE_F16, YM_DTYPE_F32, YM_DTYPE_I8, YM_DTYPE_F8, YM_DTYPE_X3 */
   int reserved[2];
 } ym_model_desc;
 
@@ -49,6 +49,7 @@ typedef struct {
 #define YM_DTYPE_F32 2 /* exact-f32 MFMA (parity plan) */
 #define YM_DTYPE_I8 3  /* PTQ int8 (torch.ao qconfig of optimization/quantization/quantizers.py:124-131) */
 #define YM_DTYPE_F8 4  /* PTQ fp8 e4m3 (OCP) operands, fp32 accumulation */
+#define YM_DTYPE_X3 5  /* fp32 storage, split-fp16 MFMA (x = hi + lo, three f16 MFMAs per K chunk): f16 tolerance plan */
 
 /* An RCCL unique id (ncclUniqueId: 128 opaque bytes). */
 typedef struct {
@@ -183,7 +184,7 @@ int ym_sync(ym_ctx* ctx);
 const char* ym_last_error(void);
 void ym_destroy(ym_ctx* ctx);
 int ym_version(void);
-/* Size of the conv tile-configuration catalogue of a plan dtype (ym_model_desc codes: 1 f16, 2 f32, 3 i8, 4 f8;
+/* Size of the conv tile-configuration catalogue of a plan dtype (ym_model_desc codes: 1 f16, 2 f32, 3 i8, 4 f8, 5 x3;
  * YM_EINVAL otherwise): the id space of the ym_get_op_cfg / ym_set_op_cfg tables, so a cached table is reused only
  * by a library with the same catalogue. */
 int ym_num_conv_cfgs(int dtype);

@@ -1,0 +1,149 @@
+"""GPU parity of the x3 plan (fp32 activations, every conv GEMM as three split-f16 MFMAs: csrc/ym_conv.hip mma<x3_t>).
+
+This is the plan that meets SURVEY §7-1(b)'s fp16-mode tolerance, which the plain f16 plan misses by 3-4x on scores
+(tools/f16_emulate.py shows the f16 error is spread over every layer, so no subset of promoted ops
+closes it).  Tolerance written here (the reference's own CPU path is fp32: /root/reference/core/model.py:133):
+  * every oracle detection matched or exempt (tests/matching.py) — no min_frac —
+    with |Δxy| <= 0.64 px (1e-3 · 640), |Δscore| <= 1e-3, class exact;
+  * per-layer outputs within 1e-4 relative of the oracle.
+"""
+import json
+import os
+
+import numpy as np
+import pytest
+import torch
+
+from oracle.predict import OracleModel
+from tests.golden.make_golden import make_input
+from tests.matching import MatchReport, match_image
+from yolomi.synth import synth_weights
+
+pytestmark = pytest.mark.gpu
+GOLD = os.path.join(os.path.dirname(os.path.abspath(__file__)), "golden")
+DEV = torch.device("cuda", 0)
+TOL_XY, TOL_S = 0.64, 1e-3
+_cache = {}
+
+
+def oracle(scale="n", task="detect"):
+    k = ("o", scale, task)
+    if k not in _cache:
+        torch.set_num_threads(min(16, os.cpu_count() or 1))
+        _cache[k] = OracleModel(scale, task, synth_weights(scale, task, 0))
+    return _cache[k]
+
+
+def model(scale="n", task="detect"):
+    from core.model import YOLO11Model
+    k = ("m", scale, task)
+    if k not in _cache:
+        _cache[k] = YOLO11Model(task=task, size=scale, device="cuda:0", dtype="x3", verbose=False)
+    return _cache[k]
+
+
+def check(ref_dets, got_results, conf=0.25, iou=0.7, max_det=300):
+    rep = MatchReport()
+    for r, g in zip(ref_dets, got_results):
+        ref = r["boxes"].numpy() if isinstance(r, dict) else np.asarray(r, np.float32).reshape(-1, 6)
+        match_image(ref, g.boxes.data.cpu().numpy(), conf, iou, TOL_XY, TOL_S, rep=rep, max_det=max_det)
+    assert rep.ok, f"{rep}; {rep.failures[:3]}"
+    assert rep.matched > 0
+    return rep
+
+
+def _rel(got, ref):
+    return (got - ref).abs().max().item() / ref.abs().max().item()
+
+
+def test_x3_layers_match_oracle():
+    eng = model("n").model.engine
+    x = make_input("uniform", (11, 12), 640)
+    _, y, ex = oracle().raw(x, keep=(2, 4, 6, 8, 9, 10, 13, 16, 19, 22))
+    eng.run(x.to(DEV), use_graph=False)
+    for b in eng.graph.buffers:
+        if b.name.startswith("L") and b.name[1:].isdigit() and int(b.name[1:]) in ex["saved"]:
+            ref = ex["saved"][int(b.name[1:])].permute(0, 2, 3, 1)
+            assert _rel(eng.read_buffer(b.id, 2), ref) < 1e-4, b.name
+    no = eng.graph.no
+    ref_h = torch.cat([f.view(2, no, -1) for f in ex["feats"]], 2).transpose(1, 2)
+    got_h = eng.read_buffer(eng.graph.anchor_buf.id, 2).reshape(2, -1, eng.graph.anchor_buf.C)[..., :no]
+    assert _rel(got_h, ref_h) < 1e-4
+
+
+@pytest.mark.parametrize("name", ["det_n_uniform", "det_n_randn", "det_n_320_lowconf", "det_s_uniform"])
+def test_x3_plan_matches_golden(name):
+    g = json.load(open(os.path.join(GOLD, name + ".json")))
+    x = make_input(g["input"]["kind"], g["input"]["seeds"], g["input"]["size"]).to(DEV)
+    res = model(g["scale"]).predict(x, conf=g["conf"], iou=g["iou"])
+    check(g["dets"], res, g["conf"], g["iou"])
+
+
+@pytest.mark.parametrize("scale", ["n", "s"])
+def test_x3_b8_matches_oracle(scale):
+    """BASELINE configs 2 and 3 (B=8, 640x640) under the tile table the bench runs, at the SURVEY f16 tolerance."""
+    x = make_input("uniform", tuple(range(7001, 7009)), 640)
+    ref = oracle(scale).predict(x)
+    m = model(scale)
+    res = m.predict(x.to(DEV))
+    rep = check(ref, res)
+    assert rep.max_dscore <= TOL_S and rep.max_dxy <= TOL_XY
+
+
+@pytest.mark.parametrize("conf", [0.05, 0.004])
+def test_x3_low_conf(conf):
+    """Thousands of candidates per image (every NMS path) at the f16-mode tolerance."""
+    x = make_input("uniform", (31, 32), 640)
+    check(oracle().predict(x, conf=conf), model("n").predict(x.to(DEV), conf=conf), conf=conf)
+
+
+def test_x3_segment_s_b4():
+    """BASELINE config 5 (yolo11s-seg, B=4): boxes, the 32 mask coefficients of every match, and masks."""
+    g = json.load(open(os.path.join(GOLD, "seg_s_uniform.json")))
+    x = make_input("uniform", g["input"]["seeds"], 640)
+    m = model("s", "segment")
+    eng = m.model.engine
+    dets, counts = eng.run(x.to(DEV), conf=g["conf"], iou=g["iou"])
+    rep, worst = MatchReport(), 0.0
+    for b, n in enumerate(counts.tolist()):
+        r = np.asarray(g["nms_rows"][b], np.float32).reshape(-1, 38)
+        got = dets[b, :int(n)].cpu().numpy()
+        before = len(rep.pairs)
+        match_image(r[:, :6], got[:, :6], g["conf"], g["iou"], TOL_XY, TOL_S, rep=rep)
+        scale = max(float(np.abs(r[:, 6:]).max()) if len(r) else 1.0, 1e-6)
+        for i, j in rep.pairs[before:]:
+            worst = max(worst, float(np.abs(r[i, 6:] - got[j, 6:]).max()) / scale)
+    assert rep.ok and rep.matched > 0, rep
+    assert worst <= 1e-3, worst
+    ref = oracle("s", "segment").predict(x, conf=0.25)
+    res = m.predict(x.to(DEV), conf=0.25)
+    for r, gg in zip(ref, res):
+        rb, gb = r["boxes"].numpy(), gg.boxes.data.cpu().numpy()
+        assert len(rb) == len(gb)
+        for i in np.argsort(-rb[:, 4]):
+            j = int(np.argmin(np.abs(gb[:, :4] - rb[i, :4]).max(1)))
+            a = (r["masks"][i] == gg.masks.data[j].cpu()).float().mean().item()
+            assert a >= 0.999, (i, j, a)
+
+
+FIRST_GEN = list(range(17))  # csrc/ym_conv.hip: 12 direct-to-register + 5 LDS-staged tile configurations
+
+
+@pytest.mark.parametrize("cfg", FIRST_GEN)
+def test_x3_conv_configs_match_oracle(cfg):
+    """Every x3 conv kernel configuration on every conv of yolo11n (1x1 two-source / up-sampled, 3x3 s1/s2,
+    residual epilogues, fp32 Detect rows): layer outputs within 1e-4 of the oracle."""
+    eng = model("n").model.engine
+    x = make_input("uniform", (11, 12), 640)
+    _, y, ex = oracle().raw(x, keep=(2, 4, 6, 8, 9, 10, 13, 16, 19, 22))
+    xd = x.to(DEV)
+    try:
+        eng.run(xd, use_graph=False)
+        eng.rt.set_op_cfg(2, 640, 640, [cfg if op.kind == "conv" else -1 for op in eng.graph.ops])
+        eng.run(xd, use_graph=False)
+        for b in eng.graph.buffers:
+            if b.name.startswith("L") and b.name[1:].isdigit() and int(b.name[1:]) in ex["saved"]:
+                ref = ex["saved"][int(b.name[1:])].permute(0, 2, 3, 1)
+                assert _rel(eng.read_buffer(b.id, 2), ref) < 1e-4, (cfg, b.name)
+    finally:
+        eng._tuned.discard((2, 640, 640))

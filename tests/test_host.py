@@ -89,6 +89,34 @@ def test_capi_exports_every_declared_symbol():
     assert lib.ym_version() == 1
     assert lib.ym_num_conv_cfgs(1) == lib.ym_num_conv_cfgs(2) > 100 and 0 < lib.ym_num_conv_cfgs(3) == lib.ym_num_conv_cfgs(4)
     assert lib.ym_num_conv_cfgs(0) < 0
+    assert lib.ym_num_conv_cfgs(5) == lib.ym_num_conv_cfgs(1) and lib.ym_num_conv_cfgs(6) < 0
+
+
+def test_x3_blob_splits_weights_into_hi_lo_planes():
+    """x3 plans: every conv but the stem packs fp16 hi = fp16(w) and lo = fp16(w - hi) planes of [N][Kpad]; hi + lo
+    restores the fp32 folded weight to ~2^-22 relative (fp16 subnormal lo parts included); the stem stays fp32."""
+    sd = synth_weights("n", "detect", 0)
+    b32, bx3 = pack_model("n", "detect", sd, "f32"), pack_model("n", "detect", sd, "x3")
+    h = struct.unpack("<32i", bx3[:128])
+    assert h[2] == 4
+    nb, nop = h[11], h[12]
+    base32 = lambda b: (128 + 32 * nb + 176 * nop + 255) // 256 * 256  # noqa: E731
+    rec = lambda b, i: struct.unpack("<32i", b[128 + 32 * nb + 128 * i: 128 + 32 * nb + 128 * (i + 1)])  # noqa: E731
+    worst, nconv = 0.0, 0
+    for i in range(nop):
+        r32, rx = rec(b32, i), rec(bx3, i)
+        if r32[0] != 2:
+            continue
+        N, Kpad = r32[4], r32[21]
+        w = np.frombuffer(b32, np.float32, N * Kpad, base32(b32) + r32[19])
+        if r32[6] == h[15]:  # the stem: fp32 weights, identical
+            assert np.array_equal(np.frombuffer(bx3, np.float32, N * Kpad, base32(bx3) + rx[19]), w)
+            continue
+        hl = np.frombuffer(bx3, np.float16, 2 * N * Kpad, base32(bx3) + rx[19]).astype(np.float64)
+        rebuilt = hl[:N * Kpad] + hl[N * Kpad:]
+        worst = max(worst, float(np.abs(rebuilt - w).max() / np.abs(w).max()))
+        nconv += 1
+    assert nconv > 70 and worst < 2 ** -21
 
 
 def test_facade_contract_without_gpu():

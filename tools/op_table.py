@@ -43,7 +43,7 @@ def main():
     B, S = a.batch, a.size
     cfg = eng.rt.get_op_cfg(B, S, S) or [-1] * eng.rt.n_ops
     t = eng.profile_replay(x, reps=20)
-    costs = eng.graph.op_costs(B, S, S, {"f16": 2, "f32": 4, "i8": 1}[a.dtype])
+    costs = eng.graph.op_costs(B, S, S, {"f16": 2, "f32": 4, "i8": 1, "f8": 1, "x3": 4}[a.dtype])
     tot = floor = 0.0
     print(f"yolo11{a.model} {a.task} B={B} {S}^2 {a.dtype}; tune source {eng.tune_source}")
     print(f"{'op':26s} {'kind':6s} {'shape':28s} {'cfg':>4s} {'us':>7s} {'floor':>6s} {'TF/s':>7s} {'GB/s':>7s}")

@@ -11,13 +11,34 @@ typedef float f32x8 __attribute__((ext_vector_type(8)));
 
 #define YM_WAVE 64
 
-// Activation storage precision of a plan: f16 (MFMA 32x32x16 f16), f32 (exact-f32 MFMA 32x32x2, parity mode) or
-// i8 (PTQ int8: activations stored as q - 128 in int8, weights int8, MFMA 32x32x32 i8 with int32 accumulation).
-enum { YM_DT_F16 = 0, YM_DT_F32 = 1, YM_DT_I8 = 2, YM_DT_F8 = 3 };
+// Activation storage precision of a plan: f16 (MFMA 32x32x16 f16), f32 (exact-f32 MFMA 32x32x2, parity mode),
+// i8 (PTQ int8: activations stored as q - 128 in int8, weights int8, MFMA 32x32x32 i8 with int32 accumulation), or
+// x3 (fp32 storage, every conv GEMM as three f16 MFMAs on split operands: x = hi + lo with hi = fp16(x),
+// lo = fp16(x - hi); x·w ≈ hi·w_hi + lo·w_hi + hi·w_lo, fp32 accumulation — ~2^-21 relative, the f16 MFMA rate / 3).
+enum { YM_DT_F16 = 0, YM_DT_F32 = 1, YM_DT_I8 = 2, YM_DT_F8 = 3, YM_DT_X3 = 4 };
+// plans whose activations are stored fp32 (the exact-f32 parity plan and the split-f16 plan share every non-GEMM kernel)
+inline bool ym_dt_f32s(int dt) { return dt == YM_DT_F32 || dt == YM_DT_X3; }
 // one-byte quantized plans (int8 affine / fp8 e4m3): same graph, storage and kernels (csrc/ym_quant.h Q8)
 inline bool ym_dt_q8(int dt) { return dt == YM_DT_I8 || dt == YM_DT_F8; }
 
 typedef signed char i8;
+
+// x3 plans: an fp32 operand fragment as its fp16 high part and the fp16 rounding of the remainder.  The remainder is
+// exact in fp32 and below 2^-11 |x|, so its fp16 rounding may be subnormal: v_mfma_f32_*_f16 keeps fp16 subnormal
+// operands (measured on gfx950, tools/x3_probe.hip), so no rescaling of the low part is needed.
+struct HL {
+  f16x8 hi, lo;
+};
+__device__ __forceinline__ HL ym_split8(const f32x8& v) {
+  HL r;
+#pragma unroll
+  for (int e = 0; e < 8; ++e) {
+    const f16 h = (f16)v[e];
+    r.hi[e] = h;
+    r.lo[e] = (f16)(v[e] - (float)h);
+  }
+  return r;
+}
 
 // 8 consecutive channels of one pixel: the unit of every NHWC load in this runtime (16 B in f16, 32 B in f32).
 template <typename T> struct Vec8;

@@ -25,21 +25,42 @@
 // f16 plans: v_mfma_f32_32x32x16_f16 (fp32 accumulate). f32 plans (parity mode): v_mfma_f32_32x32x2_f32 (exact f32).
 #include <stdlib.h>
 
+#include <type_traits>
+
 #include "ym_common.h"
 
 typedef float f32x16 __attribute__((ext_vector_type(16)));
 
 namespace {
 
-template <typename T> struct Frag;  // one lane's 8 consecutive K values of an MFMA operand
-template <> struct Frag<f16> { typedef f16x8 type; };
-template <> struct Frag<float> { typedef f32x8 type; };
+// Plan arithmetic modes: f16 (fp16 operands), float (exact-f32 MFMA) and x3_t (fp32 activations, weights packed as
+// fp16 hi/lo planes, every K chunk as three f16 MFMAs on split operands; csrc/ym_common.h YM_DT_X3).
+struct x3_t {};
+template <typename M> struct Mode;
+template <> struct Mode<f16> { typedef f16 act; typedef f16 wt; typedef f16x8 frag; };
+template <> struct Mode<float> { typedef float act; typedef float wt; typedef f32x8 frag; };
+template <> struct Mode<x3_t> { typedef float act; typedef f16 wt; typedef HL frag; };
 
-template <typename T>
-__device__ __forceinline__ typename Frag<T>::type load8(const T* p) { return Vec8<T>::load(p); }
+// one lane's 8 consecutive K values of the weight operand (x3: the hi plane, and the lo plane `lo` elements later)
+template <typename M>
+__device__ __forceinline__ typename Mode<M>::frag wload(const typename Mode<M>::wt* p, size_t lo) {
+  if constexpr (std::is_same<M, x3_t>::value) return HL{Vec8<f16>::load(p), Vec8<f16>::load(p + lo)};
+  else return Vec8<typename Mode<M>::wt>::load(p);
+}
+// an activation chunk as an MFMA operand fragment
+template <typename M>
+__device__ __forceinline__ typename Mode<M>::frag xfrag(const typename Vec8<typename Mode<M>::act>::type& v) {
+  if constexpr (std::is_same<M, x3_t>::value) return ym_split8(v);
+  else return v;
+}
+template <typename M>
+__device__ __forceinline__ typename Mode<M>::frag xzero() {
+  if constexpr (std::is_same<M, x3_t>::value) return HL{Vec8<f16>::zero(), Vec8<f16>::zero()};
+  else return Vec8<typename Mode<M>::act>::zero();
+}
 
-template <typename T>
-__device__ __forceinline__ void mma(const typename Frag<T>::type& a, const typename Frag<T>::type& b, f32x16& acc);
+template <typename M>
+__device__ __forceinline__ void mma(const typename Mode<M>::frag& a, const typename Mode<M>::frag& b, f32x16& acc);
 
 template <>
 __device__ __forceinline__ void mma<f16>(const f16x8& a, const f16x8& b, f32x16& acc) {
@@ -51,6 +72,14 @@ template <>
 __device__ __forceinline__ void mma<float>(const f32x8& a, const f32x8& b, f32x16& acc) {
 #pragma unroll
   for (int s = 0; s < 8; ++s) acc = __builtin_amdgcn_mfma_f32_32x32x2f32(a[s], b[s], acc, 0, 0, 0);
+}
+
+// split f16: the small cross terms first, then hi·hi (lo·lo, below 2^-22 relative, is dropped)
+template <>
+__device__ __forceinline__ void mma<x3_t>(const HL& a, const HL& b, f32x16& acc) {
+  acc = __builtin_amdgcn_mfma_f32_32x32x16_f16(a.lo, b.hi, acc, 0, 0, 0);
+  acc = __builtin_amdgcn_mfma_f32_32x32x16_f16(a.hi, b.lo, acc, 0, 0, 0);
+  acc = __builtin_amdgcn_mfma_f32_32x32x16_f16(a.hi, b.hi, acc, 0, 0, 0);
 }
 
 template <typename OutT> struct Out4;
@@ -81,7 +110,7 @@ __device__ __forceinline__ void load_res4(const T* p, float* v) {
 // KIND 0: the stem, a 3x3 whose source is the caller's NCHW fp32 batch (3 channels, /255 rule applied on load).
 // One K step = 64 (4 MFMAs per block pair): 4x fewer dependent memory round trips than a 16-deep step.
 constexpr int KSTEP = 64;
-constexpr int KS = KSTEP / 16;
+constexpr int KS64 = KSTEP / 16;
 
 // XCD-aware tile map: workgroups are dealt round-robin over the 8 XCDs (bid % 8), so give every N tile of one pixel
 // tile the same bid % 8 (the pixel rows they all read then sit in ONE XCD's L2), and give each XCD one contiguous run
@@ -95,9 +124,14 @@ __device__ __forceinline__ bool xcd_tile(const ConvArgs& a, int BM, int& tm, int
   return tm * BM < a.M;
 }
 
-template <typename T, typename OutT, int WTM, int WTN, int WM, int WN, int WK, int KIND>
+template <typename M, typename OutT, int WTM, int WTN, int WM, int WN, int WK, int KIND>
 __global__ __launch_bounds__(WM * WN * WK * 64) void conv_igemm(const ConvArgs a) {
-  typedef typename Frag<T>::type F;
+  typedef typename Mode<M>::act T;
+  typedef typename Mode<M>::wt WT;
+  typedef typename Mode<M>::frag F;
+  // K chunks of 16 per step: 4 (64-deep steps); x3 fragments are twice the registers, so 2 (32-deep steps) keep the
+  // two register buffers of fragments within the VGPR budget
+  constexpr int KS = std::is_same<M, x3_t>::value ? 2 : KS64;
   constexpr int BM = WM * WTM * 32, BN = WN * WTN * 32;
   const int lane = threadIdx.x & 63;
   const int wid = threadIdx.x >> 6;
@@ -141,16 +175,17 @@ __global__ __launch_bounds__(WM * WN * WK * 64) void conv_igemm(const ConvArgs a
       ix0[i] = px[i] * a.s - 1;
     }
   }
-  const T* wrow[WTN];
+  const WT* wrow[WTN];
+  const size_t wlo = (size_t)a.N * a.Kpad;  // x3: the lo weight plane follows the hi plane
 #pragma unroll
   for (int j = 0; j < WTN; ++j) {
     const int n = nbase + j * 32 + l32;
-    wrow[j] = static_cast<const T*>(a.w) + (size_t)(n < a.N ? n : 0) * a.Kpad;
+    wrow[j] = static_cast<const WT*>(a.w) + (size_t)(n < a.N ? n : 0) * a.Kpad;
   }
 
   // ---- K walk. Step g (this wave: g = wk, wk+WK, ...) covers chunks [g*2KS, (g+1)*2KS); lane half h loads
   // chunks g*2KS + 2s + h, s < KS (chunk = 8 consecutive K = 8 channels of one tap).
-  const int nsteps = a.Kpad / KSTEP;
+  const int nsteps = a.Kpad / (16 * KS);
   int g = wk;
   int tap0 = 0, cb0 = 0;  // KIND 3: tap / channel-block of chunk g*2KS + h
   if constexpr (KIND != 1) {
@@ -163,10 +198,10 @@ __global__ __launch_bounds__(WM * WN * WK * 64) void conv_igemm(const ConvArgs a
   if constexpr (KIND == 0) div255 = ym_input_max(a.ctl) > 1.0f + a.eps;
   auto gather = [&](int i, int s) -> F {
     const int chunk = g * 2 * KS + 2 * s + h;
-    if (!pv[i] || chunk >= a.Kc) return Vec8<T>::zero();
+    if (!pv[i] || chunk >= a.Kc) return xzero<M>();
     if constexpr (KIND == 1) {
       const int c = chunk * 8;
-      return load8<T>((c < a.C0 ? row0[i] : row1[i]) + c);
+      return xfrag<M>(Vec8<T>::load((c < a.C0 ? row0[i] : row1[i]) + c));
     } else if constexpr (KIND == 0) {  // Cin8 == 1: chunk = tap; channels 3..7 are zero padding
       const int ky = chunk / 3, kx = chunk - (chunk / 3) * 3;
       const int iy = iy0[i] + ky, ix = ix0[i] + kx;
@@ -183,8 +218,8 @@ __global__ __launch_bounds__(WM * WN * WK * 64) void conv_igemm(const ConvArgs a
       while (cb >= a.Cin8) { cb -= a.Cin8; ++t; }
       const int ky = t / 3, kx = t - (t / 3) * 3;
       const int iy = iy0[i] + ky, ix = ix0[i] + kx;
-      if ((unsigned)iy >= (unsigned)a.Hin || (unsigned)ix >= (unsigned)a.Win) return Vec8<T>::zero();
-      return load8<T>(row0[i] + (size_t)(iy * a.Win + ix) * a.s0_ctot + cb * 8);
+      if ((unsigned)iy >= (unsigned)a.Hin || (unsigned)ix >= (unsigned)a.Win) return xzero<M>();
+      return xfrag<M>(Vec8<T>::load(row0[i] + (size_t)(iy * a.Win + ix) * a.s0_ctot + cb * 8));
     }
   };
   auto advance = [&]() {
@@ -208,7 +243,7 @@ __global__ __launch_bounds__(WM * WN * WK * 64) void conv_igemm(const ConvArgs a
 #pragma unroll
     for (int s = 0; s < KS; ++s) {
 #pragma unroll
-      for (int j = 0; j < WTN; ++j) fa[s][j] = load8<T>(wrow[j] + (size_t)(g * 2 * KS + 2 * s + h) * 8);
+      for (int j = 0; j < WTN; ++j) fa[s][j] = wload<M>(wrow[j] + (size_t)(g * 2 * KS + 2 * s + h) * 8, wlo);
 #pragma unroll
       for (int i = 0; i < WTM; ++i) fb[s][i] = gather(i, s);
     }
@@ -219,7 +254,7 @@ __global__ __launch_bounds__(WM * WN * WK * 64) void conv_igemm(const ConvArgs a
 #pragma unroll
       for (int i = 0; i < WTM; ++i)
 #pragma unroll
-        for (int j = 0; j < WTN; ++j) mma<T>(fa[s][j], fb[s][i], acc[i][j]);
+        for (int j = 0; j < WTN; ++j) mma<M>(fa[s][j], fb[s][i], acc[i][j]);
   };
 
   // epilogue operands (bias, residual) are fetched during the last step's MFMAs
@@ -322,7 +357,7 @@ __global__ __launch_bounds__(WM * WN * WK * 64) void conv_igemm(const ConvArgs a
         for (int e = 0; e < 4; ++e) {
           const float x = acc[i][j][4 * q + e] + bias[j][q][e];
           // f16 plans: the fp16-rounded output does not see the fast SiLU's ~1 ulp (fp32) error
-          v[e] = (a.act ? (sizeof(T) == 2 ? ym_silu_fast(x) : ym_silu(x)) : x) + resv[i][j][q][e];
+          v[e] = (a.act ? (sizeof(OutT) == 2 ? ym_silu_fast(x) : ym_silu(x)) : x) + resv[i][j][q][e];
           if (a.raw) a.raw[(size_t)(pbase + i * 32 + l32) * a.N + n + e] = x;  // f32 calibration run
         }
         if (a.shuffle) {
@@ -341,7 +376,7 @@ struct Cfg {
   int wtm, wtn, wm, wn, wk;
 };
 
-template <typename T, typename OutT, int WTM, int WTN, int WM, int WN, int WK>
+template <typename M, typename OutT, int WTM, int WTN, int WM, int WN, int WK>
 hipError_t launch_cfg(ConvArgs a, int kind, hipStream_t st) {
   constexpr int BM = WM * WTM * 32, BN = WN * WTN * 32, NT = WM * WN * WK * 64;
   const int tiles_m8 = ((a.M + BM - 1) / BM + 7) / 8 * 8;
@@ -349,9 +384,9 @@ hipError_t launch_cfg(ConvArgs a, int kind, hipStream_t st) {
   const size_t lds = WK > 1 ? (size_t)(WK - 1) * WM * WN * WTM * WTN * 16 * 64 * sizeof(float) : 0;
   const dim3 grid(tiles_m8 * a.tiles_n);
   if (kind == 1)
-    hipLaunchKernelGGL((conv_igemm<T, OutT, WTM, WTN, WM, WN, WK, 1>), grid, dim3(NT), lds, st, a);
+    hipLaunchKernelGGL((conv_igemm<M, OutT, WTM, WTN, WM, WN, WK, 1>), grid, dim3(NT), lds, st, a);
   else
-    hipLaunchKernelGGL((conv_igemm<T, OutT, WTM, WTN, WM, WN, WK, 3>), grid, dim3(NT), lds, st, a);
+    hipLaunchKernelGGL((conv_igemm<M, OutT, WTM, WTN, WM, WN, WK, 3>), grid, dim3(NT), lds, st, a);
   return hipGetLastError();
 }
 
@@ -361,15 +396,22 @@ hipError_t launch_cfg(ConvArgs a, int kind, hipStream_t st) {
 // coalesced 16-byte row loads (8 lanes cover a 128-byte row), stored XOR-swizzled (chunk c of row r at c ^ ((r >> 1) & 7): conflict-free for ds_read_b128's non-contiguous lane groups)
 // so the MFMA fragment reads (ds_read_b128, 32 rows at one K offset) do not pile onto one bank group; the next
 // stage's global loads are in flight while the current stage's MFMAs run; one barrier per stage.
-template <typename T, typename OutT, int BM, int BN, int KIND>
+// x3 plans (M = x3_t): activations arrive as fp32 and are split into fp16 hi/lo planes when they are staged, the
+// weights are staged from their hi/lo planes; the fragment reads then feed the three MFMAs of mma<x3_t>.
+template <typename M, typename OutT, int BM, int BN, int KIND>
 __global__ __launch_bounds__(256) void conv_lds(const ConvArgs a) {
+  typedef typename Mode<M>::act T;
+  typedef typename Mode<M>::wt WT;
+  constexpr bool X3 = std::is_same<M, x3_t>::value;
+  constexpr int NP = X3 ? 2 : 1;   // fp16 planes per operand in LDS
   constexpr int BK = 64;
   constexpr int RB = BM * 8 / 256;  // pixel-row chunks per thread per stage
   constexpr int RA = BN * 8 / 256;  // weight-row chunks per thread per stage
   constexpr int TM = BM / 64, TN = BN / 64;  // 32x32 blocks per wave (2x2 waves)
   typedef typename Vec8<T>::type V;
-  __shared__ __attribute__((aligned(16))) T sA[2][BN * BK];
-  __shared__ __attribute__((aligned(16))) T sB[2][BM * BK];
+  typedef typename Mode<M>::frag WF;
+  __shared__ __attribute__((aligned(16))) f16 sA[2][NP][BN * BK];
+  __shared__ __attribute__((aligned(16))) f16 sB[2][NP][BM * BK];
   int tm, tn;
   if (!xcd_tile(a, BM, tm, tn)) return;
   const int tid = threadIdx.x;
@@ -405,23 +447,25 @@ __global__ __launch_bounds__(256) void conv_lds(const ConvArgs a) {
       pix0[i] = ox * a.s - 1;
     }
   }
-  const T* wrow[RA];
+  const WT* wrow[RA];
+  const size_t wlo = (size_t)a.N * a.Kpad;
 #pragma unroll
   for (int i = 0; i < RA; ++i) {
     const int n = tn * BN + (tid >> 3) + 32 * i;
-    wrow[i] = static_cast<const T*>(a.w) + (size_t)(n < a.N ? n : 0) * a.Kpad;
+    wrow[i] = static_cast<const WT*>(a.w) + (size_t)(n < a.N ? n : 0) * a.Kpad;
   }
   int tap = 0, cb = kc;  // KIND 3: tap / channel block of chunk kt*8 + kc
   if constexpr (KIND == 3) {
     tap = kc / a.Cin8;
     cb = kc - tap * a.Cin8;
   }
-  V ra[RB], rw[RA];
+  V ra[RB];
+  WF rw[RA];
   int kt = 0;
   auto load = [&]() {
     const int chunk = kt * 8 + kc;
 #pragma unroll
-    for (int i = 0; i < RA; ++i) rw[i] = Vec8<T>::load(wrow[i] + (size_t)chunk * 8);
+    for (int i = 0; i < RA; ++i) rw[i] = wload<M>(wrow[i] + (size_t)chunk * 8, wlo);
 #pragma unroll
     for (int i = 0; i < RB; ++i) {
       V v = Vec8<T>::zero();
@@ -447,12 +491,25 @@ __global__ __launch_bounds__(256) void conv_lds(const ConvArgs a) {
 #pragma unroll
     for (int i = 0; i < RA; ++i) {
       const int r = (tid >> 3) + 32 * i;
-      *reinterpret_cast<V*>(&sA[buf][r * BK + ((kc ^ ((r >> 1) & 7)) * 8)]) = rw[i];
+      const int o = r * BK + ((kc ^ ((r >> 1) & 7)) * 8);
+      if constexpr (X3) {
+        *reinterpret_cast<f16x8*>(&sA[buf][0][o]) = rw[i].hi;
+        *reinterpret_cast<f16x8*>(&sA[buf][1][o]) = rw[i].lo;
+      } else {
+        *reinterpret_cast<f16x8*>(&sA[buf][0][o]) = rw[i];
+      }
     }
 #pragma unroll
     for (int i = 0; i < RB; ++i) {
       const int r = (tid >> 3) + 32 * i;
-      *reinterpret_cast<V*>(&sB[buf][r * BK + ((kc ^ ((r >> 1) & 7)) * 8)]) = ra[i];
+      const int o = r * BK + ((kc ^ ((r >> 1) & 7)) * 8);
+      if constexpr (X3) {
+        const HL x = ym_split8(ra[i]);
+        *reinterpret_cast<f16x8*>(&sB[buf][0][o]) = x.hi;
+        *reinterpret_cast<f16x8*>(&sB[buf][1][o]) = x.lo;
+      } else {
+        *reinterpret_cast<f16x8*>(&sB[buf][0][o]) = ra[i];
+      }
     }
   };
   f32x16 acc[TM][TN];
@@ -473,21 +530,27 @@ __global__ __launch_bounds__(256) void conv_lds(const ConvArgs a) {
 #pragma unroll
     for (int s = 0; s < 4; ++s) {
       const int cc = 2 * s + h;
-      typename Frag<T>::type fa[TN], fb[TM];
+      WF fa[TN], fb[TM];
 #pragma unroll
       for (int j = 0; j < TN; ++j) {
         const int r = wn * (BN / 2) + j * 32 + l32;
-        fa[j] = *reinterpret_cast<const V*>(&sA[cur][r * BK + ((cc ^ ((r >> 1) & 7)) * 8)]);
+        const int o = r * BK + ((cc ^ ((r >> 1) & 7)) * 8);
+        if constexpr (X3) fa[j] = HL{*reinterpret_cast<const f16x8*>(&sA[cur][0][o]),
+                                     *reinterpret_cast<const f16x8*>(&sA[cur][1][o])};
+        else fa[j] = *reinterpret_cast<const f16x8*>(&sA[cur][0][o]);
       }
 #pragma unroll
       for (int i = 0; i < TM; ++i) {
         const int r = wm * (BM / 2) + i * 32 + l32;
-        fb[i] = *reinterpret_cast<const V*>(&sB[cur][r * BK + ((cc ^ ((r >> 1) & 7)) * 8)]);
+        const int o = r * BK + ((cc ^ ((r >> 1) & 7)) * 8);
+        if constexpr (X3) fb[i] = HL{*reinterpret_cast<const f16x8*>(&sB[cur][0][o]),
+                                     *reinterpret_cast<const f16x8*>(&sB[cur][1][o])};
+        else fb[i] = *reinterpret_cast<const f16x8*>(&sB[cur][0][o]);
       }
 #pragma unroll
       for (int i = 0; i < TM; ++i)
 #pragma unroll
-        for (int j = 0; j < TN; ++j) mma<T>(fa[j], fb[i], acc[i][j]);
+        for (int j = 0; j < TN; ++j) mma<M>(fa[j], fb[i], acc[i][j]);
     }
     if (kt < nk) store(cur ^ 1);
     __syncthreads();
@@ -515,7 +578,7 @@ __global__ __launch_bounds__(256) void conv_lds(const ConvArgs a) {
 #pragma unroll
         for (int e = 0; e < 4; ++e) {
           const float x = acc[i][j][4 * q + e] + b4[e];
-          v[e] = a.act ? ym_silu_fast(x) : x;  // f16 plans only (LDS variants)
+          v[e] = a.act ? (X3 ? ym_silu(x) : ym_silu_fast(x)) : x;  // fast SiLU where the output is rounded to fp16
         }
         if (a.shuffle) {
           const int sub = n / a.npr;
@@ -530,17 +593,17 @@ __global__ __launch_bounds__(256) void conv_lds(const ConvArgs a) {
   }
 }
 
-template <typename T, typename OutT, int BM, int BN>
+template <typename M, typename OutT, int BM, int BN>
 hipError_t launch_lds(ConvArgs a, int kind, hipStream_t st) {
   const int tiles_m8 = ((a.M + BM - 1) / BM + 7) / 8 * 8;
   a.tiles_n = (a.N + BN - 1) / BN;
   const dim3 grid(tiles_m8 * a.tiles_n);
-  if (kind == 1) hipLaunchKernelGGL((conv_lds<T, OutT, BM, BN, 1>), grid, dim3(256), 0, st, a);
-  else hipLaunchKernelGGL((conv_lds<T, OutT, BM, BN, 3>), grid, dim3(256), 0, st, a);
+  if (kind == 1) hipLaunchKernelGGL((conv_lds<M, OutT, BM, BN, 1>), grid, dim3(256), 0, st, a);
+  else hipLaunchKernelGGL((conv_lds<M, OutT, BM, BN, 3>), grid, dim3(256), 0, st, a);
   return hipGetLastError();
 }
 
-// LDS-variant tile configurations (f16 plans only): (id, BM, BN)
+// LDS-variant tile configurations (f16 and x3 plans): (id, BM, BN)
 #define YM_LDS_CFGS(X) \
   X(12, 128, 128)      \
   X(13, 128, 64)       \
@@ -572,18 +635,18 @@ constexpr Cfg kCfgs[kNumCfg] = {
 
 constexpr int kNumAllCfg = 17;
 
-template <typename T, typename OutT>
+template <typename M, typename OutT>
 hipError_t launch_id(int id, const ConvArgs& a, int kind, hipStream_t st) {
   switch (id) {
 #define YM_X(cid, A, B, C, D, E) \
-  case cid: return launch_cfg<T, OutT, A, B, C, D, E>(a, kind, st);
+  case cid: return launch_cfg<M, OutT, A, B, C, D, E>(a, kind, st);
     YM_CONV_CFGS(YM_X)
 #undef YM_X
   }
-  if constexpr (sizeof(T) == 2) {
+  if constexpr (!std::is_same<M, float>::value) {
     switch (id) {
 #define YM_X(cid, BM_, BN_) \
-  case cid: return launch_lds<T, OutT, BM_, BN_>(a, kind, st);
+  case cid: return launch_lds<M, OutT, BM_, BN_>(a, kind, st);
       YM_LDS_CFGS(YM_X)
 #undef YM_X
     }
@@ -690,7 +753,8 @@ hipError_t ym_launch_conv(int dtype, int out_f32, const ConvArgs& a, int cfg, hi
     cfg = -1;
   }
   int id = (cfg >= 0 && cfg < kNumAllCfg) ? cfg : choose_cfg(a);
-  if (id >= kNumCfg && dtype != YM_DT_F16) id = choose_cfg(a);  // LDS variants are instantiated for f16 only
+  if (id >= kNumCfg && dtype == YM_DT_F32) id = choose_cfg(a);  // LDS variants: f16 and x3 plans
   if (dtype == YM_DT_F16) return out_f32 ? launch_id<f16, float>(id, a, kind, st) : launch_id<f16, f16>(id, a, kind, st);
+  if (dtype == YM_DT_X3) return launch_id<x3_t, float>(id, a, kind, st);
   return launch_id<float, float>(id, a, kind, st);
 }

@@ -167,7 +167,7 @@ struct ym_ctx {
   }
   int buf_H(int b) const { return bufs[b].f == 0 ? 1 : cH / bufs[b].f; }
   int buf_Wd(int b) const { return bufs[b].f == 0 ? A : cW / bufs[b].f; }
-  int elem(int b) const { return (bufs[b].f32 || dtype == YM_DT_F32) ? 4 : (ym_dt_q8(dtype) ? 1 : 2); }
+  int elem(int b) const { return (bufs[b].f32 || ym_dt_f32s(dtype)) ? 4 : (ym_dt_q8(dtype) ? 1 : 2); }
   template <typename T> const T* wptr(int32_t off) const {
     return reinterpret_cast<const T*>(d_weights + (size_t)(uint32_t)off);
   }
@@ -309,7 +309,7 @@ int conv_args(ym_ctx* c, const Op& op, int B, const float* d_in, float in_eps, C
       a.M = B * a.Ho * a.Wo;
       a.fd_hw = ym_fdiv(a.Ho * a.Wo);
       a.fd_w = ym_fdiv(a.Wo);
-      out_f32 = c->bufs[bd].f32 && c->dtype != YM_DT_F32;
+      out_f32 = c->bufs[bd].f32 && !ym_dt_f32s(c->dtype);
       a.raw = c->raw_of(op);
       a.s0_elems = (b0 == c->input_buf) ? 0 : (long)c->cB * c->buf_P(b0) * c->bufs[b0].C;
       a.s1_elems = b1 >= 0 ? (long)c->cB * c->buf_P(b1) * c->bufs[b1].C : 0;
@@ -507,9 +507,9 @@ int check_call(ym_ctx* c, const float* d_in, int B, int H, int W, const ym_infer
 extern "C" {
 
 int ym_version(void) { return 1; }
-int ym_num_conv_cfgs(int dtype) {  // public dtype codes (ym_model_desc): 1 f16, 2 f32, 3 i8, 4 f8
-  if (dtype < 1 || dtype > 4) return YM_EINVAL;
-  return dtype >= 3 ? ym_conv_i8_num_cfgs() : ym_conv_num_cfgs();
+int ym_num_conv_cfgs(int dtype) {  // public dtype codes (ym_model_desc): 1 f16, 2 f32, 3 i8, 4 f8, 5 x3
+  if (dtype < 1 || dtype > 5) return YM_EINVAL;
+  return (dtype == 3 || dtype == 4) ? ym_conv_i8_num_cfgs() : ym_conv_num_cfgs();
 }
 
 const char* ym_last_error(void) { return g_err.c_str(); }
@@ -613,9 +613,6 @@ static void build_schedule(ym_ctx* c) {
   c->nbr = used;
 }
 
-// Structural check of a parsed plan before it is committed to a context: buffer ids of every op record in range,
-// every weight / bias / quantisation record inside the weight section.  The kernels index device memory with these
-// values, so a malformed blob must fail here (YM_EBLOB), never inside a launch.
 // OCP e4m3 (gfx950 fp8) code -> value: the fp8 plan's stem weights, re-laid out as fp32 (exact)
 static float e4m3_value(uint8_t b) {
   const int e = (b >> 3) & 15, m = b & 7;
@@ -623,27 +620,42 @@ static float e4m3_value(uint8_t b) {
   return (b & 0x80) ? -v : v;
 }
 
-static int validate_plan(const std::vector<BufDesc>& bufs, const std::vector<Op>& ops, int dtype, size_t wbytes) {
+// Structural check of a parsed plan before it is committed to a context: buffer ids and channel views
+// [coff, coff + C) of every op record inside their buffers, every weight / bias / quantisation record inside the
+// weight section.  The kernels index device memory with these values, so a malformed blob must fail here
+// (YM_EBLOB), never inside a launch.
+static int validate_plan(const std::vector<BufDesc>& bufs, const std::vector<Op>& ops, int dtype, size_t wbytes,
+                         int input_buf) {
   const int nbuf = (int)bufs.size();
   for (int i = 0; i < nbuf; ++i)
     if (bufs[i].C <= 0 || bufs[i].C > (1 << 16) || bufs[i].f < 0 || bufs[i].f > 64)
       return fail(YM_EBLOB, "buffer %d: bad geometry (C %d, f %d)", i, bufs[i].C, bufs[i].f);
-  const size_t esz = dtype == YM_DT_F32 ? 4 : (dtype == YM_DT_F16 ? 2 : 1);
+  // conv weight bytes per element: x3 plans pack an fp16 hi and an fp16 lo plane (their stem conv: fp32)
+  const size_t esz = dtype == YM_DT_F32 ? 4 : (dtype == YM_DT_F16 ? 2 : (dtype == YM_DT_X3 ? 4 : 1));
   for (const Op& o : ops) {
     const int32_t* r = o.r;
     auto buf_ok = [&](int b, bool opt) { return (opt && b == -1) || (b >= 0 && b < nbuf); };
     auto w_ok = [&](int32_t off, size_t n) { return (size_t)(uint32_t)off + n <= wbytes; };
+    // a channel view [coff, coff + C) of buffer b (b == -1: absent, when optional)
+    auto view_ok = [&](int b, int coff, int C, bool opt) {
+      if (opt && b == -1) return true;
+      return buf_ok(b, false) && coff >= 0 && C > 0 && (long)coff + C <= bufs[b].C;
+    };
     bool ok = true;
     const size_t qrec = sizeof(QRec);
     switch (r[0]) {
-      case OP_INPUT: case OP_DECODE: case OP_NMS: break;
+      case OP_INPUT: case OP_DECODE: case OP_NMS: break;  // no operands besides the header's input/anchor buffers
       case OP_CONV: {
-        const int N = r[4], Kpad = r[21];
-        ok = N > 0 && Kpad > 0 && Kpad <= (1 << 16) && buf_ok(r[6], false) && buf_ok(r[10], true) &&
-             buf_ok(r[13], false) && buf_ok(r[17], true) && w_ok(r[19], (size_t)N * Kpad * esz) &&
-             w_ok(r[20], (size_t)N * 4);
+        const int N = r[4], Kpad = r[21], fused = r[30];
+        const int Nout = fused ? r[27] : N;  // the channels the launch writes (a fused pair: its second conv's)
+        const int Cd = r[16] ? Nout / 4 : Nout;  // pixel shuffle (ConvTranspose2d 2x2): N/4 channels per pixel
+        const int C1 = r[10] >= 0 ? r[12] : 0;
+        ok = N > 0 && Kpad > 0 && Kpad <= (1 << 16) && r[3] == r[8] + C1 && view_ok(r[6], r[7], r[8], false) &&
+             view_ok(r[10], r[11], r[12], true) && view_ok(r[13], r[14], Cd, false) &&
+             view_ok(r[17], r[18], Nout, true) && (r[6] != input_buf || (r[7] == 0 && r[10] == -1)) &&
+             w_ok(r[19], (size_t)N * Kpad * esz) && w_ok(r[20], (size_t)N * 4);
         if (ok && ym_dt_q8(dtype)) ok = w_ok(r[22], qrec) && w_ok(r[23], (size_t)N * 4) && w_ok(r[24], (size_t)N * 4);
-        if (ok && r[30]) {
+        if (ok && fused) {
           const int N2 = r[27], K2 = r[29];
           ok = N2 > 0 && K2 > 0 && K2 <= (1 << 16) && buf_ok(r[31], false) && w_ok(r[25], (size_t)N2 * K2 * 2) &&
                w_ok(r[26], (size_t)N2 * 4);
@@ -652,16 +664,21 @@ static int validate_plan(const std::vector<BufDesc>& bufs, const std::vector<Op>
       }
       case OP_DW: case OP_ATTN: {
         const int C = r[3];
-        ok = C > 0 && buf_ok(r[6], false) && buf_ok(r[13], false) &&
+        // attention: the (q, k, v) channels of every head after q_coff; the output slice is C wide
+        const int Cin = r[0] == OP_ATTN ? r[4] * (2 * r[5] + r[9]) : C;
+        ok = C > 0 && view_ok(r[6], r[7], Cin, false) && view_ok(r[13], r[14], C, false) &&
+             (r[0] == OP_DW || (r[4] > 0 && r[4] * r[9] == C)) &&
              w_ok(r[19], (size_t)9 * C * (ym_dt_q8(dtype) ? 1 : 4)) && w_ok(r[20], (size_t)C * 4);
         if (ok && ym_dt_q8(dtype)) ok = w_ok(r[22], qrec) && w_ok(r[23], (size_t)C * 4);
         break;
       }
-      case OP_SPPF: ok = r[3] > 0 && buf_ok(r[13], false); break;
-      case OP_REQ: ok = r[3] > 0 && buf_ok(r[6], false) && buf_ok(r[13], false) && w_ok(r[22], qrec); break;
+      case OP_SPPF: ok = r[3] > 0 && view_ok(r[13], r[7], 4 * r[3], false); break;  // y0 and the 3 pooled slices
+      case OP_REQ:
+        ok = r[3] > 0 && view_ok(r[6], r[7], r[3], false) && view_ok(r[13], r[14], r[3], false) && w_ok(r[22], qrec);
+        break;
       default: return fail(YM_EBLOB, "op %s: unknown op kind %d", o.name, r[0]);
     }
-    if (!ok) return fail(YM_EBLOB, "op %s: buffer id or weight range out of bounds", o.name);
+    if (!ok) return fail(YM_EBLOB, "op %s: buffer id, channel view or weight range out of bounds", o.name);
   }
   return YM_OK;
 }
@@ -679,7 +696,7 @@ int ym_load_weights(ym_ctx* c, const void* blob, size_t bytes) {
   const size_t woff = align_up(need, 256);
   if (wbytes > bytes || bytes < woff + wbytes) return fail(YM_EBLOB, "blob truncated (%zu < %zu)", bytes, woff + wbytes);
   const int dtype = h[2];
-  if (dtype != YM_DT_F16 && dtype != YM_DT_F32 && !ym_dt_q8(dtype)) return fail(YM_EBLOB, "unknown dtype %d", dtype);
+  if (dtype != YM_DT_F16 && !ym_dt_f32s(dtype) && !ym_dt_q8(dtype)) return fail(YM_EBLOB, "unknown dtype %d", dtype);
   const int task = h[3], nc = h[4], nm = h[5], reg_max = h[6], nl = h[7];
   if (nl < 1 || nl > 4) return fail(YM_EBLOB, "bad level count");
   if (nc < 1 || nc > 128 || nm < 0 || nm > 64 || reg_max < 1 || reg_max > 64)
@@ -708,7 +725,7 @@ int ym_load_weights(ym_ctx* c, const void* blob, size_t bytes) {
     memcpy(ops[i].name, names + (size_t)i * kNameLen, kNameLen);
     ops[i].name[kNameLen - 1] = 0;
   }
-  int rc = validate_plan(bufs, ops, dtype, wbytes);
+  int rc = validate_plan(bufs, ops, dtype, wbytes, input_buf);
   if (rc) return rc;
   // commit: a reload drops the previous plan's workspace, graphs and per-shape tile tables (they index its ops and
   // buffers); the weights are replaced below
@@ -746,14 +763,14 @@ int ym_load_weights(ym_ctx* c, const void* blob, size_t bytes) {
     const int N = o.r[4], Kpad = o.r[21];
     if (o.r[1] != 3 || o.r[3] != 8 || Kpad < 72) return fail(YM_EBLOB, "op %s: unexpected stem geometry", o.name);
     const char* w = static_cast<const char*>(blob) + woff + (size_t)(uint32_t)o.r[19];
-    const size_t esz = c->dtype == YM_DT_F32 ? 4 : (c->dtype == YM_DT_F16 ? 2 : 1);
+    const size_t esz = ym_dt_f32s(c->dtype) ? 4 : (c->dtype == YM_DT_F16 ? 2 : 1);
     if ((size_t)(uint32_t)o.r[19] + (size_t)N * Kpad * esz > wbytes) return fail(YM_EBLOB, "stem weights out of range");
     wstem.assign((size_t)27 * N, 0.f);
     for (int n = 0; n < N; ++n)
       for (int t = 0; t < 27; ++t) {
         const size_t i = (size_t)n * Kpad + (t / 3) * 8 + t % 3;
         float v;
-        if (c->dtype == YM_DT_F32) memcpy(&v, w + 4 * i, 4);
+        if (ym_dt_f32s(c->dtype)) memcpy(&v, w + 4 * i, 4);
         else if (c->dtype == YM_DT_F16) { _Float16 h16; memcpy(&h16, w + 2 * i, 2); v = (float)h16; }
         else if (c->dtype == YM_DT_F8) v = e4m3_value(reinterpret_cast<const uint8_t*>(w)[i]);
         else v = (float)reinterpret_cast<const int8_t*>(w)[i];

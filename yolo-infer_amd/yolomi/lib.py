@@ -23,7 +23,7 @@ class ModelDesc(C.Structure):
 
 
 TASK_CODES = {"detect": 1, "segment": 2}
-DTYPE_CODES = {"f16": 1, "f32": 2, "i8": 3, "f8": 4}
+DTYPE_CODES = {"f16": 1, "f32": 2, "i8": 3, "f8": 4, "x3": 5}
 
 
 class RcclId(C.Structure):

@@ -12,6 +12,9 @@ backend, K padded to 16-channel granules per tap, and per op a `QRec` (csrc/ym_c
 output, the 256-entry post-activation table, the stored tensor's / residual's / input's quantisation), the fp32
 s_in·s_w per output channel and the int32 zero-point correction Σ_k (128 - z_in)·w (activations are stored as q - 128).
 
+x3 plans (dtype "x3", the f16-tolerance plan): fp32 activations; every conv weight matrix except the stem's is packed
+as two fp16 planes, hi = fp16(w) then lo = fp16(w - hi), for the split-f16 MFMA GEMMs of csrc/ym_conv.hip.
+
 Blob layout (int32 little-endian; parsed by `csrc/ym_runtime.cpp:ym_load_weights`):
   header[32] | buffers[nbuf][8] | ops[nop][32] | names[nop][48 bytes] | pad to 256 | weights
 Conv op record: [1..5] k, s, Cin, N, act | [6..9] src0 buf, coff, C, up0 | [10..12] src1 | [13..16] dst buf, coff,
@@ -32,7 +35,7 @@ from .arch import REG_MAX, STRIDES, GraphBuilder
 MAGIC = 0x4C504D59
 VERSION = 1
 OP_IDS = {"input": 1, "conv": 2, "dwconv": 3, "sppf": 4, "attn": 5, "decode": 6, "nms": 7, "requant": 8}
-DTYPES = {"f16": 0, "f32": 1, "i8": 2, "f8": 3}
+DTYPES = {"f16": 0, "f32": 1, "i8": 2, "f8": 3, "x3": 4}
 QUANT_DTYPES = ("i8", "f8")  # one-byte PTQ plans: int8 affine (torch.ao qconfig) and fp8 e4m3 (yolomi/quant.py)
 BK = 64  # conv K is padded to the kernel K step (csrc/ym_conv.hip KSTEP)
 
@@ -192,7 +195,12 @@ def pack_graph(g: GraphBuilder, sd: Dict[str, np.ndarray], dtype: str = "f16", q
             r[10:13] = [src1.buf.id, src1.coff, C1] if src1 is not None else [-1, 0, 0]
             r[13:17] = [dst.buf.id, dst.coff, a["anchor_level"], int(bool(a["shuffle2x2"]))]
             r[17:19] = [res.buf.id, res.coff] if res is not None else [-1, 0]
-            r[19] = arena.add(wp if quant else wp.astype(np_dt))
+            if dtype == "x3" and not stem:  # split-f16 plan: fp16 hi plane [N][Kpad], then the fp16 rounding of the rest
+                hi = wp.astype(np.float16)
+                lo = (wp - hi.astype(np.float32)).astype(np.float16)
+                r[19] = arena.add(np.concatenate([hi.reshape(-1), lo.reshape(-1)]))
+            else:  # (the x3 stem runs the fp32 VALU stem kernel on fp32 weights)
+                r[19] = arena.add(wp if quant else wp.astype(np_dt))
             r[20] = arena.add(b.astype(np.float32))
             r[21] = Kpad
             pair = a.get("pair")
