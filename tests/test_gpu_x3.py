@@ -126,13 +126,16 @@ def test_x3_segment_s_b4():
             assert a >= 0.999, (i, j, a)
 
 
-FIRST_GEN = list(range(17))  # csrc/ym_conv.hip: 12 direct-to-register + 5 LDS-staged tile configurations
+# csrc/ym_conv.hip: 12 direct-to-register + 5 LDS-staged tile configurations, then the 30 LDS-DMA ones
+# (csrc/ym_conv_dma.hip, x3 pairing mode)
+X3_CFGS = list(range(17)) + list(range(17, 47))
 
 
-@pytest.mark.parametrize("cfg", FIRST_GEN)
+@pytest.mark.parametrize("cfg", X3_CFGS)
 def test_x3_conv_configs_match_oracle(cfg):
     """Every x3 conv kernel configuration on every conv of yolo11n (1x1 two-source / up-sampled, 3x3 s1/s2,
-    residual epilogues, fp32 Detect rows): layer outputs within 1e-4 of the oracle."""
+    residual epilogues, fp32 Detect rows; ops a configuration does not take fall back to the heuristic tile): layer
+    outputs within 1e-4 of the oracle."""
     eng = model("n").model.engine
     x = make_input("uniform", (11, 12), 640)
     _, y, ex = oracle().raw(x, keep=(2, 4, 6, 8, 9, 10, 13, 16, 19, 22))

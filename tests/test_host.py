@@ -92,32 +92,36 @@ def test_capi_exports_every_declared_symbol():
     assert lib.ym_num_conv_cfgs(5) == lib.ym_num_conv_cfgs(1) and lib.ym_num_conv_cfgs(6) < 0
 
 
-def test_x3_blob_splits_weights_into_hi_lo_planes():
-    """x3 plans: every conv but the stem packs fp16 hi = fp16(w) and lo = fp16(w - hi) planes of [N][Kpad]; hi + lo
-    restores the fp32 folded weight to ~2^-22 relative (fp16 subnormal lo parts included); the stem stays fp32."""
+def test_x3_blob_packs_pair_chunk_weights():
+    """x3 plans: every conv but the stem packs [N][Kpad] fp16 rows with each 8-channel K chunk as [hi x8 | lo x8],
+    hi = fp16(w), lo = fp16(w - hi) (Kpad = 2K padded to 128); hi + lo restores the fp32 folded weight to ~2^-22
+    relative (fp16 subnormal lo parts included); the stem stays fp32."""
     sd = synth_weights("n", "detect", 0)
     b32, bx3 = pack_model("n", "detect", sd, "f32"), pack_model("n", "detect", sd, "x3")
     h = struct.unpack("<32i", bx3[:128])
     assert h[2] == 4
     nb, nop = h[11], h[12]
-    base32 = lambda b: (128 + 32 * nb + 176 * nop + 255) // 256 * 256  # noqa: E731
+    base = (128 + 32 * nb + 176 * nop + 255) // 256 * 256
     rec = lambda b, i: struct.unpack("<32i", b[128 + 32 * nb + 128 * i: 128 + 32 * nb + 128 * (i + 1)])  # noqa: E731
     worst, nconv = 0.0, 0
     for i in range(nop):
         r32, rx = rec(b32, i), rec(bx3, i)
         if r32[0] != 2:
             continue
-        N, Kpad = r32[4], r32[21]
-        w = np.frombuffer(b32, np.float32, N * Kpad, base32(b32) + r32[19])
+        N, Kpad, K = r32[4], r32[21], r32[1] ** 2 * r32[3]
+        w = np.frombuffer(b32, np.float32, N * Kpad, base + r32[19]).reshape(N, Kpad)[:, :K]
         if r32[6] == h[15]:  # the stem: fp32 weights, identical
-            assert np.array_equal(np.frombuffer(bx3, np.float32, N * Kpad, base32(bx3) + rx[19]), w)
+            assert rx[21] == Kpad and np.array_equal(np.frombuffer(bx3, np.float32, N * Kpad, base + rx[19]),
+                                                     np.frombuffer(b32, np.float32, N * Kpad, base + r32[19]))
             continue
-        hl = np.frombuffer(bx3, np.float16, 2 * N * Kpad, base32(bx3) + rx[19]).astype(np.float64)
-        rebuilt = hl[:N * Kpad] + hl[N * Kpad:]
+        assert rx[21] % 128 == 0 and rx[21] >= 2 * K
+        hl = np.frombuffer(bx3, np.float16, N * rx[21], base + rx[19]).reshape(N, rx[21])
+        assert not hl[:, 2 * K:].any()
+        pairs = hl[:, :2 * K].reshape(N, K // 8, 2, 8).astype(np.float64)
+        rebuilt = (pairs[:, :, 0] + pairs[:, :, 1]).reshape(N, K)
         worst = max(worst, float(np.abs(rebuilt - w).max() / np.abs(w).max()))
         nconv += 1
     assert nconv > 70 and worst < 2 ** -21
-
 
 def test_facade_contract_without_gpu():
     from core.model import YOLO11Model

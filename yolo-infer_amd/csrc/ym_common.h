@@ -44,12 +44,14 @@ __device__ __forceinline__ HL ym_split8(const f32x8& v) {
 template <typename T> struct Vec8;
 template <> struct Vec8<f16> {
   typedef f16x8 type;
+  typedef f16 elem;  // element type of `type`
   static __device__ __forceinline__ type load(const f16* p) { return *reinterpret_cast<const f16x8*>(p); }
   static __device__ __forceinline__ void store(f16* p, type v) { *reinterpret_cast<f16x8*>(p) = v; }
   static __device__ __forceinline__ type zero() { return type{0, 0, 0, 0, 0, 0, 0, 0}; }
 };
 template <> struct Vec8<float> {
   typedef f32x8 type;
+  typedef float elem;
   static __device__ __forceinline__ type load(const float* p) {
     f32x4 a = *reinterpret_cast<const f32x4*>(p);
     f32x4 b = *reinterpret_cast<const f32x4*>(p + 4);
@@ -64,10 +66,78 @@ template <> struct Vec8<float> {
 
 template <> struct Vec8<i8> {  // int8 plans (8 bytes)
   typedef i8 type __attribute__((ext_vector_type(8)));
+  typedef i8 elem;
   static __device__ __forceinline__ type load(const i8* p) { return *reinterpret_cast<const type*>(p); }
   static __device__ __forceinline__ void store(i8* p, type v) { *reinterpret_cast<type*>(p) = v; }
   static __device__ __forceinline__ type zero() { return type{0, 0, 0, 0, 0, 0, 0, 0}; }
 };
+
+// x3 activation storage ("pair" layout): every chunk of 8 logical channels is 32 bytes, [fp16 hi x8 | fp16 lo x8], the
+// split made once by the producer's epilogue.  A P2 is one logical element (4 bytes), so NHWC pointer arithmetic in
+// P2 units (pixel * ctot + coff + c) lands on chunk starts for c % 8 == 0 exactly as with f16 / fp32 storage; every
+// buffer is 256-byte aligned and its channel counts are multiples of 8, so chunks are 32-byte aligned.  Seen as fp16,
+// a pair buffer is an NHWC tensor of 2C channels whose chunk 2j is the hi part of logical chunk j and 2j + 1 its lo
+// part: the LDS-DMA / streaming GEMM loaders fetch it unchanged, with doubled channel counts.
+struct P2 {
+  unsigned bits;
+};
+template <> struct Vec8<P2> {
+  typedef f32x8 type;  // hi + lo (one fp32 rounding: exact for every split value pair the epilogues store)
+  typedef float elem;
+  static __device__ __forceinline__ type load(const P2* p) {
+    const f16x8 h = *reinterpret_cast<const f16x8*>(p), lo = *(reinterpret_cast<const f16x8*>(p) + 1);
+    type v;
+#pragma unroll
+    for (int e = 0; e < 8; ++e) v[e] = (float)h[e] + (float)lo[e];
+    return v;
+  }
+  static __device__ __forceinline__ void store(P2* p, type v) {
+    const HL x = ym_split8(v);
+    *reinterpret_cast<f16x8*>(p) = x.hi;
+    *(reinterpret_cast<f16x8*>(p) + 1) = x.lo;
+  }
+  static __device__ __forceinline__ type zero() { return type{0, 0, 0, 0, 0, 0, 0, 0}; }
+};
+__device__ __forceinline__ HL ym_load_hl(const P2* p) {
+  return HL{*reinterpret_cast<const f16x8*>(p), *(reinterpret_cast<const f16x8*>(p) + 1)};
+}
+// 4 consecutive logical channels (c % 4 == 0) at P2 address p: their hi halves sit at byte 2 (c % 8) of the chunk,
+// the lo halves 16 bytes further
+__device__ __forceinline__ f16* ym_p2_hi4(P2* p) {
+  const uintptr_t u = reinterpret_cast<uintptr_t>(p);
+  return reinterpret_cast<f16*>((u & ~(uintptr_t)31) + ((u & 31) >> 1));
+}
+__device__ __forceinline__ const f16* ym_p2_hi4(const P2* p) { return ym_p2_hi4(const_cast<P2*>(p)); }
+__device__ __forceinline__ void ym_p2_store4(P2* p, const float* v) {
+  f16x4 h, l;
+#pragma unroll
+  for (int e = 0; e < 4; ++e) {
+    h[e] = (f16)v[e];
+    l[e] = (f16)(v[e] - (float)h[e]);
+  }
+  f16* q = ym_p2_hi4(p);
+  *reinterpret_cast<f16x4*>(q) = h;
+  *reinterpret_cast<f16x4*>(q + 8) = l;
+}
+__device__ __forceinline__ void ym_p2_load4(const P2* p, float* v) {  // v[e] = hi + lo
+  const f16* q = ym_p2_hi4(p);
+  const f16x4 h = *reinterpret_cast<const f16x4*>(q), l = *reinterpret_cast<const f16x4*>(q + 8);
+#pragma unroll
+  for (int e = 0; e < 4; ++e) v[e] = (float)h[e] + (float)l[e];
+}
+// one logical element (scalar paths)
+__device__ __forceinline__ float ym_p2_get(const P2* p) {
+  const uintptr_t u = reinterpret_cast<uintptr_t>(p);
+  const f16* q = reinterpret_cast<const f16*>((u & ~(uintptr_t)31) + ((u & 31) >> 1));
+  return (float)q[0] + (float)q[8];
+}
+__device__ __forceinline__ void ym_p2_set(P2* p, float v) {
+  const uintptr_t u = reinterpret_cast<uintptr_t>(p);
+  f16* q = reinterpret_cast<f16*>((u & ~(uintptr_t)31) + ((u & 31) >> 1));
+  const f16 h = (f16)v;
+  q[0] = h;
+  q[8] = (f16)(v - (float)h);
+}
 
 // order-preserving float <-> int map (atomicMax on floats of either sign)
 __device__ __forceinline__ int f2ord(float f) {
@@ -174,6 +244,10 @@ struct ConvArgs {
   // successor kernel size: 1 = the 1x1 above (streaming FUSE); 3 = a YOLO11 Bottleneck's second 3x3 conv, dst/res the
   // Bottleneck output / shortcut (csrc/ym_conv_bneck.hip); w2 then [N2][Kpad2] with K = (ky, kx, mid channel)
   int k2;
+  // x3 plans: activations in the pair layout (P2), weights [N][Kpad] fp16 with every 8-channel K chunk as [hi x8 |
+  // lo x8]; Cin8 / Kc / Kpad then count fp16 storage chunks (twice the logical ones), ctot / coff / C0 / C1 / d_* / r_*
+  // stay logical channels, s0_elems / s1_elems count fp16 elements
+  int x3;
 };
 
 struct DwArgs {

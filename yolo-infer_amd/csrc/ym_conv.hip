@@ -39,19 +39,21 @@ struct x3_t {};
 template <typename M> struct Mode;
 template <> struct Mode<f16> { typedef f16 act; typedef f16 wt; typedef f16x8 frag; };
 template <> struct Mode<float> { typedef float act; typedef float wt; typedef f32x8 frag; };
-template <> struct Mode<x3_t> { typedef float act; typedef f16 wt; typedef HL frag; };
+template <> struct Mode<x3_t> { typedef P2 act; typedef f16 wt; typedef HL frag; };
+// fp16 weight elements per logical 8-channel K chunk (x3: the [hi x8 | lo x8] pair)
+template <typename M> constexpr int kWChunk = std::is_same<M, x3_t>::value ? 16 : 8;
 
-// one lane's 8 consecutive K values of the weight operand (x3: the hi plane, and the lo plane `lo` elements later)
+// one lane's 8 consecutive K values of the weight operand (p: the chunk's first element)
 template <typename M>
-__device__ __forceinline__ typename Mode<M>::frag wload(const typename Mode<M>::wt* p, size_t lo) {
-  if constexpr (std::is_same<M, x3_t>::value) return HL{Vec8<f16>::load(p), Vec8<f16>::load(p + lo)};
+__device__ __forceinline__ typename Mode<M>::frag wload(const typename Mode<M>::wt* p) {
+  if constexpr (std::is_same<M, x3_t>::value) return HL{Vec8<f16>::load(p), Vec8<f16>::load(p + 8)};
   else return Vec8<typename Mode<M>::wt>::load(p);
 }
-// an activation chunk as an MFMA operand fragment
+// one lane's 8 consecutive K values of the activation operand (p: a logical chunk start)
 template <typename M>
-__device__ __forceinline__ typename Mode<M>::frag xfrag(const typename Vec8<typename Mode<M>::act>::type& v) {
-  if constexpr (std::is_same<M, x3_t>::value) return ym_split8(v);
-  else return v;
+__device__ __forceinline__ typename Mode<M>::frag xload(const typename Mode<M>::act* p) {
+  if constexpr (std::is_same<M, x3_t>::value) return ym_load_hl(p);
+  else return Vec8<typename Mode<M>::act>::load(p);
 }
 template <typename M>
 __device__ __forceinline__ typename Mode<M>::frag xzero() {
@@ -83,6 +85,9 @@ __device__ __forceinline__ void mma<x3_t>(const HL& a, const HL& b, f32x16& acc)
 }
 
 template <typename OutT> struct Out4;
+template <> struct Out4<P2> {
+  static __device__ __forceinline__ void store(P2* p, const float* v) { ym_p2_store4(p, v); }
+};
 template <> struct Out4<f16> {
   static __device__ __forceinline__ void store(f16* p, const float* v) {
     *reinterpret_cast<f16x4*>(p) = f16x4{(f16)v[0], (f16)v[1], (f16)v[2], (f16)v[3]};
@@ -96,7 +101,11 @@ template <> struct Out4<float> {
 
 template <typename T>
 __device__ __forceinline__ void load_res4(const T* p, float* v) {
-  if constexpr (sizeof(T) == 2) {
+  if constexpr (std::is_same<T, P2>::value) {
+    float r[4];
+    ym_p2_load4(p, r);
+    v[0] += r[0]; v[1] += r[1]; v[2] += r[2]; v[3] += r[3];
+  } else if constexpr (sizeof(T) == 2) {
     const f16x4 r = *reinterpret_cast<const f16x4*>(p);
     v[0] += (float)r[0]; v[1] += (float)r[1]; v[2] += (float)r[2]; v[3] += (float)r[3];
   } else {
@@ -176,7 +185,9 @@ __global__ __launch_bounds__(WM * WN * WK * 64) void conv_igemm(const ConvArgs a
     }
   }
   const WT* wrow[WTN];
-  const size_t wlo = (size_t)a.N * a.Kpad;  // x3: the lo weight plane follows the hi plane
+  // x3: Cin8 / Kc / Kpad count fp16 storage chunks; this kernel walks logical chunks (a [hi | lo] pair each)
+  constexpr int XS = std::is_same<M, x3_t>::value ? 2 : 1;
+  const int Cin8 = a.Cin8 / XS, Kc = a.Kc / XS;
 #pragma unroll
   for (int j = 0; j < WTN; ++j) {
     const int n = nbase + j * 32 + l32;
@@ -185,23 +196,23 @@ __global__ __launch_bounds__(WM * WN * WK * 64) void conv_igemm(const ConvArgs a
 
   // ---- K walk. Step g (this wave: g = wk, wk+WK, ...) covers chunks [g*2KS, (g+1)*2KS); lane half h loads
   // chunks g*2KS + 2s + h, s < KS (chunk = 8 consecutive K = 8 channels of one tap).
-  const int nsteps = a.Kpad / (16 * KS);
+  const int nsteps = a.Kpad / XS / (16 * KS);
   int g = wk;
   int tap0 = 0, cb0 = 0;  // KIND 3: tap / channel-block of chunk g*2KS + h
   if constexpr (KIND != 1) {
     const int c = g * 2 * KS + h;
-    tap0 = c / a.Cin8;
-    cb0 = c - tap0 * a.Cin8;
+    tap0 = c / Cin8;
+    cb0 = c - tap0 * Cin8;
   }
 
   bool div255 = false;
   if constexpr (KIND == 0) div255 = ym_input_max(a.ctl) > 1.0f + a.eps;
   auto gather = [&](int i, int s) -> F {
     const int chunk = g * 2 * KS + 2 * s + h;
-    if (!pv[i] || chunk >= a.Kc) return xzero<M>();
+    if (!pv[i] || chunk >= Kc) return xzero<M>();
     if constexpr (KIND == 1) {
       const int c = chunk * 8;
-      return xfrag<M>(Vec8<T>::load((c < a.C0 ? row0[i] : row1[i]) + c));
+      return xload<M>((c < a.C0 ? row0[i] : row1[i]) + c);
     } else if constexpr (KIND == 0) {  // Cin8 == 1: chunk = tap; channels 3..7 are zero padding
       const int ky = chunk / 3, kx = chunk - (chunk / 3) * 3;
       const int iy = iy0[i] + ky, ix = ix0[i] + kx;
@@ -215,18 +226,18 @@ __global__ __launch_bounds__(WM * WN * WK * 64) void conv_igemm(const ConvArgs a
       return v;
     } else {
       int cb = cb0 + 2 * s, t = tap0;
-      while (cb >= a.Cin8) { cb -= a.Cin8; ++t; }
+      while (cb >= Cin8) { cb -= Cin8; ++t; }
       const int ky = t / 3, kx = t - (t / 3) * 3;
       const int iy = iy0[i] + ky, ix = ix0[i] + kx;
       if ((unsigned)iy >= (unsigned)a.Hin || (unsigned)ix >= (unsigned)a.Win) return xzero<M>();
-      return xfrag<M>(Vec8<T>::load(row0[i] + (size_t)(iy * a.Win + ix) * a.s0_ctot + cb * 8));
+      return xload<M>(row0[i] + (size_t)(iy * a.Win + ix) * a.s0_ctot + cb * 8);
     }
   };
   auto advance = [&]() {
     g += WK;
     if constexpr (KIND != 1) {
       cb0 += 2 * KS * WK;
-      while (cb0 >= a.Cin8) { cb0 -= a.Cin8; ++tap0; }
+      while (cb0 >= Cin8) { cb0 -= Cin8; ++tap0; }
     }
   };
 
@@ -243,7 +254,7 @@ __global__ __launch_bounds__(WM * WN * WK * 64) void conv_igemm(const ConvArgs a
 #pragma unroll
     for (int s = 0; s < KS; ++s) {
 #pragma unroll
-      for (int j = 0; j < WTN; ++j) fa[s][j] = wload<M>(wrow[j] + (size_t)(g * 2 * KS + 2 * s + h) * 8, wlo);
+      for (int j = 0; j < WTN; ++j) fa[s][j] = wload<M>(wrow[j] + (size_t)(g * 2 * KS + 2 * s + h) * kWChunk<M>);
 #pragma unroll
       for (int i = 0; i < WTM; ++i) fb[s][i] = gather(i, s);
     }
@@ -396,8 +407,8 @@ hipError_t launch_cfg(ConvArgs a, int kind, hipStream_t st) {
 // coalesced 16-byte row loads (8 lanes cover a 128-byte row), stored XOR-swizzled (chunk c of row r at c ^ ((r >> 1) & 7): conflict-free for ds_read_b128's non-contiguous lane groups)
 // so the MFMA fragment reads (ds_read_b128, 32 rows at one K offset) do not pile onto one bank group; the next
 // stage's global loads are in flight while the current stage's MFMAs run; one barrier per stage.
-// x3 plans (M = x3_t): activations arrive as fp32 and are split into fp16 hi/lo planes when they are staged, the
-// weights are staged from their hi/lo planes; the fragment reads then feed the three MFMAs of mma<x3_t>.
+// x3 plans (M = x3_t): the [hi | lo] chunk pairs of activations and weights are staged as separate fp16 hi / lo
+// planes; the fragment reads then feed the three MFMAs of mma<x3_t>.
 template <typename M, typename OutT, int BM, int BN, int KIND>
 __global__ __launch_bounds__(256) void conv_lds(const ConvArgs a) {
   typedef typename Mode<M>::act T;
@@ -448,7 +459,8 @@ __global__ __launch_bounds__(256) void conv_lds(const ConvArgs a) {
     }
   }
   const WT* wrow[RA];
-  const size_t wlo = (size_t)a.N * a.Kpad;
+  constexpr int XS = X3 ? 2 : 1;  // x3: Cin8 / Kc / Kpad count fp16 storage chunks, a logical chunk is a pair
+  const int Cin8 = a.Cin8 / XS, Kc = a.Kc / XS;
 #pragma unroll
   for (int i = 0; i < RA; ++i) {
     const int n = tn * BN + (tid >> 3) + 32 * i;
@@ -456,35 +468,35 @@ __global__ __launch_bounds__(256) void conv_lds(const ConvArgs a) {
   }
   int tap = 0, cb = kc;  // KIND 3: tap / channel block of chunk kt*8 + kc
   if constexpr (KIND == 3) {
-    tap = kc / a.Cin8;
-    cb = kc - tap * a.Cin8;
+    tap = kc / Cin8;
+    cb = kc - tap * Cin8;
   }
-  V ra[RB];
+  WF ra[RB];
   WF rw[RA];
   int kt = 0;
   auto load = [&]() {
     const int chunk = kt * 8 + kc;
 #pragma unroll
-    for (int i = 0; i < RA; ++i) rw[i] = wload<M>(wrow[i] + (size_t)chunk * 8, wlo);
+    for (int i = 0; i < RA; ++i) rw[i] = wload<M>(wrow[i] + (size_t)chunk * kWChunk<M>);
 #pragma unroll
     for (int i = 0; i < RB; ++i) {
-      V v = Vec8<T>::zero();
-      if (pok[i] && chunk < a.Kc) {
+      WF v = xzero<M>();
+      if (pok[i] && chunk < Kc) {
         if constexpr (KIND == 1) {
           const int c = chunk * 8;
-          v = Vec8<T>::load((c < a.C0 ? prow0[i] : prow1[i]) + c);
+          v = xload<M>((c < a.C0 ? prow0[i] : prow1[i]) + c);
         } else {
           const int ky = tap / 3, kx = tap - (tap / 3) * 3;
           const int iy = piy[i] + ky, ix = pix0[i] + kx;
           if ((unsigned)iy < (unsigned)a.Hin && (unsigned)ix < (unsigned)a.Win)
-            v = Vec8<T>::load(prow0[i] + (size_t)(iy * a.Win + ix) * a.s0_ctot + cb * 8);
+            v = xload<M>(prow0[i] + (size_t)(iy * a.Win + ix) * a.s0_ctot + cb * 8);
         }
       }
       ra[i] = v;
     }
     if constexpr (KIND == 3) {  // advance this thread's chunk by one stage (8 chunks)
       cb += 8;
-      while (cb >= a.Cin8) { cb -= a.Cin8; ++tap; }
+      while (cb >= Cin8) { cb -= Cin8; ++tap; }
     }
   };
   auto store = [&](int buf) {
@@ -504,9 +516,8 @@ __global__ __launch_bounds__(256) void conv_lds(const ConvArgs a) {
       const int r = (tid >> 3) + 32 * i;
       const int o = r * BK + ((kc ^ ((r >> 1) & 7)) * 8);
       if constexpr (X3) {
-        const HL x = ym_split8(ra[i]);
-        *reinterpret_cast<f16x8*>(&sB[buf][0][o]) = x.hi;
-        *reinterpret_cast<f16x8*>(&sB[buf][1][o]) = x.lo;
+        *reinterpret_cast<f16x8*>(&sB[buf][0][o]) = ra[i].hi;
+        *reinterpret_cast<f16x8*>(&sB[buf][1][o]) = ra[i].lo;
       } else {
         *reinterpret_cast<f16x8*>(&sB[buf][0][o]) = ra[i];
       }
@@ -519,7 +530,7 @@ __global__ __launch_bounds__(256) void conv_lds(const ConvArgs a) {
     for (int j = 0; j < TN; ++j)
 #pragma unroll
       for (int r = 0; r < 16; ++r) acc[i][j][r] = 0.f;
-  const int nk = a.Kpad / BK;
+  const int nk = a.Kpad / XS / BK;
   load();
   store(0);
   __syncthreads();
@@ -743,7 +754,7 @@ hipError_t ym_launch_conv(int dtype, int out_f32, const ConvArgs& a, int cfg, hi
     // candidate (strict); a pinned table falls back to the heuristic
     const int ndma = ym_conv_dma_num_cfgs(), nstr = ym_conv_stream_num_cfgs();
     hipError_t e = hipErrorInvalidValue;
-    if (dtype == YM_DT_F16) {
+    if (dtype == YM_DT_F16 || (dtype == YM_DT_X3 && cfg - kNumAllCfg < ndma)) {  // x3: the LDS-DMA kernels
       const int i = cfg - kNumAllCfg;
       e = i < ndma ? ym_launch_conv_dma(out_f32, a, i, st)
                    : (i < ndma + nstr ? ym_launch_conv_stream(out_f32, a, i - ndma, st)
@@ -755,6 +766,6 @@ hipError_t ym_launch_conv(int dtype, int out_f32, const ConvArgs& a, int cfg, hi
   int id = (cfg >= 0 && cfg < kNumAllCfg) ? cfg : choose_cfg(a);
   if (id >= kNumCfg && dtype == YM_DT_F32) id = choose_cfg(a);  // LDS variants: f16 and x3 plans
   if (dtype == YM_DT_F16) return out_f32 ? launch_id<f16, float>(id, a, kind, st) : launch_id<f16, f16>(id, a, kind, st);
-  if (dtype == YM_DT_X3) return launch_id<x3_t, float>(id, a, kind, st);
+  if (dtype == YM_DT_X3) return out_f32 ? launch_id<x3_t, float>(id, a, kind, st) : launch_id<x3_t, P2>(id, a, kind, st);
   return launch_id<float, float>(id, a, kind, st);
 }

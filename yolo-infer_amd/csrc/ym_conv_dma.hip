@@ -19,6 +19,8 @@
 //    workgroup, and no L1 invalidate.
 // Epilogue as in ym_conv.hip: + folded-BN bias, SiLU, + residual, channel-slice store (zero-copy concat), fp32
 // anchor-major Detect rows, 2x2 pixel shuffle (Proto ConvTranspose2d).
+#include <type_traits>
+
 #include "ym_common.h"
 
 typedef float f32x16 __attribute__((ext_vector_type(16)));
@@ -65,6 +67,9 @@ template <> struct Store4<float> {
     *reinterpret_cast<f32x4*>(p) = f32x4{v[0], v[1], v[2], v[3]};
   }
 };
+template <> struct Store4<P2> {
+  static __device__ __forceinline__ void st(P2* p, const float* v) { ym_p2_store4(p, v); }
+};
 
 // A workgroup = KG groups of 2x2 waves (256·KG threads).  Every wave group covers the whole BM x BN tile — a wave
 // owns (BM/2) pixels x (BN/2) channels = TM x TN blocks of 32x32 — and takes 4/KG of each stage's four 16-deep k
@@ -80,7 +85,13 @@ template <> struct Store4<float> {
 // SUB: 64-deep K sub-stages per stage (one barrier, one LDS-read latency and one wait per SUB x 64 of K): the small-M
 // layers' K loops are chains of per-stage fixed costs, which SUB 2 halves; launched only where every split's K range
 // is whole stages (no partial stage: every stage issues exactly NL DMA instructions, tools/check_dma_asm.py)
-template <typename OutT, int BM, int BN, int KIND, int SPLIT, int KG, int NSTAGE, int SUB>
+// X3 (x3 plans): activations in the pair layout and weights in pair-chunk rows, both fetched by the same DMA as fp16
+// tensors of twice the channels (storage chunk 2j = hi of logical chunk j, 2j + 1 = its lo), so a 16-deep k sub-step
+// s holds hi_s (lane half 0) and lo_s (lane half 1) of one logical chunk.  Per two sub-steps (s, s+1) three MFMAs
+// form the split product hi·hi + hi·lo + lo·hi of both chunks: A = [w_hi_s | w_hi_s] with the natural B (w_hi·x_hi +
+// w_hi·x_lo), the same for s+1, and A = [w_lo_s | w_lo_s+1] with B = [x_hi_s | x_hi_s+1] (w_lo·x_hi of both) — only
+// the chunk each lane half reads from LDS changes, the swizzle stays conflict-free.
+template <typename OutT, int BM, int BN, int KIND, int SPLIT, int KG, int NSTAGE, int SUB, bool X3 = false>
 __global__ __launch_bounds__(256 * KG) void conv_dma(const ConvArgs a) {
   constexpr int NW = 4 * KG;
   constexpr int TM = BM / 64, TN = BN / 64;
@@ -115,8 +126,13 @@ __global__ __launch_bounds__(256 * KG) void conv_dma(const ConvArgs a) {
   int ep_m[TM];
   size_t ep_obase[TM];
   f32x4 bias4[TN][4];
-  f16x4 res4[TM][TN][4];
+  typedef typename std::conditional<X3, f32x4, f16x4>::type RV;  // residual (x3: hi + lo)
+  RV res4[TM][TN][4];
   const f16* res = static_cast<const f16*>(a.res);
+  const P2* resp = static_cast<const P2*>(a.res);
+  constexpr int XS = X3 ? 2 : 1;  // fp16 storage elements per logical channel
+  const int s0_ctot = XS * a.s0_ctot, s0_coff = XS * a.s0_coff, s1_ctot = XS * a.s1_ctot, s1_coff = XS * a.s1_coff;
+  const int C0s = XS * a.C0;
   if (kg == 0) {
 #pragma unroll
     for (int j = 0; j < TN; ++j)
@@ -140,8 +156,14 @@ __global__ __launch_bounds__(256 * KG) void conv_dma(const ConvArgs a) {
 #pragma unroll
         for (int q = 0; q < 4; ++q) {
           const int n = tn * BN + wn * (BN / 2) + 32 * j + 8 * q + 4 * h;
-          res4[i][j][q] = (res && m < a.M && n < a.N) ? *reinterpret_cast<const f16x4*>(res + rbase + n)
-                                                       : f16x4{0, 0, 0, 0};
+          if constexpr (X3) {
+            float rv[4] = {0.f, 0.f, 0.f, 0.f};
+            if (res && m < a.M && n < a.N) ym_p2_load4(resp + rbase + n, rv);
+            res4[i][j][q] = f32x4{rv[0], rv[1], rv[2], rv[3]};
+          } else {
+            res4[i][j][q] = (res && m < a.M && n < a.N) ? *reinterpret_cast<const f16x4*>(res + rbase + n)
+                                                         : f16x4{0, 0, 0, 0};
+          }
         }
     }
   }
@@ -173,10 +195,10 @@ __global__ __launch_bounds__(256 * KG) void conv_dma(const ConvArgs a) {
     tmask[gi] = 0;
     if constexpr (KIND == 1) {
       const int sy = a.up0 ? (oy >> 1) : oy, sx = a.up0 ? (ox >> 1) : ox;
-      pbase0[gi] = ok ? (b * a.s0_P + sy * a.s0_W + sx) * a.s0_ctot + a.s0_coff : -1;
+      pbase0[gi] = ok ? (b * a.s0_P + sy * a.s0_W + sx) * s0_ctot + s0_coff : -1;
       // (row bases stay >= 0 for valid rows: -1 marks an M-tail row, so the -C0 of the second source's channel
       // index is applied per stage, not folded in here)
-      pbase1[gi] = ok && a.src1 ? (b * a.s1_P + oy * a.Win + ox) * a.s1_ctot + a.s1_coff : -1;
+      pbase1[gi] = ok && a.src1 ? (b * a.s1_P + oy * a.Win + ox) * s1_ctot + s1_coff : -1;
       piy[gi] = pix[gi] = 0;
     } else if constexpr (KIND == 3) {
       pbase0[gi] = ok ? b * a.s0_P : -1;  // image pixel base
@@ -187,7 +209,7 @@ __global__ __launch_bounds__(256 * KG) void conv_dma(const ConvArgs a) {
       const int iy0 = oy * a.s - 1, ix0 = ox * a.s - 1;
       // element offset of this lane's chunk at the window's top-left pixel (may be negative: only in-image taps
       // are ever added to it)
-      pbase0[gi] = (b * a.s0_P + iy0 * a.Win + ix0) * a.s0_ctot + a.s0_coff + c * 8;
+      pbase0[gi] = (b * a.s0_P + iy0 * a.Win + ix0) * s0_ctot + s0_coff + c * 8;
       pbase1[gi] = 0;
       piy[gi] = pix[gi] = 0;
       unsigned mk = 0;
@@ -228,11 +250,11 @@ __global__ __launch_bounds__(256 * KG) void conv_dma(const ConvArgs a) {
     const int chunk = kcur * 8 + c;
     // B: pixels
     if constexpr (KIND == 1) {
-      const bool second = a.src1 && kcur * DK >= a.C0;  // wave-uniform (C0 % 64 == 0 when src1 is used)
+      const bool second = a.src1 && kcur * DK >= C0s;  // wave-uniform (C0 % 64 == 0 when src1 is used)
 #pragma unroll
       for (int gi = 0; gi < GB; ++gi) {
         const int pb = second ? pbase1[gi] : pbase0[gi];
-        const unsigned off = pb >= 0 ? (unsigned)(pb + chunk * 8 - (second ? a.C0 : 0)) * 2u : OOB;
+        const unsigned off = pb >= 0 ? (unsigned)(pb + chunk * 8 - (second ? C0s : 0)) * 2u : OOB;
         dma16(second ? rs1 : rs0, sbase + (wid + NW * gi) * 1024, off);
       }
     } else if constexpr (KIND == 3) {
@@ -242,13 +264,13 @@ __global__ __launch_bounds__(256 * KG) void conv_dma(const ConvArgs a) {
         const int iy = piy[gi] + ty, ix = pix[gi] + tx;
         const bool ok = pbase0[gi] >= 0 && (unsigned)iy < (unsigned)a.Hin && (unsigned)ix < (unsigned)a.Win;
         const unsigned off =
-            ok ? (unsigned)((pbase0[gi] + iy * a.Win + ix) * a.s0_ctot + a.s0_coff + cb * 8) * 2u : OOB;
+            ok ? (unsigned)((pbase0[gi] + iy * a.Win + ix) * s0_ctot + s0_coff + cb * 8) * 2u : OOB;
         dma16(rs0, sbase + (wid + NW * gi) * 1024, off);
       }
       cb += 8;
       while (cb >= a.Cin8) { cb -= a.Cin8; ++tap; }
     } else {
-      const int S = (ky * a.Win + kx) * a.s0_ctot + cb * 8;  // uniform
+      const int S = (ky * a.Win + kx) * s0_ctot + cb * 8;  // uniform
 #pragma unroll
       for (int gi = 0; gi < GB; ++gi) {
         const unsigned off = (tmask[gi] >> tap) & 1u ? (unsigned)(pbase0[gi] + S) * 2u : OOB;
@@ -287,33 +309,72 @@ __global__ __launch_bounds__(256 * KG) void conv_dma(const ConvArgs a) {
   const int key = (l32 >> 1) & 7;
   // this wave's k sub-steps of the stage: fragment reads first, then the MFMAs (one LDS latency per stage)
   auto compute = [&](int slot) {
-    f16x8 fb[SUB][SPW][TM], fa[SUB][SPW][TN];
+    if constexpr (X3) {
+      static_assert(SPW % 2 == 0, "x3: a wave's k sub-steps come in pairs");
+      // per sub-step pair (s, s+1): A'_s = w_hi_s on both lane halves, B_s natural; the same for s+1; A'' =
+      // [w_lo_s | w_lo_s+1], B'' = [x_hi_s | x_hi_s+1]
+      f16x8 fb[SUB][SPW / 2][3][TM], fa[SUB][SPW / 2][3][TN];
 #pragma unroll
-    for (int su = 0; su < SUB; ++su) {
-      const char* sb = smem + slot * SB + su * SBS;
-      const char* sa = sb + BM * 128;
+      for (int su = 0; su < SUB; ++su) {
+        const char* sb = smem + slot * SB + su * SBS;
+        const char* sa = sb + BM * 128;
 #pragma unroll
-      for (int u = 0; u < SPW; ++u) {
-        const int s = kg * SPW + u;
-        const int off = ((((2 * s + h) ^ key)) << 4) + l32 * 128;
+        for (int u = 0; u < SPW / 2; ++u) {
+          const int s = kg * SPW + 2 * u;
+          const int ca[3] = {2 * s, 2 * s + 2, 2 * (s + h) + 1}, cbx[3] = {2 * s + h, 2 * s + 2 + h, 2 * (s + h)};
 #pragma unroll
-        for (int i = 0; i < TM; ++i)
-          fb[su][u][i] = *reinterpret_cast<const f16x8*>(sb + (wm * (BM / 2) + 32 * i) * 128 + off);
+          for (int v = 0; v < 3; ++v) {
+            const int offa = ((ca[v] ^ key) << 4) + l32 * 128, offb = ((cbx[v] ^ key) << 4) + l32 * 128;
 #pragma unroll
-        for (int j = 0; j < TN; ++j)
-          fa[su][u][j] = *reinterpret_cast<const f16x8*>(sa + (wn * (BN / 2) + 32 * j) * 128 + off);
+            for (int i = 0; i < TM; ++i)
+              fb[su][u][v][i] = *reinterpret_cast<const f16x8*>(sb + (wm * (BM / 2) + 32 * i) * 128 + offb);
+#pragma unroll
+            for (int j = 0; j < TN; ++j)
+              fa[su][u][v][j] = *reinterpret_cast<const f16x8*>(sa + (wn * (BN / 2) + 32 * j) * 128 + offa);
+          }
+        }
       }
-    }
 #pragma unroll
-    for (int su = 0; su < SUB; ++su)
+      for (int su = 0; su < SUB; ++su)
 #pragma unroll
-      for (int u = 0; u < SPW; ++u)
+        for (int u = 0; u < SPW / 2; ++u)
 #pragma unroll
-        for (int i = 0; i < TM; ++i)
+          for (int v = 0; v < 3; ++v)
+#pragma unroll
+            for (int i = 0; i < TM; ++i)
+#pragma unroll
+              for (int j = 0; j < TN; ++j)
+                acc[v % NACC][i][j] = __builtin_amdgcn_mfma_f32_32x32x16_f16(fa[su][u][v][j], fb[su][u][v][i],
+                                                                             acc[v % NACC][i][j], 0, 0, 0);
+    } else {
+      f16x8 fb[SUB][SPW][TM], fa[SUB][SPW][TN];
+#pragma unroll
+      for (int su = 0; su < SUB; ++su) {
+        const char* sb = smem + slot * SB + su * SBS;
+        const char* sa = sb + BM * 128;
+#pragma unroll
+        for (int u = 0; u < SPW; ++u) {
+          const int s = kg * SPW + u;
+          const int off = ((((2 * s + h) ^ key)) << 4) + l32 * 128;
+#pragma unroll
+          for (int i = 0; i < TM; ++i)
+            fb[su][u][i] = *reinterpret_cast<const f16x8*>(sb + (wm * (BM / 2) + 32 * i) * 128 + off);
 #pragma unroll
           for (int j = 0; j < TN; ++j)
-            acc[u % NACC][i][j] =
-                __builtin_amdgcn_mfma_f32_32x32x16_f16(fa[su][u][j], fb[su][u][i], acc[u % NACC][i][j], 0, 0, 0);
+            fa[su][u][j] = *reinterpret_cast<const f16x8*>(sa + (wn * (BN / 2) + 32 * j) * 128 + off);
+        }
+      }
+#pragma unroll
+      for (int su = 0; su < SUB; ++su)
+#pragma unroll
+        for (int u = 0; u < SPW; ++u)
+#pragma unroll
+          for (int i = 0; i < TM; ++i)
+#pragma unroll
+            for (int j = 0; j < TN; ++j)
+              acc[u % NACC][i][j] =
+                  __builtin_amdgcn_mfma_f32_32x32x16_f16(fa[su][u][j], fb[su][u][i], acc[u % NACC][i][j], 0, 0, 0);
+    }
   };
 
   static_assert(NSTAGE >= 2 && NSTAGE <= 4, "ring depth");
@@ -447,7 +508,7 @@ __global__ __launch_bounds__(256 * KG) void conv_dma(const ConvArgs a) {
 #pragma unroll
         for (int e = 0; e < 4; ++e) {
           const float x = acc[0][i][j][4 * q + e] + bias4[j][q][e];
-          v[e] = (a.act ? ym_silu_fast(x) : x) + (float)res4[i][j][q][e];
+          v[e] = (a.act ? (X3 ? ym_silu(x) : ym_silu_fast(x)) : x) + (float)res4[i][j][q][e];
         }
         if (a.shuffle) {
           const int sub = n / a.npr;
@@ -485,8 +546,9 @@ constexpr DmaCfg kDma[] = {
 };
 constexpr int kNumDma = sizeof(kDma) / sizeof(kDma[0]);
 
-template <typename OutT, int BM, int BN, int SPLIT, int KG, int NS, int SUB>
+template <typename OutT, int BM, int BN, int SPLIT, int KG, int NS, int SUB, bool X3 = false>
 hipError_t launch_dma(ConvArgs a, int kind, hipStream_t st) {
+  if (X3 && (4 / KG) % 2) return hipErrorInvalidValue;
   const int tiles_m8 = ((a.M + BM - 1) / BM + 7) / 8 * 8;
   a.tiles_n = (a.N + BN - 1) / BN;
   if (SPLIT > 1) {
@@ -497,23 +559,23 @@ hipError_t launch_dma(ConvArgs a, int kind, hipStream_t st) {
   if (SUB > 1 && (a.Kpad / DK) % (SPLIT * SUB)) return hipErrorInvalidValue;  // whole stages in every split
   const dim3 grid(tiles_m8 * a.tiles_n * SPLIT), block(256 * KG);
   if (kind == 1) {
-    hipLaunchKernelGGL((conv_dma<OutT, BM, BN, 1, SPLIT, KG, NS, SUB>), grid, block, 0, st, a);
-  } else if constexpr (sizeof(OutT) == 2) {  // fp32 outputs exist only for the Detect head's 1x1 convs
+    hipLaunchKernelGGL((conv_dma<OutT, BM, BN, 1, SPLIT, KG, NS, SUB, X3>), grid, block, 0, st, a);
+  } else if constexpr (!std::is_same<OutT, float>::value) {  // fp32 outputs: only the Detect head's 1x1 convs
     if (kind == 4)
-      hipLaunchKernelGGL((conv_dma<OutT, BM, BN, 4, SPLIT, KG, NS, SUB>), grid, block, 0, st, a);
+      hipLaunchKernelGGL((conv_dma<OutT, BM, BN, 4, SPLIT, KG, NS, SUB, X3>), grid, block, 0, st, a);
     else
-      hipLaunchKernelGGL((conv_dma<OutT, BM, BN, 3, SPLIT, KG, NS, SUB>), grid, block, 0, st, a);
+      hipLaunchKernelGGL((conv_dma<OutT, BM, BN, 3, SPLIT, KG, NS, SUB, X3>), grid, block, 0, st, a);
   } else {
     return hipErrorInvalidValue;
   }
   return hipGetLastError();
 }
 
-template <typename OutT>
+template <typename OutT, bool X3 = false>
 hipError_t dispatch(const ConvArgs& a, int kind, int i, hipStream_t st) {
   switch (i) {
 #define YM_X(id, bm, bn, sp, kg, ns, sub) \
-  case id: return launch_dma<OutT, bm, bn, sp, kg, ns, sub>(a, kind, st);
+  case id: return launch_dma<OutT, bm, bn, sp, kg, ns, sub, X3>(a, kind, st);
     YM_DMA_CFGS(YM_X)
 #undef YM_X
   }
@@ -533,9 +595,10 @@ hipError_t ym_launch_conv_dma(int out_f32, const ConvArgs& a, int i, hipStream_t
   else if (a.k == 3) kind = a.Cin8 % 8 == 0 ? 4 : 3;
   else return hipErrorInvalidValue;
   if (a.Kpad % DK || !a.src0 || a.nchw) return hipErrorInvalidValue;
-  if (kind == 1 && a.src1 && a.C0 % DK) return hipErrorInvalidValue;
+  if (kind == 1 && a.src1 && (a.x3 ? 2 : 1) * a.C0 % DK) return hipErrorInvalidValue;
   const long lim = 0x7FFFFFF0L / 2;  // elements
   if ((long)a.N * a.Kpad > lim || a.s0_elems > lim || a.s1_elems > lim) return hipErrorInvalidValue;
   if ((a.N & 3) || (a.d_ctot & 3) || (a.d_coff & 3)) return hipErrorInvalidValue;
+  if (a.x3) return out_f32 ? dispatch<float, true>(a, kind, i, st) : dispatch<P2, true>(a, kind, i, st);
   return out_f32 ? dispatch<float>(a, kind, i, st) : dispatch<f16>(a, kind, i, st);
 }

@@ -5,6 +5,8 @@
 // (/root/reference/core/model.py:133) — SURVEY §2.2 and §8a rows a2, a8, a9, a11-a14.
 #include <stdlib.h>
 
+#include <type_traits>
+
 #include "ym_common.h"
 
 namespace {
@@ -109,7 +111,7 @@ __global__ __launch_bounds__(256) void dwconv3x3(const DwArgs a) {
 #pragma unroll
   for (int e = 0; e < 8; ++e) {  // f16 plans: the fp16 rounding hides the fast SiLU's ~1 ulp (fp32)
     const float sv = sizeof(T) == 2 ? ym_silu_fast(acc[e]) : ym_silu(acc[e]);
-    o[e] = (T)(a.act ? sv : acc[e]);
+    o[e] = (typename Vec8<T>::elem)(a.act ? sv : acc[e]);
   }
   Vec8<T>::store(static_cast<T*>(a.dst) + (size_t)(b * a.d_P + p) * a.d_ctot + a.d_coff + c0, o);
   if (a.raw) {  // f32 calibration run: the pre-activation output
@@ -166,7 +168,7 @@ __global__ __launch_bounds__(256) void dwconv3x3_row(const DwArgs a) {
 #pragma unroll
     for (int e = 0; e < 8; ++e) {
       const float sv = sizeof(T) == 2 ? ym_silu_fast(acc[e]) : ym_silu(acc[e]);
-      o[e] = (T)(a.act ? sv : acc[e]);
+      o[e] = (typename Vec8<T>::elem)(a.act ? sv : acc[e]);
     }
     const int p = y * a.W + x0 + px;
     Vec8<T>::store(static_cast<T*>(a.dst) + (size_t)(b * a.d_P + p) * a.d_ctot + a.d_coff + c0, o);
@@ -282,6 +284,16 @@ __global__ __launch_bounds__(256) void sppf_pool(const PoolArgs a) {
 //   4. + pe(v): depthwise 3x3 + folded BN on v (the `+ self.pe(v.reshape(B,C,H,W))` term), store.
 constexpr int AKD = 32, AHD = 64;
 
+// one element of an activation tensor (x3 pair storage: hi + lo of its chunk)
+template <typename T> __device__ __forceinline__ float ld1(const T* p) {
+  if constexpr (std::is_same<T, P2>::value) return ym_p2_get(p);
+  else return (float)*p;
+}
+template <typename T> __device__ __forceinline__ void st1(T* p, float v) {
+  if constexpr (std::is_same<T, P2>::value) ym_p2_set(p, v);
+  else *p = (T)v;
+}
+
 template <typename T, int QB>
 __global__ __launch_bounds__(256) void attn_psa(const AttnArgs a) {
   extern __shared__ float S[];  // [QB][N], then Q [QB][AKD]
@@ -301,7 +313,7 @@ __global__ __launch_bounds__(256) void attn_psa(const AttnArgs a) {
   for (int i = tid; i < QB * AKD; i += 256) {
     const int r = i / AKD, c = i % AKD;
     const int n = qb * QB + r;
-    Qs[i] = (n < N && c < a.kd) ? (float)qkv[(img + n) * a.q_ctot + hq + c] : 0.f;
+    Qs[i] = (n < N && c < a.kd) ? ld1(qkv + (img + n) * a.q_ctot + hq + c) : 0.f;
   }
   __syncthreads();
   // 1. scores
@@ -389,10 +401,10 @@ __global__ __launch_bounds__(256) void attn_psa(const AttnArgs a) {
       for (int kx = 0; kx < 3; ++kx) {
         const int ix = x + kx - 1;
         if ((unsigned)ix >= (unsigned)a.W) continue;
-        pe = fmaf((float)vp[(size_t)(iy * a.W + ix) * a.q_ctot], a.pe_w[(ky * 3 + kx) * a.C + ch], pe);
+        pe = fmaf(ld1(vp + (size_t)(iy * a.W + ix) * a.q_ctot), a.pe_w[(ky * 3 + kx) * a.C + ch], pe);
       }
     }
-    dst[((size_t)b * a.d_P + n) * a.d_ctot + a.d_coff + ch] = (T)(o[i] + pe);
+    st1(dst + ((size_t)b * a.d_P + n) * a.d_ctot + a.d_coff + ch, o[i] + pe);
     if (a.raw) a.raw[((size_t)b * N + n) * a.C + ch] = pe;  // f32 calibration run: pe(v) before the add
   }
 }
@@ -1039,9 +1051,12 @@ hipError_t ym_launch_dwconv(int dtype, const DwArgs& a, hipStream_t st) {
     hipLaunchKernelGGL((dwconv3x3_row<f16, 4>), dim3((total / 4 + 255) / 256), dim3(256), 0, st, a);
   else if (pxt >= 2 && a.W % 2 == 0 && dtype == YM_DT_F16)
     hipLaunchKernelGGL((dwconv3x3_row<f16, 2>), dim3((total / 2 + 255) / 256), dim3(256), 0, st, a);
+  else if (pxt >= 2 && a.W % 2 == 0 && dtype == YM_DT_X3)
+    hipLaunchKernelGGL((dwconv3x3_row<P2, 2>), dim3((total / 2 + 255) / 256), dim3(256), 0, st, a);
   else if (pxt >= 2 && a.W % 2 == 0)
     hipLaunchKernelGGL((dwconv3x3_row<float, 2>), dim3((total / 2 + 255) / 256), dim3(256), 0, st, a);
   else if (dtype == YM_DT_F16) hipLaunchKernelGGL(dwconv3x3<f16>, g, dim3(256), 0, st, a);
+  else if (dtype == YM_DT_X3) hipLaunchKernelGGL(dwconv3x3<P2>, g, dim3(256), 0, st, a);
   else hipLaunchKernelGGL(dwconv3x3<float>, g, dim3(256), 0, st, a);
   return hipGetLastError();
 }
@@ -1057,6 +1072,7 @@ hipError_t ym_launch_sppf(int dtype, const PoolArgs& a, hipStream_t st) {
   if (dtype == YM_DT_F16) hipLaunchKernelGGL(sppf_pool<f16>, g, dim3(256), lds, st, b);
   else if (dtype == YM_DT_I8) hipLaunchKernelGGL(sppf_pool<i8>, g, dim3(256), lds, st, b);  // max on q - 128: exact
   else if (dtype == YM_DT_F8) hipLaunchKernelGGL((sppf_pool<i8, true>), g, dim3(256), lds, st, b);
+  else if (dtype == YM_DT_X3) hipLaunchKernelGGL(sppf_pool<P2>, g, dim3(256), lds, st, b);  // max of hi + lo values
   else hipLaunchKernelGGL(sppf_pool<float>, g, dim3(256), lds, st, b);
   return hipGetLastError();
 }
@@ -1099,6 +1115,7 @@ hipError_t ym_launch_attn(int dtype, const AttnArgs& a, hipStream_t st) {
     if (nkt <= 32) return launch_attn_mfma<32>(a, st);
   }
   if (a.kd > AKD || a.hd > AHD) return hipErrorInvalidValue;
+  if (dtype == YM_DT_X3) return launch_attn_t<P2>(a, st);
   return dtype == YM_DT_F16 ? launch_attn_t<f16>(a, st) : launch_attn_t<float>(a, st);
 }
 

@@ -273,6 +273,10 @@ int conv_args(ym_ctx* c, const Op& op, int B, const float* d_in, float in_eps, C
         a.sasw = c->wptr<float>(r[23]);
         a.biasi = c->wptr<int>(r[24]);
       }
+      if (c->dtype == YM_DT_X3 && b0 != c->input_buf) {  // pair layout: fp16 storage chunks per tap double
+        a.x3 = 1;
+        a.Cin8 = 2 * (cin / 8);
+      }
       a.Kc = k * k * a.Cin8;
       a.Kpad = r[21];
       a.N = cout;
@@ -309,10 +313,12 @@ int conv_args(ym_ctx* c, const Op& op, int B, const float* d_in, float in_eps, C
       a.M = B * a.Ho * a.Wo;
       a.fd_hw = ym_fdiv(a.Ho * a.Wo);
       a.fd_w = ym_fdiv(a.Wo);
-      out_f32 = c->bufs[bd].f32 && !ym_dt_f32s(c->dtype);
+      out_f32 = c->bufs[bd].f32 && c->dtype != YM_DT_F32;  // (x3: fp32 head rows, pair-layout activations)
       a.raw = c->raw_of(op);
-      a.s0_elems = (b0 == c->input_buf) ? 0 : (long)c->cB * c->buf_P(b0) * c->bufs[b0].C;
-      a.s1_elems = b1 >= 0 ? (long)c->cB * c->buf_P(b1) * c->bufs[b1].C : 0;
+      // operand extents in storage elements (the LDS-DMA buffer descriptors): fp16 halves of the x3 pairs
+      const long xs = a.x3 ? 2 : 1;
+      a.s0_elems = (b0 == c->input_buf) ? 0 : xs * c->cB * c->buf_P(b0) * c->bufs[b0].C;
+      a.s1_elems = b1 >= 0 ? xs * c->cB * c->buf_P(b1) * c->bufs[b1].C : 0;
       a.slab = reinterpret_cast<float*>(c->d_arena + c->off_slab + (size_t)c->lane * c->slab_bytes);
       a.slab_cap = (long)c->slab_bytes;
       a.cnt = reinterpret_cast<int*>(c->d_arena + c->off_cnt) + (size_t)c->lane * kSplitCounters;
@@ -630,8 +636,9 @@ static int validate_plan(const std::vector<BufDesc>& bufs, const std::vector<Op>
   for (int i = 0; i < nbuf; ++i)
     if (bufs[i].C <= 0 || bufs[i].C > (1 << 16) || bufs[i].f < 0 || bufs[i].f > 64)
       return fail(YM_EBLOB, "buffer %d: bad geometry (C %d, f %d)", i, bufs[i].C, bufs[i].f);
-  // conv weight bytes per element: x3 plans pack an fp16 hi and an fp16 lo plane (their stem conv: fp32)
-  const size_t esz = dtype == YM_DT_F32 ? 4 : (dtype == YM_DT_F16 ? 2 : (dtype == YM_DT_X3 ? 4 : 1));
+  // (x3 plans: Kpad counts the fp16 [hi | lo] storage K of the pair-chunk weight rows; their fp32 stem rows are
+  // checked again where they are read)
+  const size_t esz = dtype == YM_DT_F32 ? 4 : ((dtype == YM_DT_F16 || dtype == YM_DT_X3) ? 2 : 1);
   for (const Op& o : ops) {
     const int32_t* r = o.r;
     auto buf_ok = [&](int b, bool opt) { return (opt && b == -1) || (b >= 0 && b < nbuf); };

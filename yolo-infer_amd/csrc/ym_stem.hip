@@ -17,6 +17,8 @@
 //
 // f32 parity plan — stem_valu: one thread per output pixel, fp32 FMAs, weights read with wave-uniform addresses;
 // optionally the pre-activation output for the calibration runs.
+#include <type_traits>
+
 #include "ym_common.h"
 #include "ym_quant.h"
 
@@ -45,12 +47,16 @@ typedef _Float16 h8 __attribute__((ext_vector_type(8)));
 
 constexpr int MTH = 16;  // MFMA path: 16 output rows per workgroup (32 groups of 16 pixels, 8 per wave)
 
-// NT = Cout / 16 channel tiles; F8 (T = i8 storage): the fp8 e4m3 PTQ plan (csrc/ym_quant.h)
+// NT = Cout / 16 channel tiles; F8 (T = i8 storage): the fp8 e4m3 PTQ plan (csrc/ym_quant.h); T = P2: the x3 plan —
+// the patch and the weights are split into fp16 hi / lo parts and every tile takes the three MFMAs of the split
+// product (w_lo·x_hi + w_hi·x_lo + w_hi·x_hi), the output is stored in the pair layout with the exact SiLU
 template <typename T, int NT, bool F8 = false>
 __global__ __launch_bounds__(256) void stem_mfma(const ConvArgs a) {
   constexpr bool QUANT = sizeof(T) == 1;
+  constexpr bool X3 = std::is_same<T, P2>::value;
   constexpr int TH = MTH, PH = 2 * TH + 1;
   __shared__ __attribute__((aligned(16))) f16 patch[3 * PH * PW];
+  __shared__ __attribute__((aligned(16))) f16 patch_lo[X3 ? 3 * PH * PW : 8];
   __shared__ float post[QUANT ? 256 : 1];
   int b, oy0, ox0;
   tile_of<TH>(a, b, oy0, ox0);
@@ -110,7 +116,7 @@ __global__ __launch_bounds__(256) void stem_mfma(const ConvArgs a) {
   for (int it = 0; it < NIT; ++it) {
     const int i = threadIdx.x + 256 * it;
     if (i >= 3 * PH * PW4) break;
-    f16x4 h = {0, 0, 0, 0};
+    f16x4 h = {0, 0, 0, 0}, hl = {0, 0, 0, 0};
     if (in[it]) {
 #pragma unroll
       for (int e = 0; e < 4; ++e) {
@@ -119,15 +125,20 @@ __global__ __launch_bounds__(256) void stem_mfma(const ConvArgs a) {
         if constexpr (F8) h[e] = (f16)f8_dec(f8_enc(x, inv));  // e4m3 values are exact in f16
         else if constexpr (QUANT) h[e] = (f16)(float)(clampi((int)rintf(__fmul_rn(x, inv)) + zi, lo, hi) - zi);
         else h[e] = (f16)x;  // the activation storage precision, as the NHWC input of the MFMA path
+        if constexpr (X3) hl[e] = (f16)(x - (float)h[e]);
       }
     }
     *reinterpret_cast<f16x4*>(patch + 4 * i) = h;  // i = (c*PH + py)*PW4 + q
+    if constexpr (X3) *reinterpret_cast<f16x4*>(patch_lo + 4 * i) = hl;
   }
-  h8 wf[NT];
+  h8 wf[NT], wfl[X3 ? NT : 1];
 #pragma unroll
   for (int j = 0; j < 8; ++j)
 #pragma unroll
-    for (int t = 0; t < NT; ++t) wf[t][j] = 8 * kg + j < 27 ? (f16)wraw[t][j] : (f16)0.f;
+    for (int t = 0; t < NT; ++t) {
+      wf[t][j] = 8 * kg + j < 27 ? (f16)wraw[t][j] : (f16)0.f;
+      if constexpr (X3) wfl[t][j] = 8 * kg + j < 27 ? (f16)(wraw[t][j] - (float)wf[t][j]) : (f16)0.f;
+    }
   __syncthreads();
   // wave w: pixel groups 8w .. 8w+7 of the tile's 32 (16 consecutive columns of one row each)
 #pragma unroll
@@ -135,17 +146,32 @@ __global__ __launch_bounds__(256) void stem_mfma(const ConvArgs a) {
     const int g = 8 * wave + gi;
     const int ly = g >> 1, lx = (g & 1) * 16 + col;
     const f16* pp = patch + 2 * ly * PW + 2 * lx;
-    h8 bf;
+    h8 bf, bfl;
 #pragma unroll
     for (int j = 0; j < 8; ++j) bf[j] = pp[off[j]];
+    if constexpr (X3) {
+      const f16* pl = patch_lo + 2 * ly * PW + 2 * lx;
+#pragma unroll
+      for (int j = 0; j < 8; ++j) bfl[j] = pl[off[j]];
+    }
     const int oy = oy0 + ly, ox = ox0 + lx;
     const bool ok = oy < a.Ho && ox < a.Wo;
     T* dst = static_cast<T*>(a.dst) + (size_t)(b * a.d_P + oy * a.d_W + ox) * a.d_ctot + a.d_coff + 4 * kg;
 #pragma unroll
     for (int t = 0; t < NT; ++t) {
-      const f32x4 acc = __builtin_amdgcn_mfma_f32_16x16x32_f16(wf[t], bf, f32x4{0.f, 0.f, 0.f, 0.f}, 0, 0, 0);
+      f32x4 acc = f32x4{0.f, 0.f, 0.f, 0.f};
+      if constexpr (X3) {
+        acc = __builtin_amdgcn_mfma_f32_16x16x32_f16(wfl[t], bf, acc, 0, 0, 0);
+        acc = __builtin_amdgcn_mfma_f32_16x16x32_f16(wf[t], bfl, acc, 0, 0, 0);
+      }
+      acc = __builtin_amdgcn_mfma_f32_16x16x32_f16(wf[t], bf, acc, 0, 0, 0);
       if (!ok) continue;
-      if constexpr (QUANT) {
+      if constexpr (X3) {
+        float o[4];
+#pragma unroll
+        for (int r = 0; r < 4; ++r) o[r] = ym_silu(acc[r] + bias[t][r]);
+        ym_p2_store4(dst + 16 * t, o);
+      } else if constexpr (QUANT) {
         int ov[4];
 #pragma unroll
         for (int r = 0; r < 4; ++r) {
@@ -258,6 +284,7 @@ hipError_t ym_launch_stem(int dtype, const ConvArgs& a, hipStream_t st) {
   if (dtype == YM_DT_I8) return a.q && a.sasw ? launch_mfma<i8>(a, st) : hipErrorInvalidValue;
   if (dtype == YM_DT_F8) return a.q && a.sasw ? launch_mfma<i8, true>(a, st) : hipErrorInvalidValue;
   if (dtype == YM_DT_F16) return a.raw ? hipErrorInvalidValue : launch_mfma<f16>(a, st);
+  if (dtype == YM_DT_X3) return a.raw ? hipErrorInvalidValue : launch_mfma<P2>(a, st);
   hipLaunchKernelGGL(stem_valu, grid_of(a, 8), dim3(256), 0, st, a);
   return hipGetLastError();
 }

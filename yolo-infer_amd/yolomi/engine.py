@@ -210,9 +210,17 @@ class Engine:
         over the storage channels).  raw=True: the stored elements as they are (int8 / fp16 / fp32 tensor)."""
         _, C, H, W, eb = self.rt.buffer_info(buf_id)
         dt = {1: torch.int8, 2: torch.float16, 4: torch.float32}[eb]
-        out = torch.empty((B, H, W, C), dtype=dt)
+        pair = self.dtype == "x3" and not self.graph.buffers[buf_id].f32
+        if pair:  # x3 pair layout: every 8-channel chunk is [fp16 hi x8 | fp16 lo x8]
+            dt = torch.float16
+        out = torch.empty((B, H, W, 2 * C if pair else C), dtype=dt)
         torch.cuda.synchronize(self.device)
         self.rt.read_buffer(buf_id, out.data_ptr(), out.numel() * out.element_size())
+        if pair:
+            if raw:
+                return out
+            hl = out.float().reshape(B, H, W, C // 8, 2, 8)
+            return (hl[..., 0, :] + hl[..., 1, :]).reshape(B, H, W, C)
         if raw or eb != 1:
             return out if raw else out.float()
         if self.dtype == "f8":

@@ -12,8 +12,9 @@ backend, K padded to 16-channel granules per tap, and per op a `QRec` (csrc/ym_c
 output, the 256-entry post-activation table, the stored tensor's / residual's / input's quantisation), the fp32
 s_in·s_w per output channel and the int32 zero-point correction Σ_k (128 - z_in)·w (activations are stored as q - 128).
 
-x3 plans (dtype "x3", the f16-tolerance plan): fp32 activations; every conv weight matrix except the stem's is packed
-as two fp16 planes, hi = fp16(w) then lo = fp16(w - hi), for the split-f16 MFMA GEMMs of csrc/ym_conv.hip.
+x3 plans (dtype "x3", the f16-tolerance plan): activations in the pair layout of csrc/ym_common.h (every 8-channel
+chunk as fp16 hi = fp16(x) then lo = fp16(x - hi)); every conv weight row except the stem's likewise, [hi x8 | lo x8]
+per K chunk, so r[21] (Kpad) counts fp16 storage elements: 2·K padded to 128.  The stem keeps fp32 rows.
 
 Blob layout (int32 little-endian; parsed by `csrc/ym_runtime.cpp:ym_load_weights`):
   header[32] | buffers[nbuf][8] | ops[nop][32] | names[nop][48 bytes] | pad to 256 | weights
@@ -187,6 +188,14 @@ def pack_graph(g: GraphBuilder, sd: Dict[str, np.ndarray], dtype: str = "f16", q
             Kpad = (K + BK - 1) // BK * BK
             wp = np.zeros((N, Kpad), np.int8 if quant else np.float32)
             wp[:, :K] = w.reshape(N, K)
+            if dtype == "x3" and not stem:  # pair-chunk rows: every 8-channel K chunk as [fp16 hi x8 | fp16 lo x8]
+                wr = w.reshape(N, K // 8, 8).astype(np.float32)
+                hi = wr.astype(np.float16)
+                lo = (wr - hi.astype(np.float32)).astype(np.float16)
+                K2 = 2 * K
+                Kpad = (K2 + 2 * BK - 1) // (2 * BK) * (2 * BK)  # logical K padded to the 64-deep step
+                wp = np.zeros((N, Kpad), np.float16)
+                wp[:, :K2] = np.stack([hi, lo], axis=2).reshape(N, K2)
             src1 = a["src1"]
             C1 = src1.C if src1 is not None else 0
             dst, res = a["dst"], a["res"]
@@ -195,12 +204,7 @@ def pack_graph(g: GraphBuilder, sd: Dict[str, np.ndarray], dtype: str = "f16", q
             r[10:13] = [src1.buf.id, src1.coff, C1] if src1 is not None else [-1, 0, 0]
             r[13:17] = [dst.buf.id, dst.coff, a["anchor_level"], int(bool(a["shuffle2x2"]))]
             r[17:19] = [res.buf.id, res.coff] if res is not None else [-1, 0]
-            if dtype == "x3" and not stem:  # split-f16 plan: fp16 hi plane [N][Kpad], then the fp16 rounding of the rest
-                hi = wp.astype(np.float16)
-                lo = (wp - hi.astype(np.float32)).astype(np.float16)
-                r[19] = arena.add(np.concatenate([hi.reshape(-1), lo.reshape(-1)]))
-            else:  # (the x3 stem runs the fp32 VALU stem kernel on fp32 weights)
-                r[19] = arena.add(wp if quant else wp.astype(np_dt))
+            r[19] = arena.add(wp if quant or wp.dtype == np.float16 else wp.astype(np_dt))  # (x3 stem: fp32)
             r[20] = arena.add(b.astype(np.float32))
             r[21] = Kpad
             pair = a.get("pair")
