@@ -127,8 +127,8 @@ def test_x3_segment_s_b4():
 
 
 # csrc/ym_conv.hip: 12 direct-to-register + 5 LDS-staged tile configurations, then the 30 LDS-DMA ones
-# (csrc/ym_conv_dma.hip, x3 pairing mode)
-X3_CFGS = list(range(17)) + list(range(17, 47))
+# (csrc/ym_conv_dma.hip) and 31 streaming ones (csrc/ym_conv_stream.hip), x3 pairing mode
+X3_CFGS = list(range(17)) + list(range(17, 47)) + list(range(47, 78))
 
 
 @pytest.mark.parametrize("cfg", X3_CFGS)

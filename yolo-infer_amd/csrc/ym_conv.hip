@@ -754,7 +754,7 @@ hipError_t ym_launch_conv(int dtype, int out_f32, const ConvArgs& a, int cfg, hi
     // candidate (strict); a pinned table falls back to the heuristic
     const int ndma = ym_conv_dma_num_cfgs(), nstr = ym_conv_stream_num_cfgs();
     hipError_t e = hipErrorInvalidValue;
-    if (dtype == YM_DT_F16 || (dtype == YM_DT_X3 && cfg - kNumAllCfg < ndma)) {  // x3: the LDS-DMA kernels
+    if (dtype == YM_DT_F16 || (dtype == YM_DT_X3 && cfg - kNumAllCfg < ndma + nstr)) {  // x3: LDS-DMA, streaming
       const int i = cfg - kNumAllCfg;
       e = i < ndma ? ym_launch_conv_dma(out_f32, a, i, st)
                    : (i < ndma + nstr ? ym_launch_conv_stream(out_f32, a, i - ndma, st)

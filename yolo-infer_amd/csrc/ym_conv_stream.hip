@@ -15,6 +15,8 @@
 //     channels of one pixel → + bias, SiLU, (+ residual), one 8-byte (fp16) or 16-byte (fp32 head buffer) store.
 // Results are identical in kind to the other conv kernels (fp32 accumulation of fp16 products, one rounding to the
 // output type); only the summation order differs.
+#include <type_traits>
+
 #include "ym_common.h"
 
 namespace {
@@ -51,8 +53,48 @@ constexpr int kMaxFusedBytes = 112 * 1024;  // fused pairs: both weight matrices
 constexpr int kFuseMaxN = 128;  // first conv's N (= second conv's K) held in registers: 8 blocks of 16
 constexpr int RB = 8;           // output-channel blocks of 16 whose residuals are prefetched with the fragments
 
-template <typename OutT, int KIND, int KS, int PX, bool FUSE, int NWV>
+// x3 plans (X3): activations in the pair layout, weights in pair-chunk rows (csrc/ym_common.h), both read as fp16
+// tensors of twice the channels; a K step ks of 32 then holds the hi / lo halves of logical chunks 2ks, 2ks+1 (lane
+// group g: storage chunk 4ks + g).  Per two steps three MFMAs form the split product: A = w_hi of the group's own
+// logical chunk (storage chunk 4ks + 2(g>>1)) with the natural B, for ks and ks+1 (w_hi·x_hi + w_hi·x_lo), and
+// A = w_lo of logical chunk 2ks + g (storage 4ks + 2g + 1) with B = x_hi of that chunk (storage 4ks + 2g, one extra
+// 16-byte gather per lane and step pair) — w_lo·x_hi of all four chunks.
+template <typename T> struct SOut;  // 4 output channels of one pixel
+template <> struct SOut<f16> {
+  static __device__ __forceinline__ void st(f16* o, const float* v) {
+    *reinterpret_cast<f16x4*>(o) = f16x4{(f16)v[0], (f16)v[1], (f16)v[2], (f16)v[3]};
+  }
+};
+template <> struct SOut<float> {
+  static __device__ __forceinline__ void st(float* o, const float* v) {
+    *reinterpret_cast<f32x4*>(o) = f32x4{v[0], v[1], v[2], v[3]};
+  }
+};
+template <> struct SOut<P2> {
+  static __device__ __forceinline__ void st(P2* o, const float* v) { ym_p2_store4(o, v); }
+};
+// residual values of 4 channels (x3: hi + lo)
+template <bool X3> struct SRes {
+  typedef f16x4 type;
+  static __device__ __forceinline__ type load(const void* p) { return *reinterpret_cast<const f16x4*>(p); }
+  static __device__ __forceinline__ type zero() { return f16x4{0, 0, 0, 0}; }
+};
+template <> struct SRes<true> {
+  typedef f32x4 type;
+  static __device__ __forceinline__ type load(const void* p) {
+    float v[4];
+    ym_p2_load4(static_cast<const P2*>(p), v);
+    return f32x4{v[0], v[1], v[2], v[3]};
+  }
+  static __device__ __forceinline__ type zero() { return f32x4{0.f, 0.f, 0.f, 0.f}; }
+};
+
+template <typename OutT, int KIND, int KS, int PX, bool FUSE, int NWV, bool X3 = false>
 __global__ __launch_bounds__(64 * NWV) void conv_stream(const ConvArgs a) {
+  static_assert(!X3 || (!FUSE && KS % 2 == 0), "x3: unfused, K steps in pairs");
+  constexpr int XS = X3 ? 2 : 1;       // fp16 storage elements per logical channel
+  constexpr int KX = X3 ? KS / 2 : 0;  // x3: the extra x_hi gather per step pair
+  typedef typename SRes<X3>::type RV;
   constexpr int NT = 64 * NWV;     // threads per workgroup
   constexpr int KP = KS * 32;      // Kpad
   // LDS row pitch (halves) KP + 16 = 4·KS + 2 16-byte slots: the A-fragment reads (16 rows x one K chunk per lane
@@ -103,13 +145,20 @@ __global__ __launch_bounds__(64 * NWV) void conv_stream(const ConvArgs a) {
   const int G = (a.M + 15) >> 4;  // 16-pixel groups
   const f16* s0 = static_cast<const f16*>(a.src0);
   const f16* s1 = static_cast<const f16*>(a.src1);
-  const int K = a.C0 + a.C1;
+  const int s0_ctot = XS * a.s0_ctot, s0_coff = XS * a.s0_coff, s1_ctot = XS * a.s1_ctot, s1_coff = XS * a.s1_coff;
+  const int C0s = XS * a.C0;
+  const int K = XS * (a.C0 + a.C1);  // storage K of one pixel row (1x1)
   const unsigned c8m = (0x1000000u + a.Cin8 - 1) / a.Cin8;  // 3x3: tap = (chunk * c8m) >> 24 (chunk < 9 Cin8)
 
   // B fragments of the iteration starting at group gb: [PX][KS]; with a residual also the residual values of the
   // first RB output-channel blocks of its pixels, one iteration ahead like the fragments (a residual load placed
   // after the previous block's stores would make the compiler drain every outstanding load, the prefetch included)
   const f16* res = static_cast<const f16*>(a.res);
+  const P2* resp = static_cast<const P2*>(a.res);
+  auto res_at = [&](size_t e) -> const void* {  // residual element e (logical index)
+    if constexpr (X3) return resp + e;
+    else return res + e;
+  };
   const int NR = FUSE ? a.N2 : a.N;
   // XCD-contiguous group ranges: workgroup bid runs on XCD bid % 8 (round-robin dispatch), and each XCD sweeps one
   // contiguous range of 16-pixel groups with all of its workgroups, so the neighbouring image rows a 3x3 tap reads
@@ -119,7 +168,7 @@ __global__ __launch_bounds__(64 * NWV) void conv_stream(const ConvArgs a) {
   const int nwx = (nwg >> 3) + (xcd < (nwg & 7));                   // workgroups on this XCD
   const int v0 = xcd * (nwg >> 3) + (xcd < (nwg & 7) ? xcd : (nwg & 7));  // workgroups on lower XCDs
   const int gend = (int)((long)G * (v0 + nwx) / nwg);
-  auto load = [&](int gb, h8 (&bf)[PX][KS], f16x4 (&rr)[PX][RB]) {
+  auto load = [&](int gb, h8 (&bf)[PX][KS + KX], RV (&rr)[PX][RB]) {
 #pragma unroll
     for (int p = 0; p < PX; ++p) {
       const int m = (gb + p) * 16 + col;
@@ -128,35 +177,36 @@ __global__ __launch_bounds__(64 * NWV) void conv_stream(const ConvArgs a) {
       const int b = ym_div(mm, a.fd_hw), rem = mm - b * HW;
       const int y = ym_div(rem, a.fd_w), x = rem - y * a.Wo;
       if (res) {
-        const f16* rp = res + (size_t)(b * a.r_P + y * a.Wo + x) * a.r_ctot + a.r_coff + 4 * g;
+        const size_t rp = (size_t)(b * a.r_P + y * a.Wo + x) * a.r_ctot + a.r_coff + 4 * g;
 #pragma unroll
         for (int j = 0; j < RB; ++j)
-          rr[p][j] = (ok && 16 * j + 4 * g < NR) ? *reinterpret_cast<const f16x4*>(rp + 16 * j) : f16x4{0, 0, 0, 0};
+          rr[p][j] = (ok && 16 * j + 4 * g < NR) ? SRes<X3>::load(res_at(rp + 16 * j)) : SRes<X3>::zero();
       }
       if constexpr (KIND == 1) {
         const size_t p0 = a.up0 ? (size_t)b * a.s0_P + (y >> 1) * a.s0_W + (x >> 1) : (size_t)b * a.s0_P + y * a.s0_W + x;
         const size_t p1 = (size_t)b * a.s1_P + y * a.Win + x;
 #pragma unroll
-        for (int ks = 0; ks < KS; ++ks) {
-          const int k0 = 32 * ks + 8 * g;
+        for (int ks = 0; ks < KS + KX; ++ks) {
+          // ks >= KS (x3): x_hi of logical chunk 4 (ks - KS) + g, i.e. storage chunk 8 (ks - KS) + 2g
+          const int k0 = ks < KS ? 32 * ks + 8 * g : 64 * (ks - KS) + 16 * g;
           h8 v = Vec8<f16>::zero();
           if (ok && k0 < K)
-            v = k0 < a.C0 ? Vec8<f16>::load(s0 + p0 * a.s0_ctot + a.s0_coff + k0)
-                          : Vec8<f16>::load(s1 + p1 * a.s1_ctot + a.s1_coff + (k0 - a.C0));
+            v = k0 < C0s ? Vec8<f16>::load(s0 + p0 * s0_ctot + s0_coff + k0)
+                         : Vec8<f16>::load(s1 + p1 * s1_ctot + s1_coff + (k0 - C0s));
           bf[p][ks] = v;
         }
       } else {  // 3x3, pad 1, stride a.s: chunk c = 4 ks + g is tap c / Cin8, channels 8 (c % Cin8) ..
-        const f16* img = s0 + (size_t)b * a.s0_P * a.s0_ctot + a.s0_coff;
+        const f16* img = s0 + (size_t)b * a.s0_P * s0_ctot + s0_coff;
         const int iy0 = y * a.s - 1, ix0 = x * a.s - 1;
 #pragma unroll
-        for (int ks = 0; ks < KS; ++ks) {
-          const int c = 4 * ks + g;
+        for (int ks = 0; ks < KS + KX; ++ks) {
+          const int c = ks < KS ? 4 * ks + g : 8 * (ks - KS) + 2 * g;  // storage chunk (x3 extra: the x_hi chunks)
           const int t = (int)(((unsigned)c * c8m) >> 24), cb = c - t * a.Cin8;
           const int ky = t >= 6 ? 2 : (t >= 3 ? 1 : 0), kx = t - 3 * ky;
           const int iy = iy0 + ky, ix = ix0 + kx;
           h8 v = Vec8<f16>::zero();
           if (ok && c < a.Kc && (unsigned)iy < (unsigned)a.Hin && (unsigned)ix < (unsigned)a.Win)
-            v = Vec8<f16>::load(img + (size_t)(iy * a.Win + ix) * a.s0_ctot + 8 * cb);
+            v = Vec8<f16>::load(img + (size_t)(iy * a.Win + ix) * s0_ctot + 8 * cb);
           bf[p][ks] = v;
         }
       }
@@ -165,8 +215,8 @@ __global__ __launch_bounds__(64 * NWV) void conv_stream(const ConvArgs a) {
 
   const int step = nwx * NWV * PX;
   int gb = (int)((long)G * v0 / nwg) + (slot * NWV + wave) * PX;
-  h8 cur[PX][KS], nxt[PX][KS];
-  f16x4 rcur[PX][RB], rnxt[PX][RB];
+  h8 cur[PX][KS + KX], nxt[PX][KS + KX];
+  RV rcur[PX][RB], rnxt[PX][RB];
   load(gb, cur, rcur);
   __syncthreads();
   OutT* dst = static_cast<OutT*>(a.dst);
@@ -228,14 +278,11 @@ __global__ __launch_bounds__(64 * NWV) void conv_stream(const ConvArgs a) {
             v[r] = a.act2 ? ym_silu_fast(xv) : xv;
           }
           if (res) {
-            const f16x4 rv = nb20 == 0 ? rcur[p][j]
-                                       : *reinterpret_cast<const f16x4*>(res + (size_t)rb[p] * a.r_ctot + a.r_coff + n0);
+            const RV rv = nb20 == 0 ? rcur[p][j] : SRes<X3>::load(res_at((size_t)rb[p] * a.r_ctot + a.r_coff + n0));
 #pragma unroll
             for (int r = 0; r < 4; ++r) v[r] += (float)rv[r];
           }
-          OutT* o = dst + (size_t)ob[p] * a.d_ctot + a.d_coff + n0;
-          if constexpr (sizeof(OutT) == 2) *reinterpret_cast<f16x4*>(o) = f16x4{(f16)v[0], (f16)v[1], (f16)v[2], (f16)v[3]};
-          else *reinterpret_cast<f32x4*>(o) = f32x4{v[0], v[1], v[2], v[3]};
+          SOut<OutT>::st(dst + (size_t)ob[p] * a.d_ctot + a.d_coff + n0, v);
         }
       }
     } else
@@ -244,39 +291,39 @@ __global__ __launch_bounds__(64 * NWV) void conv_stream(const ConvArgs a) {
     for (int j = 0; j < RB; ++j) {
       const int nb = nb0 + j;
       if (nb >= NP / 16) break;
-      h8 af[KS];
+      h8 af[KS + KX];  // x3: [0, KS) = w_hi of each group's logical chunk, [KS, KS + KX) = w_lo of chunk 4ks' + g
 #pragma unroll
-      for (int ks = 0; ks < KS; ++ks)
-        af[ks] = *reinterpret_cast<const h8*>(ws + (16 * nb + col) * LDW + 32 * ks + 8 * g);
+      for (int ks = 0; ks < KS + KX; ++ks) {
+        const int c = !X3 ? 4 * ks + g : (ks < KS ? 4 * ks + 2 * (g >> 1) : 8 * (ks - KS) + 2 * g + 1);
+        af[ks] = *reinterpret_cast<const h8*>(ws + (16 * nb + col) * LDW + 8 * c);
+      }
       const int n0 = 16 * nb + 4 * g;
       const f32x4 b4 = *reinterpret_cast<const f32x4*>(bs + n0);
 #pragma unroll
       for (int p = 0; p < PX; ++p) {
         f32x4 acc = {0.f, 0.f, 0.f, 0.f};
 #pragma unroll
-        for (int ks = 0; ks < KS; ++ks) acc = __builtin_amdgcn_mfma_f32_16x16x32_f16(af[ks], cur[p][ks], acc, 0, 0, 0);
+        for (int ks = 0; ks < KS + KX; ++ks)
+          acc = __builtin_amdgcn_mfma_f32_16x16x32_f16(af[ks], cur[p][ks], acc, 0, 0, 0);
         if (ob[p] < 0 || n0 >= a.N) continue;
         float v[4];
 #pragma unroll
         for (int r = 0; r < 4; ++r) {
           const float xv = acc[r] + b4[r];
-          v[r] = a.act ? ym_silu_fast(xv) : xv;
+          v[r] = a.act ? (X3 ? ym_silu(xv) : ym_silu_fast(xv)) : xv;
         }
         if (res) {
-          const f16x4 rv = nb0 == 0 ? rcur[p][j]
-                                    : *reinterpret_cast<const f16x4*>(res + (size_t)rb[p] * a.r_ctot + a.r_coff + n0);
+          const RV rv = nb0 == 0 ? rcur[p][j] : SRes<X3>::load(res_at((size_t)rb[p] * a.r_ctot + a.r_coff + n0));
 #pragma unroll
           for (int r = 0; r < 4; ++r) v[r] += (float)rv[r];
         }
-        OutT* o = dst + (size_t)ob[p] * a.d_ctot + a.d_coff + n0;
-        if constexpr (sizeof(OutT) == 2) *reinterpret_cast<f16x4*>(o) = f16x4{(f16)v[0], (f16)v[1], (f16)v[2], (f16)v[3]};
-        else *reinterpret_cast<f32x4*>(o) = f32x4{v[0], v[1], v[2], v[3]};
+        SOut<OutT>::st(dst + (size_t)ob[p] * a.d_ctot + a.d_coff + n0, v);
       }
     }
 #pragma unroll
     for (int p = 0; p < PX; ++p) {
 #pragma unroll
-      for (int ks = 0; ks < KS; ++ks) cur[p][ks] = nxt[p][ks];
+      for (int ks = 0; ks < KS + KX; ++ks) cur[p][ks] = nxt[p][ks];
 #pragma unroll
       for (int j = 0; j < RB; ++j) rcur[p][j] = rnxt[p][j];
     }
@@ -413,9 +460,12 @@ hipError_t launch_small(const ConvArgs& a, hipStream_t st) {
   return hipGetLastError();
 }
 
-template <typename OutT, int KIND, int KS, int PX, int CAP, int NWV>
+template <typename OutT, int KIND, int KS, int PX, int CAP, int NWV, bool X3 = false>
 hipError_t launch(const ConvArgs& a, hipStream_t st) {
   if (a.Kpad != KS * 32 || a.k != KIND) return hipErrorInvalidValue;
+  if constexpr (X3) {
+    if (KS % 2 || a.w2) return hipErrorInvalidValue;
+  }
   const int G = (a.M + 15) / 16;
   long wgs = (G + NWV * PX - 1) / (NWV * PX);
   if (wgs > CAP) wgs = CAP;  // the persistent grid: CAP workgroups, the rest streams through them
@@ -429,19 +479,20 @@ hipError_t launch(const ConvArgs& a, hipStream_t st) {
     if constexpr (NWV == 8 && PX > 1) return hipErrorInvalidValue;  // 256 VGPRs per wave: the pair would spill
     else hipLaunchKernelGGL((conv_stream<OutT, KIND, KS, PX, true, NWV>), dim3(wgs), dim3(64 * NWV), lds, st, a);
   } else {
-    hipLaunchKernelGGL((conv_stream<OutT, KIND, KS, PX, false, NWV>), dim3(wgs), dim3(64 * NWV), lds, st, a);
+    hipLaunchKernelGGL((conv_stream<OutT, KIND, KS, PX, false, NWV, X3>), dim3(wgs), dim3(64 * NWV), lds, st, a);
   }
   return hipGetLastError();
 }
 
-template <typename OutT>
+template <typename OutT, bool X3 = false>
 hipError_t dispatch(const ConvArgs& a, int i, hipStream_t st) {
   switch (i) {
 #define YM_X(id, kind, ks, px, cap, nw) \
-  case id: return launch<OutT, kind, ks, px, cap, nw>(a, st);
+  case id: return launch<OutT, kind, ks, px, cap, nw, X3>(a, st);
     YM_STREAM_CFGS(YM_X)
 #undef YM_X
   }
+  if constexpr (X3) return hipErrorInvalidValue;  // the small-M kernels split K four ways: no x3 pairing
   switch (i - kNumStream) {
 #define YM_X(id, kind, ksw, pxg) \
   case id: return launch_small<OutT, kind, ksw, pxg>(a, st);
@@ -462,7 +513,7 @@ hipError_t ym_launch_conv_stream(int out_f32, const ConvArgs& a, int i, hipStrea
   if (i < 0 || i >= kNumStream + kNumSmall) return hipErrorInvalidValue;
   if (a.shuffle || a.raw || a.nchw || !a.src0 || (a.N & 3) || a.Kpad % 32) return hipErrorInvalidValue;
   if (a.k == 1) {
-    if (a.s != 1 || a.C0 % 8 || a.C1 % 8) return hipErrorInvalidValue;
+    if (a.s != 1 || a.C0 % 8 || a.C1 % 8) return hipErrorInvalidValue;  // (logical channels; x3: pair chunks)
     if (a.src1 && (a.s1_coff % 8 || a.s1_ctot % 8)) return hipErrorInvalidValue;
   } else if (a.k == 3) {
     if (a.src1 || a.up0 || a.pad != 1 || a.Cin8 > 1024) return hipErrorInvalidValue;
@@ -472,5 +523,6 @@ hipError_t ym_launch_conv_stream(int out_f32, const ConvArgs& a, int i, hipStrea
   if ((a.d_ctot & 3) || (a.d_coff & 3) || (a.res && ((a.r_ctot & 3) || (a.r_coff & 3)))) return hipErrorInvalidValue;
   if (a.s0_coff % 8 || a.s0_ctot % 8) return hipErrorInvalidValue;
   if (a.w2 && (a.N > kFuseMaxN || (a.N2 & 3) || a.Kpad2 < a.N || (a.Kpad2 & 3) || !a.bias2)) return hipErrorInvalidValue;
+  if (a.x3) return out_f32 ? dispatch<float, true>(a, i, st) : dispatch<P2, true>(a, i, st);
   return out_f32 ? dispatch<float>(a, i, st) : dispatch<f16>(a, i, st);
 }

@@ -546,6 +546,130 @@ __global__ __launch_bounds__(256) void attn_psa_mfma(const AttnArgs a) {
   }
 }
 
+// x3 plans, kd = 32 / hd = 64, N <= 512 tokens: attn_psa_mfma's structure on the pair layout, every product split
+// (hi·hi + lo·hi + hi·lo on v_mfma_f32_16x16x32_f16, fp32 accumulation).  V^T of the (image, head) is staged in LDS
+// as hi and lo planes (the two planes of K as well would not fit beside them), K fragments stream from global
+// (32 bytes = the [hi | lo] pair of one key chunk per lane and key tile; L2-resident), P is split in registers.
+template <int NKT>
+__global__ __launch_bounds__(256) void attn_psa_x3(const AttnArgs a) {
+  extern __shared__ __attribute__((aligned(16))) f16 vt[];  // [2][64][LDV]: V^T hi, lo; then pe weights + bias f32
+  constexpr int LDV = 16 * NKT + 4;
+  f16* vtl = vt + 64 * LDV;
+  float* pw = reinterpret_cast<float*>(vtl + 64 * LDV);
+  const int N = a.N;
+  const int nqb = (N + 63) / 64;
+  const int vb = ym_xcd_block(blockIdx.x, gridDim.x);
+  const int qb = vb % nqb, bh = vb / nqb;
+  const int h = bh % a.nh, b = bh / a.nh;
+  const int tid = threadIdx.x, lane = tid & 63, wave = tid >> 6;
+  const int g = lane >> 4, c = lane & 15;
+  const P2* qkv = static_cast<const P2*>(a.qkv);
+  const size_t img = (size_t)b * a.q_P;
+  const int hq = a.q_coff + h * 128;  // per head: q 32, k 32, v 64 logical channels
+  for (int i = tid; i < 640; i += 256)
+    pw[i] = i < 576 ? a.pe_w[(i >> 6) * a.C + h * 64 + (i & 63)] : a.pe_b[h * 64 + i - 576];
+  // 1. V^T hi / lo planes (keys >= N zero): 8 chunks of 8 v channels per key
+  for (int i = tid; i < 16 * NKT * 8; i += 256) {
+    const int key = i >> 3, ch = i & 7;
+    HL v{Vec8<f16>::zero(), Vec8<f16>::zero()};
+    if (key < N) v = ym_load_hl(qkv + (img + key) * a.q_ctot + hq + 64 + 8 * ch);
+#pragma unroll
+    for (int e = 0; e < 8; ++e) {
+      vt[(8 * ch + e) * LDV + key] = v.hi[e];
+      vtl[(8 * ch + e) * LDV + key] = v.lo[e];
+    }
+  }
+  const int q = qb * 64 + wave * 16 + c;
+  HL qf{Vec8<f16>::zero(), Vec8<f16>::zero()};
+  if (q < N) qf = ym_load_hl(qkv + (img + q) * a.q_ctot + hq + 8 * g);
+  // 2. scores S^T = K·Q^T (log2 units): lane (g, c) supplies key 16t + c, logical chunk g of K
+  const float sl2 = a.scale * 1.4426950408889634f;
+  float s[NKT][4];
+#pragma unroll
+  for (int t = 0; t < NKT; ++t) {
+    const int key = 16 * t + c;
+    HL kf{Vec8<f16>::zero(), Vec8<f16>::zero()};
+    if (key < N) kf = ym_load_hl(qkv + (img + key) * a.q_ctot + hq + 32 + 8 * g);
+    f32x4 d = __builtin_amdgcn_mfma_f32_16x16x32_f16(kf.lo, qf.hi, f32x4{0.f, 0.f, 0.f, 0.f}, 0, 0, 0);
+    d = __builtin_amdgcn_mfma_f32_16x16x32_f16(kf.hi, qf.lo, d, 0, 0, 0);
+    d = __builtin_amdgcn_mfma_f32_16x16x32_f16(kf.hi, qf.hi, d, 0, 0, 0);
+#pragma unroll
+    for (int r = 0; r < 4; ++r) s[t][r] = 16 * t + 4 * g + r < N ? d[r] * sl2 : -INFINITY;
+  }
+  __syncthreads();
+  // 3. softmax over the keys of query l&15 (fp32, exact exp2)
+  float m = -INFINITY;
+#pragma unroll
+  for (int t = 0; t < NKT; ++t)
+#pragma unroll
+    for (int r = 0; r < 4; ++r) m = fmaxf(m, s[t][r]);
+  m = fmaxf(m, __shfl_xor(m, 16));
+  m = fmaxf(m, __shfl_xor(m, 32));
+  float sum = 0.f;
+#pragma unroll
+  for (int t = 0; t < NKT; ++t)
+#pragma unroll
+    for (int r = 0; r < 4; ++r) {
+      s[t][r] = exp2f(s[t][r] - m);
+      sum += s[t][r];
+    }
+  sum += __shfl_xor(sum, 16);
+  sum += __shfl_xor(sum, 32);
+  const float rs = 1.0f / sum;
+  // 4. O^T = V^T P^T, K = 32 keys per MFMA in the lane-group order of step 2 (as attn_psa_mfma), P split hi / lo
+  f32x4 o[4];
+#pragma unroll
+  for (int dt = 0; dt < 4; ++dt) o[dt] = f32x4{0.f, 0.f, 0.f, 0.f};
+#pragma unroll
+  for (int ks = 0; ks < NKT / 2; ++ks) {
+    h8v ph, pl;
+#pragma unroll
+    for (int r = 0; r < 4; ++r) {
+      const float p0 = s[2 * ks][r] * rs, p1 = s[2 * ks + 1][r] * rs;
+      ph[r] = (f16)p0;
+      pl[r] = (f16)(p0 - (float)ph[r]);
+      ph[4 + r] = (f16)p1;
+      pl[4 + r] = (f16)(p1 - (float)ph[4 + r]);
+    }
+#pragma unroll
+    for (int dt = 0; dt < 4; ++dt) {
+      const int row = (16 * dt + c) * LDV + 32 * ks + 4 * g;
+      const f16x4 hlo = *reinterpret_cast<const f16x4*>(vt + row), hhi = *reinterpret_cast<const f16x4*>(vt + row + 16);
+      const f16x4 llo = *reinterpret_cast<const f16x4*>(vtl + row), lhi = *reinterpret_cast<const f16x4*>(vtl + row + 16);
+      const h8v vh = {hlo[0], hlo[1], hlo[2], hlo[3], hhi[0], hhi[1], hhi[2], hhi[3]};
+      const h8v vl = {llo[0], llo[1], llo[2], llo[3], lhi[0], lhi[1], lhi[2], lhi[3]};
+      o[dt] = __builtin_amdgcn_mfma_f32_16x16x32_f16(vl, ph, o[dt], 0, 0, 0);
+      o[dt] = __builtin_amdgcn_mfma_f32_16x16x32_f16(vh, pl, o[dt], 0, 0, 0);
+      o[dt] = __builtin_amdgcn_mfma_f32_16x16x32_f16(vh, ph, o[dt], 0, 0, 0);
+    }
+  }
+  // 5. + pe(v) (v = hi + lo from LDS), store in the pair layout: lane = channels 16dt + 4g .. +3 of query q
+  if (q >= N) return;
+  const int y = q / a.W, x = q - (q / a.W) * a.W;
+  P2* dst = static_cast<P2*>(a.dst) + ((size_t)b * a.d_P + q) * a.d_ctot + a.d_coff + h * 64;
+#pragma unroll
+  for (int dt = 0; dt < 4; ++dt) {
+    const int d0 = 16 * dt + 4 * g;
+    float pe[4];
+#pragma unroll
+    for (int r = 0; r < 4; ++r) pe[r] = pw[576 + d0 + r];
+#pragma unroll
+    for (int t = 0; t < 9; ++t) {
+      const int iy = y + t / 3 - 1, ix = x + t % 3 - 1;
+      if ((unsigned)iy >= (unsigned)a.H || (unsigned)ix >= (unsigned)a.W) continue;
+      const int nb = iy * a.W + ix;
+      const f32x4 w = *reinterpret_cast<const f32x4*>(pw + 64 * t + d0);
+#pragma unroll
+      for (int r = 0; r < 4; ++r)
+        pe[r] = fmaf((float)vt[(d0 + r) * LDV + nb] + (float)vtl[(d0 + r) * LDV + nb], w[r], pe[r]);
+    }
+    float out[4];
+#pragma unroll
+    for (int r = 0; r < 4; ++r) out[r] = o[dt][r] + pe[r];
+    ym_p2_store4(dst + d0, out);
+  }
+}
+
 // ------------------------------------------------------------------------------------------------- decode
 // Detect._inference + the candidate stage of non_max_suppression; 4 lanes per anchor (lane s: DFL side s and a
 // quarter of the classes):
@@ -1104,8 +1228,23 @@ hipError_t launch_attn_mfma(const AttnArgs& a, hipStream_t st) {
   return hipGetLastError();
 }
 
+template <int NKT>
+hipError_t launch_attn_x3(const AttnArgs& a, hipStream_t st) {
+  const size_t lds = (size_t)2 * 64 * (16 * NKT + 4) * sizeof(f16) + 640 * sizeof(float);
+  hipLaunchKernelGGL((attn_psa_x3<NKT>), dim3(a.B * a.nh * ((a.N + 63) / 64)), dim3(256), lds, st, a);
+  return hipGetLastError();
+}
+
 hipError_t ym_launch_attn(int dtype, const AttnArgs& a, hipStream_t st) {
   if (ym_dt_q8(dtype)) return ym_launch_attn_i8(a, st, dtype == YM_DT_F8);
+  if (dtype == YM_DT_X3 && a.kd == 32 && a.hd == 64 && !a.raw && a.nh * 128 <= a.q_ctot && a.d_ctot % 4 == 0 &&
+      a.d_coff % 4 == 0 && a.q_ctot % 8 == 0 && a.q_coff % 8 == 0) {
+    const int nkt = (a.N + 15) / 16;
+    if (nkt <= 8) return launch_attn_x3<8>(a, st);
+    if (nkt <= 16) return launch_attn_x3<16>(a, st);
+    if (nkt <= 26) return launch_attn_x3<26>(a, st);
+    if (nkt <= 32) return launch_attn_x3<32>(a, st);
+  }
   if (dtype == YM_DT_F16 && a.kd == 32 && a.hd == 64 && !a.raw && a.nh * 128 <= a.q_ctot && a.d_ctot % 4 == 0 &&
       a.d_coff % 4 == 0 && a.q_ctot % 8 == 0 && a.q_coff % 8 == 0) {
     const int nkt = (a.N + 15) / 16;
