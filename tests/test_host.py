@@ -162,6 +162,22 @@ def test_metrics_map():
     assert evaluate([np.zeros((0, 6))], gt)["map"] == 0.0
 
 
+def test_match_predictions_prediction_order_known_answer():
+    """One ground truth, two same-class candidates: upstream match_predictions keeps, per ground truth, the first
+    remaining pair in PREDICTION order (the more confident prediction, IoU 0.6), not the higher-IoU one (0.9) — the
+    IoU re-sort between its two unique() steps is commented out upstream.  At t >= 0.65 only the IoU-0.9 prediction
+    qualifies."""
+    from yolomi.metrics import IOUV, match_predictions
+    gt = np.array([[0, 0, 100, 100, 1, 7]], np.float64)
+    p0 = [0, 0, 100, 60, 0.9, 7]   # IoU 0.6
+    p1 = [0, 0, 100, 90, 0.8, 7]   # IoU 0.9
+    tp = match_predictions(np.array([p0, p1], np.float64), gt)
+    k50, k65 = 0, int(np.argmin(np.abs(IOUV - 0.65)))
+    assert tp[0, k50] and not tp[1, k50]
+    assert not tp[0, k65] and tp[1, k65]
+    assert tp[1, int(np.argmin(np.abs(IOUV - 0.9)))] and not tp[:, -1].any()
+
+
 def test_matching_protocol():
     ref = np.array([[0, 0, 10, 10, 0.9, 1], [20, 20, 40, 40, 0.2505, 2]], np.float32)
     got = np.array([[0, 0, 10, 10.0005, 0.9002, 1]], np.float32)
@@ -299,3 +315,19 @@ def test_checkpoint_architecture_is_inferred_and_mismatches_rejected():
         pack_graph(GraphBuilder("n", "detect"), sd20, "f16")
     blob = pack_model("s", "detect", sd_s, "f16")
     assert struct.unpack("<32i", blob[:128])[19] == ord("s")  # ym_model_desc.scale is checked against this
+
+
+def test_resource_monitor_contract():
+    """utils/helpers.ResourceMonitor keeps the reference's data-point keys and averages (helpers.py:715-834); on a
+    host without a GPU driver the AMD SMI side degrades to an empty gpu_usage list."""
+    import time as _t
+    from utils.helpers import ResourceMonitor
+    m = ResourceMonitor(interval=0.05)
+    m.start_monitoring()
+    _t.sleep(0.5)
+    m.stop_monitoring()
+    assert len(m.history) >= 2
+    p = m.get_current_usage()
+    assert {"timestamp", "cpu_percent", "memory_percent", "memory_used", "memory_total", "gpu_usage"} <= set(p)
+    avg = m.get_average_usage()
+    assert "avg_cpu_percent" in avg and "avg_memory_percent" in avg

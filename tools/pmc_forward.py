@@ -37,7 +37,7 @@ def main():
     if a.ops_out:
         # name, kind, kernel launches of the op (a split pair launches two), algorithmic FLOPs and bytes
         cfg = eng.rt.get_op_cfg(a.batch, a.size, a.size) or [0] * len(eng.graph.ops)
-        costs = eng.graph.op_costs(a.batch, a.size, a.size, 1 if a.dtype == "i8" else 4 if a.dtype == "f32" else 2)
+        costs = eng.graph.op_costs(a.batch, a.size, a.size, {"i8": 1, "f8": 1, "f32": 4, "x3": 4}.get(a.dtype, 2))
         with open(a.ops_out, "w") as f:
             for op, c, (fl, by) in zip(eng.graph.ops, cfg, costs):
                 n = 2 if op.kind == "input" or (op.kind == "conv" and c >= (1 << 20)) else 1

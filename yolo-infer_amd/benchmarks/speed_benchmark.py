@@ -4,8 +4,8 @@ Same protocol and result keys as the reference: `_benchmark_inference` (`speed_b
 model in eval mode, runs warm-up predicts, then times each `predict(test_input)` with wall clock and reports
 avg/min/max/stdev, `fps = 1/avg` and `throughput = B/avg`; `benchmark_model_sizes` (`:61-122`) sweeps sizes x
 image sizes x batch sizes; `benchmark_quantization` (`:124-209`) is the PTQ A/B (`speedup = t_original / t_quant`,
-`:191`); `benchmark_throughput` (`:211-305`) is the sustained loop.  The GPUtil resource monitor (NVIDIA-only) is not
-part of this path.
+`:191`); `benchmark_throughput` (`:211-305`) is the sustained loop, with the reference's resource monitor
+(`:243-244`) sampling AMD SMI instead of GPUtil (utils/helpers.py).
 """
 from __future__ import annotations
 
@@ -22,6 +22,7 @@ import torch
 
 from core.model import YOLO11Model
 from optimization.quantization.quantizers import create_quantizer
+from utils.helpers import ResourceMonitor
 
 logger = logging.getLogger(__name__)
 
@@ -63,14 +64,15 @@ class SpeedBenchmark:
 
     def benchmark_quantization(self, model_size: str = "n", task: str = "detect",
                                quantization_methods: List[str] = ["dynamic", "ptq"], image_size: int = 640,
-                               batch_size: int = 1, original_dtype: str = "f16") -> Dict[str, Any]:
+                               batch_size: int = 1, original_dtype: str = "f32") -> Dict[str, Any]:
         """The reference's quantization A/B (`speed_benchmark.py:124-209`): time the original model, then each
         method's quantized model on the same randn input, `speedup = original avg / quantized avg`.  'ptq' calibrates
         on ten copies of the test input (`:180-183`) with the quantizer's default config (qnnpack int8); 'ptq_fp8'
         is the same flow on the fp8 e4m3 plan (BASELINE config 4).  A method that fails is recorded as
         {'error': ...} like the reference's except path (`:196-201`): 'dynamic' is one (a no-op on this conv-only
-        graph, SURVEY §2.1).  `original_dtype` is the original model's plan ('f16' throughput plan by default;
-        'f32' = the exact parity plan, the reference's FP32 model)."""
+        graph).  `original_dtype` is the original model's plan: 'f32' by default — the exact-f32 plan,
+        the reference's FP32 model (`:157-158`), so `speedup` is the reference's quantity; 'f16' / 'x3' time a
+        faster float plan instead."""
         logger.info(f"Benchmarking quantization methods: {quantization_methods}")
         results = {"model_size": model_size, "task": task, "image_size": image_size, "batch_size": batch_size,
                    "original_dtype": original_dtype, "system_info": self.system_info, "methods": {}}
@@ -106,6 +108,8 @@ class SpeedBenchmark:
         test_input = torch.randn(batch_size, 3, image_size, image_size)
         if torch.cuda.is_available():
             test_input = test_input.cuda()
+        monitor = ResourceMonitor(interval=1.0)  # reference :243-244
+        monitor.start_monitoring()
         for _ in range(self.warmup_runs):
             model.predict(test_input, verbose=False)
         start = time.time()
@@ -116,11 +120,13 @@ class SpeedBenchmark:
             times.append(time.time() - t0)
             count += 1
         total = time.time() - start
+        monitor.stop_monitoring()
         fps = count / total
         results = {"model_size": model_size, "task": task, "image_size": image_size, "batch_size": batch_size,
                    "duration_seconds": total, "total_inferences": count,
                    "avg_inference_time": statistics.mean(times), "fps": fps, "images_per_second": fps * batch_size,
-                   "system_info": self.system_info}
+                   "resource_usage": monitor.get_average_usage(), "system_info": self.system_info}
+        monitor.save_history(self.output_dir / "resource_history.json")
         self._save_results(results, "throughput_benchmark.json")
         return results
 

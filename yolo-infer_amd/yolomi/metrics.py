@@ -2,9 +2,9 @@
 
 Semantics of the numbers the reference reads from Ultralytics val (`core/validator.py:339-352`:
 `results.box.map`, `.map50`, `.map75`, `.mp`, `.mr`): per class, predictions sorted by confidence, a prediction is
-a TP at IoU threshold t if it matches an unmatched same-class ground truth with IoU >= t (greedy by IoU, as
-upstream `match_predictions`); AP = area under the 101-point COCO-interpolated precision envelope; mAP = mean over
-classes present in the ground truth, mAP50-95 = mean over t ∈ {0.50, 0.55, ..., 0.95}.
+a TP at IoU threshold t as upstream `BaseValidator.match_predictions` decides it (ultralytics 8.3.x,
+engine/validator.py); AP = area under the 101-point COCO-interpolated precision envelope; mAP = mean over classes
+present in the ground truth, mAP50-95 = mean over t ∈ {0.50, 0.55, ..., 0.95}.
 """
 from __future__ import annotations
 
@@ -27,7 +27,13 @@ def box_iou(a: np.ndarray, b: np.ndarray) -> np.ndarray:
 
 
 def match_predictions(pred: np.ndarray, gt: np.ndarray) -> np.ndarray:
-    """pred (n,6) [xyxy,conf,cls], gt (m,5+) [xyxy,...,cls at col 5 or 4] → TP (n, 10) bool."""
+    """pred (n,6) [xyxy,conf,cls] in NMS (confidence-descending) order, gt (m,6) [xyxy,-,cls] → TP (n, 10) bool.
+
+    Upstream's non-scipy branch: the (gt, pred) pairs with IoU >= t and equal class, sorted by IoU descending; keep
+    each prediction's best pair (np.unique on the prediction index, which leaves the pairs in prediction-index
+    order); then each ground truth keeps its FIRST remaining pair in that order — the lowest prediction index, i.e.
+    the most confident prediction, not the highest IoU (upstream's re-sort by IoU between the two steps is commented
+    out).  Equal IoUs: upstream's `argsort()[::-1]` leaves their order to numpy's quicksort; here it is stable."""
     tp = np.zeros((len(pred), len(IOUV)), bool)
     if len(pred) == 0 or len(gt) == 0:
         return tp
@@ -36,11 +42,11 @@ def match_predictions(pred: np.ndarray, gt: np.ndarray) -> np.ndarray:
     for k, t in enumerate(IOUV):
         m = np.argwhere(iou >= t)
         if len(m):
-            v = iou[m[:, 0], m[:, 1]]
-            m = m[np.argsort(-v, kind="stable")]
-            m = m[np.unique(m[:, 1], return_index=True)[1]]
-            m = m[np.argsort(-iou[m[:, 0], m[:, 1]], kind="stable")]
-            m = m[np.unique(m[:, 0], return_index=True)[1]]
+            if len(m) > 1:
+                v = iou[m[:, 0], m[:, 1]]
+                m = m[np.argsort(-v, kind="stable")]
+                m = m[np.unique(m[:, 1], return_index=True)[1]]
+                m = m[np.unique(m[:, 0], return_index=True)[1]]
             tp[m[:, 1], k] = True
     return tp
 
