@@ -9,13 +9,16 @@ batch 8 per GPU, on the x3 plan — fp16 MFMAs on split operands with fp32-equiv
 meet SURVEY §7-1(b)'s fp16-mode tolerance (0.64 px, 1e-3 score; the plain f16 plan misses the score bar 3-4x,
 DESIGN.md §3), reported with its parity against the CPU oracle on the timed batch (`parity`) and beside the f16
 throughput plan measured in the same run (`f16_throughput_plan`).  (`--model n` gives config 2, `--dtype i8`
-config 4, `--model s --task segment --batch 4` config 5.)  One step = one `YOLO11Model.predict(batch)` call (the reference's timed unit: core/model.py:277-282,
+config 4, `--model s --task segment --batch 4` config 5.)
+
+One step = one `YOLO11Model.predict(batch)` call (the reference's timed unit: core/model.py:277-282,
 benchmarks/speed_benchmark.py:330-335) over synthetic U[0,1) 640x640 images already resident in HBM: input /255
 rule → forward (one HIP-graph replay) → decode → NMS → per-image Results (one D2H sync).
 Multi-GPU: one process per GPU (`--gpus N` without a launcher spawns the N ranks itself through
-torch.distributed.run, as a child process); rank 0 packs the weights once and broadcasts the blob over RCCL (xGMI,
-yolomi.dist.broadcast_blob); each rank runs its own batch shard; per step the ranks exchange one fp32 (all-reduce MAX:
-LoadTensor's /255 rule over the global batch, yolomi.dist.GlobalBatchMax) — "weak" scaling, 8 images per GPU.
+torch.distributed.run, as a child process); rank 0 packs the weights once and broadcasts the blob over RCCL (xGMI)
+through the C-ABI (yolomi.dist.rccl_broadcast_model → ym_broadcast_weights); each rank runs its own batch shard;
+per step the ranks exchange one fp32 (all-reduce MAX: LoadTensor's /255 rule over the global batch,
+yolomi.dist.GlobalBatchMax) — "weak" scaling, 8 images per GPU.
 
 Rank 0 prints ONE JSON line.  Extra fields: `roofline` (conv implicit-GEMM kernels, live HIP-event timing),
 `kernels` (per-kind device time and achieved HBM GB/s of the non-conv kernels), `cpu_baseline` (the oracle on host
@@ -344,11 +347,11 @@ def main():
         dist.init_process_group("nccl", device_id=dev)
 
     from core.model import YOLO11Model
-    from yolomi.dist import broadcast_blob, enable_global_rule
+    from yolomi.dist import enable_global_rule, rccl_broadcast_model
     from yolomi.plan import pack_model
     from yolomi.synth import synth_weights
 
-    # weights: packed once on rank 0, broadcast over RCCL as one uint8 blob.  i8: rank 0 first runs the PTQ
+    # weights: packed once on rank 0, broadcast over RCCL by the C-ABI.  i8: rank 0 first runs the PTQ
     # calibration (exact-f32 plan + torch.ao observers, yolomi.quant) on synthetic batches disjoint from the timed one
     t_init = time.perf_counter()
     qp = None
@@ -360,9 +363,13 @@ def main():
                        "fp8" if a.dtype == "f8" else a.backend)
         del ce
     blob = pack_model(a.model, a.task, synth_weights(a.model, a.task, 0), a.dtype, qp) if rank == 0 else None
-    if world > 1:
-        blob = broadcast_blob(blob, dev)
-    model = YOLO11Model(task=a.task, size=a.model, device=f"cuda:{local}", dtype=a.dtype, weights_blob=blob)
+
+    def make_model(**kw):
+        return YOLO11Model(task=a.task, size=a.model, device=f"cuda:{local}", dtype=a.dtype, **kw)
+    if world > 1:  # rank 0's blob to every rank's context over RCCL through the C-ABI (ym_broadcast_weights)
+        model = rccl_broadcast_model(make_model, blob, dev)
+    else:
+        model = make_model(weights_blob=blob)
     model.model.engine.lanes = a.lanes
     if world > 1:  # LoadTensor's /255 rule over the global batch: one fp32 all-reduce per step
         enable_global_rule(model)

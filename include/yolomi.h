@@ -93,7 +93,9 @@ int ym_load_weights(ym_ctx* ctx, const void* blob, size_t bytes);
  * `YOLO(model_path)` load of core/model.py:100-116 on every rank by ONE load on `root` and an RCCL broadcast over
  * xGMI.  `comm` is an ncclComm_t of the RCCL library the process has loaded (e.g. from ym_rccl_comm_init).  On
  * `root` the context must hold weights (ym_load_weights); every other rank's context receives the root's blob and
- * loads it.  Collective: every rank of `comm` calls it.  Synchronous. */
+ * loads it.  Collective: every rank of `comm` calls it.  Synchronous.  Every rank runs the same collectives whatever
+ * fails locally (a root without weights, a staging allocation or a load failing on some rank) and all ranks then
+ * return the same verdict, so no rank is left waiting inside RCCL. */
 int ym_broadcast_weights(ym_ctx* ctx, void* comm, int root, void* stream);
 /* Minimal RCCL bootstrap for C hosts without their own communicator: rank 0 creates the id, the host ships the 128
  * bytes to the other ranks (any channel), every rank creates its communicator on `device`. */

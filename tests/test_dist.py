@@ -96,3 +96,24 @@ def test_bench_refuses_mislabelled_world():
     p = subprocess.run([sys.executable, os.path.join(root, "bench.py"), "--gpus", "2", "--plumbing"],
                        capture_output=True, text=True, timeout=120, env=env)
     assert p.returncode == 2 and "WORLD_SIZE=1" in p.stderr
+
+
+@pytest.mark.gpu
+def test_rccl_cabi_broadcast_two_ranks():
+    """ym_broadcast_weights with a receiving rank: rank 1's empty context gets rank 0's blob over RCCL
+    and both compute the same detections.  Ranks go to separate GPUs when the box has two; on a one-GPU box both
+    share GPU 0 where RCCL allows it (its duplicate-GPU check may refuse: then skipped)."""
+    import subprocess
+    import sys
+    root = os.path.dirname(os.path.dirname(os.path.abspath(__file__)))
+    port = 29500 + (os.getpid() % 2000)
+    env = dict(os.environ, HSA_ENABLE_IPC_MODE_LEGACY=os.environ.get("HSA_ENABLE_IPC_MODE_LEGACY", "0"))
+    p = subprocess.run([sys.executable, "-m", "torch.distributed.run", "--nnodes=1", "--nproc-per-node=2",
+                        "--master-addr", "127.0.0.1", "--master-port", str(port),
+                        os.path.join(root, "tools", "rccl_bcast_check.py")],
+                       capture_output=True, text=True, timeout=240, env=env)
+    out = p.stdout + p.stderr
+    if p.returncode != 0 and "uplicate GPU" in out:
+        pytest.skip("RCCL refuses two ranks on one GPU")
+    assert p.returncode == 0, out[-3000:]
+    assert "digests equal: True" in out

@@ -445,6 +445,19 @@ def test_segment_slot_masks_equal_exact_size_masks():
     for ra, rb in zip(a, b):
         assert torch.equal(ra.boxes.data, rb.boxes.data)
         assert torch.equal(ra.masks.data, rb.masks.data)
+    # over the memory budget the exact-size path runs; the cap follows the counts down again; a mostly
+    # empty slot buffer is compacted — all three give the same results
+    os.environ["YM_MASK_BUDGET_MB"] = "0"
+    try:
+        c = m.predict(x, conf=0.25)
+    finally:
+        del os.environ["YM_MASK_BUDGET_MB"]
+    m._mask_cap = 128
+    d = m.predict(x, conf=0.25)  # 4 x 128 slots (210 MB), a few dozen kept: compacted
+    assert m._mask_cap <= 4 * max(len(r) for r in d) + 16  # next power of two of 2x the maximum
+    for ra, rc, rd in zip(a, c, d):
+        assert torch.equal(ra.masks.data, rc.masks.data) and torch.equal(ra.masks.data, rd.masks.data)
+        assert torch.equal(ra.boxes.data, rc.boxes.data) and torch.equal(ra.boxes.data, rd.boxes.data)
 
 
 def test_ultralytics_pt_model_path(tmp_path):

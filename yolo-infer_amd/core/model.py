@@ -10,6 +10,7 @@ LoadTensor's /255 rule).  There is no CPU fallback: a CPU device or a missing li
 from __future__ import annotations
 
 import logging
+import os
 import time
 from pathlib import Path
 from typing import Any, Dict, List, Optional, Union
@@ -41,6 +42,7 @@ class _ModelHandle:
 
     def __init__(self, state_dict: Dict[str, np.ndarray], engine: Engine, names: Dict[int, str]):
         self._sd = state_dict
+        self._weights_from = weights_from
         self._params = {k: torch.from_numpy(np.asarray(v)) for k, v in state_dict.items()
                         if not k.endswith("num_batches_tracked")}
         for p in self._params.values():
@@ -103,12 +105,13 @@ class YOLO11Model:
     def __init__(self, model_path: Optional[Union[str, Path]] = None, task: str = "detect", size: str = "n",
                  device: Optional[str] = None, verbose: bool = True, dtype: str = "f16", seed: int = 0,
                  weights_blob: Optional[bytes] = None, qparams: Optional[Dict] = None,
-                 state_dict: Optional[Dict[str, np.ndarray]] = None):
+                 state_dict: Optional[Dict[str, np.ndarray]] = None, weights_from: Optional[tuple] = None):
         """Extra keyword arguments over the reference: `dtype` ('f16' storage + fp32 accumulate, 'f32' = exact
         parity mode, or 'i8' = the PTQ int8 plan, which needs calibrated `qparams`; see
         optimization.quantization.PostTrainingQuantizer), `seed` of the synthetic weights used when no `model_path`
         is given, `weights_blob` = an already packed model (e.g. received over an RCCL broadcast from rank 0), and
-        `state_dict` = weights already in memory."""
+        `state_dict` = weights already in memory, `weights_from` = (rccl comm, root): receive the root rank's model
+        over RCCL (yolomi.dist.rccl_broadcast_model)."""
         self.task = task
         self.size = size
         self.device = device or self._get_default_device()
@@ -147,7 +150,7 @@ class YOLO11Model:
             dev = torch.device("cuda", torch.cuda.current_device())
         self._dev = dev
         try:
-            if self._blob is not None:
+            if self._blob is not None or self._weights_from is not None:
                 sd = self._sd or {}
             elif self._sd is not None:
                 sd = self._sd
@@ -163,7 +166,8 @@ class YOLO11Model:
                     logger.warning(f"{self.model_path or 'state_dict'} holds a yolo11{scale} {task} model "
                                    f"(nc={nc}); using it instead of size={self.size!r} task={self.task!r}")
                     self.size, self.task = scale, task
-            engine = Engine(self.size, self.task, sd, dev, self.dtype, blob=self._blob, qparams=self._qparams, nc=nc)
+            engine = Engine(self.size, self.task, sd, dev, self.dtype, blob=self._blob, qparams=self._qparams, nc=nc,
+                            receive=self._weights_from)
             names = COCO_NAMES if nc == 80 else {i: f"class{i}" for i in range(nc)}
         except Exception as e:
             logger.error(f"Failed to load model: {e}")
@@ -220,19 +224,36 @@ class YOLO11Model:
             # the masks of the first `cap` detections per image are enqueued behind the forward, reading the device
             # counts, so ONE device→host read returns counts and non-empty flags; a batch with more detections per
             # image than `cap` takes the exact-size two-read path (and raises `cap` for the next call)
+            # Memory: the slot buffer is B x cap x H x W bytes, so it is only used within
+            # YM_MASK_BUDGET_MB (256 MB by default; larger batches take the exact-size path), `cap` follows the recent
+            # detection counts down as well as up (the power of two >= 2x the last maximum, 16..max_det), and a
+            # mostly empty slot buffer is compacted before the Results views are taken, so results kept by the
+            # caller retain at most twice the bytes of their masks.
             H, W = im.shape[2:]
             cap = min(self._mask_cap, max_det)
-            mslots, flags = eng.masks_slots(out, counts[:B], cap, H, W)
-            fl = flags.tolist()  # the device→host sync of a segment predict call
-            n = fl[B * cap:]
-            if max(n) <= cap:
-                masks = mslots
-                keep = fl
-                offs = [b * cap for b in range(B + 1)]
+            budget = int(os.environ.get("YM_MASK_BUDGET_MB", "256")) << 20
+            fl = None
+            if B * cap * H * W <= budget:
+                mslots, flags = eng.masks_slots(out, counts[:B], cap, H, W)
+                fl = flags.tolist()  # the device→host sync of a segment predict call
+                n = fl[B * cap:]
             else:
-                self._mask_cap = min(max_det, 1 << (max(n) - 1).bit_length())
+                n = counts[:B].tolist()
+            if fl is not None and max(n) <= cap:
+                masks, keep = mslots, fl
+                offs = [b * cap for b in range(B + 1)]
+                if 2 * sum(n) < B * cap:  # compact the kept slots: one gather
+                    rows = [b * cap + i for b in range(B) for i in range(n[b])]
+                    masks = mslots.reshape(B * cap, H, W).index_select(
+                        0, torch.tensor(rows, dtype=torch.long, device=mslots.device))
+                    keep = [fl[r] for r in rows]
+                    offs = [0]
+                    for b in range(B):
+                        offs.append(offs[-1] + n[b])
+            else:
                 masks, nonempty, offs = eng.masks(out, n, H, W)
                 keep = nonempty.tolist()
+            self._mask_cap = max(16, min(max_det, 1 << (2 * max(max(n), 1) - 1).bit_length()))
         else:
             n = counts[:B].tolist()  # the device→host sync of a predict call
         if imsrc is not None:  # ops.scale_boxes back to each original image

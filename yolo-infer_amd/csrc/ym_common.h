@@ -213,7 +213,9 @@ struct QRec {
 // own L2.  Renumber so XCD x runs one contiguous range of logical blocks: neighbouring output tiles (whose 3x3
 // windows share input rows) then read those rows through the same L2 instead of fetching them from HBM once per
 // XCD.  A bijection for any grid size; placement only affects speed, never results.  Used by the stem (yolo11n
-// B=8: 22.7 -> 19.8 us); measured neutral-to-negative on the conv families, whose orders stay as they are.
+// B=8: 22.7 -> 19.8 us), the depthwise / SPPF / attention kernels, conv_small, conv_halo, conv_bneck and the int8
+// convs; conv_igemm / conv_lds / conv_dma (xcd_tile) and conv_stream (per-XCD group ranges) map their tiles
+// XCD-contiguously in their own tile maps — conv HBM traffic of yolo11s B=8 1.46x -> 1.21x the algorithmic bytes.
 __device__ __forceinline__ int ym_xcd_block(int bid, int n) {
   const int q = n >> 3, r = n & 7, x = bid & 7;
   return x * q + (x < r ? x : r) + (bid >> 3);

@@ -80,7 +80,7 @@ struct ym_ctx {
   int strides[4] = {8, 16, 32, 0};
   int input_buf = -1, anchor_buf = -1, proto_buf = -1, no = 0;
   float* d_lowres = nullptr;  // Segment mask assembly scratch (ym_masks)
-  char* d_misc = nullptr;     // ym_input_max statistics slots
+  char* d_misc = nullptr;     // 4 KB: ym_input_max statistics slots, ym_broadcast_weights control words
   size_t lowres_bytes = 0;
   std::vector<BufDesc> bufs;
   std::vector<Op> ops;
@@ -532,6 +532,7 @@ int ym_create(int device, const ym_model_desc* desc, ym_ctx** out) {
   hipError_t e = hipStreamCreateWithFlags(&c->cap_stream, hipStreamNonBlocking);
   for (int l = 1; l < kMaxLanes && e == hipSuccess; ++l) e = hipStreamCreateWithFlags(&c->lane_streams[l], hipStreamNonBlocking);
   if (e == hipSuccess) e = hipEventCreateWithFlags(&c->fork_ev, hipEventDisableTiming);
+  if (e == hipSuccess) e = hipMalloc(&c->d_misc, 4096);  // ym_input_max slots [0, 2048), broadcast control words
   for (int l = 1; l < kMaxLanes && e == hipSuccess; ++l) e = hipEventCreateWithFlags(&c->join_ev[l], hipEventDisableTiming);
   if (e != hipSuccess) {
     delete c;
@@ -902,7 +903,6 @@ int ym_infer(ym_ctx* c, const float* d_in, int B, int H, int W, const ym_infer_a
 int ym_input_max(ym_ctx* c, const float* d_in, size_t n, float* d_max, void* stream) {
   if (!c || !d_in || !d_max || n == 0) return fail(YM_EINVAL, "bad ym_input_max arguments");
   HIPCK(hipSetDevice(c->device));
-  if (!c->d_misc) HIPCK(hipMalloc(&c->d_misc, 4096));
   const hipError_t e = ym_launch_input_max(d_in, (long)n, reinterpret_cast<float*>(c->d_misc), d_max,
                                            static_cast<hipStream_t>(stream));
   if (e != hipSuccess) return fail(YM_EHIP, "input max: %s", hipGetErrorString(e));
@@ -1208,6 +1208,7 @@ struct Rccl {
   typedef int (*CommUserRank)(void*, int*);
   typedef int (*CommCount)(void*, int*);
   typedef int (*Broadcast)(const void*, void*, size_t, int, int, void*, hipStream_t);
+  typedef int (*AllReduce)(const void*, void*, size_t, int, int, void*, hipStream_t);
   typedef const char* (*ErrStr)(int);
   GetUniqueId get_id = nullptr;
   CommInitRank init = nullptr;
@@ -1215,6 +1216,7 @@ struct Rccl {
   CommUserRank user_rank = nullptr;
   CommCount count = nullptr;
   Broadcast bcast = nullptr;
+  AllReduce allreduce = nullptr;
   ErrStr err = nullptr;
   bool ok = false;
 };
@@ -1234,8 +1236,9 @@ const Rccl* rccl() {
     x.user_rank = (Rccl::CommUserRank)dlsym(h, "ncclCommUserRank");
     x.count = (Rccl::CommCount)dlsym(h, "ncclCommCount");
     x.bcast = (Rccl::Broadcast)dlsym(h, "ncclBroadcast");
+    x.allreduce = (Rccl::AllReduce)dlsym(h, "ncclAllReduce");
     x.err = (Rccl::ErrStr)dlsym(h, "ncclGetErrorString");
-    x.ok = x.get_id && x.init && x.destroy && x.user_rank && x.count && x.bcast && x.err;
+    x.ok = x.get_id && x.init && x.destroy && x.user_rank && x.count && x.bcast && x.allreduce && x.err;
     return x;
   }();
   return r.ok ? &r : nullptr;
@@ -1246,7 +1249,9 @@ const Rccl* rccl() {
     const int r_ = (x);                                                                                 \
     if (r_ != 0) return fail(YM_EHIP, "%s: RCCL error %d (%s)", #x, r_, R->err ? R->err(r_) : "?");     \
   } while (0)
-constexpr int kNcclUint8 = 1;  // ncclDataType_t ncclUint8
+constexpr int kNcclUint8 = 1, kNcclUint64 = 5;  // ncclDataType_t
+constexpr int kNcclSum = 0;                       // ncclRedOp_t
+constexpr size_t kBcastChunk = 16u << 20;         // blob bytes per broadcast (one staging buffer per rank)
 }  // namespace
 
 int ym_rccl_get_unique_id(ym_rccl_id* id) {
@@ -1276,8 +1281,14 @@ int ym_rccl_comm_destroy(void* comm) {
 }
 
 // The root rank's loaded blob (plan + weights, exactly the bytes its ym_load_weights received) goes to every rank
-// of `comm` as two RCCL broadcasts over xGMI — its size, then the bytes — and each non-root rank loads it into `c`
-// (ym_load_weights), so every rank ends with an identical model without touching the file system.  Synchronous.
+// of `comm` over RCCL (xGMI) and each non-root rank loads it into `c` (ym_load_weights), so every rank ends with an
+// identical model without touching the file system.  Synchronous.
+// Every rank issues the same sequence of collectives whatever fails locally, so no rank is left waiting inside RCCL
+// for one that returned early: (1) an all-reduce (sum) of {root's blob size (0: the root has no weights), ranks
+// whose staging buffer failed to allocate}; only if both are valid, (2) the blob broadcast in kBcastChunk pieces
+// and (3) an all-reduce of the per-rank copy / load failures, so every rank returns the same verdict.  Errors in the
+// arguments themselves (null pointers, root out of range) are identical on every rank and return before any
+// collective; an RCCL error is communicator-wide.
 int ym_broadcast_weights(ym_ctx* c, void* comm, int root, void* stream) {
   if (!c || !comm) return fail(YM_EINVAL, "null argument");
   const Rccl* R = rccl();
@@ -1286,40 +1297,58 @@ int ym_broadcast_weights(ym_ctx* c, void* comm, int root, void* stream) {
   RCCLCK(R->user_rank(comm, &rank));
   RCCLCK(R->count(comm, &n));
   if (root < 0 || root >= n) return fail(YM_EINVAL, "root %d out of range (%d ranks)", root, n);
-  if (rank == root && !c->loaded) return fail(YM_ESTATE, "the root context has no weights to broadcast");
-  HIPCK(hipSetDevice(c->device));
-  hipStream_t st = static_cast<hipStream_t>(stream);
-  unsigned long long nbytes = rank == root ? (unsigned long long)c->blob_host.size() : 0ull;
+  const hipStream_t st = static_cast<hipStream_t>(stream);
+  bool hip_ok = hipSetDevice(c->device) == hipSuccess;
+  // control words: the context's 4 KB scratch (allocated by ym_create, so nothing can fail before step 1)
+  unsigned long long* dctl = reinterpret_cast<unsigned long long*>(c->d_misc + 2048);
+  auto allreduce_sum = [&](unsigned long long* h, int cnt) -> int {
+    hip_ok = hip_ok && hipMemcpyAsync(dctl, h, 8 * cnt, hipMemcpyHostToDevice, st) == hipSuccess;
+    const int r = R->allreduce(dctl, dctl, cnt, kNcclUint64, kNcclSum, comm, st);
+    if (r) return r;
+    hip_ok = hip_ok && hipMemcpyAsync(h, dctl, 8 * cnt, hipMemcpyDeviceToHost, st) == hipSuccess &&
+             hipStreamSynchronize(st) == hipSuccess;
+    return 0;
+  };
+  const unsigned long long mine = (rank == root && c->loaded) ? (unsigned long long)c->blob_host.size() : 0ull;
+  const size_t chunk_cap = kBcastChunk;
   char* d = nullptr;
-  HIPCK(hipMalloc(&d, 256));
-  int rc = YM_OK;
+  const bool alloc_ok = hip_ok && hipMalloc(&d, chunk_cap) == hipSuccess;
+  unsigned long long h1[2] = {mine, alloc_ok ? 0ull : 1ull};
+  int r = allreduce_sum(h1, 2);  // (1)
   auto done = [&](int code) {
-    (void)hipFree(d);
+    if (d) (void)hipFree(d);
     return code;
   };
-  if (hipMemcpyAsync(d, &nbytes, 8, hipMemcpyHostToDevice, st) != hipSuccess) return done(fail(YM_EHIP, "size copy"));
-  int r = R->bcast(d, d, 8, kNcclUint8, root, comm, st);
-  if (r) return done(fail(YM_EHIP, "ncclBroadcast(size): %s", R->err(r)));
-  if (hipMemcpyAsync(&nbytes, d, 8, hipMemcpyDeviceToHost, st) != hipSuccess || hipStreamSynchronize(st) != hipSuccess)
-    return done(fail(YM_EHIP, "size read-back"));
-  (void)hipFree(d);
-  d = nullptr;
-  if (nbytes < kHdr * 4 || nbytes > (1ull << 34)) return fail(YM_EBLOB, "broadcast blob size %llu", nbytes);
-  HIPCK(hipMalloc(&d, nbytes));
-  if (rank == root && hipMemcpyAsync(d, c->blob_host.data(), nbytes, hipMemcpyHostToDevice, st) != hipSuccess)
-    return done(fail(YM_EHIP, "blob upload"));
-  r = R->bcast(d, d, nbytes, kNcclUint8, root, comm, st);
-  if (r) return done(fail(YM_EHIP, "ncclBroadcast(blob): %s", R->err(r)));
-  if (rank != root) {
-    std::vector<char> h(nbytes);
-    if (hipMemcpyAsync(h.data(), d, nbytes, hipMemcpyDeviceToHost, st) != hipSuccess ||
-        hipStreamSynchronize(st) != hipSuccess)
-      return done(fail(YM_EHIP, "blob read-back"));
-    rc = ym_load_weights(c, h.data(), nbytes);
-  } else if (hipStreamSynchronize(st) != hipSuccess) {
-    return done(fail(YM_EHIP, "stream sync"));
+  if (r) return done(fail(YM_EHIP, "ncclAllReduce(size): %s", R->err(r)));
+  const unsigned long long nbytes = h1[0];
+  if (nbytes == 0)
+    return done(fail(YM_ESTATE, rank == root ? "the root context has no weights to broadcast"
+                                             : "the root rank %d has no weights to broadcast", root));
+  if (nbytes < kHdr * 4 || nbytes > (1ull << 34)) return done(fail(YM_EBLOB, "broadcast blob size %llu", nbytes));
+  if (h1[1]) return done(fail(YM_ENOMEM, "%llu rank(s) could not allocate the %zu-byte staging buffer", h1[1], chunk_cap));
+  // (2) the blob, chunk by chunk through the staging buffer
+  std::vector<char> h;
+  if (rank != root) h.resize(nbytes);
+  bool copy_ok = hip_ok;
+  for (unsigned long long off = 0; off < nbytes; off += chunk_cap) {
+    const size_t len = (size_t)std::min<unsigned long long>(chunk_cap, nbytes - off);
+    if (rank == root)
+      copy_ok = copy_ok && hipMemcpyAsync(d, c->blob_host.data() + off, len, hipMemcpyHostToDevice, st) == hipSuccess;
+    r = R->bcast(d, d, len, kNcclUint8, root, comm, st);
+    if (r) return done(fail(YM_EHIP, "ncclBroadcast(blob): %s", R->err(r)));
+    if (rank != root)
+      copy_ok = copy_ok && hipMemcpyAsync(h.data() + off, d, len, hipMemcpyDeviceToHost, st) == hipSuccess;
+    copy_ok = copy_ok && hipStreamSynchronize(st) == hipSuccess;  // the staging buffer is reused
   }
-  return done(rc);
+  // (3) load on the receivers, then agree on the outcome
+  int rc = copy_ok ? YM_OK : fail(YM_EHIP, "blob staging copy failed");
+  if (rc == YM_OK && rank != root) rc = ym_load_weights(c, h.data(), nbytes);
+  unsigned long long h3[1] = {rc == YM_OK ? 0ull : 1ull};
+  r = allreduce_sum(h3, 1);
+  if (r) return done(fail(YM_EHIP, "ncclAllReduce(status): %s", R->err(r)));
+  if (rc != YM_OK) return done(rc);
+  if (h3[0]) return done(fail(YM_EBLOB, "the weight broadcast failed on %llu other rank(s)", h3[0]));
+  return done(YM_OK);
 }
 
 int ym_sync(ym_ctx* c) {

@@ -1,7 +1,8 @@
 """Multi-GPU plumbing for batch-sharded inference.
 
 One process per GPU.  At init rank 0 packs the model blob (BN-folded, NHWC packed weights + plan) and broadcasts it
-as ONE uint8 tensor (RCCL over xGMI on MI355X when the process group is `nccl`; gloo on CPU for tests).  Per batch,
+over RCCL (xGMI) through the C-ABI (`rccl_broadcast_model` → ym_broadcast_weights; `broadcast_blob` is the same
+exchange as one torch.distributed uint8 tensor, used by the gloo CPU tests).  Per batch,
 rank r runs images [r*B_local, (r+1)*B_local) of the global batch on its own stream/graph; the only exchange is one
 fp32 all-reduce (MAX) so that LoadTensor's /255 rule — a whole-batch decision in the reference — is taken over the
 global batch, not per shard (`GlobalBatchMax`).  The reference itself is single-device for inference
@@ -32,6 +33,31 @@ def broadcast_blob(blob: Optional[bytes], device: torch.device, src: int = 0) ->
         buf = torch.empty(int(n.item()), dtype=torch.uint8, device=device)
     dist.broadcast(buf, src)
     return blob if rank == src else bytes(buf.cpu().numpy())
+
+
+def rccl_broadcast_model(make_model, blob: Optional[bytes], device: torch.device, root: int = 0):
+    """The C-ABI path of the init-time weight broadcast (include/yolomi.h ym_broadcast_weights): the root's packed
+    blob goes to every rank over RCCL (xGMI) straight into each rank's context.  The RCCL unique id travels over the
+    default torch.distributed group; `make_model(**kw)` builds the rank's YOLO11Model (root: weights_blob=blob,
+    others: weights_from=(comm, root)).  Collective: every rank calls it."""
+    from . import lib as L
+    rank, world = dist.get_rank(), dist.get_world_size()
+    if rank == root and blob is None:
+        raise ValueError("the root rank must provide the blob")
+    uid = [L.rccl_unique_id() if rank == root else None]
+    dist.broadcast_object_list(uid, src=root)
+    comm = L.rccl_comm_init(device.index if device.index is not None else torch.cuda.current_device(), world, uid[0],
+                            rank)
+    try:
+        if rank == root:
+            model = make_model(weights_blob=blob)
+            model.model.engine.broadcast_weights(comm, root)
+        else:
+            model = make_model(weights_from=(comm, root))
+        torch.cuda.synchronize(device)
+    finally:
+        L.rccl_comm_destroy(comm)
+    return model
 
 
 def shard(global_batch: int, rank: int, world: int) -> Tuple[int, int]:

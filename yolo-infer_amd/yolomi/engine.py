@@ -27,9 +27,12 @@ def tune_cache_dir() -> str:
 
 class Engine:
     def __init__(self, scale: str, task: str, state_dict: Dict[str, np.ndarray], device: torch.device,
-                 dtype: str = "f16", blob: Optional[bytes] = None, qparams: Optional[Dict] = None, nc: int = 80):
-        """dtype: 'f16' (throughput), 'f32' (exact parity mode), 'i8' (PTQ int8) or 'f8' (PTQ fp8 e4m3); the
-        quantized plans need `qparams` from yolomi.quant.calibrate (backend 'fp8' for 'f8'), or a packed `blob`."""
+                 dtype: str = "f16", blob: Optional[bytes] = None, qparams: Optional[Dict] = None, nc: int = 80,
+                 receive: Optional[tuple] = None):
+        """dtype: 'x3' (split-f16 MFMA, the f16-tolerance plan), 'f16' (throughput), 'f32' (exact parity mode),
+        'i8' (PTQ int8) or 'f8' (PTQ fp8 e4m3); the quantized plans need `qparams` from yolomi.quant.calibrate
+        (backend 'fp8' for 'f8'), or a packed `blob`.  receive = (rccl comm, root): this rank's context receives the
+        root's blob over RCCL (ym_broadcast_weights, a collective the root joins with broadcast_weights())."""
         if device.type != "cuda":
             raise RuntimeError(f"the yolomi engine runs on a gfx950 GPU (got device {device}); there is no CPU path")
         self.scale, self.task, self.dtype = scale, task, dtype
@@ -37,9 +40,14 @@ class Engine:
         self.qparams = qparams
         self.graph = GraphBuilder(scale, task, nc=nc, quant=dtype in QUANT_DTYPES,
                                   fuse=fuse_default(dtype))
-        self.blob = blob if blob is not None else pack_graph(self.graph, state_dict, dtype, qparams)
-        self.rt = Runtime(device.index if device.index is not None else torch.cuda.current_device(), self.blob,
-                          scale=scale, task=task, dtype=dtype)
+        dev_index = device.index if device.index is not None else torch.cuda.current_device()
+        if receive is not None:  # a non-root rank: the model arrives over RCCL from the root's context
+            self.blob = None
+            self.rt = Runtime(dev_index, None, scale=scale, task=task, dtype=dtype)
+            self.rt.broadcast_weights(receive[0], receive[1], torch.cuda.current_stream(device).cuda_stream)
+        else:
+            self.blob = blob if blob is not None else pack_graph(self.graph, state_dict, dtype, qparams)
+            self.rt = Runtime(dev_index, self.blob, scale=scale, task=task, dtype=dtype)
         self.nm = self.graph.nm
         self._out: Dict[int, tuple] = {}
         # Per-shape conv tile tables: on the first call of each (B, H, W) a table is taken from the writable tune
@@ -54,17 +62,26 @@ class Engine:
         self._args_cache = {}
         self.tune_source: Dict[tuple, str] = {}
 
+    def broadcast_weights(self, comm: int, root: int = 0):
+        """The root's side of the RCCL weight broadcast (ym_broadcast_weights): every rank of `comm` calls it or
+        constructs its Engine with receive=(comm, root)."""
+        self.rt.broadcast_weights(comm, root, torch.cuda.current_stream(self.device).cuda_stream)
+
     def _table_name(self, B, H, W):
         return f"{self.scale}-{self.task}-{self.dtype}-b{B}-{H}x{W}.json"
 
     def _load_table(self, B, H, W):
-        """The committed table first (the one the tests and the bench pin), then this machine's tune cache.  A table
-        is used only when its version, op-name list, device architecture and conv-config catalogue size
-        (ym_num_conv_cfgs: the id space its entries index) all match this engine."""
+        """The committed table first (the one the tests and the bench pin), then this machine's tune cache — so a
+        table this machine tuned (ym_tune) for a shape that also has a committed table is cached but not read back
+        unless YM_PREFER_CACHE=1 puts the cache first.  A table is used only when its version, op-name list, device
+        architecture and conv-config catalogue size (ym_num_conv_cfgs: the id space its entries index) all match."""
         name = self._table_name(B, H, W)
         arch = torch.cuda.get_device_properties(self.device).gcnArchName
         ops = [op.name for op in self.graph.ops]
-        for tag, d in (("committed", TUNED_DIR), ("cache", tune_cache_dir())):
+        order = [("committed", TUNED_DIR), ("cache", tune_cache_dir())]
+        if os.environ.get("YM_PREFER_CACHE", "0") == "1":
+            order.reverse()
+        for tag, d in order:
             p = os.path.join(d, name)
             try:
                 t = json.load(open(p))

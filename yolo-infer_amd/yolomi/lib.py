@@ -7,6 +7,7 @@ from __future__ import annotations
 import ctypes as C
 import os
 from pathlib import Path
+from typing import Optional
 
 LIB_PATH = Path(__file__).resolve().parent / "libyolomi.so"
 
@@ -126,8 +127,10 @@ def rccl_comm_destroy(comm: int):
 class Runtime:
     """One ym_ctx on one device holding one packed model."""
 
-    def __init__(self, device_index: int, blob: bytes, scale: str = None, task: str = None, dtype: str = None):
-        """scale / task / dtype (optional): what the blob must be (ym_model_desc; a mismatch raises YMError)."""
+    def __init__(self, device_index: int, blob: Optional[bytes], scale: str = None, task: str = None,
+                 dtype: str = None):
+        """scale / task / dtype (optional): what the blob must be (ym_model_desc; a mismatch raises YMError).
+        blob None: an empty context that receives its model through broadcast_weights."""
         self.lib = load_library()
         self.ctx = C.c_void_p()
         self.device_index = device_index
@@ -136,7 +139,9 @@ class Runtime:
         desc.task = TASK_CODES.get(task, 0)
         desc.dtype = DTYPE_CODES.get(dtype, 0)
         _check(self.lib.ym_create(device_index, C.byref(desc), C.byref(self.ctx)))
-        self.load(blob)
+        self.n_ops, self.op_names = 0, []
+        if blob is not None:
+            self.load(blob)
 
     def load(self, blob: bytes):
         buf = C.create_string_buffer(blob, len(blob))
