@@ -107,13 +107,15 @@ def test_rccl_cabi_broadcast_two_ranks():
     import sys
     root = os.path.dirname(os.path.dirname(os.path.abspath(__file__)))
     port = 29500 + (os.getpid() % 2000)
-    env = dict(os.environ, HSA_ENABLE_IPC_MODE_LEGACY=os.environ.get("HSA_ENABLE_IPC_MODE_LEGACY", "0"))
+    env = dict(os.environ, HSA_ENABLE_IPC_MODE_LEGACY=os.environ.get("HSA_ENABLE_IPC_MODE_LEGACY", "0"),
+               NCCL_DEBUG="WARN")
     p = subprocess.run([sys.executable, "-m", "torch.distributed.run", "--nnodes=1", "--nproc-per-node=2",
                         "--master-addr", "127.0.0.1", "--master-port", str(port),
                         os.path.join(root, "tools", "rccl_bcast_check.py")],
                        capture_output=True, text=True, timeout=240, env=env)
     out = p.stdout + p.stderr
-    if p.returncode != 0 and "uplicate GPU" in out:
-        pytest.skip("RCCL refuses two ranks on one GPU")
+    one_gpu = torch.cuda.device_count() < 2
+    if p.returncode != 0 and one_gpu and ("uplicate GPU" in out or "invalid usage" in out):
+        pytest.skip("RCCL refuses two ranks on one GPU (ncclCommInitRank: invalid usage)")
     assert p.returncode == 0, out[-3000:]
     assert "digests equal: True" in out

@@ -779,3 +779,57 @@ def test_decode_staged_variant_bitwise_equals_register_variant():
         outs.append(np.load(path))
     assert outs[0].shape == outs[1].shape and outs[0].shape[0] > 100
     assert np.array_equal(outs[0], outs[1])
+
+
+# ------------------------------------------------------------------------------------------------ 1280² (N = 1600)
+def test_f16_1280_attention_and_layers():
+    """benchmark_speed's 1280² size (core/validator.py:188): C2PSA attention over N = 1600 tokens runs the block-wise
+    MFMA attention (csrc/ym_misc.hip attn_psa_flash, online softmax) — equal to the scalar kernel within fp16
+    rounding, and every checked layer within the f16 plan's 1e-2 of the oracle."""
+    import subprocess
+    import sys
+    x = make_input("uniform", (8001,), 1280)
+    _, y, ex = oracle().raw(x, keep=(9, 10, 13, 22))
+    m = model("n", "f16")
+    eng = m.model.engine
+    eng.run(x.to(DEV), use_graph=False)
+    l10 = None
+    for b in eng.graph.buffers:
+        if b.name in ("L9", "L10", "L13", "L22"):
+            ref = ex["saved"][int(b.name[1:])].permute(0, 2, 3, 1)
+            got = eng.read_buffer(b.id, 1)
+            rel = (got - ref).abs().max().item() / ref.abs().max().item()
+            assert rel < 1e-2, (b.name, rel)
+            if b.name == "L10":
+                l10 = got
+    # the same layer with the scalar attention kernel (YM_ATTN_FLASH_OFF is read once per process: a child run)
+    root = os.path.dirname(os.path.dirname(os.path.abspath(__file__)))
+    out = os.path.join(root, "gpurun_out") if os.path.isdir(os.path.join(root, "gpurun_out")) else "/tmp"
+    path = os.path.join(out, "l10_scalar.npy")
+    code = ("import sys, numpy as np; sys.path[:0] = [%r, %r];"
+            "from tests.golden.make_golden import make_input; from core.model import YOLO11Model;"
+            "m = YOLO11Model(size='n', device='cuda:0', dtype='f16'); e = m.model.engine;"
+            "e.run(make_input('uniform', (8001,), 1280).cuda(), use_graph=False);"
+            "b = [b for b in e.graph.buffers if b.name == 'L10'][0];"
+            "np.save(sys.argv[1], e.read_buffer(b.id, 1).numpy())" % (os.path.join(root, "yolo-infer_amd"), root))
+    subprocess.run([sys.executable, "-c", code, path], check=True, timeout=240,
+                   env=dict(os.environ, YM_ATTN_FLASH_OFF="1"))
+    ls = torch.from_numpy(np.load(path))
+    assert (ls - l10).abs().max().item() / ls.abs().max().item() < 5e-3
+
+
+@pytest.mark.parametrize("dtype", ["f32", "f16"])
+def test_max_nms_truncation_1280_conf0001(dtype):
+    """The validation default conf 0.001 (core/validator.py:91) at 1280²: more than max_nms = 30000 candidates per
+    image, so nms_image takes the `n > max_nms` branch (top 30000 by score, csrc/ym_misc.hip) exactly as the oracle's
+    argsort[:max_nms] does.  f32 plan: every detection within 1e-3; f16 plan: its own tolerance (1 px / 1e-2)."""
+    x = make_input("uniform", (8101,), 1280)
+    _, y, _ = oracle().raw(x)
+    n_cand = int((y[0, 4:84].amax(0) > 0.001).sum())
+    assert n_cand > 30000, n_cand
+    ref = oracle().predict(x, conf=0.001)
+    res = model("n", dtype).predict(x.to(DEV), conf=0.001)
+    if dtype == "f32":
+        check(ref, res, 0.001, 0.7, 1e-3, 1e-3)
+    else:
+        check(ref, res, 0.001, 0.7, 1.0, 1e-2, min_frac=0.9)

@@ -150,3 +150,16 @@ def test_x3_conv_configs_match_oracle(cfg):
                 assert _rel(eng.read_buffer(b.id, 2), ref) < 1e-4, (cfg, b.name)
     finally:
         eng._tuned.discard((2, 640, 640))
+
+
+def test_x3_1280_n1600_attention_and_max_nms():
+    """x3 at 1280² (N = 1600: the block-wise x3 MFMA attention) and conf 0.001 (> max_nms candidates): every
+    detection within the SURVEY f16-mode tolerance, and the attention layer within 1e-4 of the oracle."""
+    x = make_input("uniform", (8101,), 1280)
+    _, y, ex = oracle().raw(x, keep=(10,))
+    eng = model("n").model.engine
+    eng.run(x.to(DEV), use_graph=False)
+    b = [b for b in eng.graph.buffers if b.name == "L10"][0]
+    assert _rel(eng.read_buffer(b.id, 1), ex["saved"][10].permute(0, 2, 3, 1)) < 1e-4
+    assert int((y[0, 4:84].amax(0) > 0.001).sum()) > 30000
+    check(oracle().predict(x, conf=0.001), model("n").predict(x.to(DEV), conf=0.001), conf=0.001)

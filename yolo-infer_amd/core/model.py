@@ -42,7 +42,6 @@ class _ModelHandle:
 
     def __init__(self, state_dict: Dict[str, np.ndarray], engine: Engine, names: Dict[int, str]):
         self._sd = state_dict
-        self._weights_from = weights_from
         self._params = {k: torch.from_numpy(np.asarray(v)) for k, v in state_dict.items()
                         if not k.endswith("num_batches_tracked")}
         for p in self._params.values():
@@ -122,6 +121,7 @@ class YOLO11Model:
         self._blob = weights_blob
         self._qparams = qparams
         self._sd = state_dict
+        self._weights_from = weights_from
         self.optimization_history: List[Dict[str, Any]] = []
         # batch-sharded multi-GPU (yolomi.dist.enable_global_rule): callable x -> (1,) device max of the GLOBAL batch
         self.global_batch_max = None

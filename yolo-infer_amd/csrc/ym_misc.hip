@@ -670,6 +670,153 @@ __global__ __launch_bounds__(256) void attn_psa_x3(const AttnArgs a) {
   }
 }
 
+// Any N (the 1280² input: 1600 tokens, core/validator.py:188): the MFMA attention with the keys in blocks of 256
+// and an online softmax (running max / sum per query, O rescaled when the max grows), so neither the scores nor
+// V^T of the whole (image, head) need to fit: per block, V^T (f16, or hi / lo planes for x3) is staged in LDS, K
+// fragments stream from global; pe(v) reads its 3x3 taps from global.  X3: every product split as in attn_psa_x3.
+template <bool X3>
+__global__ __launch_bounds__(256) void attn_psa_flash(const AttnArgs a) {
+  constexpr int KB = 256, NKT = KB / 16, LDV = KB + 4;
+  typedef typename std::conditional<X3, P2, f16>::type T;
+  extern __shared__ __attribute__((aligned(16))) f16 vt[];  // [X3 ? 2 : 1][64][LDV]
+  f16* vtl = vt + 64 * LDV;
+  const int N = a.N;
+  const int nqb = (N + 63) / 64;
+  const int vb = ym_xcd_block(blockIdx.x, gridDim.x);
+  const int qb = vb % nqb, bh = vb / nqb;
+  const int h = bh % a.nh, b = bh / a.nh;
+  const int tid = threadIdx.x, lane = tid & 63, wave = tid >> 6;
+  const int g = lane >> 4, c = lane & 15;
+  const T* qkv = static_cast<const T*>(a.qkv);
+  const size_t img = (size_t)b * a.q_P;
+  const int hq = a.q_coff + h * 128;  // per head: q 32, k 32, v 64 channels
+  auto frag = [&](const T* p) -> HL {  // 8 channels of one token (hi and, for x3, lo)
+    if constexpr (X3) return ym_load_hl(p);
+    else return HL{Vec8<f16>::load(p), Vec8<f16>::zero()};
+  };
+  const int q = qb * 64 + wave * 16 + c;
+  HL qf{Vec8<f16>::zero(), Vec8<f16>::zero()};
+  if (q < N) qf = frag(qkv + (img + q) * a.q_ctot + hq + 8 * g);
+  const float sl2 = a.scale * 1.4426950408889634f;
+  float m = -INFINITY, l = 0.f;  // running max (log2 units) and this lane's partial sum of its query's weights
+  f32x4 o[4];
+#pragma unroll
+  for (int dt = 0; dt < 4; ++dt) o[dt] = f32x4{0.f, 0.f, 0.f, 0.f};
+  for (int k0 = 0; k0 < N; k0 += KB) {
+    __syncthreads();  // every wave is done with the previous block's V^T
+    for (int i = tid; i < KB * 8; i += 256) {
+      const int key = i >> 3, ch = i & 7;
+      HL v{Vec8<f16>::zero(), Vec8<f16>::zero()};
+      if (k0 + key < N) v = frag(qkv + (img + k0 + key) * a.q_ctot + hq + 64 + 8 * ch);
+#pragma unroll
+      for (int e = 0; e < 8; ++e) {
+        vt[(8 * ch + e) * LDV + key] = v.hi[e];
+        if constexpr (X3) vtl[(8 * ch + e) * LDV + key] = v.lo[e];
+      }
+    }
+    float s[NKT][4];
+#pragma unroll
+    for (int t = 0; t < NKT; ++t) {
+      const int key = k0 + 16 * t + c;
+      HL kf{Vec8<f16>::zero(), Vec8<f16>::zero()};
+      if (key < N) kf = frag(qkv + (img + key) * a.q_ctot + hq + 32 + 8 * g);
+      f32x4 d = f32x4{0.f, 0.f, 0.f, 0.f};
+      if constexpr (X3) {
+        d = __builtin_amdgcn_mfma_f32_16x16x32_f16(kf.lo, qf.hi, d, 0, 0, 0);
+        d = __builtin_amdgcn_mfma_f32_16x16x32_f16(kf.hi, qf.lo, d, 0, 0, 0);
+      }
+      d = __builtin_amdgcn_mfma_f32_16x16x32_f16(kf.hi, qf.hi, d, 0, 0, 0);
+#pragma unroll
+      for (int r = 0; r < 4; ++r) s[t][r] = k0 + 16 * t + 4 * g + r < N ? d[r] * sl2 : -INFINITY;
+    }
+    float mb = -INFINITY;
+#pragma unroll
+    for (int t = 0; t < NKT; ++t)
+#pragma unroll
+      for (int r = 0; r < 4; ++r) mb = fmaxf(mb, s[t][r]);
+    mb = fmaxf(mb, __shfl_xor(mb, 16));
+    mb = fmaxf(mb, __shfl_xor(mb, 32));
+    const float mn = fmaxf(m, mb);
+    const float sc = exp2f(m - mn);  // 0 on the first block (m = -inf)
+    m = mn;
+    l *= sc;
+#pragma unroll
+    for (int dt = 0; dt < 4; ++dt) o[dt] *= sc;
+#pragma unroll
+    for (int t = 0; t < NKT; ++t)
+#pragma unroll
+      for (int r = 0; r < 4; ++r) {
+        s[t][r] = exp2f(s[t][r] - mn);
+        l += s[t][r];
+      }
+    __syncthreads();  // this block's V^T is staged
+#pragma unroll
+    for (int ks = 0; ks < NKT / 2; ++ks) {
+      h8v ph, pl;
+#pragma unroll
+      for (int r = 0; r < 4; ++r) {
+        ph[r] = (f16)s[2 * ks][r];
+        ph[4 + r] = (f16)s[2 * ks + 1][r];
+        if constexpr (X3) {
+          pl[r] = (f16)(s[2 * ks][r] - (float)ph[r]);
+          pl[4 + r] = (f16)(s[2 * ks + 1][r] - (float)ph[4 + r]);
+        }
+      }
+#pragma unroll
+      for (int dt = 0; dt < 4; ++dt) {
+        const int row = (16 * dt + c) * LDV + 32 * ks + 4 * g;
+        const f16x4 hlo = *reinterpret_cast<const f16x4*>(vt + row), hhi = *reinterpret_cast<const f16x4*>(vt + row + 16);
+        const h8v vh = {hlo[0], hlo[1], hlo[2], hlo[3], hhi[0], hhi[1], hhi[2], hhi[3]};
+        if constexpr (X3) {
+          const f16x4 llo = *reinterpret_cast<const f16x4*>(vtl + row), lhi = *reinterpret_cast<const f16x4*>(vtl + row + 16);
+          const h8v vl = {llo[0], llo[1], llo[2], llo[3], lhi[0], lhi[1], lhi[2], lhi[3]};
+          o[dt] = __builtin_amdgcn_mfma_f32_16x16x32_f16(vl, ph, o[dt], 0, 0, 0);
+          o[dt] = __builtin_amdgcn_mfma_f32_16x16x32_f16(vh, pl, o[dt], 0, 0, 0);
+        }
+        o[dt] = __builtin_amdgcn_mfma_f32_16x16x32_f16(vh, ph, o[dt], 0, 0, 0);
+      }
+    }
+  }
+  l += __shfl_xor(l, 16);
+  l += __shfl_xor(l, 32);
+  const float rs = 1.0f / l;
+  if (q >= N) return;
+  const int y = q / a.W, x = q - (q / a.W) * a.W;
+  T* dst = static_cast<T*>(a.dst) + ((size_t)b * a.d_P + q) * a.d_ctot + a.d_coff + h * 64;
+#pragma unroll
+  for (int dt = 0; dt < 4; ++dt) {
+    const int d0 = 16 * dt + 4 * g;
+    float pe[4];
+#pragma unroll
+    for (int r = 0; r < 4; ++r) pe[r] = a.pe_b[h * 64 + d0 + r];
+#pragma unroll
+    for (int t = 0; t < 9; ++t) {
+      const int iy = y + t / 3 - 1, ix = x + t % 3 - 1;
+      if ((unsigned)iy >= (unsigned)a.H || (unsigned)ix >= (unsigned)a.W) continue;
+      const T* vp = qkv + (img + iy * a.W + ix) * a.q_ctot + hq + 64 + d0;
+      float v[4];
+      if constexpr (X3) {
+        ym_p2_load4(vp, v);
+      } else {
+        const f16x4 hv = *reinterpret_cast<const f16x4*>(vp);
+#pragma unroll
+        for (int r = 0; r < 4; ++r) v[r] = (float)hv[r];
+      }
+      const f32x4 w = *reinterpret_cast<const f32x4*>(a.pe_w + t * a.C + h * 64 + d0);
+#pragma unroll
+      for (int r = 0; r < 4; ++r) pe[r] = fmaf(v[r], w[r], pe[r]);
+    }
+    float out[4];
+#pragma unroll
+    for (int r = 0; r < 4; ++r) out[r] = o[dt][r] * rs + pe[r];
+    if constexpr (X3) {
+      ym_p2_store4(dst + d0, out);
+    } else {
+      *reinterpret_cast<f16x4*>(dst + d0) = f16x4{(f16)out[0], (f16)out[1], (f16)out[2], (f16)out[3]};
+    }
+  }
+}
+
 // ------------------------------------------------------------------------------------------------- decode
 // Detect._inference + the candidate stage of non_max_suppression; 4 lanes per anchor (lane s: DFL side s and a
 // quarter of the classes):
@@ -1228,6 +1375,15 @@ hipError_t launch_attn_mfma(const AttnArgs& a, hipStream_t st) {
   return hipGetLastError();
 }
 
+template <bool X3>
+hipError_t launch_attn_flash(const AttnArgs& a, hipStream_t st) {
+  static const bool off = [] { const char* e = getenv("YM_ATTN_FLASH_OFF"); return e && *e == '1'; }();
+  if (off) return hipErrorInvalidValue;
+  const size_t lds = (size_t)(X3 ? 2 : 1) * 64 * (256 + 4) * sizeof(f16);
+  hipLaunchKernelGGL((attn_psa_flash<X3>), dim3(a.B * a.nh * ((a.N + 63) / 64)), dim3(256), lds, st, a);
+  return hipGetLastError();
+}
+
 template <int NKT>
 hipError_t launch_attn_x3(const AttnArgs& a, hipStream_t st) {
   const size_t lds = (size_t)2 * 64 * (16 * NKT + 4) * sizeof(f16) + 640 * sizeof(float);
@@ -1244,6 +1400,8 @@ hipError_t ym_launch_attn(int dtype, const AttnArgs& a, hipStream_t st) {
     if (nkt <= 16) return launch_attn_x3<16>(a, st);
     if (nkt <= 26) return launch_attn_x3<26>(a, st);
     if (nkt <= 32) return launch_attn_x3<32>(a, st);
+    const hipError_t e = launch_attn_flash<true>(a, st);
+    if (e != hipErrorInvalidValue) return e;
   }
   if (dtype == YM_DT_F16 && a.kd == 32 && a.hd == 64 && !a.raw && a.nh * 128 <= a.q_ctot && a.d_ctot % 4 == 0 &&
       a.d_coff % 4 == 0 && a.q_ctot % 8 == 0 && a.q_coff % 8 == 0) {
@@ -1252,6 +1410,8 @@ hipError_t ym_launch_attn(int dtype, const AttnArgs& a, hipStream_t st) {
     if (nkt <= 16) return launch_attn_mfma<16>(a, st);
     if (nkt <= 26) return launch_attn_mfma<26>(a, st);
     if (nkt <= 32) return launch_attn_mfma<32>(a, st);
+    const hipError_t e = launch_attn_flash<false>(a, st);  // N > 512 tokens (inputs above 724 px)
+    if (e != hipErrorInvalidValue) return e;  // (YM_ATTN_FLASH_OFF=1: the scalar kernel, tests)
   }
   if (a.kd > AKD || a.hd > AHD) return hipErrorInvalidValue;
   if (dtype == YM_DT_X3) return launch_attn_t<P2>(a, st);
