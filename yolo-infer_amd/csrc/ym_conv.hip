@@ -606,6 +606,8 @@ __global__ __launch_bounds__(256) void conv_lds(const ConvArgs a) {
 
 template <typename M, typename OutT, int BM, int BN>
 hipError_t launch_lds(ConvArgs a, int kind, hipStream_t st) {
+  // x3: the 64-deep logical stage needs a storage Kpad of a multiple of 128 (pair-chunk rows are padded to 64)
+  if (std::is_same<M, x3_t>::value && a.Kpad % 128) return hipErrorInvalidValue;
   const int tiles_m8 = ((a.M + BM - 1) / BM + 7) / 8 * 8;
   a.tiles_n = (a.N + BN - 1) / BN;
   const dim3 grid(tiles_m8 * a.tiles_n);
@@ -766,6 +768,12 @@ hipError_t ym_launch_conv(int dtype, int out_f32, const ConvArgs& a, int cfg, hi
   int id = (cfg >= 0 && cfg < kNumAllCfg) ? cfg : choose_cfg(a);
   if (id >= kNumCfg && dtype == YM_DT_F32) id = choose_cfg(a);  // LDS variants: f16 and x3 plans
   if (dtype == YM_DT_F16) return out_f32 ? launch_id<f16, float>(id, a, kind, st) : launch_id<f16, f16>(id, a, kind, st);
-  if (dtype == YM_DT_X3) return out_f32 ? launch_id<x3_t, float>(id, a, kind, st) : launch_id<x3_t, P2>(id, a, kind, st);
+  if (dtype == YM_DT_X3) {
+    auto go = [&](int i) { return out_f32 ? launch_id<x3_t, float>(i, a, kind, st) : launch_id<x3_t, P2>(i, a, kind, st); };
+    const hipError_t e = go(id);
+    // an LDS tile whose 64-deep stage does not divide this op's K: the tuner skips it (strict), a pinned table
+    // falls back to the heuristic direct-to-register tile
+    return (e == hipErrorInvalidValue && !strict && id >= kNumCfg) ? go(choose_cfg(a)) : e;
+  }
   return launch_id<float, float>(id, a, kind, st);
 }

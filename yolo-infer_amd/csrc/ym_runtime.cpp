@@ -580,9 +580,10 @@ static void build_schedule(ym_ctx* c) {
   // box, bench.py device img/s, serial -> 4 streams): yolo11s f16 B=8 8.06k -> 8.51k, yolo11n f16 12.1k -> 13.0k (the
   // Detect-head chains of one level overlap the neck's 20x20 / 40x40 layers, whose launches leave most CUs idle), but
   // yolo11s-seg f16 B=4 4.35k -> 3.84k, yolo11n int8 8.62k -> 7.39k and fp8 9.25k -> 7.87k (their head / requant /
-  // float-island kernels contend with the neck instead of filling idle CUs).
+  // float-island kernels contend with the neck instead of filling idle CUs).  Round 3, x3 detect plans: yolo11s B=8
+  // 4.47k -> 4.68k predict img/s, yolo11n device 6.88k -> 7.31k: on by default too.
   const char* env = getenv("YM_BRANCHES");
-  const int def = c->dtype == YM_DT_F16 && c->task == 0 ? S : 1;
+  const int def = (c->dtype == YM_DT_F16 || c->dtype == YM_DT_X3) && c->task == 0 ? S : 1;
   const int maxs = env && *env ? (atoi(env) < 1 ? 1 : (atoi(env) > S ? S : atoi(env))) : def;
   for (int i = 0; i < nop; ++i) {
     rw(c->ops[i], rd, wr);

@@ -14,7 +14,7 @@ s_in·s_w per output channel and the int32 zero-point correction Σ_k (128 - z_i
 
 x3 plans (dtype "x3", the f16-tolerance plan): activations in the pair layout of csrc/ym_common.h (every 8-channel
 chunk as fp16 hi = fp16(x) then lo = fp16(x - hi)); every conv weight row except the stem's likewise, [hi x8 | lo x8]
-per K chunk, so r[21] (Kpad) counts fp16 storage elements: 2·K padded to 128.  The stem keeps fp32 rows.
+per K chunk, so r[21] (Kpad) counts fp16 storage elements: 2·K padded to 64.  The stem keeps fp32 rows.
 
 Blob layout (int32 little-endian; parsed by `csrc/ym_runtime.cpp:ym_load_weights`):
   header[32] | buffers[nbuf][8] | ops[nop][32] | names[nop][48 bytes] | pad to 256 | weights
@@ -193,7 +193,7 @@ def pack_graph(g: GraphBuilder, sd: Dict[str, np.ndarray], dtype: str = "f16", q
                 hi = wr.astype(np.float16)
                 lo = (wr - hi.astype(np.float32)).astype(np.float16)
                 K2 = 2 * K
-                Kpad = (K2 + 2 * BK - 1) // (2 * BK) * (2 * BK)  # logical K padded to the 64-deep step
+                Kpad = (K2 + BK - 1) // BK * BK  # the 64-deep storage step (32 logical K)
                 wp = np.zeros((N, Kpad), np.float16)
                 wp[:, :K2] = np.stack([hi, lo], axis=2).reshape(N, K2)
             src1 = a["src1"]
