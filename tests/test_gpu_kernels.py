@@ -1,0 +1,60 @@
+"""GPU checks of individual kernel variants against a float64 torch reference computed from the kernel's own input
+buffer (read back from the plan's arena), so each variant is judged on its own arithmetic, not on upstream error.
+
+Tolerances (written here): fp32-storage plans (f32, x3) within 2e-6 of the output's max magnitude — the kernels
+accumulate in fp32 with fmaf, the reference in float64; f16 within 2e-3 (one fp16 rounding of the output)."""
+import numpy as np
+import pytest
+import torch
+import torch.nn.functional as F
+
+from bench import synthetic_batch
+from yolomi.plan import _dw_weights
+from yolomi.synth import synth_weights
+
+pytestmark = pytest.mark.gpu
+DEV = torch.device("cuda", 0)
+TOL = {"f32": 2e-6, "x3": 2e-6, "f16": 2e-3}
+
+
+_models = {}
+
+
+@pytest.mark.parametrize("mode", ["0", "1", "2"])
+@pytest.mark.parametrize("scale,B", [("s", 8), ("n", 8), ("s", 1)])
+@pytest.mark.parametrize("dtype", ["x3", "f16", "f32"])
+def test_dwconv_variants_match_float64(scale, B, dtype, mode):
+    """csrc/ym_misc.hip depthwise 3x3 (Detect cv3 DWConv) in each YM_DW_MODE: 0 the LDS-tile kernel
+    (default; partial tiles at 20² / 40²), 1 the row variant and one-pixel kernel, 2 the column strips (rows per
+    thread 2 or 4 by grid size), on every dwconv of the Detect head at 640² (80², 40², 20² maps), eager forwards:
+    output = SiLU(bias + Σ_taps w·x) of the stored input."""
+    from core.model import YOLO11Model
+    import os
+    sd = synth_weights(scale, "detect", 0)
+    if (scale, dtype) not in _models:
+        _models[(scale, dtype)] = YOLO11Model(task="detect", size=scale, device="cuda:0", dtype=dtype, verbose=False)
+    eng = _models[(scale, dtype)].model.engine
+    x = synthetic_batch(B, 640, 77, DEV)
+    os.environ["YM_DW_MODE"] = mode
+    try:
+        eng.run(x, use_graph=False)
+    finally:
+        del os.environ["YM_DW_MODE"]
+    n = 0
+    for op in eng.graph.ops:
+        if op.kind != "dwconv":
+            continue
+        a = op.args
+        src = eng.read_buffer(a["src"].buf.id, B)[..., a["src"].coff:a["src"].coff + a["C"]]
+        got = eng.read_buffer(a["dst"].buf.id, B)[..., a["dst"].coff:a["dst"].coff + a["C"]].double()
+        w9, b = _dw_weights(a["wkey"], sd)  # [9][C] fp32, [C]
+        C = a["C"]
+        w = torch.from_numpy(np.ascontiguousarray(w9.T)).double().reshape(C, 1, 3, 3)
+        ref = F.conv2d(src.double().permute(0, 3, 1, 2), w, torch.from_numpy(b).double(), padding=1, groups=C)
+        if a["act"]:
+            ref = F.silu(ref)
+        ref = ref.permute(0, 2, 3, 1)
+        err = (got - ref).abs().max().item() / ref.abs().max().item()
+        assert err < TOL[dtype], (op.name, err)
+        n += 1
+    assert n == 6

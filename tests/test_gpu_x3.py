@@ -163,3 +163,47 @@ def test_x3_1280_n1600_attention_and_max_nms():
     assert _rel(eng.read_buffer(b.id, 1), ex["saved"][10].permute(0, 2, 3, 1)) < 1e-4
     assert int((y[0, 4:84].amax(0) > 0.001).sum()) > 30000
     check(oracle().predict(x, conf=0.001), model("n").predict(x.to(DEV), conf=0.001), conf=0.001)
+
+
+SPLIT_TAG = 1 << 20  # csrc/ym_runtime.cpp kSplitTag: op cfg of a fused pair run as its two convs
+STREAM_BASE, N_STREAM = 17 + 30, 31  # csrc/ym_conv.hip: first-gen + LDS-DMA ids, then the streaming kernels
+BNECK_BASE, N_BNECK = 17 + 30 + 43 + 12, 14  # ... + streaming/small-M + halo ids, then the fused Bottleneck kernels
+
+
+@pytest.mark.parametrize("scale", ["n", "s"])
+def test_x3_fused_pairs_match_split(scale):
+    """x3 fused pairs against the same plan with its pairs run as two launches, Detect rows within 2e-6 relative (the
+    same split products summed in another order; the plan's own per-layer parity is test_x3_layers_match_oracle):
+      * conv -> 1x1 pairs (csrc/ym_conv_stream.hip FUSE in the x3 mode: the intermediate split hi/lo in registers,
+        three 16x16x16 MFMAs per K block of the second GEMM) on every streaming configuration;
+      * Bottlenecks (csrc/ym_conv_bneck.hip in the x3 mode: hi / lo LDS planes, three MFMAs per K step) on every
+        tile variant (the ones whose doubled LDS does not fit fall back to the split pair)."""
+    eng = model(scale).model.engine
+    x = make_input("uniform", (21, 22), 640).to(DEV)
+    B, _, H, W = x.shape
+    ops = eng.graph.ops
+    pairs = [i for i, op in enumerate(ops) if op.args.get("pair")]
+    bneck = [i for i in pairs if ops[i].args["pair"]["k"] == 3]
+    assert len(pairs) - len(bneck) >= 4 and len(bneck) >= 2
+    eng.run(x, use_graph=False)
+    tuned = eng.rt.get_op_cfg(B, H, W)
+    base = [c if op.kind == "conv" and not op.args.get("pair") else -1 for c, op in zip(tuned, ops)]
+    try:
+        split = list(base)
+        for i in pairs:
+            split[i] = SPLIT_TAG + 128 * 127 + 127  # heuristic tiles for both convs
+        eng.rt.set_op_cfg(B, H, W, split)
+        eng.run(x, use_graph=False)
+        ref = eng.read_buffer(eng.graph.anchor_buf.id, B)
+        for cfgs, ids in ((range(STREAM_BASE, STREAM_BASE + N_STREAM), [i for i in pairs if i not in bneck]),
+                          (range(BNECK_BASE, BNECK_BASE + N_BNECK), bneck)):
+            for c in cfgs:
+                cfg = list(split)
+                for i in ids:
+                    cfg[i] = c
+                eng.rt.set_op_cfg(B, H, W, cfg)
+                eng.run(x, use_graph=False)
+                got = eng.read_buffer(eng.graph.anchor_buf.id, B)
+                assert _rel(got, ref) < 2e-6, c
+    finally:
+        eng.rt.set_op_cfg(B, H, W, tuned)

@@ -12,7 +12,7 @@ import torch
 from tests.matching import MatchReport, match_image
 from yolomi.arch import GraphBuilder, param_specs
 from yolomi.metrics import evaluate
-from yolomi.plan import MAGIC, fuse_conv_bn, fuse_default, pack_model
+from yolomi.plan import MAGIC, fuse_conv_bn, fuse_default, pack_graph, pack_model
 from yolomi.synth import splitmix64, synth_weights, uniform
 
 ROOT = os.path.dirname(os.path.dirname(os.path.abspath(__file__)))
@@ -95,9 +95,11 @@ def test_capi_exports_every_declared_symbol():
 def test_x3_blob_packs_pair_chunk_weights():
     """x3 plans: every conv but the stem packs [N][Kpad] fp16 rows with each 8-channel K chunk as [hi x8 | lo x8],
     hi = fp16(w), lo = fp16(w - hi) (Kpad = 2K padded to 64); hi + lo restores the fp32 folded weight to ~2^-22
-    relative (fp16 subnormal lo parts included); the stem stays fp32."""
+    relative (fp16 subnormal lo parts included); the stem stays fp32.  (Both blobs packed from the graph with C3k
+    cv1 ‖ cv2 merged and no fused pairs, so they compare op by op; the x3 pairs' W2: test_x3_fused_pairs_pack_w2.)"""
     sd = synth_weights("n", "detect", 0)
-    b32, bx3 = pack_model("n", "detect", sd, "f32"), pack_model("n", "detect", sd, "x3")
+    b32 = pack_graph(GraphBuilder("n", "detect", fuse="merge"), sd, "f32")
+    bx3 = pack_graph(GraphBuilder("n", "detect", fuse="merge"), sd, "x3")
     h = struct.unpack("<32i", bx3[:128])
     assert h[2] == 4
     nb, nop = h[11], h[12]
@@ -122,6 +124,38 @@ def test_x3_blob_packs_pair_chunk_weights():
         worst = max(worst, float(np.abs(rebuilt - w).max() / np.abs(w).max()))
         nconv += 1
     assert nconv > 70 and worst < 2 ** -21
+
+
+@pytest.mark.parametrize("scale", ["n", "s"])
+def test_x3_fused_pairs_pack_w2(scale):
+    """x3 plans fuse conv → 1x1 pairs (GraphBuilder fuse="x3": storage K even and within the streaming kernel's K
+    steps) and Bottlenecks (3x3 → 3x3 + shortcut); the successor's W2 is packed in pair-chunk rows whose hi + lo
+    rebuild the folded fp32 weights to ~2^-22 relative, and Kpad2 counts the fp16 storage K."""
+    from yolomi.plan import _conv_weights
+    sd = synth_weights(scale, "detect", 0)
+    assert fuse_default("x3") == "x3"
+    g = GraphBuilder(scale, "detect", fuse="x3")
+    pairs = [op for op in g.ops if op.args.get("pair")]
+    assert pairs and any(op.args["pair"]["k"] == 3 for op in pairs) and any(op.args["pair"]["k"] == 1 for op in pairs)
+    assert any(op.name.startswith("model.23.cv3.0.1.1") for op in pairs)
+    blob = pack_model(scale, "detect", sd, "x3")
+    h = struct.unpack("<32i", blob[:128])
+    nb, nop = h[11], h[12]
+    assert nop == len(g.ops)
+    base = (128 + 32 * nb + 176 * nop + 255) // 256 * 256
+    for i, op in enumerate(g.ops):
+        r = struct.unpack("<32i", blob[128 + 32 * nb + 128 * i: 128 + 32 * nb + 128 * (i + 1)])
+        assert bool(r[30]) == bool(op.args.get("pair")), op.name
+        if not r[30]:
+            continue
+        w2, _ = _conv_weights(op.args["pair"], sd)
+        N2, K2 = w2.shape[0], w2.shape[1] * w2.shape[2] * w2.shape[3]
+        assert r[27] == N2 and r[29] % 64 == 0 and 2 * K2 <= r[29] < 2 * K2 + 64 and (r[29] // 32) % 2 == 0
+        hl = np.frombuffer(blob, np.float16, N2 * r[29], base + r[25]).reshape(N2, r[29])
+        pr = hl[:, :2 * K2].reshape(N2, K2 // 8, 2, 8).astype(np.float64)
+        rebuilt = (pr[:, :, 0] + pr[:, :, 1]).reshape(N2, K2)
+        ref = w2.reshape(N2, K2)
+        assert np.abs(rebuilt - ref).max() / np.abs(ref).max() < 2 ** -21, op.name
 
 def test_facade_contract_without_gpu():
     from core.model import YOLO11Model

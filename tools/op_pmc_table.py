@@ -9,7 +9,8 @@ order).  Counters of an op's launches are summed.  Derived columns (MI355X_MICRO
   * kernel cycles = GRBM_GUI_ACTIVE / 8 (summed over the 8 XCDs);
   * MFMA busy = SQ_VALU_MFMA_BUSY_CYCLES / (kernel cycles x 1024 SIMDs): the fraction of the chip's MFMA pipe time
     the op kept busy while it ran; achieved TFLOP/s = FLOPs / (kernel cycles / clock), clock = 2.4 GHz nominal.
-Writes profiles/<tag>_ops.md and profiles/<tag>_ops.json.
+Writes profiles/<tag>_ops.md and profiles/<tag>_ops.json (its "workload": $YM_OPS_WORKLOAD, the bench.py workload
+string bench.py matches to report the time-weighted MFMA busy of the conv family).
 """
 import csv
 import glob
@@ -76,7 +77,8 @@ def main():
             r["wait_frac"] = c.get("SQ_WAIT_ANY", 0.0) / c["SQ_WAVE_CYCLES"]
         rows.append(r)
     out = os.path.join(ROOT, "profiles", tag)
-    json.dump({"sources": [os.path.relpath(d, ROOT) for d in dirs], "clock_hz": CLOCK, "ops": rows},
+    json.dump({"sources": [os.path.relpath(d, ROOT) for d in dirs], "clock_hz": CLOCK,
+               "workload": os.environ.get("YM_OPS_WORKLOAD"), "ops": rows},
               open(out + "_ops.json", "w"), indent=1)
     conv = [r for r in rows if r["kind"] == "conv"]
     lines = [f"# Per-op PMC table ({tag})", "",

@@ -1,7 +1,7 @@
 #!/usr/bin/env python3
 """Turn rocprofv3 output into the per-round evidence committed under profiles/.
 
-    python tools/rocprof_summary.py stats  <rocprof_dir> <tag>   # --kernel-trace --stats run of bench.py
+    python tools/rocprof_summary.py stats  <rocprof_dir> <tag> [workload description]   # --stats run of bench.py
     python tools/rocprof_summary.py pmc    <fetch_dir> <write_dir> <tag> [workload description]
 
 `stats`: copies kernel_stats.csv to profiles/<tag>_kernel_stats.csv and writes profiles/<tag>_summary.json with the
@@ -48,7 +48,7 @@ def find(d, suffix):
     return hits[0]
 
 
-def stats(d, tag):
+def stats(d, tag, workload=None):
     ks = find(d, "kernel_stats.csv")
     os.makedirs(PROF, exist_ok=True)
     shutil.copy(ks, os.path.join(PROF, f"{tag}_kernel_stats.csv"))
@@ -60,7 +60,7 @@ def stats(d, tag):
         e["calls"] += int(r["Calls"])
         e["total_ns"] += float(r["TotalDurationNs"])
     nfwd = fam.get("stem", {}).get("calls", 0)
-    out = {"source": os.path.relpath(ks, ROOT), "forwards": nfwd, "families": {}}
+    out = {"source": os.path.relpath(ks, ROOT), "workload": workload, "forwards": nfwd, "families": {}}
     for f, e in sorted(fam.items(), key=lambda kv: -kv[1]["total_ns"]):
         out["families"][f] = {"calls": e["calls"], "total_ms": round(e["total_ns"] / 1e6, 3),
                               "avg_us": round(e["total_ns"] / e["calls"] / 1e3, 3),
@@ -111,7 +111,7 @@ def pmc(fetch_dir, write_dir, tag, reps=3, workload=None):
 
 if __name__ == "__main__":
     if sys.argv[1] == "stats":
-        stats(sys.argv[2], sys.argv[3])
+        stats(sys.argv[2], sys.argv[3], workload=sys.argv[4] if len(sys.argv) > 4 else None)
     elif sys.argv[1] == "pmc":
         pmc(sys.argv[2], sys.argv[3], sys.argv[4], workload=sys.argv[5] if len(sys.argv) > 5 else None)
     else:

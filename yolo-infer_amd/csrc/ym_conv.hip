@@ -714,8 +714,8 @@ hipError_t ym_launch_conv(int dtype, int out_f32, const ConvArgs& a, int cfg, hi
   if (ym_dt_q8(dtype)) return ym_launch_conv_i8(a, cfg, st, strict, dtype == YM_DT_F8);  // csrc/ym_conv_i8.hip
   // (concat/upsample sources only feed 1x1 convs; YOLO11 has k in {1, 3})
   if (a.Kpad % KSTEP) return hipErrorInvalidValue;
-  if (a.w2 && a.k2 == 3) {  // fused Bottleneck (3x3 -> 3x3): csrc/ym_conv_bneck.hip
-    if (dtype != YM_DT_F16) return hipErrorInvalidValue;
+  if (a.w2 && a.k2 == 3) {  // fused Bottleneck (3x3 -> 3x3): csrc/ym_conv_bneck.hip (f16 and x3 plans)
+    if (dtype != YM_DT_F16 && dtype != YM_DT_X3) return hipErrorInvalidValue;
     const int bb = kNumAllCfg + ym_conv_dma_num_cfgs() + ym_conv_stream_num_cfgs() + ym_conv_halo_num_cfgs();
     const int nb = ym_conv_bneck_num_cfgs();
     if (cfg >= bb && cfg < bb + nb) {
@@ -731,8 +731,8 @@ hipError_t ym_launch_conv(int dtype, int out_f32, const ConvArgs& a, int cfg, hi
     return hipErrorInvalidValue;
   }
   if (a.w2) {  // fused pair: the streaming kernels hold a whole N in one wave (csrc/ym_conv_stream.hip); a stride-2
-    // 3x3 followed by a 1x1 can also take the band kernel of csrc/ym_conv_bneck.hip
-    if (dtype != YM_DT_F16) return hipErrorInvalidValue;
+    // 3x3 followed by a 1x1 can also take the band kernel of csrc/ym_conv_bneck.hip (f16 only)
+    if (dtype != YM_DT_F16 && dtype != YM_DT_X3) return hipErrorInvalidValue;
     const int bb = kNumAllCfg + ym_conv_dma_num_cfgs() + ym_conv_stream_num_cfgs() + ym_conv_halo_num_cfgs();
     if (cfg >= bb && cfg < bb + ym_conv_bneck_num_cfgs()) {
       const hipError_t e = ym_launch_conv_bneck(out_f32, a, cfg - bb, st);

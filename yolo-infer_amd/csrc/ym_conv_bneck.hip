@@ -25,6 +25,11 @@
 // are pitched 64·KS + 32 bytes (4·KS + 2 slots), conflict-free for the same groups.
 // Results: fp32 accumulation of fp16 products with one fp16 rounding of the mid tensor and of the output, like the
 // unfused pair (only the summation order differs; f16-plan tolerance, tests/test_gpu_parity.py).
+// x3 plans (X3): the input tile, the mid image and both weight matrices live in LDS as two planes each — the fp16 hi
+// halves, then the lo halves, in the f16 layout (same swizzle, same conflict-free reads per plane) — and every K
+// step runs three MFMAs (w_lo·x_hi, w_hi·x_lo, w_hi·x_hi).  The mid image holds the exact split of the activated
+// fp32 value (hi = fp16(v), lo = fp16(v - hi)), as the unfused pair's stored pair-layout tensor; outputs are stored
+// in the pair layout.  Twice the LDS of the f16 kernel: the geometry check keeps only the tiles that fit.
 #include <stdlib.h>
 
 #include "ym_common.h"
@@ -48,6 +53,7 @@ struct BneckGeom {
   int MR, MC;      // mid tile rows / columns (K2 = 3: + 1-pixel halo)
   int XR, XC, XE;  // input tile rows / columns; S1 = 2: even columns first (XE of them), then the odd ones
   int offM, offW, offB;  // LDS byte offsets: mid image, weight slot, biases (input image at 0)
+  int plW;               // x3: weight slot plane size (bytes)
   int lds;
   int dbg;  // tools/bneck_ablate.py timing ablations (YM_BNECK_DBG): 1 no input loads, 2 no cv1, 4 no cv2, 8 no stores
 };
@@ -68,9 +74,10 @@ __device__ __forceinline__ int xpix(int row, int xc, int XC, int XE) {
 
 // S1: stride of the first 3x3 conv (1: Bottleneck, 2: a downsampling Conv); K2: kernel of the second conv (3: the
 // Bottleneck's cv2 with its 1-pixel halo on the mid image; 1: a following 1x1 such as C3k2.cv1, no halo).
-template <int C, int CM, int N2, int PX, int NW, int S1, int K2>
+template <int C, int CM, int N2, int PX, int NW, int S1, int K2, bool X3>
 __global__ __launch_bounds__(64 * NW) void conv_bneck(const ConvArgs a, const BneckGeom g) {
   constexpr int NT = 64 * NW;
+  constexpr int XS = X3 ? 2 : 1;  // fp16 storage elements per logical channel (global pair layout)
   constexpr int CH = C / 8, CHM = CM / 8;
   constexpr int NB1 = (CM + 15) / 16, NB2 = N2 / 16;
   constexpr int KS1 = (9 * C + 31) / 32, KS2 = (K2 * K2 * CM + 31) / 32;
@@ -93,51 +100,65 @@ __global__ __launch_bounds__(64 * NW) void conv_bneck(const ConvArgs a, const Bn
   const f16* src = static_cast<const f16*>(a.src0);
   const f16* W1 = static_cast<const f16*>(a.w);
   const f16* W2 = static_cast<const f16*>(a.w2);
+  // x3: byte distance from a hi plane to its lo plane (input tile, mid image, weight slot)
+  const int plX = g.XR * g.XC * C * 2, plM = g.MR * g.MC * CM * 2, plW = g.plW;
 
   // ---- phase 0: W2 prefetch (registers), W1 + biases, input tile (zeros outside the input map), zeroed mid image
-  constexpr int W2CH = N2 * KS2 * 4;  // 16-byte chunks of W2 rows [N2][KS2 * 32]
+  constexpr int W2CH = N2 * KS2 * 4;  // 16-byte chunks of W2 rows [N2][KS2 * 32] (x3: per plane)
   constexpr int W2PT = (W2CH + NT - 1) / NT;
-  f16x8 w2r[W2PT];
+  f16x8 w2r[W2PT], w2l[X3 ? W2PT : 1];
 #pragma unroll
   for (int u = 0; u < W2PT; ++u) {
     const int i = tid + NT * u;
     const int n = i / (KS2 * 4), c = i - n * (KS2 * 4);
-    w2r[u] = i < W2CH ? *reinterpret_cast<const f16x8*>(W2 + (size_t)n * a.Kpad2 + 8 * c) : Vec8<f16>::zero();
+    // (x3: the weight rows are pair chunks — logical chunk c's hi half at 16 c, its lo half 8 further; the K padding
+    // chunks past 9 CM / 8 read zeros inside the padded row)
+    const f16* q = W2 + (size_t)n * a.Kpad2 + 8 * XS * c;
+    w2r[u] = i < W2CH ? *reinterpret_cast<const f16x8*>(q) : Vec8<f16>::zero();
+    if constexpr (X3) w2l[u] = i < W2CH ? *reinterpret_cast<const f16x8*>(q + 8) : Vec8<f16>::zero();
   }
   for (int i = tid; i < 16 * NB1 * KS1 * 4; i += NT) {
     const int n = i / (KS1 * 4), c = i - n * (KS1 * 4);
-    const f16x8 v = n < CM ? *reinterpret_cast<const f16x8*>(W1 + (size_t)n * a.Kpad + 8 * c) : Vec8<f16>::zero();
+    const f16* q = W1 + (size_t)n * a.Kpad + 8 * XS * c;
+    const f16x8 v = n < CM ? *reinterpret_cast<const f16x8*>(q) : Vec8<f16>::zero();
     *reinterpret_cast<f16x8*>(sW + n * g.P1 + 16 * c) = v;
+    if constexpr (X3) {
+      const f16x8 vl = n < CM ? *reinterpret_cast<const f16x8*>(q + 8) : Vec8<f16>::zero();
+      *reinterpret_cast<f16x8*>(sW + plW + n * g.P1 + 16 * c) = vl;
+    }
   }
   for (int i = tid; i < 16 * NB1; i += NT) sB1[i] = i < CM ? a.bias[i] : 0.f;
   for (int i = tid; i < N2; i += NT) sB2[i] = a.bias2[i];
   {
     const int nx = XR * XC * CH;  // input tile chunks, in input-map order
     const size_t img = (size_t)b * a.s0_P;
-    for (int i0 = tid; i0 < nx; i0 += NT * 8) {
-      f16x8 v[8];
+    constexpr int UN = X3 ? 4 : 8;  // loads in flight per thread and round (x3: two 16-byte halves each)
+    for (int i0 = tid; i0 < nx; i0 += NT * UN) {
+      f16x8 v[UN], vl[X3 ? UN : 1];
 #pragma unroll
-      for (int u = 0; u < 8; ++u) {
+      for (int u = 0; u < UN; ++u) {
         const int i = i0 + NT * u;
         const int q = i / CH, c = i - q * CH;
         const int row = q / XC, xc = q - row * XC;
         const int gy = xr0 + row, gx = xc0 + xc;
-        v[u] = (i < nx && !(g.dbg & 1) && (unsigned)gy < (unsigned)a.Hin && (unsigned)gx < (unsigned)a.Win)
-                   ? *reinterpret_cast<const f16x8*>(src + (img + (size_t)gy * a.Win + gx) * a.s0_ctot + a.s0_coff + 8 * c)
-                   : Vec8<f16>::zero();
+        const bool in = i < nx && !(g.dbg & 1) && (unsigned)gy < (unsigned)a.Hin && (unsigned)gx < (unsigned)a.Win;
+        const f16* p = src + ((img + (size_t)gy * a.Win + gx) * a.s0_ctot + a.s0_coff + 8 * c) * XS;
+        v[u] = in ? *reinterpret_cast<const f16x8*>(p) : Vec8<f16>::zero();
+        if constexpr (X3) vl[u] = in ? *reinterpret_cast<const f16x8*>(p + 8) : Vec8<f16>::zero();
       }
 #pragma unroll
-      for (int u = 0; u < 8; ++u) {
+      for (int u = 0; u < UN; ++u) {
         const int i = i0 + NT * u;
         if (i < nx) {
           const int q = i / CH, c = i - q * CH;
           const int row = q / XC, xc = q - row * XC;
           const int p = xpix<S1>(row, xc, XC, XE);
           *reinterpret_cast<f16x8*>(sX + ((p * CH + (c ^ swz<CH>(p))) << 4)) = v[u];
+          if constexpr (X3) *reinterpret_cast<f16x8*>(sX + plX + ((p * CH + (c ^ swz<CH>(p))) << 4)) = vl[u];
         }
       }
     }
-    const int nm = MR * MC * CHM;
+    const int nm = MR * MC * CHM * XS;  // (x3: both planes, contiguous)
     for (int i = tid; i < nm; i += NT) *reinterpret_cast<f16x8*>(sM + (i << 4)) = Vec8<f16>::zero();
   }
   __syncthreads();
@@ -171,17 +192,28 @@ __global__ __launch_bounds__(64 * NW) void conv_bneck(const ConvArgs a, const Bn
         const int ch = (K - tap * C) >> 3;
         if (tap > 8) tap = 8;  // K padding: finite pixels times zero weights
         const int ky = tap / 3, kx = tap - 3 * ky;
-        f16x8 wa[NB1], xb[PX];
+        f16x8 wa[NB1], xb[PX], wl[X3 ? NB1 : 1], xl[X3 ? PX : 1];
 #pragma unroll
-        for (int nb = 0; nb < NB1; ++nb)
+        for (int nb = 0; nb < NB1; ++nb) {
           wa[nb] = *reinterpret_cast<const f16x8*>(sW + (16 * nb + col) * g.P1 + 2 * K);
+          if constexpr (X3) wl[nb] = *reinterpret_cast<const f16x8*>(sW + plW + (16 * nb + col) * g.P1 + 2 * K);
+        }
 #pragma unroll
-        for (int q = 0; q < PX; ++q)
-          xb[q] = ld_px<CH>(sX, xpix<S1>(prow[q] * S1 + ky, pm[q] * S1 + kx, XC, XE), ch);
+        for (int q = 0; q < PX; ++q) {
+          const int px = xpix<S1>(prow[q] * S1 + ky, pm[q] * S1 + kx, XC, XE);
+          xb[q] = ld_px<CH>(sX, px, ch);
+          if constexpr (X3) xl[q] = ld_px<CH>(sX + plX, px, ch);
+        }
 #pragma unroll
         for (int nb = 0; nb < NB1; ++nb)
 #pragma unroll
-          for (int q = 0; q < PX; ++q) acc[nb][q] = __builtin_amdgcn_mfma_f32_16x16x32_f16(wa[nb], xb[q], acc[nb][q], 0, 0, 0);
+          for (int q = 0; q < PX; ++q) {
+            if constexpr (X3) {
+              acc[nb][q] = __builtin_amdgcn_mfma_f32_16x16x32_f16(wl[nb], xb[q], acc[nb][q], 0, 0, 0);
+              acc[nb][q] = __builtin_amdgcn_mfma_f32_16x16x32_f16(wa[nb], xl[q], acc[nb][q], 0, 0, 0);
+            }
+            acc[nb][q] = __builtin_amdgcn_mfma_f32_16x16x32_f16(wa[nb], xb[q], acc[nb][q], 0, 0, 0);
+          }
       }
       // lane: channels 16 nb + 4 kg .. + 3 of its pixel -> 8 bytes of the mid image
 #pragma unroll
@@ -192,14 +224,22 @@ __global__ __launch_bounds__(64 * NW) void conv_bneck(const ConvArgs a, const Bn
         for (int nb = 0; nb < NB1; ++nb) {
           const int n0 = 16 * nb + 4 * kg;
           if (n0 >= CM) continue;
-          f16x4 h;
+          f16x4 h, hl;
 #pragma unroll
           for (int r = 0; r < 4; ++r) {
             const float v = acc[nb][q][r] + sB1[n0 + r];
-            h[r] = (f16)(a.act ? ym_silu_fast(v) : v);
+            if constexpr (X3) {
+              const float vv = a.act ? ym_silu(v) : v;
+              h[r] = (f16)vv;
+              hl[r] = (f16)(vv - (float)h[r]);
+            } else {
+              h[r] = (f16)(a.act ? ym_silu_fast(v) : v);
+            }
           }
           const int c = n0 >> 3;
-          *reinterpret_cast<f16x4*>(sM + ((p * CHM + (c ^ swz<CHM>(p))) << 4) + ((n0 & 4) << 1)) = h;
+          const int off = ((p * CHM + (c ^ swz<CHM>(p))) << 4) + ((n0 & 4) << 1);
+          *reinterpret_cast<f16x4*>(sM + off) = h;
+          if constexpr (X3) *reinterpret_cast<f16x4*>(sM + plM + off) = hl;
         }
       }
     }
@@ -211,6 +251,7 @@ __global__ __launch_bounds__(64 * NW) void conv_bneck(const ConvArgs a, const Bn
     if (i < W2CH) {
       const int n = i / (KS2 * 4), c = i - n * (KS2 * 4);
       *reinterpret_cast<f16x8*>(sW + n * g.P2 + 16 * c) = w2r[u];
+      if constexpr (X3) *reinterpret_cast<f16x8*>(sW + plW + n * g.P2 + 16 * c) = w2l[u];
     }
   }
   __syncthreads();
@@ -223,6 +264,7 @@ __global__ __launch_bounds__(64 * NW) void conv_bneck(const ConvArgs a, const Bn
     const int gpr = (TW + 15) / 16;
     const int ng = (g.dbg & 4) ? 0 : rows * gpr;
     f16* dst = static_cast<f16*>(a.dst);
+    P2* dstp = static_cast<P2*>(a.dst);
     const bool res = S1 == 1 && K2 == 3 && a.res != nullptr;
     for (int it = wave * PX; it < ng; it += NW * PX) {
       int prow[PX], pc[PX];  // output row, this lane's output column (both within the tile)
@@ -245,16 +287,28 @@ __global__ __launch_bounds__(64 * NW) void conv_bneck(const ConvArgs a, const Bn
         const int ch = (K - tap * CM) >> 3;
         if (tap > K2 * K2 - 1) tap = K2 * K2 - 1;
         const int ky = tap / 3, kx = tap - 3 * ky;
-        f16x8 wa[NB2], xb[PX];
+        f16x8 wa[NB2], xb[PX], wl[X3 ? NB2 : 1], xl[X3 ? PX : 1];
 #pragma unroll
-        for (int nb = 0; nb < NB2; ++nb)
+        for (int nb = 0; nb < NB2; ++nb) {
           wa[nb] = *reinterpret_cast<const f16x8*>(sW + (16 * nb + col) * g.P2 + 2 * K);
+          if constexpr (X3) wl[nb] = *reinterpret_cast<const f16x8*>(sW + plW + (16 * nb + col) * g.P2 + 2 * K);
+        }
 #pragma unroll
-        for (int q = 0; q < PX; ++q) xb[q] = ld_px<CHM>(sM, (prow[q] + ky) * MC + pc[q] + kx, ch);
+        for (int q = 0; q < PX; ++q) {
+          const int pm2 = (prow[q] + ky) * MC + pc[q] + kx;
+          xb[q] = ld_px<CHM>(sM, pm2, ch);
+          if constexpr (X3) xl[q] = ld_px<CHM>(sM + plM, pm2, ch);
+        }
 #pragma unroll
         for (int nb = 0; nb < NB2; ++nb)
 #pragma unroll
-          for (int q = 0; q < PX; ++q) acc[nb][q] = __builtin_amdgcn_mfma_f32_16x16x32_f16(wa[nb], xb[q], acc[nb][q], 0, 0, 0);
+          for (int q = 0; q < PX; ++q) {
+            if constexpr (X3) {
+              acc[nb][q] = __builtin_amdgcn_mfma_f32_16x16x32_f16(wl[nb], xb[q], acc[nb][q], 0, 0, 0);
+              acc[nb][q] = __builtin_amdgcn_mfma_f32_16x16x32_f16(wa[nb], xl[q], acc[nb][q], 0, 0, 0);
+            }
+            acc[nb][q] = __builtin_amdgcn_mfma_f32_16x16x32_f16(wa[nb], xb[q], acc[nb][q], 0, 0, 0);
+          }
       }
 #pragma unroll
       for (int q = 0; q < PX; ++q) {
@@ -265,18 +319,36 @@ __global__ __launch_bounds__(64 * NW) void conv_bneck(const ConvArgs a, const Bn
 #pragma unroll
         for (int nb = 0; nb < NB2; ++nb) {
           const int n0 = 16 * nb + 4 * kg;
-          f16x4 rv = {0, 0, 0, 0};
+          float rv[4] = {0.f, 0.f, 0.f, 0.f};
           if (res) {
             const int c = n0 >> 3;
-            rv = *reinterpret_cast<const f16x4*>(sX + ((px * CH + (c ^ swz<CH>(px))) << 4) + ((n0 & 4) << 1));
-          }
-          f16x4 o;
+            const int off = ((px * CH + (c ^ swz<CH>(px))) << 4) + ((n0 & 4) << 1);
+            const f16x4 rh = *reinterpret_cast<const f16x4*>(sX + off);
 #pragma unroll
-          for (int r = 0; r < 4; ++r) {
-            const float v = acc[nb][q][r] + sB2[n0 + r];
-            o[r] = (f16)((a.act2 ? ym_silu_fast(v) : v) + (float)rv[r]);
+            for (int r = 0; r < 4; ++r) rv[r] = (float)rh[r];
+            if constexpr (X3) {
+              const f16x4 rl = *reinterpret_cast<const f16x4*>(sX + plX + off);
+#pragma unroll
+              for (int r = 0; r < 4; ++r) rv[r] += (float)rl[r];
+            }
           }
-          if (!(g.dbg & 8)) *reinterpret_cast<f16x4*>(dst + obase + n0) = o;
+          if constexpr (X3) {
+            float o[4];
+#pragma unroll
+            for (int r = 0; r < 4; ++r) {
+              const float v = acc[nb][q][r] + sB2[n0 + r];
+              o[r] = (a.act2 ? ym_silu(v) : v) + rv[r];
+            }
+            if (!(g.dbg & 8)) ym_p2_store4(dstp + obase + n0, o);
+          } else {
+            f16x4 o;
+#pragma unroll
+            for (int r = 0; r < 4; ++r) {
+              const float v = acc[nb][q][r] + sB2[n0 + r];
+              o[r] = (f16)((a.act2 ? ym_silu_fast(v) : v) + rv[r]);
+            }
+            if (!(g.dbg & 8)) *reinterpret_cast<f16x4*>(dst + obase + n0) = o;
+          }
         }
       }
     }
@@ -293,7 +365,7 @@ __global__ __launch_bounds__(64 * NW) void conv_bneck(const ConvArgs a, const Bn
 constexpr int kNumBneck = 14;
 constexpr int kMaxLds = 160 * 1024;
 
-bool bneck_geom(const ConvArgs& a, int C, int CM, int N2, int S1, int K2, int RB, int TW, BneckGeom& g) {
+bool bneck_geom(const ConvArgs& a, int C, int CM, int N2, int S1, int K2, int RB, int TW, BneckGeom& g, int xs) {
   g.RB = RB;
   g.nbands = (a.Ho + RB - 1) / RB;
   if (TW >= a.Wo) TW = 0;
@@ -310,12 +382,13 @@ bool bneck_geom(const ConvArgs& a, int C, int CM, int N2, int S1, int K2, int RB
   g.XR = (g.MR - 1) * S1 + 3;
   g.XC = (g.MC - 1) * S1 + 3;
   g.XE = (g.XC + 1) / 2;
-  const int sx = g.XR * g.XC * C * 2, sm = g.MR * g.MC * CM * 2;
+  const int sx = g.XR * g.XC * C * 2 * xs, sm = g.MR * g.MC * CM * 2 * xs;  // (x3: hi and lo planes)
   const int nb1 = (CM + 15) / 16;
   const int w1 = 16 * nb1 * g.P1, w2 = N2 * g.P2;
+  g.plW = w1 > w2 ? w1 : w2;
   g.offM = sx;
   g.offW = sx + sm;
-  g.offB = g.offW + (w1 > w2 ? w1 : w2);
+  g.offB = g.offW + g.plW * xs;
   g.lds = g.offB + (16 * nb1 + N2) * 4;
   static const int dbg = [] {
     const char* e = getenv("YM_BNECK_DBG");
@@ -325,20 +398,22 @@ bool bneck_geom(const ConvArgs& a, int C, int CM, int N2, int S1, int K2, int RB
   return g.lds <= kMaxLds;
 }
 
-template <int C, int CM, int N2, int S1, int K2, int RB, int TW, int PX, int NW>
+template <int C, int CM, int N2, int S1, int K2, int RB, int TW, int PX, int NW, bool X3>
 hipError_t launch(const ConvArgs& a, hipStream_t st) {
   BneckGeom g;
-  if ((TW && TW >= a.Wo) || !bneck_geom(a, C, CM, N2, S1, K2, RB, TW, g)) return hipErrorInvalidValue;  // (TW: a real split)
+  if ((TW && TW >= a.Wo) || !bneck_geom(a, C, CM, N2, S1, K2, RB, TW, g, X3 ? 2 : 1))
+    return hipErrorInvalidValue;  // (TW: a real split)
   const int B = a.M / (a.Ho * a.Wo);
-  hipLaunchKernelGGL((conv_bneck<C, CM, N2, PX, NW, S1, K2>), dim3(B * g.nbands * g.ntx), dim3(64 * NW), g.lds, st, a, g);
+  hipLaunchKernelGGL((conv_bneck<C, CM, N2, PX, NW, S1, K2, X3>), dim3(B * g.nbands * g.ntx), dim3(64 * NW), g.lds, st,
+                     a, g);
   return hipGetLastError();
 }
 
-template <int C, int CM, int N2, int S1, int K2>
+template <int C, int CM, int N2, int S1, int K2, bool X3>
 hipError_t dispatch_cfg(const ConvArgs& a, int i, hipStream_t st) {
   switch (i) {
 #define YM_X(id, rb, tw, px, nw) \
-  case id: return launch<C, CM, N2, S1, K2, rb, tw, px, nw>(a, st);
+  case id: return launch<C, CM, N2, S1, K2, rb, tw, px, nw, X3>(a, st);
     YM_BNECK_CFGS(YM_X)
 #undef YM_X
   }
@@ -364,17 +439,28 @@ hipError_t ym_launch_conv_bneck(int out_f32, const ConvArgs& a, int i, hipStream
   if (a.res && (down || a.res != a.src0 || a.r_ctot != a.s0_ctot || a.r_coff != a.s0_coff || a.r_P != a.s0_P))
     return hipErrorInvalidValue;
   const int C = a.C0, CM = a.N, N2 = a.N2, K2 = a.k2;
-  if (C != 8 * a.Cin8 || a.Kpad < 32 * ((9 * C + 31) / 32) || a.Kpad2 < 32 * ((K2 * K2 * CM + 31) / 32))
+  // x3: Cin8 / Kpad / Kpad2 count fp16 storage (the pair chunks); the kernel walks logical K chunks of 8 channels
+  const int xs = a.x3 ? 2 : 1;
+  if (xs * C != 8 * a.Cin8 || a.Kpad < xs * 32 * ((9 * C + 31) / 32) || a.Kpad2 < xs * 32 * ((K2 * K2 * CM + 31) / 32))
     return hipErrorInvalidValue;
+  if (a.x3) {  // the Bottleneck shapes (the stride-2 "down" pairs do not fit twice the LDS)
+    if (!bneck) return hipErrorInvalidValue;
+    if (C == 16 && CM == 8 && N2 == 16) return dispatch_cfg<16, 8, 16, 1, 3, true>(a, i, st);
+    if (C == 32 && CM == 16 && N2 == 32) return dispatch_cfg<32, 16, 32, 1, 3, true>(a, i, st);
+    if (C == 64 && CM == 32 && N2 == 64) return dispatch_cfg<64, 32, 64, 1, 3, true>(a, i, st);
+    if (C == 32 && CM == 32 && N2 == 32) return dispatch_cfg<32, 32, 32, 1, 3, true>(a, i, st);
+    if (C == 64 && CM == 64 && N2 == 64) return dispatch_cfg<64, 64, 64, 1, 3, true>(a, i, st);
+    return hipErrorInvalidValue;
+  }
   if (bneck) {
-    if (C == 16 && CM == 8 && N2 == 16) return dispatch_cfg<16, 8, 16, 1, 3>(a, i, st);
-    if (C == 32 && CM == 16 && N2 == 32) return dispatch_cfg<32, 16, 32, 1, 3>(a, i, st);
-    if (C == 64 && CM == 32 && N2 == 64) return dispatch_cfg<64, 32, 64, 1, 3>(a, i, st);
-    if (C == 32 && CM == 32 && N2 == 32) return dispatch_cfg<32, 32, 32, 1, 3>(a, i, st);
-    if (C == 64 && CM == 64 && N2 == 64) return dispatch_cfg<64, 64, 64, 1, 3>(a, i, st);  // s: C3k at 40x40
+    if (C == 16 && CM == 8 && N2 == 16) return dispatch_cfg<16, 8, 16, 1, 3, false>(a, i, st);
+    if (C == 32 && CM == 16 && N2 == 32) return dispatch_cfg<32, 16, 32, 1, 3, false>(a, i, st);
+    if (C == 64 && CM == 32 && N2 == 64) return dispatch_cfg<64, 32, 64, 1, 3, false>(a, i, st);
+    if (C == 32 && CM == 32 && N2 == 32) return dispatch_cfg<32, 32, 32, 1, 3, false>(a, i, st);
+    if (C == 64 && CM == 64 && N2 == 64) return dispatch_cfg<64, 64, 64, 1, 3, false>(a, i, st);  // s: C3k at 40x40
   } else {
-    if (C == 32 && CM == 64 && N2 == 64) return dispatch_cfg<32, 64, 64, 2, 1>(a, i, st);  // s model.1, n model.3
-    if (C == 16 && CM == 32 && N2 == 32) return dispatch_cfg<16, 32, 32, 2, 1>(a, i, st);  // n model.1
+    if (C == 32 && CM == 64 && N2 == 64) return dispatch_cfg<32, 64, 64, 2, 1, false>(a, i, st);  // s model.1, n model.3
+    if (C == 16 && CM == 32 && N2 == 32) return dispatch_cfg<16, 32, 32, 2, 1, false>(a, i, st);  // n model.1
   }
   return hipErrorInvalidValue;
 }

@@ -59,6 +59,10 @@ constexpr int RB = 8;           // output-channel blocks of 16 whose residuals a
 // logical chunk (storage chunk 4ks + 2(g>>1)) with the natural B, for ks and ks+1 (w_hi·x_hi + w_hi·x_lo), and
 // A = w_lo of logical chunk 2ks + g (storage 4ks + 2g + 1) with B = x_hi of that chunk (storage 4ks + 2g, one extra
 // 16-byte gather per lane and step pair) — w_lo·x_hi of all four chunks.
+// x3 fused pairs: the first conv's activated fp32 output is split in registers exactly as its producer epilogue
+// would store it (hi = fp16(v), lo = fp16(v - hi)), and the second GEMM runs three 16x16x16 MFMAs per K block
+// (w2_lo·h_hi, w2_hi·h_lo, w2_hi·h_hi) with W2's hi and lo halves in two LDS planes: the same products as the unfused
+// x3 pair, summed in another order.
 template <typename T> struct SOut;  // 4 output channels of one pixel
 template <> struct SOut<f16> {
   static __device__ __forceinline__ void st(f16* o, const float* v) {
@@ -91,7 +95,7 @@ template <> struct SRes<true> {
 
 template <typename OutT, int KIND, int KS, int PX, bool FUSE, int NWV, bool X3 = false>
 __global__ __launch_bounds__(64 * NWV) void conv_stream(const ConvArgs a) {
-  static_assert(!X3 || (!FUSE && KS % 2 == 0), "x3: unfused, K steps in pairs");
+  static_assert(!X3 || KS % 2 == 0, "x3: K steps in pairs");
   constexpr int XS = X3 ? 2 : 1;       // fp16 storage elements per logical channel
   constexpr int KX = X3 ? KS / 2 : 0;  // x3: the extra x_hi gather per step pair
   typedef typename SRes<X3>::type RV;
@@ -109,7 +113,8 @@ __global__ __launch_bounds__(64 * NWV) void conv_stream(const ConvArgs a) {
                                  // distinct 8-byte slots of a ds_read_b64 half-wave (+4 was 2-way)
   f16* w2s = reinterpret_cast<f16*>(bs + 16 * NB);
   const int NB2 = FUSE ? (a.N2 + 15) >> 4 : 0;
-  float* bs2 = reinterpret_cast<float*>(w2s + 16 * NB2 * LDW2);
+  f16* w2l = w2s + (X3 ? 16 * NB2 * LDW2 : 0);  // x3: the lo plane of W2
+  float* bs2 = reinterpret_cast<float*>(w2l + 16 * NB2 * LDW2);
   const int tid = threadIdx.x, lane = tid & 63, wave = tid >> 6;
   const int g = lane >> 4, col = lane & 15;
   const f16* W = static_cast<const f16*>(a.w);
@@ -134,9 +139,18 @@ __global__ __launch_bounds__(64 * NWV) void conv_stream(const ConvArgs a) {
     const int q4 = 4 * NB;  // 4-channel quads per row
     for (int i = tid; i < 16 * NB2 * q4; i += NT) {
       const int n = i / q4, c = 4 * (i - n * q4);
-      f16x4 v = {0, 0, 0, 0};
-      if (n < a.N2 && c < a.N) v = *reinterpret_cast<const f16x4*>(W2 + (size_t)n * a.Kpad2 + c);
+      f16x4 v = {0, 0, 0, 0}, vl = {0, 0, 0, 0};
+      if (n < a.N2 && c < a.N) {
+        if constexpr (X3) {  // pair-chunk row: logical channel c's hi half at 2 (c & ~7) + (c & 7), its lo 8 further
+          const f16* q = W2 + (size_t)n * a.Kpad2 + 2 * (c & ~7) + (c & 7);
+          v = *reinterpret_cast<const f16x4*>(q);
+          vl = *reinterpret_cast<const f16x4*>(q + 8);
+        } else {
+          v = *reinterpret_cast<const f16x4*>(W2 + (size_t)n * a.Kpad2 + c);
+        }
+      }
       *reinterpret_cast<f16x4*>(w2s + n * LDW2 + c) = v;
+      if constexpr (X3) *reinterpret_cast<f16x4*>(w2l + n * LDW2 + c) = vl;
     }
     for (int i = tid; i < 16 * NB2; i += NT) bs2[i] = i < a.N2 ? a.bias2[i] : 0.f;
   }
@@ -232,24 +246,35 @@ __global__ __launch_bounds__(64 * NWV) void conv_stream(const ConvArgs a) {
       rb[p] = b * a.r_P + y * a.Wo + x;
     }
     if constexpr (FUSE) {
-      f16x4 h[PX][NBF];  // the first conv's activated output, fp16, in registers
+      f16x4 h[PX][NBF];  // the first conv's activated output, fp16, in registers (x3: its hi half)
+      f16x4 hl[X3 ? PX : 1][X3 ? NBF : 1];  // x3: the lo half
 #pragma unroll
       for (int nb = 0; nb < NBF; ++nb) {
         if (nb >= NB) break;
-        h8 af[KS];
+        h8 af[KS + KX];
 #pragma unroll
-        for (int ks = 0; ks < KS; ++ks)
-          af[ks] = *reinterpret_cast<const h8*>(ws + (16 * nb + col) * LDW + 32 * ks + 8 * g);
+        for (int ks = 0; ks < KS + KX; ++ks) {
+          const int c = !X3 ? 4 * ks + g : (ks < KS ? 4 * ks + 2 * (g >> 1) : 8 * (ks - KS) + 2 * g + 1);
+          af[ks] = *reinterpret_cast<const h8*>(ws + (16 * nb + col) * LDW + 8 * c);
+        }
         const f32x4 b4 = *reinterpret_cast<const f32x4*>(bs + 16 * nb + 4 * g);
 #pragma unroll
         for (int p = 0; p < PX; ++p) {
           f32x4 acc = {0.f, 0.f, 0.f, 0.f};
 #pragma unroll
-          for (int ks = 0; ks < KS; ++ks) acc = __builtin_amdgcn_mfma_f32_16x16x32_f16(af[ks], cur[p][ks], acc, 0, 0, 0);
+          for (int ks = 0; ks < KS + KX; ++ks)
+            acc = __builtin_amdgcn_mfma_f32_16x16x32_f16(af[ks], cur[p][ks], acc, 0, 0, 0);
 #pragma unroll
           for (int r = 0; r < 4; ++r) {
             const float xv = acc[r] + b4[r];
-            h[p][nb][r] = (f16)(a.act ? ym_silu_fast(xv) : xv);
+            if constexpr (X3) {
+              const float v = a.act ? ym_silu(xv) : xv;
+              const f16 hi = (f16)v;
+              h[p][nb][r] = hi;
+              hl[p][nb][r] = (f16)(v - (float)hi);
+            } else {
+              h[p][nb][r] = (f16)(a.act ? ym_silu_fast(xv) : xv);
+            }
           }
         }
       }
@@ -258,10 +283,13 @@ __global__ __launch_bounds__(64 * NWV) void conv_stream(const ConvArgs a) {
       for (int j = 0; j < RB; ++j) {
         const int nb2 = nb20 + j;
         if (nb2 >= NB2) break;
-        f16x4 a2[NBF];
+        f16x4 a2[NBF], a2l[X3 ? NBF : 1];
 #pragma unroll
         for (int nb = 0; nb < NBF; ++nb)
-          if (nb < NB) a2[nb] = *reinterpret_cast<const f16x4*>(w2s + (16 * nb2 + col) * LDW2 + 16 * nb + 4 * g);
+          if (nb < NB) {
+            a2[nb] = *reinterpret_cast<const f16x4*>(w2s + (16 * nb2 + col) * LDW2 + 16 * nb + 4 * g);
+            if constexpr (X3) a2l[nb] = *reinterpret_cast<const f16x4*>(w2l + (16 * nb2 + col) * LDW2 + 16 * nb + 4 * g);
+          }
         const int n0 = 16 * nb2 + 4 * g;
         const f32x4 b4 = *reinterpret_cast<const f32x4*>(bs2 + n0);
 #pragma unroll
@@ -269,13 +297,19 @@ __global__ __launch_bounds__(64 * NWV) void conv_stream(const ConvArgs a) {
           f32x4 acc = {0.f, 0.f, 0.f, 0.f};
 #pragma unroll
           for (int nb = 0; nb < NBF; ++nb)
-            if (nb < NB) acc = __builtin_amdgcn_mfma_f32_16x16x16f16(a2[nb], h[p][nb], acc, 0, 0, 0);
+            if (nb < NB) {
+              if constexpr (X3) {
+                acc = __builtin_amdgcn_mfma_f32_16x16x16f16(a2l[nb], h[p][nb], acc, 0, 0, 0);
+                acc = __builtin_amdgcn_mfma_f32_16x16x16f16(a2[nb], hl[p][nb], acc, 0, 0, 0);
+              }
+              acc = __builtin_amdgcn_mfma_f32_16x16x16f16(a2[nb], h[p][nb], acc, 0, 0, 0);
+            }
           if (ob[p] < 0 || n0 >= a.N2) continue;
           float v[4];
 #pragma unroll
           for (int r = 0; r < 4; ++r) {
             const float xv = acc[r] + b4[r];
-            v[r] = a.act2 ? ym_silu_fast(xv) : xv;
+            v[r] = a.act2 ? (X3 ? ym_silu(xv) : ym_silu_fast(xv)) : xv;
           }
           if (res) {
             const RV rv = nb20 == 0 ? rcur[p][j] : SRes<X3>::load(res_at((size_t)rb[p] * a.r_ctot + a.r_coff + n0));
@@ -464,7 +498,7 @@ template <typename OutT, int KIND, int KS, int PX, int CAP, int NWV, bool X3 = f
 hipError_t launch(const ConvArgs& a, hipStream_t st) {
   if (a.Kpad != KS * 32 || a.k != KIND) return hipErrorInvalidValue;
   if constexpr (X3) {
-    if (KS % 2 || a.w2) return hipErrorInvalidValue;
+    if (KS % 2) return hipErrorInvalidValue;
   }
   const int G = (a.M + 15) / 16;
   long wgs = (G + NWV * PX - 1) / (NWV * PX);
@@ -474,10 +508,10 @@ hipError_t launch(const ConvArgs& a, hipStream_t st) {
   if (lds > kMaxWBytes) return hipErrorInvalidValue;
   if (a.w2) {  // fused pair: + W2 [N2P][NP + 8] and bias2 (checked by ym_launch_conv_stream: N <= 128)
     const int N2P = (a.N2 + 15) & ~15;
-    lds += (size_t)N2P * (NP + 8) * sizeof(f16) + (size_t)N2P * sizeof(float);
+    lds += (size_t)N2P * (NP + 8) * sizeof(f16) * (X3 ? 2 : 1) + (size_t)N2P * sizeof(float);
     if (lds > kMaxFusedBytes) return hipErrorInvalidValue;
     if constexpr (NWV == 8 && PX > 1) return hipErrorInvalidValue;  // 256 VGPRs per wave: the pair would spill
-    else hipLaunchKernelGGL((conv_stream<OutT, KIND, KS, PX, true, NWV>), dim3(wgs), dim3(64 * NWV), lds, st, a);
+    else hipLaunchKernelGGL((conv_stream<OutT, KIND, KS, PX, true, NWV, X3>), dim3(wgs), dim3(64 * NWV), lds, st, a);
   } else {
     hipLaunchKernelGGL((conv_stream<OutT, KIND, KS, PX, false, NWV, X3>), dim3(wgs), dim3(64 * NWV), lds, st, a);
   }
@@ -522,7 +556,8 @@ hipError_t ym_launch_conv_stream(int out_f32, const ConvArgs& a, int i, hipStrea
   }
   if ((a.d_ctot & 3) || (a.d_coff & 3) || (a.res && ((a.r_ctot & 3) || (a.r_coff & 3)))) return hipErrorInvalidValue;
   if (a.s0_coff % 8 || a.s0_ctot % 8) return hipErrorInvalidValue;
-  if (a.w2 && (a.N > kFuseMaxN || (a.N2 & 3) || a.Kpad2 < a.N || (a.Kpad2 & 3) || !a.bias2)) return hipErrorInvalidValue;
+  if (a.w2 && (a.N > kFuseMaxN || (a.N2 & 3) || a.Kpad2 < (a.x3 ? 2 : 1) * a.N || (a.Kpad2 & 3) || !a.bias2 || a.k2 != 1))
+    return hipErrorInvalidValue;
   if (a.x3) return out_f32 ? dispatch<float, true>(a, i, st) : dispatch<P2, true>(a, i, st);
   return out_f32 ? dispatch<float>(a, i, st) : dispatch<f16>(a, i, st);
 }

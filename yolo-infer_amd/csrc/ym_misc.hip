@@ -179,6 +179,159 @@ __global__ __launch_bounds__(256) void dwconv3x3_row(const DwArgs a) {
   }
 }
 
+// Column-strip variant: one thread = 8 channels of PXT consecutive pixels in RT consecutive rows.  The 3-row window
+// rolls down the strip: each new output row loads one input row of PXT + 2 pixels, so (RT + 2)(PXT + 2) vector loads
+// serve RT·PXT outputs (PXT 4, RT 4: 2.25 loads per output against 4.5 for the row variant).  Same fmaf order per
+// output as dwconv3x3 (bias, then taps 0..8): bit-identical results.
+template <typename T, int PXT, int RT>
+__global__ __launch_bounds__(256) void dwconv3x3_strip(const DwArgs a) {
+  const int C8 = a.C >> 3;
+  const int Wq = a.W / PXT, Hq = (a.H + RT - 1) / RT;
+  const int idx = ym_xcd_block(blockIdx.x, gridDim.x) * blockDim.x + threadIdx.x;  // contiguous run per XCD
+  const int total = a.B * Hq * Wq * C8;
+  if (idx >= total) return;
+  const int q = idx / C8;
+  const int cg = idx - q * C8;
+  const int rb = q / Wq;  // b * Hq + row block
+  const int x0 = (q - rb * Wq) * PXT;
+  const int b = rb / Hq, y0 = (rb - b * Hq) * RT;
+  const int c0 = cg * 8;
+  const T* src = static_cast<const T*>(a.src) + (size_t)b * a.s_P * a.s_ctot + a.s_coff + c0;
+  typedef typename Vec8<T>::type V;
+  auto load_row = [&](V* r, int iy) {
+#pragma unroll
+    for (int cc = 0; cc < PXT + 2; ++cc) {
+      const int ix = x0 + cc - 1;
+      r[cc] = ((unsigned)iy < (unsigned)a.H && (unsigned)ix < (unsigned)a.W)
+                  ? Vec8<T>::load(src + (size_t)(iy * a.W + ix) * a.s_ctot)
+                  : Vec8<T>::zero();
+    }
+  };
+  f32x4 w[9][2];
+#pragma unroll
+  for (int t = 0; t < 9; ++t) {
+    w[t][0] = *reinterpret_cast<const f32x4*>(a.w + t * a.C + c0);
+    w[t][1] = *reinterpret_cast<const f32x4*>(a.w + t * a.C + c0 + 4);
+  }
+  const f32x4 b0 = *reinterpret_cast<const f32x4*>(a.bias + c0), b1 = *reinterpret_cast<const f32x4*>(a.bias + c0 + 4);
+  V v[3][PXT + 2];  // v[(y - y0 + 1 + r) % 3] holds input row y + r - 1 while output row y is computed
+  load_row(v[0], y0 - 1);
+  load_row(v[1], y0);
+#pragma unroll
+  for (int j = 0; j < RT; ++j) {
+    const int y = y0 + j;
+    if (y >= a.H) break;
+    load_row(v[(j + 2) % 3], y + 1);
+#pragma unroll
+    for (int px = 0; px < PXT; ++px) {
+      float acc[8] = {b0[0], b0[1], b0[2], b0[3], b1[0], b1[1], b1[2], b1[3]};
+#pragma unroll
+      for (int t = 0; t < 9; ++t)
+#pragma unroll
+        for (int e = 0; e < 8; ++e) acc[e] = fmaf((float)v[(j + t / 3) % 3][px + t % 3][e], w[t][e >> 2][e & 3], acc[e]);
+      V o;
+#pragma unroll
+      for (int e = 0; e < 8; ++e) {
+        const float sv = sizeof(T) == 2 ? ym_silu_fast(acc[e]) : ym_silu(acc[e]);
+        o[e] = (typename Vec8<T>::elem)(a.act ? sv : acc[e]);
+      }
+      const int p = y * a.W + x0 + px;
+      Vec8<T>::store(static_cast<T*>(a.dst) + (size_t)(b * a.d_P + p) * a.d_ctot + a.d_coff + c0, o);
+      if (a.raw) {
+#pragma unroll
+        for (int e = 0; e < 8; ++e) a.raw[((size_t)b * a.H * a.W + p) * a.C + c0 + e] = acc[e];
+      }
+    }
+  }
+}
+
+// LDS-tile variant: a workgroup owns TH x TW output pixels x CG 8-channel chunks of one image.  Phase 1: the
+// (TH + 2) x (TW + 2) input window of those chunks (zeros outside the map) and the tile's weights / bias go into LDS,
+// every global load of the workgroup issued before the barrier — one memory round trip per workgroup, each input
+// chunk fetched ~(TH+2)(TW+2)/(TH·TW) times instead of the 9 (one-pixel) or 3(PXT+2)/PXT (row variant) per output.
+// Phase 2: each thread computes its outputs from LDS in the fmaf order of dwconv3x3 (bias, then taps 0..8):
+// bit-identical results.  LDS holds the values as the other variants compute with them (fp16, or fp32 = hi + lo).
+template <typename T, int TH, int TW, int CG>
+__global__ __launch_bounds__(256) void dwconv3x3_lds(const DwArgs a) {
+  typedef typename std::conditional<sizeof(T) == 2, f16x8, f32x8>::type LV;  // one chunk as the kernel computes it
+  constexpr int IH = TH + 2, IW = TW + 2;
+  __shared__ LV xin[IH * IW * CG];
+  __shared__ f32x8 wl[10 * CG];  // taps 0..8, then the bias
+  const int C8 = a.C >> 3;
+  const int ntx = (a.W + TW - 1) / TW, nty = (a.H + TH - 1) / TH, ncg = (C8 + CG - 1) / CG;
+  int vb = ym_xcd_block(blockIdx.x, gridDim.x);  // neighbouring tiles (shared halo rows) on one XCD
+  const int cgi = vb % ncg; vb /= ncg;
+  const int tx = vb % ntx; vb /= ntx;
+  const int ty = vb % nty;
+  const int b = vb / nty;
+  const int x0 = tx * TW, y0 = ty * TH, c0 = cgi * CG;  // c0: first chunk
+  const T* src = static_cast<const T*>(a.src) + (size_t)b * a.s_P * a.s_ctot + a.s_coff;
+  constexpr int NIN = IH * IW * CG;
+  constexpr int PER = (NIN + 255) / 256;
+  LV v[PER];
+#pragma unroll
+  for (int u = 0; u < PER; ++u) {
+    const int i = threadIdx.x + 256 * u;
+    const int c = i % CG, q = i / CG;
+    const int iy = y0 - 1 + q / IW, ix = x0 - 1 + q % IW;
+    LV z;
+#pragma unroll
+    for (int e = 0; e < 8; ++e) z[e] = 0;
+    if (i < NIN && c0 + c < C8 && (unsigned)iy < (unsigned)a.H && (unsigned)ix < (unsigned)a.W) {
+      const auto t = Vec8<T>::load(src + (size_t)(iy * a.W + ix) * a.s_ctot + 8 * (c0 + c));
+#pragma unroll
+      for (int e = 0; e < 8; ++e) z[e] = t[e];
+    }
+    v[u] = z;
+  }
+  if (threadIdx.x < 10 * CG) {
+    const int t = threadIdx.x / CG, c = threadIdx.x % CG;
+    f32x8 w8;
+#pragma unroll
+    for (int e = 0; e < 8; ++e) w8[e] = 0.f;
+    if (c0 + c < C8) {
+      const float* p = t < 9 ? a.w + t * a.C + 8 * (c0 + c) : a.bias + 8 * (c0 + c);
+      const f32x4 lo4 = *reinterpret_cast<const f32x4*>(p), hi4 = *reinterpret_cast<const f32x4*>(p + 4);
+      w8 = f32x8{lo4[0], lo4[1], lo4[2], lo4[3], hi4[0], hi4[1], hi4[2], hi4[3]};
+    }
+    wl[threadIdx.x] = w8;
+  }
+#pragma unroll
+  for (int u = 0; u < PER; ++u) {
+    const int i = threadIdx.x + 256 * u;
+    if (i < NIN) xin[i] = v[u];
+  }
+  __syncthreads();
+  constexpr int NOUT = TH * TW * CG;
+  T* dst = static_cast<T*>(a.dst);
+#pragma unroll
+  for (int u = 0; u < (NOUT + 255) / 256; ++u) {
+    const int i = threadIdx.x + 256 * u;
+    const int c = i % CG, q = i / CG;
+    const int oy = q / TW, ox = q % TW;
+    const int y = y0 + oy, x = x0 + ox;
+    if (i >= NOUT || y >= a.H || x >= a.W || c0 + c >= C8) continue;
+    const f32x8 bv = wl[9 * CG + c];
+    float acc[8];
+#pragma unroll
+    for (int e = 0; e < 8; ++e) acc[e] = bv[e];
+#pragma unroll
+    for (int t = 0; t < 9; ++t) {
+      const LV xv = xin[((oy + t / 3) * IW + ox + t % 3) * CG + c];
+      const f32x8 wv = wl[t * CG + c];
+#pragma unroll
+      for (int e = 0; e < 8; ++e) acc[e] = fmaf((float)xv[e], wv[e], acc[e]);
+    }
+    typename Vec8<T>::type o;
+#pragma unroll
+    for (int e = 0; e < 8; ++e) {
+      const float sv = sizeof(T) == 2 ? ym_silu_fast(acc[e]) : ym_silu(acc[e]);
+      o[e] = (typename Vec8<T>::elem)(a.act ? sv : acc[e]);
+    }
+    Vec8<T>::store(dst + (size_t)(b * a.d_P + y * a.W + x) * a.d_ctot + a.d_coff + 8 * (c0 + c), o);
+  }
+}
+
 // ------------------------------------------------------------------------------------------------- SPPF pools
 // y1 = max5(y0), y2 = max5(y1) = max9(y0), y3 = max13(y0) (stride 1, -inf padding: the cascade is exactly the
 // wider window).  Separable: row maxima of radius 2/4/6 in one pass over the 13-wide row window, then column
@@ -1317,6 +1470,41 @@ hipError_t ym_launch_dwconv(int dtype, const DwArgs& a, hipStream_t st) {
   if (a.C % 8) return hipErrorInvalidValue;
   // pixels per thread: 4 where that still leaves >= 128 workgroups (measured best at 80²/160²), else 2 (20²/40²)
   static const int env_pxt = [] { const char* e = getenv("YM_DW_PXT"); return e ? atoi(e) : 0; }();
+  // YM_DW_MODE (A/B and tests; read at every launch, i.e. at graph capture): 0 = LDS tiles (default), 1 = row /
+  // one-pixel variants, 2 = column strips
+  const char* em = getenv("YM_DW_MODE");
+  const int mode = em ? atoi(em) : 0;
+  if (mode == 0 && !a.raw) {
+    const long tiles = (long)a.B * ((a.H + 7) / 8) * ((a.W + 15) / 16) * ((a.C / 8 + 3) / 4);
+    if (tiles >= 0x7FFFFFFFL) return hipErrorInvalidValue;
+    if (dtype == YM_DT_F16) hipLaunchKernelGGL((dwconv3x3_lds<f16, 8, 16, 4>), dim3(tiles), dim3(256), 0, st, a);
+    else if (dtype == YM_DT_X3) hipLaunchKernelGGL((dwconv3x3_lds<P2, 8, 16, 4>), dim3(tiles), dim3(256), 0, st, a);
+    else hipLaunchKernelGGL((dwconv3x3_lds<float, 8, 16, 4>), dim3(tiles), dim3(256), 0, st, a);
+    return hipGetLastError();
+  }
+  // column strips (dwconv3x3_strip): rows per thread where the grid keeps >= 256 workgroups (YM_DW_RT forces 2 / 4)
+  static const int env_rt = [] { const char* e = getenv("YM_DW_RT"); return e ? atoi(e) : 0; }();
+  if (mode == 2 && !a.raw) {
+    const bool is16 = dtype == YM_DT_F16, x3 = dtype == YM_DT_X3;
+    const int px = (a.W % 4 == 0) ? 4 : (a.W % 2 == 0 ? 2 : 0);
+    auto blocks = [&](int p, int rt) { return ((long)a.B * ((a.H + rt - 1) / rt) * (a.W / p) * (a.C / 8) + 255) / 256; };
+    int rt = env_rt ? env_rt : 0;
+    if (!rt && px) rt = blocks(px, 4) >= 256 ? 4 : (blocks(px, 2) >= 256 ? 2 : 0);
+    if (px == 4 && rt == 4) {
+      const dim3 gs(blocks(4, 4));
+      if (is16) hipLaunchKernelGGL((dwconv3x3_strip<f16, 4, 4>), gs, dim3(256), 0, st, a);
+      else if (x3) hipLaunchKernelGGL((dwconv3x3_strip<P2, 4, 4>), gs, dim3(256), 0, st, a);
+      else hipLaunchKernelGGL((dwconv3x3_strip<float, 4, 4>), gs, dim3(256), 0, st, a);
+      return hipGetLastError();
+    }
+    if (px && rt == 2) {
+      const dim3 gs(blocks(2, 2));
+      if (is16) hipLaunchKernelGGL((dwconv3x3_strip<f16, 2, 2>), gs, dim3(256), 0, st, a);
+      else if (x3) hipLaunchKernelGGL((dwconv3x3_strip<P2, 2, 2>), gs, dim3(256), 0, st, a);
+      else hipLaunchKernelGGL((dwconv3x3_strip<float, 2, 2>), gs, dim3(256), 0, st, a);
+      return hipGetLastError();
+    }
+  }
   const int pxt = env_pxt ? env_pxt : (total / 4 >= 128 * 256 ? 4 : 2);
   if (dtype == YM_DT_F16 && pxt == 4 && a.W % 4 == 0)
     hipLaunchKernelGGL((dwconv3x3_row<f16, 4>), dim3((total / 4 + 255) / 256), dim3(256), 0, st, a);

@@ -284,11 +284,12 @@ int conv_args(ym_ctx* c, const Op& op, int B, const float* d_in, float in_eps, C
       a.bias = reinterpret_cast<const float*>(c->d_weights + (size_t)(uint32_t)r[20]);
       a.act = r[5];
       if (r[30]) {  // fused pair (yolomi/arch.py fuse_pairs): a following 1x1 conv, output in dst/res
-        if (c->dtype != YM_DT_F16) return fail(YM_EBLOB, "op %s: fused conv pairs are f16-only", op.name);
+        if (c->dtype != YM_DT_F16 && c->dtype != YM_DT_X3)
+          return fail(YM_EBLOB, "op %s: fused conv pairs are f16 / x3 only", op.name);
         a.w2 = c->d_weights + (size_t)(uint32_t)r[25];
         a.bias2 = reinterpret_cast<const float*>(c->d_weights + (size_t)(uint32_t)r[26]);
         a.N2 = r[27]; a.act2 = r[28]; a.Kpad2 = r[29]; a.k2 = r[30];
-        if ((a.k2 != 1 && a.k2 != 3) || a.N2 <= 0 || a.Kpad2 < a.k2 * a.k2 * cout || r[31] < 0 || r[31] >= (int)c->bufs.size() || cout % 8 ||
+        if ((a.k2 != 1 && a.k2 != 3) || a.N2 <= 0 || a.Kpad2 < a.k2 * a.k2 * cout * (a.x3 ? 2 : 1) || r[31] < 0 || r[31] >= (int)c->bufs.size() || cout % 8 ||
             c->buf_H(r[31]) != a.Ho || c->buf_Wd(r[31]) != a.Wo || c->bufs[r[31]].C != cout || c->bufs[r[31]].f32)
           return fail(YM_EBLOB, "op %s: bad fused-pair geometry", op.name);
         if (ym_conv_num_cfgs() > 127) return fail(YM_EBLOB, "split cfg encoding needs < 128 conv configs");
@@ -341,9 +342,10 @@ void split_args(ym_ctx* c, const Op& op, const ConvArgs& a, ConvArgs& A, ConvArg
   Bc.s0_P = c->buf_P(mid); Bc.up0 = 0;
   Bc.src1 = nullptr; Bc.C1 = 0; Bc.s1_elems = 0;
   Bc.Hin = a.Ho; Bc.Win = a.Wo; Bc.k = a.k2; Bc.s = 1; Bc.pad = a.k2 / 2;
-  Bc.Cin8 = a.N / 8; Bc.Kc = a.k2 * a.k2 * Bc.Cin8; Bc.Kpad = a.Kpad2; Bc.N = a.N2; Bc.npr = a.N2;
+  const int xs = a.x3 ? 2 : 1;  // x3: fp16 storage chunks of the pair layout
+  Bc.Cin8 = xs * a.N / 8; Bc.Kc = a.k2 * a.k2 * Bc.Cin8; Bc.Kpad = a.Kpad2; Bc.N = a.N2; Bc.npr = a.N2;
   Bc.w = a.w2; Bc.bias = a.bias2; Bc.act = a.act2;
-  Bc.s0_elems = (long)c->cB * c->buf_P(mid) * c->bufs[mid].C;
+  Bc.s0_elems = (long)xs * c->cB * c->buf_P(mid) * c->bufs[mid].C;
 }
 
 hipError_t launch_fused(ym_ctx* c, const Op& op, const ConvArgs& a, int out_f32, int cfg, hipStream_t st) {

@@ -84,11 +84,14 @@ class Param:
 
 class GraphBuilder:
     def __init__(self, scale: str = "n", task: str = "detect", nc: int = NC, quant: bool = False,
-                 fuse: bool = False):
+                 fuse=False):
         """quant=True builds the int8 (PTQ) plan: 16-channel storage granules and materialised concats (a concat is
         one quantized tensor with its own observer, so the two-source A loader is replaced by requant copies).
         fuse=True (f16 plans) merges each conv that feeds only a following 1x1 conv into one launch (fuse_pairs)
-        and runs C3k's two 1x1 convs on the same input as one GEMM."""
+        and runs C3k's two 1x1 convs on the same input as one GEMM; fuse="merge" only the latter (a GEMM with the two
+        weight matrices stacked along N: per output channel the same arithmetic as the two convs); fuse="x3" (x3
+        plans) both, the conv → 1x1 pairs sized by the pair layout's doubled storage K (the streaming kernel's x3
+        FUSE mode) and the Bottlenecks on conv_bneck's x3 mode."""
         if scale not in SCALES:
             raise ValueError(f"Unsupported size: {scale}")
         if task not in ("detect", "segment"):
@@ -99,9 +102,10 @@ class GraphBuilder:
         self.ops: List[Op] = []
         self.params: List[Param] = []
         self.flops_per_pixel: List[Tuple[str, int, int]] = []  # (op name, factor, MACs per output pixel)
-        self.fuse = fuse
+        self.fuse = bool(fuse)  # C3k cv1 ‖ cv2 merged
+        self.x3 = fuse == "x3"  # pair-layout storage: fused pairs sized for it, 1x1 successors only
         self._build()
-        if fuse:
+        if fuse is True or fuse == "x3":
             if quant:
                 raise ValueError("fused conv pairs are f16-only (int8 plans requantise every conv output)")
             self.fuse_pairs()
@@ -420,13 +424,16 @@ class GraphBuilder:
         if a["k"] == 3 and (a["src1"] is not None or a["up0"]):
             return False
         N, N2 = a["c2"], b["c2"]
-        kpad = -(-a["k"] * a["k"] * a["c1"] // 64) * 64
+        xs = 2 if self.x3 else 1  # x3: fp16 storage K of the pair-chunk rows, W2 in hi and lo planes
+        kpad = -(-xs * a["k"] * a["k"] * a["c1"] // 64) * 64
         if N > self.FUSE_MAX_N or N % 4 or N2 % 4 or kpad // 32 not in self.STREAM_KS[a["k"]]:
+            return False
+        if self.x3 and (kpad // 32) % 2:
             return False
         NP, N2P = -(-N // 16) * 16, -(-N2 // 16) * 16
         if NP * (kpad + 16) * 2 + NP * 4 > 80 * 1024:  # csrc/ym_conv_stream.hip LDS: W [NP][Kpad + 16], W2 [N2P][NP + 8]
             return False
-        return NP * (kpad + 16) * 2 + NP * 4 + N2P * (NP + 8) * 2 + N2P * 4 <= self.FUSE_MAX_LDS
+        return NP * (kpad + 16) * 2 + NP * 4 + xs * N2P * (NP + 8) * 2 + N2P * 4 <= self.FUSE_MAX_LDS
 
     # ------------------------------------------------------------------ accounting
     def op_costs(self, B: int, H: int, W: int, act_bytes: int = 2):

@@ -102,10 +102,13 @@ def _qrec(inv_sc, zc, qlo, qhi, mode, post, inv_so=1.0, zo=0, s_r=0.0, z_r=0, s_
     return head + np.asarray(post, np.float32).tobytes()
 
 
-def fuse_default(dtype: str) -> bool:
-    """Fused conv pairs (GraphBuilder.fuse_pairs) in f16 plans unless YM_FUSE=0."""
+def fuse_default(dtype: str):
+    """GraphBuilder `fuse` of a plan unless YM_FUSE=0: f16 plans fuse conv pairs (GraphBuilder.fuse_pairs) and merge
+    C3k's cv1 ‖ cv2; x3 plans merge and fuse the pairs with a 1x1 successor ("x3": GraphBuilder)."""
     import os
-    return dtype == "f16" and os.environ.get("YM_FUSE", "1") != "0"
+    if os.environ.get("YM_FUSE", "1") == "0":
+        return False
+    return {"f16": True, "x3": "x3"}.get(dtype, False)
 
 
 def check_state_dict(g: GraphBuilder, sd: Dict[str, np.ndarray]) -> None:
@@ -209,16 +212,25 @@ def pack_graph(g: GraphBuilder, sd: Dict[str, np.ndarray], dtype: str = "f16", q
             r[21] = Kpad
             pair = a.get("pair")
             if pair is not None:  # fused successor (GraphBuilder.fuse_pairs): W2 [N2][Kpad2], K = (ky, kx, this conv's N)
-                if dtype != "f16":
-                    raise ValueError(f"op {op.name}: fused conv pairs are f16-only")
+                if dtype not in ("f16", "x3"):
+                    raise ValueError(f"op {op.name}: fused conv pairs are f16 / x3 only")
                 w2, b2 = _conv_weights(pair, sd)  # (N2, k2, k2, N)
                 N2, k2 = w2.shape[0], pair["k"]
                 assert w2.shape[1:] == (k2, k2, N)
                 K2 = k2 * k2 * N
-                Kpad2 = (K2 + BK - 1) // BK * BK
-                w2p = np.zeros((N2, Kpad2), np.float32)
-                w2p[:, :K2] = w2.reshape(N2, K2)
-                r[25], r[26] = arena.add(w2p.astype(np.float16)), arena.add(b2.astype(np.float32))
+                if dtype == "x3":  # pair-chunk rows like W (storage K 2·K2, padded to 64)
+                    wr2 = w2.reshape(N2, K2 // 8, 8).astype(np.float32)
+                    hi2 = wr2.astype(np.float16)
+                    lo2 = (wr2 - hi2.astype(np.float32)).astype(np.float16)
+                    Kpad2 = (2 * K2 + BK - 1) // BK * BK
+                    w2h = np.zeros((N2, Kpad2), np.float16)
+                    w2h[:, :2 * K2] = np.stack([hi2, lo2], axis=2).reshape(N2, 2 * K2)
+                else:
+                    Kpad2 = (K2 + BK - 1) // BK * BK
+                    w2p = np.zeros((N2, Kpad2), np.float32)
+                    w2p[:, :K2] = w2.reshape(N2, K2)
+                    w2h = w2p.astype(np.float16)
+                r[25], r[26] = arena.add(w2h), arena.add(b2.astype(np.float32))
                 r[27:32] = [N2, int(bool(pair["act"])), Kpad2, k2, pair["mid"].buf.id]
             if quant:
                 s_in, z_in = qp("act:input" if stem else src0.buf.qkey)
