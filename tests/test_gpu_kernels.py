@@ -58,3 +58,22 @@ def test_dwconv_variants_match_float64(scale, B, dtype, mode):
         assert err < TOL[dtype], (op.name, err)
         n += 1
     assert n == 6
+
+
+def test_predict_rows_are_per_call():
+    """predict() hands the NMS kernel a fresh rows tensor per call (no device copy; a cached graph re-points its NMS
+    nodes): Results of earlier calls keep their detections after later calls on other inputs, and the same input
+    gives the same rows again (f16 and x3 plans, graph replays, lanes 1 and 2)."""
+    from core.model import YOLO11Model
+    for dtype, lanes in (("x3", 1), ("f16", 1), ("f16", 2)):
+        m = YOLO11Model(task="detect", size="n", device="cuda:0", dtype=dtype, verbose=False)
+        m.model.engine.lanes = lanes
+        xa, xb = synthetic_batch(4, 320, 5, DEV), synthetic_batch(4, 320, 6, DEV)
+        ra = m.predict(xa, conf=0.05)
+        da = [r.boxes.data.clone() for r in ra]
+        assert sum(len(d) for d in da) > 0
+        rb = m.predict(xb, conf=0.05)
+        ra2 = m.predict(xa, conf=0.05)
+        for r, r2, d in zip(ra, ra2, da):
+            assert torch.equal(r.boxes.data, d) and torch.equal(r2.boxes.data, d)
+        assert any(not torch.equal(a.boxes.data, b.boxes.data) for a, b in zip(ra, rb))

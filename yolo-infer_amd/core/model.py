@@ -214,10 +214,11 @@ class YOLO11Model:
         t1 = time.perf_counter()
         eng = self.model.engine
         bm = self.global_batch_max(im) if self.global_batch_max is not None and imsrc is None else None
-        dets, counts = eng.run(im, conf=conf, iou=iou, max_det=max_det, classes=classes, agnostic=agnostic,
-                               in_eps=eps, batch_max=bm)
         B = im.shape[0]
-        out = dets[:B].clone()
+        # the NMS kernel writes this call's rows straight into a fresh tensor (the Results keep views into it)
+        out = torch.empty((B, max_det, 6 + eng.nm), dtype=torch.float32, device=im.device)
+        dets, counts = eng.run(im, conf=conf, iou=iou, max_det=max_det, classes=classes, agnostic=agnostic,
+                               in_eps=eps, batch_max=bm, dets_out=out)
         names = self.model.names
         masks = None
         if self.task == "segment":  # process_mask(upsample=True) on the GPU, in letterboxed coordinates

@@ -166,6 +166,16 @@ __device__ __forceinline__ float ym_opaque(float x) {
 }
 
 __device__ __forceinline__ float ym_silu(float x) { return x / (1.0f + expf(-x)); }
+// x3 plans: SiLU from the hardware exp2 and reciprocal, the reciprocal refined by one Newton step (denominator
+// clamped below inf so the step stays finite): ~2 ulp plus the exp2 argument's rounding (|x|·2^-24·ln 2 relative) —
+// far below the x3 GEMMs' ~2^-21 operand precision, in ~7 VALU instructions instead of expf + IEEE division's ~25
+// (the x3 epilogues were VALU-bound on them: every conv output element pays one SiLU)
+__device__ __forceinline__ float ym_silu_x3(float x) {
+  const float d = fminf(1.0f + __builtin_amdgcn_exp2f(-1.4426950408889634f * x), 1e30f);
+  float r = __builtin_amdgcn_rcpf(d);
+  r = fmaf(r, fmaf(-d, r, 1.0f), r);
+  return x * r;
+}
 // SiLU from the hardware exp2 / reciprocal (each ~1 ulp): for epilogues whose outputs are rounded to fp16 anyway
 __device__ __forceinline__ float ym_silu_fast(float x) {
   return x * __builtin_amdgcn_rcpf(1.0f + __builtin_amdgcn_exp2f(-1.4426950408889634f * x));
@@ -344,11 +354,14 @@ hipError_t ym_launch_prep(int dtype, const PrepArgs& a, int* counts, int B, hipS
 hipError_t ym_launch_input_max(const float* x, long n, float* ctl, float* out, hipStream_t st);
 hipError_t ym_launch_decode(const DecodeArgs& a, hipStream_t st);
 hipError_t ym_launch_nms(const NmsArgs& a, hipStream_t st);
+const void* ym_nms_kernel();  // the NMS kernel's function (graph replays re-point its output rows: ym_infer)
 hipError_t ym_launch_stem(int dtype, const ConvArgs& a, hipStream_t st);
 hipError_t ym_launch_letterbox(const LetterboxArgs& a, hipStream_t st);
 hipError_t ym_launch_spin(int usec, hipStream_t st);  // profiling: park the stream for usec (wall clock)
 hipError_t ym_launch_conv_dma(int out_f32, const ConvArgs& a, int i, hipStream_t st);  // f16 plans only
 int ym_conv_dma_num_cfgs();
+int ym_conv_dma_x3_num_cfgs();  // x3-only LDS-DMA configurations (op cfg ids from ym_conv_num_cfgs() on)
+int ym_conv_num_cfgs_dt(int dtype);  // conv-config catalogue size of a plan dtype (YM_DT_*)
 hipError_t ym_launch_conv_bneck(int out_f32, const ConvArgs& a, int i, hipStream_t st);  // fused Bottleneck
 int ym_conv_bneck_num_cfgs();
 hipError_t ym_launch_conv_stream(int out_f32, const ConvArgs& a, int i, hipStream_t st);  // f16 1x1 only

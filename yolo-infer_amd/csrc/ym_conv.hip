@@ -368,7 +368,9 @@ __global__ __launch_bounds__(WM * WN * WK * 64) void conv_igemm(const ConvArgs a
         for (int e = 0; e < 4; ++e) {
           const float x = acc[i][j][4 * q + e] + bias[j][q][e];
           // f16 plans: the fp16-rounded output does not see the fast SiLU's ~1 ulp (fp32) error
-          v[e] = (a.act ? (sizeof(OutT) == 2 ? ym_silu_fast(x) : ym_silu(x)) : x) + resv[i][j][q][e];
+          v[e] = (a.act ? (sizeof(OutT) == 2 ? ym_silu_fast(x)
+                                             : (std::is_same<M, x3_t>::value ? ym_silu_x3(x) : ym_silu(x)))
+                        : x) + resv[i][j][q][e];
           if (a.raw) a.raw[(size_t)(pbase + i * 32 + l32) * a.N + n + e] = x;  // f32 calibration run
         }
         if (a.shuffle) {
@@ -589,7 +591,7 @@ __global__ __launch_bounds__(256) void conv_lds(const ConvArgs a) {
 #pragma unroll
         for (int e = 0; e < 4; ++e) {
           const float x = acc[i][j][4 * q + e] + b4[e];
-          v[e] = a.act ? (X3 ? ym_silu(x) : ym_silu_fast(x)) : x;  // fast SiLU where the output is rounded to fp16
+          v[e] = a.act ? (X3 ? ym_silu_x3(x) : ym_silu_fast(x)) : x;  // fast SiLU where the output is rounded to fp16
         }
         if (a.shuffle) {
           const int sub = n / a.npr;
@@ -703,6 +705,11 @@ int ym_conv_num_cfgs() {
   return kNumAllCfg + ym_conv_dma_num_cfgs() + ym_conv_stream_num_cfgs() + ym_conv_halo_num_cfgs() +
          ym_conv_bneck_num_cfgs();
 }
+// x3 plans: + the x3-only LDS-DMA configurations, appended (the f16 ids, and so the f16 tables, are unchanged)
+int ym_conv_num_cfgs_dt(int dtype) {
+  if (ym_dt_q8(dtype)) return ym_conv_i8_num_cfgs();
+  return ym_conv_num_cfgs() + (dtype == YM_DT_X3 ? ym_conv_dma_x3_num_cfgs() : 0);
+}
 
 hipError_t ym_launch_conv(int dtype, int out_f32, const ConvArgs& a, int cfg, hipStream_t st, bool strict) {
   int kind;
@@ -750,6 +757,11 @@ hipError_t ym_launch_conv(int dtype, int out_f32, const ConvArgs& a, int cfg, hi
       if (e != hipErrorInvalidValue) return e;
     }
     return hipErrorInvalidValue;
+  }
+  if (dtype == YM_DT_X3 && cfg >= ym_conv_num_cfgs()) {  // the x3-only LDS-DMA configurations
+    const hipError_t e = ym_launch_conv_dma(out_f32, a, ym_conv_dma_num_cfgs() + cfg - ym_conv_num_cfgs(), st);
+    if (e != hipErrorInvalidValue || strict) return e;
+    cfg = -1;
   }
   if (cfg >= kNumAllCfg) {
     // a DMA config that does not apply to this op (checked before anything is launched): the tuner skips the

@@ -229,7 +229,7 @@ __global__ __launch_bounds__(64 * NW) void conv_bneck(const ConvArgs a, const Bn
           for (int r = 0; r < 4; ++r) {
             const float v = acc[nb][q][r] + sB1[n0 + r];
             if constexpr (X3) {
-              const float vv = a.act ? ym_silu(v) : v;
+              const float vv = a.act ? ym_silu_x3(v) : v;
               h[r] = (f16)vv;
               hl[r] = (f16)(vv - (float)h[r]);
             } else {
@@ -337,7 +337,7 @@ __global__ __launch_bounds__(64 * NW) void conv_bneck(const ConvArgs a, const Bn
 #pragma unroll
             for (int r = 0; r < 4; ++r) {
               const float v = acc[nb][q][r] + sB2[n0 + r];
-              o[r] = (a.act2 ? ym_silu(v) : v) + rv[r];
+              o[r] = (a.act2 ? ym_silu_x3(v) : v) + rv[r];
             }
             if (!(g.dbg & 8)) ym_p2_store4(dstp + obase + n0, o);
           } else {

@@ -508,7 +508,7 @@ __global__ __launch_bounds__(256 * KG) void conv_dma(const ConvArgs a) {
 #pragma unroll
         for (int e = 0; e < 4; ++e) {
           const float x = acc[0][i][j][4 * q + e] + bias4[j][q][e];
-          v[e] = (a.act ? (X3 ? ym_silu(x) : ym_silu_fast(x)) : x) + (float)res4[i][j][q][e];
+          v[e] = (a.act ? (X3 ? ym_silu_x3(x) : ym_silu_fast(x)) : x) + (float)res4[i][j][q][e];
         }
         if (a.shuffle) {
           const int sub = n / a.npr;
@@ -571,6 +571,26 @@ hipError_t launch_dma(ConvArgs a, int kind, hipStream_t st) {
   return hipGetLastError();
 }
 
+// x3-only configurations (op cfg ids appended after the whole f16 catalogue, so the f16 tables keep their ids): the
+// pair layout doubles a conv's storage K, and with it the chain of K stages of the latency-bound 20² / 40² layers —
+// split K 3-8 ways over workgroups with 128-192-deep stages to shorten it.
+#define YM_DMA_X3_CFGS(X)                                                                                      \
+  X(0, 64, 64, 4, 2, 2, 3) X(1, 64, 64, 4, 2, 2, 2) X(2, 64, 64, 3, 2, 2, 2) X(3, 64, 64, 6, 2, 2, 2)          \
+  X(4, 64, 64, 8, 2, 2, 2) X(5, 64, 64, 4, 1, 2, 2) X(6, 64, 128, 4, 2, 2, 2) X(7, 64, 64, 2, 2, 2, 4)         \
+  X(8, 64, 64, 4, 2, 3, 2)
+constexpr int kNumDmaX3 = 9;
+
+template <typename OutT>
+hipError_t dispatch_x3only(const ConvArgs& a, int kind, int i, hipStream_t st) {
+  switch (i) {
+#define YM_X(id, bm, bn, sp, kg, ns, sub) \
+  case id: return launch_dma<OutT, bm, bn, sp, kg, ns, sub, true>(a, kind, st);
+    YM_DMA_X3_CFGS(YM_X)
+#undef YM_X
+  }
+  return hipErrorInvalidValue;
+}
+
 template <typename OutT, bool X3 = false>
 hipError_t dispatch(const ConvArgs& a, int kind, int i, hipStream_t st) {
   switch (i) {
@@ -585,11 +605,12 @@ hipError_t dispatch(const ConvArgs& a, int kind, int i, hipStream_t st) {
 }  // namespace
 
 int ym_conv_dma_num_cfgs() { return kNumDma; }
+int ym_conv_dma_x3_num_cfgs() { return kNumDmaX3; }
 
 // Host-side applicability: f16 plans, 1x1 stride-1 or 3x3 convs, byte offsets < 2^31 for every operand, and a
-// 64-aligned concat split (a stage never straddles the two sources).
+// 64-aligned concat split (a stage never straddles the two sources).  i >= kNumDma: the x3-only configurations.
 hipError_t ym_launch_conv_dma(int out_f32, const ConvArgs& a, int i, hipStream_t st) {
-  if (i < 0 || i >= kNumDma) return hipErrorInvalidValue;
+  if (i < 0 || i >= kNumDma + (a.x3 ? kNumDmaX3 : 0)) return hipErrorInvalidValue;
   int kind;
   if (a.k == 1 && a.s == 1) kind = 1;
   else if (a.k == 3) kind = a.Cin8 % 8 == 0 ? 4 : 3;
@@ -599,6 +620,8 @@ hipError_t ym_launch_conv_dma(int out_f32, const ConvArgs& a, int i, hipStream_t
   const long lim = 0x7FFFFFF0L / 2;  // elements
   if ((long)a.N * a.Kpad > lim || a.s0_elems > lim || a.s1_elems > lim) return hipErrorInvalidValue;
   if ((a.N & 3) || (a.d_ctot & 3) || (a.d_coff & 3)) return hipErrorInvalidValue;
+  if (a.x3 && i >= kNumDma)
+    return out_f32 ? dispatch_x3only<float>(a, kind, i - kNumDma, st) : dispatch_x3only<P2>(a, kind, i - kNumDma, st);
   if (a.x3) return out_f32 ? dispatch<float, true>(a, kind, i, st) : dispatch<P2, true>(a, kind, i, st);
   return out_f32 ? dispatch<float>(a, kind, i, st) : dispatch<f16>(a, kind, i, st);
 }

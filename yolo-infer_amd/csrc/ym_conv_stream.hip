@@ -268,7 +268,7 @@ __global__ __launch_bounds__(64 * NWV) void conv_stream(const ConvArgs a) {
           for (int r = 0; r < 4; ++r) {
             const float xv = acc[r] + b4[r];
             if constexpr (X3) {
-              const float v = a.act ? ym_silu(xv) : xv;
+              const float v = a.act ? ym_silu_x3(xv) : xv;
               const f16 hi = (f16)v;
               h[p][nb][r] = hi;
               hl[p][nb][r] = (f16)(v - (float)hi);
@@ -309,7 +309,7 @@ __global__ __launch_bounds__(64 * NWV) void conv_stream(const ConvArgs a) {
 #pragma unroll
           for (int r = 0; r < 4; ++r) {
             const float xv = acc[r] + b4[r];
-            v[r] = a.act2 ? (X3 ? ym_silu(xv) : ym_silu_fast(xv)) : xv;
+            v[r] = a.act2 ? (X3 ? ym_silu_x3(xv) : ym_silu_fast(xv)) : xv;
           }
           if (res) {
             const RV rv = nb20 == 0 ? rcur[p][j] : SRes<X3>::load(res_at((size_t)rb[p] * a.r_ctot + a.r_coff + n0));
@@ -344,7 +344,7 @@ __global__ __launch_bounds__(64 * NWV) void conv_stream(const ConvArgs a) {
 #pragma unroll
         for (int r = 0; r < 4; ++r) {
           const float xv = acc[r] + b4[r];
-          v[r] = a.act ? (X3 ? ym_silu(xv) : ym_silu_fast(xv)) : xv;
+          v[r] = a.act ? (X3 ? ym_silu_x3(xv) : ym_silu_fast(xv)) : xv;
         }
         if (res) {
           const RV rv = nb0 == 0 ? rcur[p][j] : SRes<X3>::load(res_at((size_t)rb[p] * a.r_ctot + a.r_coff + n0));

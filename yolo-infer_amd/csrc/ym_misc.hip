@@ -110,7 +110,7 @@ __global__ __launch_bounds__(256) void dwconv3x3(const DwArgs a) {
   typename Vec8<T>::type o;
 #pragma unroll
   for (int e = 0; e < 8; ++e) {  // f16 plans: the fp16 rounding hides the fast SiLU's ~1 ulp (fp32)
-    const float sv = sizeof(T) == 2 ? ym_silu_fast(acc[e]) : ym_silu(acc[e]);
+    const float sv = sizeof(T) == 2 ? ym_silu_fast(acc[e]) : (std::is_same<T, P2>::value ? ym_silu_x3(acc[e]) : ym_silu(acc[e]));
     o[e] = (typename Vec8<T>::elem)(a.act ? sv : acc[e]);
   }
   Vec8<T>::store(static_cast<T*>(a.dst) + (size_t)(b * a.d_P + p) * a.d_ctot + a.d_coff + c0, o);
@@ -167,7 +167,7 @@ __global__ __launch_bounds__(256) void dwconv3x3_row(const DwArgs a) {
     typename Vec8<T>::type o;
 #pragma unroll
     for (int e = 0; e < 8; ++e) {
-      const float sv = sizeof(T) == 2 ? ym_silu_fast(acc[e]) : ym_silu(acc[e]);
+      const float sv = sizeof(T) == 2 ? ym_silu_fast(acc[e]) : (std::is_same<T, P2>::value ? ym_silu_x3(acc[e]) : ym_silu(acc[e]));
       o[e] = (typename Vec8<T>::elem)(a.act ? sv : acc[e]);
     }
     const int p = y * a.W + x0 + px;
@@ -232,7 +232,7 @@ __global__ __launch_bounds__(256) void dwconv3x3_strip(const DwArgs a) {
       V o;
 #pragma unroll
       for (int e = 0; e < 8; ++e) {
-        const float sv = sizeof(T) == 2 ? ym_silu_fast(acc[e]) : ym_silu(acc[e]);
+        const float sv = sizeof(T) == 2 ? ym_silu_fast(acc[e]) : (std::is_same<T, P2>::value ? ym_silu_x3(acc[e]) : ym_silu(acc[e]));
         o[e] = (typename Vec8<T>::elem)(a.act ? sv : acc[e]);
       }
       const int p = y * a.W + x0 + px;
@@ -325,7 +325,7 @@ __global__ __launch_bounds__(256) void dwconv3x3_lds(const DwArgs a) {
     typename Vec8<T>::type o;
 #pragma unroll
     for (int e = 0; e < 8; ++e) {
-      const float sv = sizeof(T) == 2 ? ym_silu_fast(acc[e]) : ym_silu(acc[e]);
+      const float sv = sizeof(T) == 2 ? ym_silu_fast(acc[e]) : (std::is_same<T, P2>::value ? ym_silu_x3(acc[e]) : ym_silu(acc[e]));
       o[e] = (typename Vec8<T>::elem)(a.act ? sv : acc[e]);
     }
     Vec8<T>::store(dst + (size_t)(b * a.d_P + y * a.W + x) * a.d_ctot + a.d_coff + 8 * (c0 + c), o);
@@ -1630,3 +1630,5 @@ hipError_t ym_launch_nms(const NmsArgs& a0, hipStream_t st) {
   hipLaunchKernelGGL(nms_image, dim3(a.B), dim3(NMS_T), 0, st, a);
   return hipGetLastError();
 }
+
+const void* ym_nms_kernel() { return reinterpret_cast<const void*>(&nms_image); }

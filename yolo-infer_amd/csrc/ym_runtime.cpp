@@ -63,11 +63,59 @@ struct GraphKey {
   bool operator==(const GraphKey& o) const { return memcmp(this, &o, sizeof(GraphKey)) == 0; }
 };
 
+// A captured forward.  The detection rows are the caller's (a fresh tensor per predict() call, so the Results of
+// earlier calls stay valid without a copy): the key leaves `dets` out when the graph's NMS nodes were found, and a
+// replay for other rows re-points those nodes (hipGraphExecKernelNodeSetParams; the lanes' row offsets kept).
 struct GraphEntry {
   GraphKey key;
   hipGraph_t graph;
   hipGraphExec_t exec;
+  float* dets = nullptr;                 // the rows the exec's NMS nodes write now
+  std::vector<hipGraphNode_t> nms_nodes;  // empty: dets is part of the key
+  std::vector<NmsArgs> nms_args;
 };
+
+// The NMS kernel nodes of a captured forward and their arguments (false when none is found: the caller keys the
+// graph on the output pointer instead)
+bool find_nms_nodes(GraphEntry& ge) {
+  size_t nn = 0;
+  if (hipGraphGetNodes(ge.graph, nullptr, &nn) != hipSuccess || nn == 0) return false;
+  std::vector<hipGraphNode_t> nodes(nn);
+  if (hipGraphGetNodes(ge.graph, nodes.data(), &nn) != hipSuccess) return false;
+  for (hipGraphNode_t n : nodes) {
+    hipGraphNodeType t;
+    if (hipGraphNodeGetType(n, &t) != hipSuccess || t != hipGraphNodeTypeKernel) continue;
+    hipKernelNodeParams p{};
+    if (hipGraphKernelNodeGetParams(n, &p) != hipSuccess || p.func != ym_nms_kernel()) continue;
+    if (!p.kernelParams || !p.kernelParams[0]) return false;
+    ge.nms_nodes.push_back(n);
+    ge.nms_args.push_back(*static_cast<const NmsArgs*>(p.kernelParams[0]));
+  }
+  if (ge.nms_nodes.empty()) return false;
+  for (const NmsArgs& a : ge.nms_args)  // every node writes inside the captured rows
+    if (a.dets < ge.dets) {
+      ge.nms_nodes.clear();
+      ge.nms_args.clear();
+      return false;
+    }
+  return true;
+}
+
+int repoint_dets(GraphEntry& ge, float* d_dets) {
+  for (size_t j = 0; j < ge.nms_nodes.size(); ++j) {
+    NmsArgs na = ge.nms_args[j];
+    na.dets = d_dets + (na.dets - ge.dets);
+    hipKernelNodeParams p{};
+    HIPCK(hipGraphKernelNodeGetParams(ge.nms_nodes[j], &p));
+    void* args[] = {&na};
+    p.kernelParams = args;
+    p.extra = nullptr;
+    HIPCK(hipGraphExecKernelNodeSetParams(ge.exec, ge.nms_nodes[j], &p));
+    ge.nms_args[j] = na;
+  }
+  ge.dets = d_dets;
+  return YM_OK;
+}
 
 }  // namespace
 
@@ -292,7 +340,7 @@ int conv_args(ym_ctx* c, const Op& op, int B, const float* d_in, float in_eps, C
         if ((a.k2 != 1 && a.k2 != 3) || a.N2 <= 0 || a.Kpad2 < a.k2 * a.k2 * cout * (a.x3 ? 2 : 1) || r[31] < 0 || r[31] >= (int)c->bufs.size() || cout % 8 ||
             c->buf_H(r[31]) != a.Ho || c->buf_Wd(r[31]) != a.Wo || c->bufs[r[31]].C != cout || c->bufs[r[31]].f32)
           return fail(YM_EBLOB, "op %s: bad fused-pair geometry", op.name);
-        if (ym_conv_num_cfgs() > 127) return fail(YM_EBLOB, "split cfg encoding needs < 128 conv configs");
+        if (ym_conv_num_cfgs_dt(c->dtype) > 127) return fail(YM_EBLOB, "split cfg encoding needs < 128 conv configs");
       }
       a.shuffle = r[16];
       a.npr = a.shuffle ? cout / 4 : cout;
@@ -517,7 +565,8 @@ extern "C" {
 int ym_version(void) { return 1; }
 int ym_num_conv_cfgs(int dtype) {  // public dtype codes (ym_model_desc): 1 f16, 2 f32, 3 i8, 4 f8, 5 x3
   if (dtype < 1 || dtype > 5) return YM_EINVAL;
-  return (dtype == 3 || dtype == 4) ? ym_conv_i8_num_cfgs() : ym_conv_num_cfgs();
+  static const int dt[6] = {0, YM_DT_F16, YM_DT_F32, YM_DT_I8, YM_DT_F8, YM_DT_X3};
+  return ym_conv_num_cfgs_dt(dt[dtype]);
 }
 
 const char* ym_last_error(void) { return g_err.c_str(); }
@@ -875,12 +924,20 @@ int ym_infer(ym_ctx* c, const float* d_in, int B, int H, int W, const ym_infer_a
   if (!args->use_graph) return launch_forward(c, d_in, B, args, d_dets, d_counts, st);
   GraphKey key;
   memset(&key, 0, sizeof(key));
-  key.B = B; key.H = H; key.W = W; key.in = d_in; key.dets = d_dets; key.counts = d_counts; key.args = *args;
-  for (auto& g : c->graphs)
-    if (g.key == key) {
+  key.B = B; key.H = H; key.W = W; key.in = d_in; key.dets = nullptr; key.counts = d_counts; key.args = *args;
+  GraphKey key_d = key;  // the key of a graph whose NMS nodes could not be re-pointed
+  key_d.dets = d_dets;
+  for (auto& g : c->graphs) {
+    if (g.key == key) {  // re-pointable: new rows through the NMS nodes' parameters
+      if (g.dets != d_dets && (rc = repoint_dets(g, d_dets))) return rc;
       HIPCK(hipGraphLaunch(g.exec, st));
       return YM_OK;
     }
+    if (g.key == key_d) {
+      HIPCK(hipGraphLaunch(g.exec, st));
+      return YM_OK;
+    }
+  }
   if (c->graphs.size() >= 16) {
     (void)hipGraphExecDestroy(c->graphs.front().exec);
     (void)hipGraphDestroy(c->graphs.front().graph);
@@ -895,9 +952,11 @@ int ym_infer(ym_ctx* c, const float* d_in, int B, int H, int W, const ym_infer_a
     return rc;
   }
   GraphEntry ge;
-  ge.key = key;
   HIPCK(hipStreamEndCapture(c->cap_stream, &ge.graph));
   HIPCK(hipGraphInstantiate(&ge.exec, ge.graph, nullptr, nullptr, 0));
+  ge.dets = d_dets;
+  static const bool no_repoint = [] { const char* e = getenv("YM_GRAPH_REPOINT"); return e && *e == '0'; }();
+  ge.key = (!no_repoint && find_nms_nodes(ge)) ? key : key_d;
   c->graphs.push_back(ge);
   HIPCK(hipGraphLaunch(ge.exec, st));
   return YM_OK;
@@ -1021,7 +1080,7 @@ int ym_tune(ym_ctx* c, const float* d_in, int B, int H, int W, const ym_infer_ar
   hipEvent_t e0, e1;
   HIPCK(hipEventCreate(&e0));
   HIPCK(hipEventCreate(&e1));
-  const int ncfg = ym_dt_q8(c->dtype) ? ym_conv_i8_num_cfgs() : ym_conv_num_cfgs();
+  const int ncfg = ym_conv_num_cfgs_dt(c->dtype);
   const char* tl = getenv("YM_TUNE_LOG");  // per-candidate timings to stderr (tools/)
   const bool tune_log = tl && *tl && *tl != '0';
   for (size_t i = 0; i < c->ops.size(); ++i) {
@@ -1092,9 +1151,10 @@ int ym_set_op_cfg(ym_ctx* c, int B, int H, int W, const int* cfg, int n) {
   if (!c || !cfg || n != (int)c->ops.size()) return fail(YM_EINVAL, "cfg array must hold %zu entries", c ? c->ops.size() : 0);
   for (int i = 0; i < n; ++i) {
     if (cfg[i] >= kSplitTag && c->ops[i].r[0] == OP_CONV && c->ops[i].r[30] &&
-        ((cfg[i] - kSplitTag) >> 7) < ym_conv_num_cfgs() && ((cfg[i] - kSplitTag) & 127) < ym_conv_num_cfgs())
+        ((cfg[i] - kSplitTag) >> 7) < ym_conv_num_cfgs_dt(c->dtype) &&
+        ((cfg[i] - kSplitTag) & 127) < ym_conv_num_cfgs_dt(c->dtype))
       continue;  // a fused pair run as two launches
-    if (cfg[i] >= ym_conv_num_cfgs()) return fail(YM_EINVAL, "cfg[%d] = %d out of range", i, cfg[i]);
+    if (cfg[i] >= ym_conv_num_cfgs_dt(c->dtype)) return fail(YM_EINVAL, "cfg[%d] = %d out of range", i, cfg[i]);
   }
   c->put_cfg(B, H, W, std::vector<int>(cfg, cfg + n));
   c->clear_graphs();

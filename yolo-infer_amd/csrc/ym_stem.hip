@@ -169,7 +169,7 @@ __global__ __launch_bounds__(256) void stem_mfma(const ConvArgs a) {
       if constexpr (X3) {
         float o[4];
 #pragma unroll
-        for (int r = 0; r < 4; ++r) o[r] = ym_silu(acc[r] + bias[t][r]);
+        for (int r = 0; r < 4; ++r) o[r] = ym_silu_x3(acc[r] + bias[t][r]);
         ym_p2_store4(dst + 16 * t, o);
       } else if constexpr (QUANT) {
         int ov[4];

@@ -135,8 +135,10 @@ class Engine:
 
     def run(self, x: torch.Tensor, conf=0.25, iou=0.7, max_det=300, classes: Optional[Sequence[int]] = None,
             agnostic=False, in_eps=None, use_graph=True, max_nms=30000, max_wh=7680.0, lanes=None,
-            batch_max: Optional[torch.Tensor] = None):
-        """x: (B,3,H,W) float32 contiguous on this device. Returns the engine-owned (dets, counts) tensors.
+            batch_max: Optional[torch.Tensor] = None, dets_out: Optional[torch.Tensor] = None):
+        """x: (B,3,H,W) float32 contiguous on this device. Returns the engine-owned (dets, counts) tensors, or
+        (dets_out, counts) when the caller hands in its own (>= B, max_det, 6 + nm) fp32 rows (predict(): a fresh
+        tensor per call, written by the NMS kernel directly — a cached graph re-points its NMS nodes, no copy).
         batch_max: optional (1,) fp32 device tensor, the max over the GLOBAL batch (yolomi.dist: a batch-sharded
         rank takes LoadTensor's /255 decision from it instead of from its own shard)."""
         assert x.is_cuda and x.dtype == torch.float32 and x.is_contiguous() and x.dim() == 4 and x.shape[1] == 3
@@ -158,6 +160,10 @@ class Engine:
             args = self._args_cache[akey] = Runtime.make_args(conf, iou, max_det, max_nms, agnostic, max_wh, in_eps,
                                                               classes, use_graph, lanes, bm)
         dets, counts = self.outputs(B, max_det)
+        if dets_out is not None:
+            assert (dets_out.is_cuda and dets_out.dtype == torch.float32 and dets_out.is_contiguous()
+                    and dets_out.dim() == 3 and dets_out.shape[0] >= B and tuple(dets_out.shape[1:]) == tuple(dets.shape[1:]))
+            dets = dets_out
         stream = torch.cuda.current_stream(self.device).cuda_stream
         Bl = self.lane_batch(B, lanes)
         if (Bl, H, W) not in self._tuned:
