@@ -106,7 +106,9 @@ int ym_rccl_comm_destroy(void* comm);
 /* Replaces `YOLO11Model.predict(tensor)` (core/model.py:118-133) for tensor sources: asynchronous on `stream`
  * (a hipStream_t, NULL = default).  d_input: B×3×H×W fp32 NCHW device tensor (H, W multiples of 32).
  * d_dets: B×max_det×(6+nm) fp32 [x1,y1,x2,y2,conf,cls,(mask coeffs)], rows ordered by NMS keep order;
- * d_counts: B int32 kept counts.  d_dets / d_counts must be device pointers. */
+ * d_counts: B int32 kept counts.  d_dets / d_counts must be device pointers.  The forward of a (shape, input,
+ * counts, args) key is captured once as a HIP graph; a later call with other d_dets rows replays it with its NMS
+ * nodes re-pointed (no recapture, no copy), so a caller may hand in fresh output rows every call. */
 int ym_infer(ym_ctx* ctx, const float* d_input, int B, int H, int W, const ym_infer_args* args, float* d_dets,
              int* d_counts, void* stream);
 

@@ -43,14 +43,17 @@ def main():
     torch.cuda.synchronize()
     base = eng.rt.get_op_cfg(B, S, S)
     ops = eng.graph.ops
-    ncfg = 102  # csrc/ym_conv.hip ym_conv_num_cfgs() without the Bottleneck ids: 17 first-gen + 30 DMA + 43 stream + 12 halo
-    print(f"source {eng.tune_source}, {ncfg} conv configs", flush=True)
-    # (ops on a fused Bottleneck id, base >= ncfg, keep it: the other families do not take a fused pair's shape)
-    conv = [i for i, op in enumerate(ops) if op.kind == "conv" and i > 1 and 0 <= base[i] < ncfg]
+    # csrc/ym_conv.hip ids without the Bottleneck ones (17 first-gen + 30 DMA + 43 stream + 12 halo = 102, then 14
+    # Bottleneck ids), plus the x3-only LDS-DMA ids appended after them in x3 plans
+    nb0, nb1 = 102, 116
+    cands_all = [c for c in range(eng._ncfg()) if not nb0 <= c < nb1]
+    print(f"source {eng.tune_source}, {len(cands_all)} conv configs", flush=True)
+    # (ops on a fused Bottleneck id or a split pair keep it: the other families do not take a fused pair's shape)
+    conv = [i for i, op in enumerate(ops) if op.kind == "conv" and i > 1 and base[i] in cands_all]
 
     # isolated per-op times of every config (graph of back-to-back launches per op, as ym_tune)
     iso = {}
-    for c in range(ncfg):
+    for c in cands_all:
         cfg = list(base)
         for i in conv:
             cfg[i] = c
@@ -83,7 +86,7 @@ def main():
     print(f"base forward {t_base * 1e3:.1f} us", flush=True)
     changed = 0
     for i in sorted(conv, key=lambda i: -iso.get((i, base[i]), 0.0)):
-        ranked = sorted((iso[(i, c)], c) for c in range(ncfg) if iso[(i, c)] > 0)
+        ranked = sorted((iso[(i, c)], c) for c in cands_all if iso[(i, c)] > 0)
         cands = []
         for _, c in ranked:
             if c != cur[i] and c not in cands:

@@ -29,7 +29,19 @@ def main():
     a = ap.parse_args()
     from bench import synthetic_batch
     from core.model import YOLO11Model
-    m = YOLO11Model(task=a.task, size=a.model, device="cuda:0", dtype=a.dtype)
+    blob = None
+    if a.dtype in ("i8", "f8"):  # the PTQ plan of bench.py: calibration through the exact-f32 plan
+        from yolomi.engine import Engine
+        from yolomi.plan import pack_model
+        from yolomi.quant import calibrate
+        from yolomi.synth import synth_weights
+        d0 = torch.device("cuda", 0)
+        ce = Engine(a.model, a.task, synth_weights(a.model, a.task, 0), d0, "f32")
+        qp = calibrate(ce, [synthetic_batch(a.batch, a.size, 500 + i, d0) for i in range(4)],
+                       "fp8" if a.dtype == "f8" else "qnnpack")
+        del ce
+        blob = pack_model(a.model, a.task, synth_weights(a.model, a.task, 0), a.dtype, qp)
+    m = YOLO11Model(task=a.task, size=a.model, device="cuda:0", dtype=a.dtype, weights_blob=blob)
     x = synthetic_batch(a.batch, a.size, 1000, torch.device("cuda", 0))
     eng = m.model.engine
     eng.run(x, use_graph=False)  # table lookup (or tuning) happens here
