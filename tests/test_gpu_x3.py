@@ -168,6 +168,7 @@ def test_x3_1280_n1600_attention_and_max_nms():
 SPLIT_TAG = 1 << 20  # csrc/ym_runtime.cpp kSplitTag: op cfg of a fused pair run as its two convs
 STREAM_BASE, N_STREAM = 17 + 30, 31  # csrc/ym_conv.hip: first-gen + LDS-DMA ids, then the streaming kernels
 BNECK_BASE, N_BNECK = 17 + 30 + 43 + 12, 14  # ... + streaming/small-M + halo ids, then the fused Bottleneck kernels
+X3_BNECK = (116 + 9, 116 + 11)  # x3-only ids: after the f16 catalogue and the 9 x3-only LDS-DMA configurations
 
 
 @pytest.mark.parametrize("scale", ["n", "s"])
@@ -177,7 +178,8 @@ def test_x3_fused_pairs_match_split(scale):
       * conv -> 1x1 pairs (csrc/ym_conv_stream.hip FUSE in the x3 mode: the intermediate split hi/lo in registers,
         three 16x16x16 MFMAs per K block of the second GEMM) on every streaming configuration;
       * Bottlenecks (csrc/ym_conv_bneck.hip in the x3 mode: hi / lo LDS planes, three MFMAs per K step) on every
-        tile variant (the ones whose doubled LDS does not fit fall back to the split pair)."""
+        tile variant, the x3-only 2 x 32 tiles included (the ones whose doubled LDS does not fit fall back to the
+        split pair)."""
     eng = model(scale).model.engine
     x = make_input("uniform", (21, 22), 640).to(DEV)
     B, _, H, W = x.shape
@@ -196,7 +198,7 @@ def test_x3_fused_pairs_match_split(scale):
         eng.run(x, use_graph=False)
         ref = eng.read_buffer(eng.graph.anchor_buf.id, B)
         for cfgs, ids in ((range(STREAM_BASE, STREAM_BASE + N_STREAM), [i for i in pairs if i not in bneck]),
-                          (range(BNECK_BASE, BNECK_BASE + N_BNECK), bneck)):
+                          (list(range(BNECK_BASE, BNECK_BASE + N_BNECK)) + list(range(*X3_BNECK)), bneck)):
             for c in cfgs:
                 cfg = list(split)
                 for i in ids:

@@ -46,7 +46,8 @@ def main():
     # csrc/ym_conv.hip ids without the Bottleneck ones (17 first-gen + 30 DMA + 43 stream + 12 halo = 102, then 14
     # Bottleneck ids), plus the x3-only LDS-DMA ids appended after them in x3 plans
     nb0, nb1 = 102, 116
-    cands_all = [c for c in range(eng._ncfg()) if not nb0 <= c < nb1]
+    nx = eng._ncfg() - (2 if a.dtype == "x3" else 0)  # x3: the last 2 ids are x3-only Bottleneck variants
+    cands_all = [c for c in range(nx) if not nb0 <= c < nb1]
     print(f"source {eng.tune_source}, {len(cands_all)} conv configs", flush=True)
     # (ops on a fused Bottleneck id or a split pair keep it: the other families do not take a fused pair's shape)
     conv = [i for i, op in enumerate(ops) if op.kind == "conv" and i > 1 and base[i] in cands_all]

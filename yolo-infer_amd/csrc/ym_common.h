@@ -364,6 +364,7 @@ int ym_conv_dma_x3_num_cfgs();  // x3-only LDS-DMA configurations (op cfg ids fr
 int ym_conv_num_cfgs_dt(int dtype);  // conv-config catalogue size of a plan dtype (YM_DT_*)
 hipError_t ym_launch_conv_bneck(int out_f32, const ConvArgs& a, int i, hipStream_t st);  // fused Bottleneck
 int ym_conv_bneck_num_cfgs();
+int ym_conv_bneck_x3_num_cfgs();  // x3-only Bottleneck variants (launch indices from ym_conv_bneck_num_cfgs() on)
 hipError_t ym_launch_conv_stream(int out_f32, const ConvArgs& a, int i, hipStream_t st);  // f16 1x1 only
 int ym_conv_stream_num_cfgs();
 hipError_t ym_launch_conv_halo(int out_f32, const ConvArgs& a, int i, hipStream_t st);  // f16 3x3 halo tiles

@@ -708,7 +708,7 @@ int ym_conv_num_cfgs() {
 // x3 plans: + the x3-only LDS-DMA configurations, appended (the f16 ids, and so the f16 tables, are unchanged)
 int ym_conv_num_cfgs_dt(int dtype) {
   if (ym_dt_q8(dtype)) return ym_conv_i8_num_cfgs();
-  return ym_conv_num_cfgs() + (dtype == YM_DT_X3 ? ym_conv_dma_x3_num_cfgs() : 0);
+  return ym_conv_num_cfgs() + (dtype == YM_DT_X3 ? ym_conv_dma_x3_num_cfgs() + ym_conv_bneck_x3_num_cfgs() : 0);
 }
 
 hipError_t ym_launch_conv(int dtype, int out_f32, const ConvArgs& a, int cfg, hipStream_t st, bool strict) {
@@ -725,8 +725,12 @@ hipError_t ym_launch_conv(int dtype, int out_f32, const ConvArgs& a, int cfg, hi
     if (dtype != YM_DT_F16 && dtype != YM_DT_X3) return hipErrorInvalidValue;
     const int bb = kNumAllCfg + ym_conv_dma_num_cfgs() + ym_conv_stream_num_cfgs() + ym_conv_halo_num_cfgs();
     const int nb = ym_conv_bneck_num_cfgs();
+    const int xb = ym_conv_num_cfgs() + ym_conv_dma_x3_num_cfgs();  // x3-only Bottleneck ids
     if (cfg >= bb && cfg < bb + nb) {
       const hipError_t e = ym_launch_conv_bneck(out_f32, a, cfg - bb, st);
+      if (e != hipErrorInvalidValue || strict) return e;
+    } else if (dtype == YM_DT_X3 && cfg >= xb && cfg < xb + ym_conv_bneck_x3_num_cfgs()) {
+      const hipError_t e = ym_launch_conv_bneck(out_f32, a, nb + cfg - xb, st);
       if (e != hipErrorInvalidValue || strict) return e;
     } else if (strict) {
       return hipErrorInvalidValue;
@@ -758,7 +762,8 @@ hipError_t ym_launch_conv(int dtype, int out_f32, const ConvArgs& a, int cfg, hi
     }
     return hipErrorInvalidValue;
   }
-  if (dtype == YM_DT_X3 && cfg >= ym_conv_num_cfgs()) {  // the x3-only LDS-DMA configurations
+  if (dtype == YM_DT_X3 && cfg >= ym_conv_num_cfgs()) {  // the x3-only LDS-DMA configurations (and, past them, the
+                                                          // x3-only Bottleneck ids: inapplicable to a single conv)
     const hipError_t e = ym_launch_conv_dma(out_f32, a, ym_conv_dma_num_cfgs() + cfg - ym_conv_num_cfgs(), st);
     if (e != hipErrorInvalidValue || strict) return e;
     cfg = -1;

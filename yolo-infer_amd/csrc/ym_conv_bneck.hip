@@ -363,6 +363,10 @@ __global__ __launch_bounds__(64 * NW) void conv_bneck(const ConvArgs a, const Bn
   X(6, 8, 0, 2, 16) X(7, 2, 0, 2, 16) X(8, 4, 80, 2, 8) X(9, 5, 80, 2, 8) X(10, 8, 80, 2, 8) X(11, 4, 48, 2, 8) \
   X(12, 8, 48, 2, 8) X(13, 2, 80, 2, 8)
 constexpr int kNumBneck = 14;
+// x3-only variants (ids appended to the x3 id space): 2-row x 32-pixel tiles, the one geometry in which the 80²
+// (64, 32, 64) Bottleneck's doubled LDS (hi / lo planes of input tile, mid image and weights: 151 KB) fits
+#define YM_BNECK_X3_CFGS(X) X(14, 2, 32, 2, 8) X(15, 2, 32, 2, 4)
+constexpr int kNumBneckX3 = 2;
 constexpr int kMaxLds = 160 * 1024;
 
 bool bneck_geom(const ConvArgs& a, int C, int CM, int N2, int S1, int K2, int RB, int TW, BneckGeom& g, int xs) {
@@ -417,19 +421,28 @@ hipError_t dispatch_cfg(const ConvArgs& a, int i, hipStream_t st) {
     YM_BNECK_CFGS(YM_X)
 #undef YM_X
   }
+  if constexpr (X3) {
+    switch (i) {
+#define YM_X(id, rb, tw, px, nw) \
+  case id: return launch<C, CM, N2, S1, K2, rb, tw, px, nw, true>(a, st);
+      YM_BNECK_X3_CFGS(YM_X)
+#undef YM_X
+    }
+  }
   return hipErrorInvalidValue;
 }
 
 }  // namespace
 
 int ym_conv_bneck_num_cfgs() { return kNumBneck; }
+int ym_conv_bneck_x3_num_cfgs() { return kNumBneckX3; }
 
 // Host-side applicability: a fused pair (w2) of a 3x3 / pad 1 conv on one plain source followed by either
 //   * a 3x3 stride-1 conv (k2 == 3, first conv stride 1): a Bottleneck; the residual, if any, IS the input view, or
 //   * a 1x1 conv (k2 == 1, first conv stride 2): a downsampling Conv and the next C3k2's cv1, no residual;
 // (C, Cm, N2) one of the YOLO11 shapes instantiated below; fp16 output into a 4-aligned channel slice.
 hipError_t ym_launch_conv_bneck(int out_f32, const ConvArgs& a, int i, hipStream_t st) {
-  if (i < 0 || i >= kNumBneck || out_f32) return hipErrorInvalidValue;
+  if (i < 0 || i >= kNumBneck + (a.x3 ? kNumBneckX3 : 0) || out_f32) return hipErrorInvalidValue;
   if (!a.w2 || a.k != 3 || a.pad != 1 || a.src1 || a.up0 || a.shuffle || a.raw || a.nchw) return hipErrorInvalidValue;
   const bool bneck = a.k2 == 3 && a.s == 1, down = a.k2 == 1 && a.s == 2;
   if (!bneck && !down) return hipErrorInvalidValue;

@@ -1475,12 +1475,22 @@ hipError_t ym_launch_dwconv(int dtype, const DwArgs& a, hipStream_t st) {
   const char* em = getenv("YM_DW_MODE");
   const int mode = em ? atoi(em) : 0;
   if (mode == 0 && !a.raw) {
-    const long tiles = (long)a.B * ((a.H + 7) / 8) * ((a.W + 15) / 16) * ((a.C / 8 + 3) / 4);
-    if (tiles >= 0x7FFFFFFFL) return hipErrorInvalidValue;
-    if (dtype == YM_DT_F16) hipLaunchKernelGGL((dwconv3x3_lds<f16, 8, 16, 4>), dim3(tiles), dim3(256), 0, st, a);
-    else if (dtype == YM_DT_X3) hipLaunchKernelGGL((dwconv3x3_lds<P2, 8, 16, 4>), dim3(tiles), dim3(256), 0, st, a);
-    else hipLaunchKernelGGL((dwconv3x3_lds<float, 8, 16, 4>), dim3(tiles), dim3(256), 0, st, a);
-    return hipGetLastError();
+    // LDS tile shape (TH x TW pixels x CG chunks; YM_DW_TILE=0..3 for A/B, read at every launch): 0 = 8 x 16 x 4
+    const char* et = getenv("YM_DW_TILE");
+    const int ti = et ? atoi(et) : 0;
+    auto go = [&](auto th, auto tw, auto cg) -> hipError_t {
+      constexpr int TH = decltype(th)::value, TW = decltype(tw)::value, CG = decltype(cg)::value;
+      const long tiles = (long)a.B * ((a.H + TH - 1) / TH) * ((a.W + TW - 1) / TW) * ((a.C / 8 + CG - 1) / CG);
+      if (tiles >= 0x7FFFFFFFL) return hipErrorInvalidValue;
+      if (dtype == YM_DT_F16) hipLaunchKernelGGL((dwconv3x3_lds<f16, TH, TW, CG>), dim3(tiles), dim3(256), 0, st, a);
+      else if (dtype == YM_DT_X3) hipLaunchKernelGGL((dwconv3x3_lds<P2, TH, TW, CG>), dim3(tiles), dim3(256), 0, st, a);
+      else hipLaunchKernelGGL((dwconv3x3_lds<float, TH, TW, CG>), dim3(tiles), dim3(256), 0, st, a);
+      return hipGetLastError();
+    };
+    if (ti == 1) return go(std::integral_constant<int, 4>(), std::integral_constant<int, 32>(), std::integral_constant<int, 4>());
+    if (ti == 2) return go(std::integral_constant<int, 8>(), std::integral_constant<int, 32>(), std::integral_constant<int, 2>());
+    if (ti == 3) return go(std::integral_constant<int, 16>(), std::integral_constant<int, 16>(), std::integral_constant<int, 2>());
+    return go(std::integral_constant<int, 8>(), std::integral_constant<int, 16>(), std::integral_constant<int, 4>());
   }
   // column strips (dwconv3x3_strip): rows per thread where the grid keeps >= 256 workgroups (YM_DW_RT forces 2 / 4)
   static const int env_rt = [] { const char* e = getenv("YM_DW_RT"); return e ? atoi(e) : 0; }();
