@@ -721,55 +721,33 @@ __global__ __launch_bounds__(256) void attn_psa_x3(const AttnArgs a) {
   const int hq = a.q_coff + h * 128;  // per head: q 32, k 32, v 64 logical channels
   for (int i = tid; i < 640; i += 256)
     pw[i] = i < 576 ? a.pe_w[(i >> 6) * a.C + h * 64 + (i & 63)] : a.pe_b[h * 64 + i - 576];
-  // 1. V^T hi / lo planes (keys >= N zero): 8 chunks of 8 v channels per key.  Every load of the thread is issued
-  // before the first LDS write (a load -> scatter loop waited one memory latency per iteration)
-  constexpr int NVI = 16 * NKT * 8, NV = (NVI + 255) / 256;
-  {
-    HL v[NV];
+  // 1. V^T hi / lo planes (keys >= N zero): 8 chunks of 8 v channels per key
+  for (int i = tid; i < 16 * NKT * 8; i += 256) {
+    const int key = i >> 3, ch = i & 7;
+    HL v{Vec8<f16>::zero(), Vec8<f16>::zero()};
+    if (key < N) v = ym_load_hl(qkv + (img + key) * a.q_ctot + hq + 64 + 8 * ch);
 #pragma unroll
-    for (int u = 0; u < NV; ++u) {
-      const int i = tid + 256 * u, key = i >> 3, ch = i & 7;
-      v[u] = HL{Vec8<f16>::zero(), Vec8<f16>::zero()};
-      if (i < NVI && key < N) v[u] = ym_load_hl(qkv + (img + key) * a.q_ctot + hq + 64 + 8 * ch);
-    }
-#pragma unroll
-    for (int u = 0; u < NV; ++u) {
-      const int i = tid + 256 * u, key = i >> 3, ch = i & 7;
-      if (i >= NVI) continue;
-#pragma unroll
-      for (int e = 0; e < 8; ++e) {
-        vt[(8 * ch + e) * LDV + key] = v[u].hi[e];
-        vtl[(8 * ch + e) * LDV + key] = v[u].lo[e];
-      }
+    for (int e = 0; e < 8; ++e) {
+      vt[(8 * ch + e) * LDV + key] = v.hi[e];
+      vtl[(8 * ch + e) * LDV + key] = v.lo[e];
     }
   }
   const int q = qb * 64 + wave * 16 + c;
   HL qf{Vec8<f16>::zero(), Vec8<f16>::zero()};
   if (q < N) qf = ym_load_hl(qkv + (img + q) * a.q_ctot + hq + 8 * g);
-  // 2. scores S^T = K·Q^T (log2 units): lane (g, c) supplies key 16t + c, logical chunk g of K; the K fragments of
-  // KT key tiles are loaded together, then their MFMAs run
+  // 2. scores S^T = K·Q^T (log2 units): lane (g, c) supplies key 16t + c, logical chunk g of K
   const float sl2 = a.scale * 1.4426950408889634f;
   float s[NKT][4];
-  constexpr int KT = NKT > 13 ? 13 : NKT;
 #pragma unroll
-  for (int t0 = 0; t0 < NKT; t0 += KT) {
-    HL kf[KT];
+  for (int t = 0; t < NKT; ++t) {
+    const int key = 16 * t + c;
+    HL kf{Vec8<f16>::zero(), Vec8<f16>::zero()};
+    if (key < N) kf = ym_load_hl(qkv + (img + key) * a.q_ctot + hq + 32 + 8 * g);
+    f32x4 d = __builtin_amdgcn_mfma_f32_16x16x32_f16(kf.lo, qf.hi, f32x4{0.f, 0.f, 0.f, 0.f}, 0, 0, 0);
+    d = __builtin_amdgcn_mfma_f32_16x16x32_f16(kf.hi, qf.lo, d, 0, 0, 0);
+    d = __builtin_amdgcn_mfma_f32_16x16x32_f16(kf.hi, qf.hi, d, 0, 0, 0);
 #pragma unroll
-    for (int u = 0; u < KT; ++u) {
-      const int key = 16 * (t0 + u) + c;
-      kf[u] = HL{Vec8<f16>::zero(), Vec8<f16>::zero()};
-      if (t0 + u < NKT && key < N) kf[u] = ym_load_hl(qkv + (img + key) * a.q_ctot + hq + 32 + 8 * g);
-    }
-#pragma unroll
-    for (int u = 0; u < KT; ++u) {
-      const int t = t0 + u;
-      if (t >= NKT) break;
-      f32x4 d = __builtin_amdgcn_mfma_f32_16x16x32_f16(kf[u].lo, qf.hi, f32x4{0.f, 0.f, 0.f, 0.f}, 0, 0, 0);
-      d = __builtin_amdgcn_mfma_f32_16x16x32_f16(kf[u].hi, qf.lo, d, 0, 0, 0);
-      d = __builtin_amdgcn_mfma_f32_16x16x32_f16(kf[u].hi, qf.hi, d, 0, 0, 0);
-#pragma unroll
-      for (int r = 0; r < 4; ++r) s[t][r] = 16 * t + 4 * g + r < N ? d[r] * sl2 : -INFINITY;
-    }
+    for (int r = 0; r < 4; ++r) s[t][r] = 16 * t + 4 * g + r < N ? d[r] * sl2 : -INFINITY;
   }
   __syncthreads();
   // 3. softmax over the keys of query l&15 (fp32, exact exp2)
