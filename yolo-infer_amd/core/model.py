@@ -227,9 +227,10 @@ class YOLO11Model:
             # image than `cap` takes the exact-size two-read path (and raises `cap` for the next call)
             # Memory: the slot buffer is B x cap x H x W bytes, so it is only used within
             # YM_MASK_BUDGET_MB (256 MB by default; larger batches take the exact-size path), `cap` follows the recent
-            # detection counts down as well as up (the power of two >= 2x the last maximum, 16..max_det), and a
-            # mostly empty slot buffer is compacted before the Results views are taken, so results kept by the
-            # caller retain at most twice the bytes of their masks.
+            # detection counts down as well as up (1.25x the last maximum rounded up to 16, 16..max_det: a steady
+            # stream of batches keeps its slots over half full, so no compaction copy runs), and a mostly empty slot
+            # buffer is compacted before the Results views are taken, so results kept by the caller retain at most
+            # twice the bytes of their masks.
             H, W = im.shape[2:]
             cap = min(self._mask_cap, max_det)
             budget = int(os.environ.get("YM_MASK_BUDGET_MB", "256")) << 20
@@ -254,7 +255,7 @@ class YOLO11Model:
             else:
                 masks, nonempty, offs = eng.masks(out, n, H, W)
                 keep = nonempty.tolist()
-            self._mask_cap = max(16, min(max_det, 1 << (2 * max(max(n), 1) - 1).bit_length()))
+            self._mask_cap = max(16, min(max_det, -(-(5 * max(max(n), 1)) // 64) * 16))  # ceil(1.25 max / 16) * 16
         else:
             n = counts[:B].tolist()  # the device→host sync of a predict call
         if imsrc is not None:  # ops.scale_boxes back to each original image
