@@ -275,7 +275,11 @@ class YOLO11Model:
         mb = masks.view(torch.bool).reshape(-1, H, W)  # the kernel writes 0/1 bytes: a bool view, no copy
         for b in range(B):
             kb = keep[offs[b]:offs[b] + n[b]]
-            if all(kb):  # the common case: every kept detection has a mask pixel — views, no gathers
+            if all(kb) and imsrc is None:  # the common case: boxes, masks and input slice as views taken on access
+                res.append(Results.from_batch(im, b, names, out, n[b], path=f"image{b}.jpg", speed=speed, masks=mb,
+                                              moff=offs[b]))
+                continue
+            if all(kb):  # every kept detection has a mask pixel — views, no gathers
                 bx, mk = out[b, :n[b], :6], mb[offs[b]:offs[b] + n[b]]
             else:
                 sel = torch.tensor([i for i, k in enumerate(kb) if k], dtype=torch.long, device=out.device)

@@ -133,9 +133,11 @@ class Results:
 
     @classmethod
     def from_batch(cls, batch: torch.Tensor, b: int, names: Dict[int, str], dets: torch.Tensor, n: int,
-                   path: str = "image0.jpg", speed=None) -> "Results":
-        """Image b of a predict() batch: boxes = dets[b, :n, :6] and the input slice batch[b], both taken (as tensor
-        views) on first access, so building the B Results of a call costs no tensor operations."""
+                   path: str = "image0.jpg", speed=None, masks: Optional[torch.Tensor] = None,
+                   moff: int = 0) -> "Results":
+        """Image b of a predict() batch: boxes = dets[b, :n, :6], the input slice batch[b] and (Segment) the masks
+        masks[moff : moff + n], all taken (as tensor views) on first access, so building the B Results of a call
+        costs no tensor operations."""
         r = cls.__new__(cls)
         r._batch, r._b, r._dets, r._n = batch, b, dets, n
         r._orig_tensor_v = None
@@ -143,7 +145,8 @@ class Results:
         r.orig_shape = tuple(batch.shape[-2:])
         r.names = names
         r._boxes = None
-        r.masks = None
+        r._masks = None
+        r._msrc = (masks, moff) if masks is not None else None
         r.path = path
         r.speed = speed or {"preprocess": None, "inference": None, "postprocess": None}
         r.probs = r.keypoints = r.obb = None
@@ -182,6 +185,18 @@ class Results:
     @boxes.setter
     def boxes(self, b):
         self._boxes = b
+
+    @property
+    def masks(self) -> Optional["Masks"]:
+        if self._masks is None and getattr(self, "_msrc", None) is not None:
+            mb, moff = self._msrc
+            self._masks = Masks(mb[moff:moff + self._n], self.orig_shape)
+        return self._masks
+
+    @masks.setter
+    def masks(self, m):
+        self._masks = m
+        self._msrc = None
 
     @property
     def orig_img(self) -> np.ndarray:
