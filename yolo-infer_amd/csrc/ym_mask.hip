@@ -178,7 +178,6 @@ __global__ __launch_bounds__(256) void mask_upsample16(const MaskArgs a) {
         if (v > 0.f) w[i >> 2] |= 1u << (8 * (i & 3));
       }
       on = on || (w[0] | w[1] | w[2] | w[3]) != 0u;
-    }
       typedef unsigned u32x4 __attribute__((ext_vector_type(4)));
       *reinterpret_cast<u32x4*>(a.masks + (size_t)d * a.H * a.W + (size_t)oy * a.W + ox0) = u32x4{w[0], w[1], w[2], w[3]};
     }  // (runs outside the box's reach: zero from the memset)
