@@ -95,10 +95,7 @@ __global__ __launch_bounds__(256) void mask_upsample(const MaskArgs a) {
 // bilinear reach) are all zero — crop_mask zeroes the prototype mask there — and are stored without evaluation.
 // A workgroup covers RPT x 256 runs (~26 rows at 640 px): its dependent chain (detection row -> coefficients ->
 // prototype rows -> masks) is paid once per 16 KB of mask instead of once per 4 KB (yolo11s-seg B=4: 25,600
-// workgroups of ~5 us chains made the masks ~130 us per predict, well above their ~12 us of stores).  The mask
-// bytes are zeroed by one memset before the launch; workgroups whose rows miss the box exit after reading the
-// detection row, and the others store only the runs within the box's bilinear reach (round 3: most workgroups of a
-// mask were storing zeros: 64 us per yolo11s-seg B=4 predict).
+// workgroups of ~5 us chains made the masks ~130 us per predict, well above their ~12 us of stores).
 constexpr int LROWS = 12, LMW = 512, RPT = 4;
 __global__ __launch_bounds__(256) void mask_upsample16(const MaskArgs a) {
   __shared__ float tile[LROWS * LMW];
@@ -119,8 +116,6 @@ __global__ __launch_bounds__(256) void mask_upsample16(const MaskArgs a) {
   auto src_y = [&](int oy) { const float f = ((float)oy + 0.5f) * rh - 0.5f; return f < 0.f ? 0 : (int)f; };
   const int ya = src_y(oyA), yb = min(src_y(oyB) + 1, a.MH - 1);
   const bool rows_hit = (float)oyB >= lo_y && (float)oyA < hi_y;
-  if (!rows_hit) return;  // every run of these rows lies outside the box: zero, as the memset before the launch left
-                          // it (uniform per workgroup)
   // the prototype-resolution mask of rows ya..yb, computed here (mask_lowres's arithmetic: crop test in fp32, the
   // coefficient dot product as the same fmaf chain), so no (total, MH, MW) intermediate is written or re-read
   __shared__ float coef[64];
@@ -161,7 +156,7 @@ __global__ __launch_bounds__(256) void mask_upsample16(const MaskArgs a) {
     if (q >= a.H * runs) break;
     const int oy = q / runs, ox0 = (q - oy * runs) * 16;
     unsigned w[4] = {0u, 0u, 0u, 0u};
-    if ((float)oy >= lo_y && (float)oy < hi_y && (float)(ox0 + 16) > lo_x && (float)ox0 < hi_x) {
+    if (rows_hit && (float)oy >= lo_y && (float)oy < hi_y && (float)(ox0 + 16) > lo_x && (float)ox0 < hi_x) {
       float fy = ((float)oy + 0.5f) * rh - 0.5f;
       fy = fy < 0.f ? 0.f : fy;
       const int y0 = (int)fy, y1 = y0 < a.MH - 1 ? y0 + 1 : y0;
@@ -178,9 +173,9 @@ __global__ __launch_bounds__(256) void mask_upsample16(const MaskArgs a) {
         if (v > 0.f) w[i >> 2] |= 1u << (8 * (i & 3));
       }
       on = on || (w[0] | w[1] | w[2] | w[3]) != 0u;
-      typedef unsigned u32x4 __attribute__((ext_vector_type(4)));
-      *reinterpret_cast<u32x4*>(a.masks + (size_t)d * a.H * a.W + (size_t)oy * a.W + ox0) = u32x4{w[0], w[1], w[2], w[3]};
-    }  // (runs outside the box's reach: zero from the memset)
+    }
+    typedef unsigned u32x4 __attribute__((ext_vector_type(4)));
+    *reinterpret_cast<u32x4*>(a.masks + (size_t)d * a.H * a.W + (size_t)oy * a.W + ox0) = u32x4{w[0], w[1], w[2], w[3]};
   }
   const unsigned long long bal = __ballot(on);
   if (bal && (threadIdx.x & 63) == __builtin_ctzll(bal)) a.nonempty[d] = 1;
@@ -211,9 +206,7 @@ hipError_t ym_launch_masks(const MaskArgs& a, hipStream_t st) {
     hipLaunchKernelGGL(mask_flags_init, dim3((a.total + a.B + 255) / 256), dim3(256), 0, st, a);
   else
     (void)hipMemsetAsync(a.nonempty, 0, (size_t)a.total * sizeof(int), st);
-  if (ym_masks_fused(a)) {  // fused: prototype masks computed per workgroup in LDS, zeros from one memset
-    const hipError_t e = hipMemsetAsync(a.masks, 0, (size_t)a.total * a.H * a.W, st);
-    if (e != hipSuccess) return e;
+  if (ym_masks_fused(a)) {  // fused: prototype masks computed per workgroup in LDS
     hipLaunchKernelGGL(mask_upsample16, dim3((a.H * (a.W / 16) + 256 * RPT - 1) / (256 * RPT), a.total), dim3(256), 0,
                        st, a);
   } else {
