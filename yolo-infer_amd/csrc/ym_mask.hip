@@ -133,36 +133,7 @@ __global__ __launch_bounds__(256) void mask_upsample16(const MaskArgs a) {
       if (!(x >= cx0 && x < cx1 && y >= cy0 && y < cy1)) tile[i] = 0.f;
     }
     const int bw = cx1 - cx0, nin = cx1 > cx0 && cy1 > cy0 ? (cy1 - cy0) * bw : 0;
-    // nm = 32 (every YOLO11 Segment head): four pixels per thread and round, their 32 prototype loads all in flight
-    // (one memory round trip per 1024 in-box pixels instead of per 256); the same fmaf chain per pixel
-    const int nin4 = a.nm == 32 ? nin : 0;
-    for (int j0 = threadIdx.x; j0 < nin4; j0 += 1024) {
-      f32x4 p4[4][8];
-#pragma unroll
-      for (int u = 0; u < 4; ++u) {
-        const int j = j0 + 256 * u;
-        const int y = cy0 + j / bw, x = cx0 + (j - (j / bw) * bw);
-        const f32x4* pr = reinterpret_cast<const f32x4*>(a.proto + ((size_t)b * a.MH * a.MW + (size_t)y * a.MW + x) * 32);
-#pragma unroll
-        for (int c4 = 0; c4 < 8; ++c4) p4[u][c4] = j < nin ? pr[c4] : f32x4{0.f, 0.f, 0.f, 0.f};
-      }
-#pragma unroll
-      for (int u = 0; u < 4; ++u) {
-        const int j = j0 + 256 * u;
-        if (j >= nin) break;
-        const int y = cy0 + j / bw, x = cx0 + (j - (j / bw) * bw);
-        float v = 0.f;
-#pragma unroll
-        for (int c4 = 0; c4 < 8; ++c4) {
-          v = fmaf(coef[4 * c4], p4[u][c4][0], v);
-          v = fmaf(coef[4 * c4 + 1], p4[u][c4][1], v);
-          v = fmaf(coef[4 * c4 + 2], p4[u][c4][2], v);
-          v = fmaf(coef[4 * c4 + 3], p4[u][c4][3], v);
-        }
-        tile[(y - ya) * a.MW + x] = v;
-      }
-    }
-    for (int j = nin4 ? nin : threadIdx.x; j < nin; j += 256) {
+    for (int j = threadIdx.x; j < nin; j += 256) {
       const int y = cy0 + j / bw, x = cx0 + (j - (j / bw) * bw);
       const f32x4* pr = reinterpret_cast<const f32x4*>(a.proto + ((size_t)b * a.MH * a.MW + (size_t)y * a.MW + x) * a.nm);
       float v = 0.f;
