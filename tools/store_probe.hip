@@ -8,6 +8,8 @@
 //   4  the x3 pair-layout epilogue (ym_p2_store4): 64-B rows (16 channels = two [hi x8 | lo x8] chunks), lane (g, c)
 //      writes 8 B of hi at row c, byte 32 (g >> 1) + 8 (g & 1), then 8 B of lo 16 bytes further: per instruction 16
 //      rows x two 16-B runs
+//   5  the lane-pair x3 epilogue (ym_p2_store4_pair): lanes (g, c) of the same 64-B row exchange halves, lane g writes
+//      16 B at byte 16 g: per instruction 16 rows x one 64-B run
 #include <hip/hip_runtime.h>
 
 #include <cstdio>
@@ -60,6 +62,13 @@ __global__ __launch_bounds__(256) void st_p4(float2* p, long rows) {
   }
 }
 
+__global__ __launch_bounds__(256) void st_p5(float4* p, long rows) {
+  const int lane = threadIdx.x & 63, wave = threadIdx.x >> 6;
+  const int g = lane >> 4, c = lane & 15;
+  for (long r0 = ((long)blockIdx.x * 4 + wave) * 16; r0 < rows; r0 += (long)gridDim.x * 4 * 16)
+    p[(r0 + c) * 4 + g] = make_float4(1.f, 2.f, 3.f, 4.f);
+}
+
 int main() {
   const size_t bytes = 256ull << 20;
   void* d = nullptr;
@@ -67,16 +76,17 @@ int main() {
   hipEvent_t e0, e1;
   hipEventCreate(&e0);
   hipEventCreate(&e1);
-  const char* names[5] = {"contiguous 1 KiB / instr", "32 B runs, 128-B rows", "8 B x 4 per 64-B row", "32 B runs, 256-B rows",
-                          "x3 pair epilogue (2x16 B/row)"};
+  const char* names[6] = {"contiguous 1 KiB / instr", "32 B runs, 128-B rows", "8 B x 4 per 64-B row", "32 B runs, 256-B rows",
+                          "x3 pair epilogue (2x16 B/row)", "x3 lane-pair epilogue (64 B/row)"};
   for (int grid : {1024, 2048, 4096}) {
-    for (int pat = 0; pat < 5; ++pat) {
+    for (int pat = 0; pat < 6; ++pat) {
       auto launch = [&]() {
         if (pat == 0) hipLaunchKernelGGL(st_contig, dim3(grid), dim3(256), 0, 0, (float4*)d, (long)(bytes / 16));
         if (pat == 1) hipLaunchKernelGGL(st_p1, dim3(grid), dim3(256), 0, 0, (float4*)d, (long)(bytes / 128));
         if (pat == 2) hipLaunchKernelGGL(st_p2, dim3(grid), dim3(256), 0, 0, (float2*)d, (long)(bytes / 64));
         if (pat == 3) hipLaunchKernelGGL(st_p3, dim3(grid), dim3(256), 0, 0, (float4*)d, (long)(bytes / 256));
         if (pat == 4) hipLaunchKernelGGL(st_p4, dim3(grid), dim3(256), 0, 0, (float2*)d, (long)(bytes / 64));
+        if (pat == 5) hipLaunchKernelGGL(st_p5, dim3(grid), dim3(256), 0, 0, (float4*)d, (long)(bytes / 64));
       };
       launch();
       hipDeviceSynchronize();

@@ -119,6 +119,33 @@ __device__ __forceinline__ void ym_p2_store4(P2* p, const float* v) {
   *reinterpret_cast<f16x4*>(q) = h;
   *reinterpret_cast<f16x4*>(q + 8) = l;
 }
+// The same 4 channels stored by a LANE PAIR: the lane holding channels c .. c+3 of a chunk (c % 8 == 0, `odd` false)
+// and its partner lane (lane ^ XOR, same pixel) holding c+4 .. c+7 swap halves, so the even lane writes the chunk's
+// hi x8 (16 B) and the odd lane its lo x8 (16 B) — the chunk is one 32-byte run, not four 8-byte pieces
+// (tools/store_probe.hip: the 8-byte pattern of ym_p2_store4 writes HBM at 4.8-5.4 TB/s, 32-byte runs at 6.5-6.9).
+// Same stored bits as ym_p2_store4.  Both lanes of a pair must execute it (the exchange is a cross-lane read);
+// `ok` predicates only the store, and p may be any address when !ok.
+template <int XOR>
+__device__ __forceinline__ void ym_p2_store4_pair(P2* p, const float* v, bool odd, bool ok) {
+  f16x4 h, l;
+#pragma unroll
+  for (int e = 0; e < 4; ++e) {
+    h[e] = (f16)v[e];
+    l[e] = (f16)(v[e] - (float)h[e]);
+  }
+  typedef unsigned u32x2_t __attribute__((ext_vector_type(2)));
+  const u32x2_t s = __builtin_bit_cast(u32x2_t, odd ? h : l);  // the half the partner stores
+  u32x2_t r;
+  r[0] = (unsigned)__shfl_xor((int)s[0], XOR);
+  r[1] = (unsigned)__shfl_xor((int)s[1], XOR);
+  const f16x4 q = __builtin_bit_cast(f16x4, r);
+  const f16x8 o = odd ? f16x8{q[0], q[1], q[2], q[3], l[0], l[1], l[2], l[3]}
+                      : f16x8{h[0], h[1], h[2], h[3], q[0], q[1], q[2], q[3]};
+  if (ok) {
+    const uintptr_t u = reinterpret_cast<uintptr_t>(p);
+    *reinterpret_cast<f16x8*>((u & ~(uintptr_t)31) + (odd ? 16 : 0)) = o;
+  }
+}
 __device__ __forceinline__ void ym_p2_load4(const P2* p, float* v) {  // v[e] = hi + lo
   const f16* q = ym_p2_hi4(p);
   const f16x4 h = *reinterpret_cast<const f16x4*>(q), l = *reinterpret_cast<const f16x4*>(q + 8);
@@ -260,6 +287,10 @@ struct ConvArgs {
   // lo x8]; Cin8 / Kc / Kpad then count fp16 storage chunks (twice the logical ones), ctot / coff / C0 / C1 / d_* / r_*
   // stay logical channels, s0_elems / s1_elems count fp16 elements
   int x3;
+  // x3 pair-layout outputs: lane-pair whole-chunk epilogue stores (ym_p2_store4_pair) where the output slice allows
+  // them; a bit mask per kernel family (1 LDS-DMA, 2 streaming, 4 stem, 8 fused Bottleneck; YM_PAIRST for A/B,
+  // default 15); a clear bit keeps the per-lane ym_p2_store4.  Same stored bits either way.
+  int pst;
 };
 
 struct DwArgs {

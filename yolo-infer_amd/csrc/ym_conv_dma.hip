@@ -495,6 +495,11 @@ __global__ __launch_bounds__(256 * KG) void conv_dma(const ConvArgs a) {
 
   // ---- epilogue: lane owns channels nb + 32j + 8q + 4h + {0..3} of pixel pbm + 32i + l32
   OutT* dst = static_cast<OutT*>(a.dst);
+  // x3 pair-layout outputs: lanes l and l ^ 32 (h = 0 / 1: channels +0..3 / +4..7 of one chunk of one pixel) write
+  // the chunk as one 32-byte run (ym_p2_store4_pair) where the slice, the channel count and the pixel-shuffle
+  // sub-pixel width keep every chunk whole (uniform)
+  constexpr bool PAIRST = X3 && std::is_same<OutT, P2>::value;
+  const bool pairst = PAIRST && (a.pst & 1) && ((a.N | a.d_coff | a.d_ctot) & 7) == 0 && (!a.shuffle || (a.npr & 7) == 0);
 #pragma unroll
   for (int i = 0; i < TM; ++i) {
     if (ep_m[i] >= a.M) continue;
@@ -503,6 +508,25 @@ __global__ __launch_bounds__(256 * KG) void conv_dma(const ConvArgs a) {
 #pragma unroll
       for (int q = 0; q < 4; ++q) {
         const int n = tn * BN + wn * (BN / 2) + 32 * j + 8 * q + 4 * h;
+        if constexpr (PAIRST) {
+          if (pairst) {  // both lanes of a pair take this branch together (same pixel, n < N alike)
+            const bool okn = n < a.N;
+            float v[4];
+#pragma unroll
+            for (int e = 0; e < 4; ++e) {
+              const float x = acc[0][i][j][4 * q + e] + bias4[j][q][e];
+              v[e] = (a.act ? ym_silu_x3(x) : x) + (float)res4[i][j][q][e];
+            }
+            size_t o = ep_obase[i] + n;
+            if (a.shuffle) {
+              const int sub = n / a.npr;
+              const int ch = n - sub * a.npr;
+              o = ep_obase[i] + (size_t)((sub >> 1) * a.d_W + (sub & 1)) * a.d_ctot + ch;
+            }
+            ym_p2_store4_pair<32>(dst + (okn ? o : 0), v, h, okn);
+            continue;
+          }
+        }
         if (n >= a.N) continue;
         float v[4];
 #pragma unroll

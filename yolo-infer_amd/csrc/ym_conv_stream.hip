@@ -234,6 +234,11 @@ __global__ __launch_bounds__(64 * NWV) void conv_stream(const ConvArgs a) {
   load(gb, cur, rcur);
   __syncthreads();
   OutT* dst = static_cast<OutT*>(a.dst);
+  // x3 pair-layout outputs: whole-chunk stores by lane pairs where every 8-channel chunk of the output slice is
+  // written by one lane pair (8-aligned slice and channel count; uniform)
+  constexpr bool PAIRST = X3 && std::is_same<OutT, P2>::value;
+  const bool pair1 = (a.pst & 2) && ((a.N | a.d_coff | a.d_ctot) & 7) == 0;
+  const bool pair2 = (a.pst & 2) && ((a.N2 | a.d_coff | a.d_ctot) & 7) == 0;
   for (; gb < gend; gb += step) {
     if (gb + step < gend) load(gb + step, nxt, rnxt);
     int ob[PX], rb[PX];  // output / residual pixel index of this lane's pixel in group p (ob -1: none)
@@ -304,6 +309,24 @@ __global__ __launch_bounds__(64 * NWV) void conv_stream(const ConvArgs a) {
               }
               acc = __builtin_amdgcn_mfma_f32_16x16x16f16(a2[nb], h[p][nb], acc, 0, 0, 0);
             }
+          if constexpr (PAIRST) {
+            if (pair2) {  // lane pair (g, g ^ 1) of one pixel writes whole 32-byte chunks
+              const bool okp = ob[p] >= 0 && n0 < a.N2;
+              float v[4];
+#pragma unroll
+              for (int r = 0; r < 4; ++r) {
+                const float xv = acc[r] + b4[r];
+                v[r] = a.act2 ? ym_silu_x3(xv) : xv;
+              }
+              if (res && okp) {
+                const RV rv = nb20 == 0 ? rcur[p][j] : SRes<X3>::load(res_at((size_t)rb[p] * a.r_ctot + a.r_coff + n0));
+#pragma unroll
+                for (int r = 0; r < 4; ++r) v[r] += (float)rv[r];
+              }
+              ym_p2_store4_pair<16>(dst + (size_t)(okp ? ob[p] : 0) * a.d_ctot + a.d_coff + n0, v, g & 1, okp);
+              continue;
+            }
+          }
           if (ob[p] < 0 || n0 >= a.N2) continue;
           float v[4];
 #pragma unroll
@@ -339,6 +362,24 @@ __global__ __launch_bounds__(64 * NWV) void conv_stream(const ConvArgs a) {
 #pragma unroll
         for (int ks = 0; ks < KS + KX; ++ks)
           acc = __builtin_amdgcn_mfma_f32_16x16x32_f16(af[ks], cur[p][ks], acc, 0, 0, 0);
+        if constexpr (PAIRST) {
+          if (pair1) {  // lane pair (g, g ^ 1) of one pixel writes whole 32-byte chunks
+            const bool okp = ob[p] >= 0 && n0 < a.N;
+            float v[4];
+#pragma unroll
+            for (int r = 0; r < 4; ++r) {
+              const float xv = acc[r] + b4[r];
+              v[r] = a.act ? ym_silu_x3(xv) : xv;
+            }
+            if (res && okp) {
+              const RV rv = nb0 == 0 ? rcur[p][j] : SRes<X3>::load(res_at((size_t)rb[p] * a.r_ctot + a.r_coff + n0));
+#pragma unroll
+              for (int r = 0; r < 4; ++r) v[r] += (float)rv[r];
+            }
+            ym_p2_store4_pair<16>(dst + (size_t)(okp ? ob[p] : 0) * a.d_ctot + a.d_coff + n0, v, g & 1, okp);
+            continue;
+          }
+        }
         if (ob[p] < 0 || n0 >= a.N) continue;
         float v[4];
 #pragma unroll

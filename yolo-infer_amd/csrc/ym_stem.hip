@@ -165,6 +165,15 @@ __global__ __launch_bounds__(256) void stem_mfma(const ConvArgs a) {
         acc = __builtin_amdgcn_mfma_f32_16x16x32_f16(wf[t], bfl, acc, 0, 0, 0);
       }
       acc = __builtin_amdgcn_mfma_f32_16x16x32_f16(wf[t], bf, acc, 0, 0, 0);
+      if constexpr (X3) {
+        if ((a.pst & 4) && ((a.d_coff | a.d_ctot) & 7) == 0) {  // lanes (kg, kg ^ 1) of a pixel write whole 32-byte chunks
+          float o[4];
+#pragma unroll
+          for (int r = 0; r < 4; ++r) o[r] = ym_silu_x3(acc[r] + bias[t][r]);
+          ym_p2_store4_pair<16>(ok ? dst + 16 * t : static_cast<T*>(a.dst), o, kg & 1, ok);
+          continue;
+        }
+      }
       if (!ok) continue;
       if constexpr (X3) {
         float o[4];
