@@ -29,3 +29,6 @@ cd "$R"
 echo "[j] sq $(date +%T)"
 bash tools/gpu_sq_table.sh r03j_s_b8_x3 --model s --dtype x3 || exit $?
 echo "[j] done $(date +%T)"
+echo "[j] suite $(date +%T)"
+bash tools/gpu_suite.sh || exit $?
+echo "[j] suite done $(date +%T)"

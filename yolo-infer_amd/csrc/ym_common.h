@@ -119,6 +119,24 @@ __device__ __forceinline__ void ym_p2_store4(P2* p, const float* v) {
   *reinterpret_cast<f16x4*>(q) = h;
   *reinterpret_cast<f16x4*>(q + 8) = l;
 }
+// v of lane ^ XOR (XOR 16 or 32): ds_bpermute (LDS crossbar), or with `vp` the VALU row swap v_permlane16_swap /
+// v_permlane32_swap with one register as both operands — the odd 16-lane rows (32: the upper half) find the partner's
+// value in the first result, the others in the second (tools/permlane_probe.hip)
+template <int XOR>
+__device__ __forceinline__ unsigned ym_lane_xor(unsigned v, bool vp) {
+  static_assert(XOR == 16 || XOR == 32, "row swaps: lane ^ 16 or lane ^ 32");
+  if (vp) {
+    const bool upper = (threadIdx.x & XOR) != 0;
+    if constexpr (XOR == 16) {
+      const auto r = __builtin_amdgcn_permlane16_swap(v, v, false, false);
+      return upper ? r[0] : r[1];
+    } else {
+      const auto r = __builtin_amdgcn_permlane32_swap(v, v, false, false);
+      return upper ? r[0] : r[1];
+    }
+  }
+  return (unsigned)__shfl_xor((int)v, XOR);
+}
 // The same 4 channels stored by a LANE PAIR: the lane holding channels c .. c+3 of a chunk (c % 8 == 0, `odd` false)
 // and its partner lane (lane ^ XOR, same pixel) holding c+4 .. c+7 swap halves, so the even lane writes the chunk's
 // hi x8 (16 B) and the odd lane its lo x8 (16 B) — the chunk is one 32-byte run, not four 8-byte pieces
@@ -126,7 +144,7 @@ __device__ __forceinline__ void ym_p2_store4(P2* p, const float* v) {
 // Same stored bits as ym_p2_store4.  Both lanes of a pair must execute it (the exchange is a cross-lane read);
 // `ok` predicates only the store, and p may be any address when !ok.
 template <int XOR>
-__device__ __forceinline__ void ym_p2_store4_pair(P2* p, const float* v, bool odd, bool ok) {
+__device__ __forceinline__ void ym_p2_store4_pair(P2* p, const float* v, bool odd, bool ok, bool vp = false) {
   f16x4 h, l;
 #pragma unroll
   for (int e = 0; e < 4; ++e) {
@@ -136,8 +154,8 @@ __device__ __forceinline__ void ym_p2_store4_pair(P2* p, const float* v, bool od
   typedef unsigned u32x2_t __attribute__((ext_vector_type(2)));
   const u32x2_t s = __builtin_bit_cast(u32x2_t, odd ? h : l);  // the half the partner stores
   u32x2_t r;
-  r[0] = (unsigned)__shfl_xor((int)s[0], XOR);
-  r[1] = (unsigned)__shfl_xor((int)s[1], XOR);
+  r[0] = ym_lane_xor<XOR>(s[0], vp);
+  r[1] = ym_lane_xor<XOR>(s[1], vp);
   const f16x4 q = __builtin_bit_cast(f16x4, r);
   const f16x8 o = odd ? f16x8{q[0], q[1], q[2], q[3], l[0], l[1], l[2], l[3]}
                       : f16x8{h[0], h[1], h[2], h[3], q[0], q[1], q[2], q[3]};
@@ -288,8 +306,11 @@ struct ConvArgs {
   // stay logical channels, s0_elems / s1_elems count fp16 elements
   int x3;
   // x3 pair-layout outputs: lane-pair whole-chunk epilogue stores (ym_p2_store4_pair) where the output slice allows
-  // them; a bit mask per kernel family (1 LDS-DMA, 2 streaming, 4 stem, 8 fused Bottleneck; YM_PAIRST for A/B,
-  // default 15); a clear bit keeps the per-lane ym_p2_store4.  Same stored bits either way.
+  // them; a bit mask per kernel family (1 LDS-DMA, 2 streaming, 4 stem, 8 fused Bottleneck; 16: the lane exchange
+  // by v_permlane*_swap instead of ds_bpermute; YM_PAIRST for A/B); a clear family bit keeps the per-lane
+  // ym_p2_store4.  Same stored bits either way.  Default 21 = LDS-DMA + stem with permlane: the families whose ops
+  // got faster in two same-box A/Bs (model.1+cv1 83 -> 79 us, stem 40 -> 38, the 80x80 head 1x1s -1.2 us each);
+  // the streaming kernel lost (model.2.cv2 55 -> 61 us) and the Bottleneck kernel ~1 us (profiles/r03i_pairst_ab.txt).
   int pst;
 };
 

@@ -340,7 +340,7 @@ __global__ __launch_bounds__(64 * NW) void conv_bneck(const ConvArgs a, const Bn
               o[r] = (a.act2 ? ym_silu_x3(v) : v) + rv[r];
             }
             // lanes (kg, kg ^ 1) of this pixel write whole 32-byte chunks where the output slice keeps them whole
-            if ((a.pst & 8) && ((a.d_coff | a.d_ctot) & 7) == 0) ym_p2_store4_pair<16>(dstp + obase + n0, o, kg & 1, !(g.dbg & 8));
+            if ((a.pst & 8) && ((a.d_coff | a.d_ctot) & 7) == 0) ym_p2_store4_pair<16>(dstp + obase + n0, o, kg & 1, !(g.dbg & 8), a.pst & 16);
             else if (!(g.dbg & 8)) ym_p2_store4(dstp + obase + n0, o);
           } else {
             f16x4 o;

@@ -523,7 +523,7 @@ __global__ __launch_bounds__(256 * KG) void conv_dma(const ConvArgs a) {
               const int ch = n - sub * a.npr;
               o = ep_obase[i] + (size_t)((sub >> 1) * a.d_W + (sub & 1)) * a.d_ctot + ch;
             }
-            ym_p2_store4_pair<32>(dst + (okn ? o : 0), v, h, okn);
+            ym_p2_store4_pair<32>(dst + (okn ? o : 0), v, h, okn, a.pst & 16);
             continue;
           }
         }

@@ -323,7 +323,7 @@ __global__ __launch_bounds__(64 * NWV) void conv_stream(const ConvArgs a) {
 #pragma unroll
                 for (int r = 0; r < 4; ++r) v[r] += (float)rv[r];
               }
-              ym_p2_store4_pair<16>(dst + (size_t)(okp ? ob[p] : 0) * a.d_ctot + a.d_coff + n0, v, g & 1, okp);
+              ym_p2_store4_pair<16>(dst + (size_t)(okp ? ob[p] : 0) * a.d_ctot + a.d_coff + n0, v, g & 1, okp, a.pst & 16);
               continue;
             }
           }
@@ -376,7 +376,7 @@ __global__ __launch_bounds__(64 * NWV) void conv_stream(const ConvArgs a) {
 #pragma unroll
               for (int r = 0; r < 4; ++r) v[r] += (float)rv[r];
             }
-            ym_p2_store4_pair<16>(dst + (size_t)(okp ? ob[p] : 0) * a.d_ctot + a.d_coff + n0, v, g & 1, okp);
+            ym_p2_store4_pair<16>(dst + (size_t)(okp ? ob[p] : 0) * a.d_ctot + a.d_coff + n0, v, g & 1, okp, a.pst & 16);
             continue;
           }
         }

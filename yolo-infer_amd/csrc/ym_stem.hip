@@ -170,7 +170,7 @@ __global__ __launch_bounds__(256) void stem_mfma(const ConvArgs a) {
           float o[4];
 #pragma unroll
           for (int r = 0; r < 4; ++r) o[r] = ym_silu_x3(acc[r] + bias[t][r]);
-          ym_p2_store4_pair<16>(ok ? dst + 16 * t : static_cast<T*>(a.dst), o, kg & 1, ok);
+          ym_p2_store4_pair<16>(ok ? dst + 16 * t : static_cast<T*>(a.dst), o, kg & 1, ok, a.pst & 16);
           continue;
         }
       }
