@@ -288,8 +288,8 @@ int ensure_workspace(ym_ctx* c, int B, int H, int W) {
 int conv_args(ym_ctx* c, const Op& op, int B, const float* d_in, float in_eps, ConvArgs& a, int& out_f32) {
       const int32_t* r = op.r;
       a = ConvArgs{};
-      static const int pst = [] { const char* e = getenv("YM_PAIRST"); return e ? atoi(e) : 21; }();
-      a.pst = pst;
+      const char* pst = getenv("YM_PAIRST");  // read at every capture: an A/B or test may switch it in one process
+      a.pst = pst ? atoi(pst) : 21;
       const int k = r[1], s = r[2], cin = r[3], cout = r[4];
       const int b0 = r[6], b1 = r[10], bd = r[13], br = r[17];
       const int up0 = r[9];
