@@ -6,8 +6,8 @@
 
 Default workload = BASELINE.json config 3, the one the 1/2/4/8-GPU metric is quoted on: yolo11s detect, 640x640,
 batch 8 per GPU, on the x3 plan — fp16 MFMAs on split operands with fp32-equivalent storage, the plan whose detections
-meet SURVEY §7-1(b)'s fp16-mode tolerance (0.64 px, 1e-3 score; the plain f16 plan misses the score bar 3-4x,
-DESIGN.md §3), reported with its parity against the CPU oracle on the timed batch (`parity`) and beside the f16
+meet the north-star bar (1e-3 px absolute on coordinates, 1e-3 on scores, class exact; the plain f16 plan is ~0.6 px
+and 3e-3 off), reported with its parity against the CPU oracle on the timed batch (`parity`) and beside the f16
 throughput plan measured in the same run (`f16_throughput_plan`).  (`--model n` gives config 2, `--dtype i8`
 config 4, `--model s --task segment --batch 4` config 5.)
 
@@ -274,9 +274,10 @@ def cpu_baseline(scale, task, x_gpu_dets, xs, seconds, qparams=None):
     return base, acc, gts
 
 
-def parity(gpu_dets, gts, conf=0.25, iou=0.7):
-    """SURVEY §8(c) matching of the timed batch's GPU detections against the oracle's (tests/matching.py) at SURVEY
-    §7-1(b)'s fp16-mode tolerance: 0.64 px, 1e-3 score, class exact, every detection matched or exempt."""
+def parity(gpu_dets, gts, conf=0.25, iou=0.7, tol_xy=1e-3, tol_s=1e-3):
+    """SURVEY §8(c) matching of the timed batch's GPU detections against the oracle's (tests/matching.py) at the
+    north-star bar (BASELINE.json): 1e-3 px absolute on coordinates, 1e-3 on scores, class exact, every detection
+    matched or exempt."""
     from tests.matching import MatchReport, match_image
     rep = MatchReport()
     dxy, ds = [], []
@@ -286,12 +287,13 @@ def parity(gpu_dets, gts, conf=0.25, iou=0.7):
         for i, j in rep.pairs[before:]:
             dxy.append(float(np.abs(r[i, :4] - g[j, :4]).max()))
             ds.append(float(abs(r[i, 4] - g[j, 4])))
-    ok = rep.ok and (not dxy or (max(dxy) <= 0.64 and max(ds) <= 1e-3))
-    return {"tolerance": "|dxy| <= 0.64 px, |dscore| <= 1e-3, class exact, all matched or exempt (SURVEY 7-1b, 8c)",
+    ok = rep.ok and (not dxy or (max(dxy) <= tol_xy and max(ds) <= tol_s))
+    return {"tolerance": f"|dxy| <= {tol_xy:g} px, |dscore| <= {tol_s:g}, class exact, all matched or exempt "
+                         "(BASELINE north star, SURVEY 8c)",
             "meets_tolerance": bool(ok), "matched": rep.matched, "exempt": rep.exempt,
             "unmatched_oracle": rep.unmatched_ref, "unmatched_gpu": rep.unmatched_build,
             "max_dxy_px": round(max(dxy), 6) if dxy else None, "max_dscore": round(max(ds), 7) if ds else None,
-            "within_tolerance_frac": round(float(np.mean([(a <= 0.64 and b <= 1e-3) for a, b in zip(dxy, ds)])), 4)
+            "within_tolerance_frac": round(float(np.mean([(a <= tol_xy and b <= tol_s) for a, b in zip(dxy, ds)])), 4)
             if dxy else None}
 
 
@@ -356,7 +358,7 @@ def main():
     ap.add_argument("--batch", type=int, default=8, help="images per GPU per step")
     ap.add_argument("--size", type=int, default=640)
     ap.add_argument("--dtype", default="x3", choices=["f16", "f32", "i8", "f8", "x3"],
-                    help="plan: x3 (default: split-f16 MFMA, meets the f16-mode tolerance), f16, f32, i8, f8")
+                    help="plan: x3 (default: split-f16 MFMA, meets the 1e-3 bar), f16, f32, i8, f8")
     ap.add_argument("--no-f16", action="store_true", help="x3 runs: skip the f16 throughput-plan comparison")
     ap.add_argument("--backend", default="qnnpack", choices=["qnnpack", "fbgemm"], help="i8: PTQ qconfig")
     ap.add_argument("--calib-batches", type=int, default=4, help="i8: calibration batches (B images each)")
@@ -486,7 +488,7 @@ def main():
             "device_images_per_s": round(B * a.steps / (time.perf_counter() - td), 2),
             "conv_tiles": e16.tune_source.get((e16.lane_batch(B), a.size, a.size), "heuristic"),
             "x3_to_f16_ratio": round(value / (B * a.steps / el16), 4),
-            "note": "fp16 storage + fp32 accumulation; misses the 1e-3 score tolerance (see parity)"}
+            "note": "fp16 storage + fp32 accumulation; misses the 1e-3 bar (see parity)"}
         del m16, e16
     if rank == 0 and world == 1 and not a.no_cpu:
         gdets = [r.boxes.data.cpu().numpy() for r in res]

@@ -1,10 +1,12 @@
 """GPU parity of the x3 plan (fp32 activations, every conv GEMM as three split-f16 MFMAs: csrc/ym_conv.hip mma<x3_t>).
 
-This is the plan that meets SURVEY §7-1(b)'s fp16-mode tolerance, which the plain f16 plan misses by 3-4x on scores
-(tools/f16_emulate.py shows the f16 error is spread over every layer, so no subset of promoted ops
-closes it).  Tolerance written here (the reference's own CPU path is fp32: /root/reference/core/model.py:133):
+The benched plan, held to the north-star bar (BASELINE.json: "within 1e-3 on coords/scores and exact on class
+indices" against the reference's fp32 CPU path, /root/reference/core/model.py:133), which the plain f16 plan misses
+by ~600x on coordinates.  Tolerance written here:
   * every oracle detection matched or exempt (tests/matching.py) — no min_frac —
-    with |Δxy| <= 0.64 px (1e-3 · 640), |Δscore| <= 1e-3, class exact;
+    with |Δxy| <= 1e-3 px ABSOLUTE, |Δscore| <= 5e-5, class exact.  The fp32 oracle itself sits up to 8.2e-4 px from
+    a float64 forward on these weights (tools/x3_emulate.py), so 1e-3 px is within ~20 % of fp32's own noise: a
+    dropped split term (~2^-11 relative: 0.3-0.6 px) or unscaled weights (1.3e-3 px) fail it;
   * per-layer outputs within 1e-4 relative of the oracle.
 """
 import json
@@ -22,7 +24,7 @@ from yolomi.synth import synth_weights
 pytestmark = pytest.mark.gpu
 GOLD = os.path.join(os.path.dirname(os.path.abspath(__file__)), "golden")
 DEV = torch.device("cuda", 0)
-TOL_XY, TOL_S = 0.64, 1e-3
+TOL_XY, TOL_S = 1e-3, 5e-5  # the north-star bar (px absolute, score)
 _cache = {}
 
 
@@ -47,6 +49,7 @@ def check(ref_dets, got_results, conf=0.25, iou=0.7, max_det=300):
     for r, g in zip(ref_dets, got_results):
         ref = r["boxes"].numpy() if isinstance(r, dict) else np.asarray(r, np.float32).reshape(-1, 6)
         match_image(ref, g.boxes.data.cpu().numpy(), conf, iou, TOL_XY, TOL_S, rep=rep, max_det=max_det)
+    print(f"x3 parity: {rep}")
     assert rep.ok, f"{rep}; {rep.failures[:3]}"
     assert rep.matched > 0
     return rep

@@ -12,7 +12,7 @@ import torch
 from tests.matching import MatchReport, match_image
 from yolomi.arch import GraphBuilder, param_specs
 from yolomi.metrics import evaluate
-from yolomi.plan import MAGIC, fuse_conv_bn, fuse_default, pack_graph, pack_model
+from yolomi.plan import MAGIC, fuse_conv_bn, fuse_default, pack_graph, pack_model, x3_weight_exp
 from yolomi.synth import splitmix64, synth_weights, uniform
 
 ROOT = os.path.dirname(os.path.dirname(os.path.abspath(__file__)))
@@ -120,9 +120,12 @@ def test_x3_blob_packs_pair_chunk_weights():
         hl = np.frombuffer(bx3, np.float16, N * rx[21], base + rx[19]).reshape(N, rx[21])
         assert not hl[:, 2 * K:].any()
         pairs = hl[:, :2 * K].reshape(N, K // 8, 2, 8).astype(np.float64)
-        rebuilt = (pairs[:, :, 0] + pairs[:, :, 1]).reshape(N, K)
-        worst = max(worst, float(np.abs(rebuilt - w).max() / np.abs(w).max()))
+        # stored scaled by 2^s, max |w·2^s| in (2^13, 2^14] (so every lo part of a weight above 2^-17 max is normal)
+        assert rx[22] == x3_weight_exp(w) and 2 ** 13 < np.abs(w).max() * 2.0 ** rx[22] <= 2 ** 14
+        rebuilt = (pairs[:, :, 0] + pairs[:, :, 1]).reshape(N, K) * 2.0 ** -rx[22]
+        worst = max(worst, float((np.abs(rebuilt - w) / np.maximum(np.abs(w), 2 ** -17 * np.abs(w).max())).max()))
         nconv += 1
+    # every weight to ~2^-22 of ITSELF (unscaled, the subnormal lo parts left ~1e-6 of a typical weight)
     assert nconv > 70 and worst < 2 ** -21
 
 
@@ -153,9 +156,11 @@ def test_x3_fused_pairs_pack_w2(scale):
         assert r[27] == N2 and r[29] % 64 == 0 and 2 * K2 <= r[29] < 2 * K2 + 64 and (r[29] // 32) % 2 == 0
         hl = np.frombuffer(blob, np.float16, N2 * r[29], base + r[25]).reshape(N2, r[29])
         pr = hl[:, :2 * K2].reshape(N2, K2 // 8, 2, 8).astype(np.float64)
-        rebuilt = (pr[:, :, 0] + pr[:, :, 1]).reshape(N2, K2)
         ref = w2.reshape(N2, K2)
-        assert np.abs(rebuilt - ref).max() / np.abs(ref).max() < 2 ** -21, op.name
+        assert r[23] == x3_weight_exp(ref), op.name
+        rebuilt = (pr[:, :, 0] + pr[:, :, 1]).reshape(N2, K2) * 2.0 ** -r[23]
+        rel = np.abs(rebuilt - ref) / np.maximum(np.abs(ref), 2 ** -17 * np.abs(ref).max())
+        assert rel.max() < 2 ** -21, op.name
 
 def test_facade_contract_without_gpu():
     from core.model import YOLO11Model

@@ -102,11 +102,13 @@ class YOLO11Model:
     HIP_TASKS = ("detect", "segment")
 
     def __init__(self, model_path: Optional[Union[str, Path]] = None, task: str = "detect", size: str = "n",
-                 device: Optional[str] = None, verbose: bool = True, dtype: str = "f16", seed: int = 0,
+                 device: Optional[str] = None, verbose: bool = True, dtype: str = "x3", seed: int = 0,
                  weights_blob: Optional[bytes] = None, qparams: Optional[Dict] = None,
                  state_dict: Optional[Dict[str, np.ndarray]] = None, weights_from: Optional[tuple] = None):
-        """Extra keyword arguments over the reference: `dtype` ('f16' storage + fp32 accumulate, 'f32' = exact
-        parity mode, or 'i8' = the PTQ int8 plan, which needs calibrated `qparams`; see
+        """Extra keyword arguments over the reference: `dtype` — 'x3' (the default: fp32 activations, every conv GEMM
+        as three fp16 MFMAs on hi/lo split operands; meets the reference fp32 path's 1e-3 px / score bar, DESIGN.md
+        §3), 'f16' (opt-in throughput mode: fp16 storage + fp32 accumulate, ~0.6 px / 3e-3 off the fp32 path),
+        'f32' (exact-f32 MFMA), or 'i8' / 'f8' = the PTQ plans, which need calibrated `qparams`; see
         optimization.quantization.PostTrainingQuantizer), `seed` of the synthetic weights used when no `model_path`
         is given, `weights_blob` = an already packed model (e.g. received over an RCCL broadcast from rank 0), and
         `state_dict` = weights already in memory, `weights_from` = (rccl comm, root): receive the root rank's model

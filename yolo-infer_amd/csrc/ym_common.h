@@ -312,7 +312,16 @@ struct ConvArgs {
   // got faster in two same-box A/Bs (model.1+cv1 83 -> 79 us, stem 40 -> 38, the 80x80 head 1x1s -1.2 us each);
   // the streaming kernel lost (model.2.cv2 55 -> 61 us) and the Bottleneck kernel ~1 us (profiles/r03i_pairst_ab.txt).
   int pst;
+  // x3 plans: every conv weight matrix (W, and W2 of a fused pair) is packed scaled by a power of two 2^s, its max |w|
+  // then in (2^13, 2^14] (yolomi/plan.py), so that the fp16 lo parts of the split stay normal: unscaled, a weight of
+  // 0.03 kept only ~1e-6 relative precision in a subnormal lo (tools/x3_emulate.py: the x3 plan's max |Δxy| 1.3e-3 ->
+  // 7.6e-4 px, the fp32 oracle's own distance from float64 being 8.2e-4).  wsc / wsc2 = 2^-s undo it exactly in the
+  // epilogue: fmaf(acc, wsc, bias) rounds once, as acc + bias did (ym_x3_pre).  1 for every other plan.
+  float wsc, wsc2;
 };
+
+// x3 epilogue pre-activation: the weight scale (exact: a power of two) and the bias in one rounding
+__device__ __forceinline__ float ym_x3_pre(float acc, float wsc, float bias) { return fmaf(acc, wsc, bias); }
 
 struct DwArgs {
   const void* src; int s_ctot, s_coff, s_P;

@@ -366,7 +366,8 @@ __global__ __launch_bounds__(WM * WN * WK * 64) void conv_igemm(const ConvArgs a
         float v[4];
 #pragma unroll
         for (int e = 0; e < 4; ++e) {
-          const float x = acc[i][j][4 * q + e] + bias[j][q][e];
+          const float x = std::is_same<M, x3_t>::value ? ym_x3_pre(acc[i][j][4 * q + e], a.wsc, bias[j][q][e])
+                                                       : acc[i][j][4 * q + e] + bias[j][q][e];
           // f16 plans: the fp16-rounded output does not see the fast SiLU's ~1 ulp (fp32) error
           v[e] = (a.act ? (sizeof(OutT) == 2 ? ym_silu_fast(x)
                                              : (std::is_same<M, x3_t>::value ? ym_silu_x3(x) : ym_silu(x)))
@@ -590,7 +591,7 @@ __global__ __launch_bounds__(256) void conv_lds(const ConvArgs a) {
         float v[4];
 #pragma unroll
         for (int e = 0; e < 4; ++e) {
-          const float x = acc[i][j][4 * q + e] + b4[e];
+          const float x = X3 ? ym_x3_pre(acc[i][j][4 * q + e], a.wsc, b4[e]) : acc[i][j][4 * q + e] + b4[e];
           v[e] = a.act ? (X3 ? ym_silu_x3(x) : ym_silu_fast(x)) : x;  // fast SiLU where the output is rounded to fp16
         }
         if (a.shuffle) {

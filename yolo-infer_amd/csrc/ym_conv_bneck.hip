@@ -227,7 +227,7 @@ __global__ __launch_bounds__(64 * NW) void conv_bneck(const ConvArgs a, const Bn
           f16x4 h, hl;
 #pragma unroll
           for (int r = 0; r < 4; ++r) {
-            const float v = acc[nb][q][r] + sB1[n0 + r];
+            const float v = X3 ? ym_x3_pre(acc[nb][q][r], a.wsc, sB1[n0 + r]) : acc[nb][q][r] + sB1[n0 + r];
             if constexpr (X3) {
               const float vv = a.act ? ym_silu_x3(v) : v;
               h[r] = (f16)vv;
@@ -336,7 +336,7 @@ __global__ __launch_bounds__(64 * NW) void conv_bneck(const ConvArgs a, const Bn
             float o[4];
 #pragma unroll
             for (int r = 0; r < 4; ++r) {
-              const float v = acc[nb][q][r] + sB2[n0 + r];
+              const float v = ym_x3_pre(acc[nb][q][r], a.wsc2, sB2[n0 + r]);
               o[r] = (a.act2 ? ym_silu_x3(v) : v) + rv[r];
             }
             // lanes (kg, kg ^ 1) of this pixel write whole 32-byte chunks where the output slice keeps them whole

@@ -514,7 +514,7 @@ __global__ __launch_bounds__(256 * KG) void conv_dma(const ConvArgs a) {
             float v[4];
 #pragma unroll
             for (int e = 0; e < 4; ++e) {
-              const float x = acc[0][i][j][4 * q + e] + bias4[j][q][e];
+              const float x = ym_x3_pre(acc[0][i][j][4 * q + e], a.wsc, bias4[j][q][e]);
               v[e] = (a.act ? ym_silu_x3(x) : x) + (float)res4[i][j][q][e];
             }
             size_t o = ep_obase[i] + n;
@@ -531,7 +531,8 @@ __global__ __launch_bounds__(256 * KG) void conv_dma(const ConvArgs a) {
         float v[4];
 #pragma unroll
         for (int e = 0; e < 4; ++e) {
-          const float x = acc[0][i][j][4 * q + e] + bias4[j][q][e];
+          const float x = X3 ? ym_x3_pre(acc[0][i][j][4 * q + e], a.wsc, bias4[j][q][e])
+                             : acc[0][i][j][4 * q + e] + bias4[j][q][e];
           v[e] = (a.act ? (X3 ? ym_silu_x3(x) : ym_silu_fast(x)) : x) + (float)res4[i][j][q][e];
         }
         if (a.shuffle) {

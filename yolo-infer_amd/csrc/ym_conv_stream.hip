@@ -271,7 +271,7 @@ __global__ __launch_bounds__(64 * NWV) void conv_stream(const ConvArgs a) {
             acc = __builtin_amdgcn_mfma_f32_16x16x32_f16(af[ks], cur[p][ks], acc, 0, 0, 0);
 #pragma unroll
           for (int r = 0; r < 4; ++r) {
-            const float xv = acc[r] + b4[r];
+            const float xv = X3 ? ym_x3_pre(acc[r], a.wsc, b4[r]) : acc[r] + b4[r];
             if constexpr (X3) {
               const float v = a.act ? ym_silu_x3(xv) : xv;
               const f16 hi = (f16)v;
@@ -315,7 +315,7 @@ __global__ __launch_bounds__(64 * NWV) void conv_stream(const ConvArgs a) {
               float v[4];
 #pragma unroll
               for (int r = 0; r < 4; ++r) {
-                const float xv = acc[r] + b4[r];
+                const float xv = ym_x3_pre(acc[r], a.wsc2, b4[r]);
                 v[r] = a.act2 ? ym_silu_x3(xv) : xv;
               }
               if (res && okp) {
@@ -331,7 +331,7 @@ __global__ __launch_bounds__(64 * NWV) void conv_stream(const ConvArgs a) {
           float v[4];
 #pragma unroll
           for (int r = 0; r < 4; ++r) {
-            const float xv = acc[r] + b4[r];
+            const float xv = X3 ? ym_x3_pre(acc[r], a.wsc2, b4[r]) : acc[r] + b4[r];
             v[r] = a.act2 ? (X3 ? ym_silu_x3(xv) : ym_silu_fast(xv)) : xv;
           }
           if (res) {
@@ -368,7 +368,7 @@ __global__ __launch_bounds__(64 * NWV) void conv_stream(const ConvArgs a) {
             float v[4];
 #pragma unroll
             for (int r = 0; r < 4; ++r) {
-              const float xv = acc[r] + b4[r];
+              const float xv = ym_x3_pre(acc[r], a.wsc, b4[r]);
               v[r] = a.act ? ym_silu_x3(xv) : xv;
             }
             if (res && okp) {
@@ -384,7 +384,7 @@ __global__ __launch_bounds__(64 * NWV) void conv_stream(const ConvArgs a) {
         float v[4];
 #pragma unroll
         for (int r = 0; r < 4; ++r) {
-          const float xv = acc[r] + b4[r];
+          const float xv = X3 ? ym_x3_pre(acc[r], a.wsc, b4[r]) : acc[r] + b4[r];
           v[r] = a.act ? (X3 ? ym_silu_x3(xv) : ym_silu_fast(xv)) : xv;
         }
         if (res) {

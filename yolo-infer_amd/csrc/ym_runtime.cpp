@@ -8,6 +8,7 @@
 #include <dlfcn.h>
 
 #include <algorithm>
+#include <cmath>
 #include <cstdarg>
 #include <cstdio>
 #include <cstring>
@@ -288,6 +289,7 @@ int ensure_workspace(ym_ctx* c, int B, int H, int W) {
 int conv_args(ym_ctx* c, const Op& op, int B, const float* d_in, float in_eps, ConvArgs& a, int& out_f32) {
       const int32_t* r = op.r;
       a = ConvArgs{};
+      a.wsc = a.wsc2 = 1.0f;
       const char* pst = getenv("YM_PAIRST");  // read at every capture: an A/B or test may switch it in one process
       a.pst = pst ? atoi(pst) : 21;
       const int k = r[1], s = r[2], cin = r[3], cout = r[4];
@@ -326,6 +328,11 @@ int conv_args(ym_ctx* c, const Op& op, int B, const float* d_in, float in_eps, C
       if (c->dtype == YM_DT_X3 && b0 != c->input_buf) {  // pair layout: fp16 storage chunks per tap double
         a.x3 = 1;
         a.Cin8 = 2 * (cin / 8);
+        // the packed weights are W·2^s (and W2·2^s2): yolomi/plan.py, record slots 22 / 23 (int8 plans only otherwise)
+        if (r[22] < -64 || r[22] > 64 || r[23] < -64 || r[23] > 64)
+          return fail(YM_EBLOB, "op %s: bad x3 weight scale exponents %d / %d", op.name, r[22], r[23]);
+        a.wsc = ldexpf(1.0f, -r[22]);
+        a.wsc2 = ldexpf(1.0f, -r[23]);
       }
       a.Kc = k * k * a.Cin8;
       a.Kpad = r[21];
@@ -394,7 +401,7 @@ void split_args(ym_ctx* c, const Op& op, const ConvArgs& a, ConvArgs& A, ConvArg
   Bc.Hin = a.Ho; Bc.Win = a.Wo; Bc.k = a.k2; Bc.s = 1; Bc.pad = a.k2 / 2;
   const int xs = a.x3 ? 2 : 1;  // x3: fp16 storage chunks of the pair layout
   Bc.Cin8 = xs * a.N / 8; Bc.Kc = a.k2 * a.k2 * Bc.Cin8; Bc.Kpad = a.Kpad2; Bc.N = a.N2; Bc.npr = a.N2;
-  Bc.w = a.w2; Bc.bias = a.bias2; Bc.act = a.act2;
+  Bc.w = a.w2; Bc.bias = a.bias2; Bc.act = a.act2; Bc.wsc = a.wsc2;
   Bc.s0_elems = (long)xs * c->cB * c->buf_P(mid) * c->bufs[mid].C;
 }
 

@@ -12,9 +12,11 @@ backend, K padded to 16-channel granules per tap, and per op a `QRec` (csrc/ym_c
 output, the 256-entry post-activation table, the stored tensor's / residual's / input's quantisation), the fp32
 s_in·s_w per output channel and the int32 zero-point correction Σ_k (128 - z_in)·w (activations are stored as q - 128).
 
-x3 plans (dtype "x3", the f16-tolerance plan): activations in the pair layout of csrc/ym_common.h (every 8-channel
+x3 plans (dtype "x3", the parity plan benched): activations in the pair layout of csrc/ym_common.h (every 8-channel
 chunk as fp16 hi = fp16(x) then lo = fp16(x - hi)); every conv weight row except the stem's likewise, [hi x8 | lo x8]
-per K chunk, so r[21] (Kpad) counts fp16 storage elements: 2·K padded to 64.  The stem keeps fp32 rows.
+per K chunk, of the weights scaled by a power of two 2^s (max |w·2^s| in (2^13, 2^14], so the lo parts stay normal;
+s in record slot 22, W2's in slot 23), so r[21] (Kpad) counts fp16 storage elements: 2·K padded to 64.  The stem
+keeps fp32 rows.
 
 Blob layout (int32 little-endian; parsed by `csrc/ym_runtime.cpp:ym_load_weights`):
   header[32] | buffers[nbuf][8] | ops[nop][32] | names[nop][48 bytes] | pad to 256 | weights
@@ -93,6 +95,31 @@ def _dw_weights(key: str, sd):
                         sd[key + ".bn.running_mean"], sd[key + ".bn.running_var"])
     C = w.shape[0]
     return np.ascontiguousarray(w.reshape(C, 9).T).astype(np.float32), b  # [9][C]
+
+
+X3_WMAX_LOG2 = 14  # x3 weight scaling: max |w|·2^s in (2^13, 2^14] (fp16 max 65504; csrc/ym_common.h ConvArgs::wsc)
+
+
+def x3_weight_exp(w: np.ndarray) -> int:
+    """Power-of-two exponent s of an x3 weight matrix: stored as w·2^s so that the fp16 lo part of the split
+    (lo = fp16(w·2^s - hi)) stays normal for every weight above 2^-17 of the matrix's max — unscaled, the typical
+    folded weight (~0.03) sits where lo is subnormal and keeps ~1e-6 relative precision (tools/x3_emulate.py).
+    The kernels multiply the accumulator by 2^-s in the epilogue (exact)."""
+    m = float(np.abs(w).max()) if w.size else 0.0
+    if not np.isfinite(m):
+        raise ValueError("non-finite conv weight")
+    if m == 0.0:
+        return 0
+    return int(X3_WMAX_LOG2 - np.ceil(np.log2(m)))
+
+
+def x3_pair_rows(w: np.ndarray, s: int) -> np.ndarray:
+    """(N, K) fp32 weights → [N][2K] fp16 pair-chunk rows of w·2^s: every 8-element K chunk as [hi x8 | lo x8]."""
+    N, K = w.shape
+    wr = (w.astype(np.float32).reshape(N, K // 8, 8) * np.float32(2.0 ** s)).astype(np.float32)
+    hi = wr.astype(np.float16)
+    lo = (wr - hi.astype(np.float32)).astype(np.float16)
+    return np.stack([hi, lo], axis=2).reshape(N, 2 * K)
 
 
 def _qrec(inv_sc, zc, qlo, qhi, mode, post, inv_so=1.0, zo=0, s_r=0.0, z_r=0, s_in=0.0, z_in=0, inv_s_in=0.0) -> bytes:
@@ -191,14 +218,13 @@ def pack_graph(g: GraphBuilder, sd: Dict[str, np.ndarray], dtype: str = "f16", q
             Kpad = (K + BK - 1) // BK * BK
             wp = np.zeros((N, Kpad), np.int8 if quant else np.float32)
             wp[:, :K] = w.reshape(N, K)
-            if dtype == "x3" and not stem:  # pair-chunk rows: every 8-channel K chunk as [fp16 hi x8 | fp16 lo x8]
-                wr = w.reshape(N, K // 8, 8).astype(np.float32)
-                hi = wr.astype(np.float16)
-                lo = (wr - hi.astype(np.float32)).astype(np.float16)
+            if dtype == "x3" and not stem:  # pair-chunk rows of W·2^s: every 8-channel K chunk as [hi x8 | lo x8]
+                ws = x3_weight_exp(w)
                 K2 = 2 * K
                 Kpad = (K2 + BK - 1) // BK * BK  # the 64-deep storage step (32 logical K)
                 wp = np.zeros((N, Kpad), np.float16)
-                wp[:, :K2] = np.stack([hi, lo], axis=2).reshape(N, K2)
+                wp[:, :K2] = x3_pair_rows(w.reshape(N, K), ws)
+                r[22] = ws
             src1 = a["src1"]
             C1 = src1.C if src1 is not None else 0
             dst, res = a["dst"], a["res"]
@@ -218,13 +244,12 @@ def pack_graph(g: GraphBuilder, sd: Dict[str, np.ndarray], dtype: str = "f16", q
                 N2, k2 = w2.shape[0], pair["k"]
                 assert w2.shape[1:] == (k2, k2, N)
                 K2 = k2 * k2 * N
-                if dtype == "x3":  # pair-chunk rows like W (storage K 2·K2, padded to 64)
-                    wr2 = w2.reshape(N2, K2 // 8, 8).astype(np.float32)
-                    hi2 = wr2.astype(np.float16)
-                    lo2 = (wr2 - hi2.astype(np.float32)).astype(np.float16)
+                if dtype == "x3":  # pair-chunk rows of W2·2^s2 like W (storage K 2·K2, padded to 64)
+                    ws2 = x3_weight_exp(w2)
                     Kpad2 = (2 * K2 + BK - 1) // BK * BK
                     w2h = np.zeros((N2, Kpad2), np.float16)
-                    w2h[:, :2 * K2] = np.stack([hi2, lo2], axis=2).reshape(N2, 2 * K2)
+                    w2h[:, :2 * K2] = x3_pair_rows(w2.reshape(N2, K2), ws2)
+                    r[23] = ws2
                 else:
                     Kpad2 = (K2 + BK - 1) // BK * BK
                     w2p = np.zeros((N2, Kpad2), np.float32)
