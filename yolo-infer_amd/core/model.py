@@ -112,7 +112,7 @@ class YOLO11Model:
         optimization.quantization.PostTrainingQuantizer), `seed` of the synthetic weights used when no `model_path`
         is given, `weights_blob` = an already packed model (e.g. received over an RCCL broadcast from rank 0), and
         `state_dict` = weights already in memory, `weights_from` = (rccl comm, root): receive the root rank's model
-        over RCCL (yolomi.dist.rccl_broadcast_model)."""
+        over RCCL, or a yolomi Runtime that already received it (yolomi.dist.rccl_broadcast_model)."""
         self.task = task
         self.size = size
         self.device = device or self._get_default_device()

@@ -1352,6 +1352,61 @@ int ym_rccl_comm_destroy(void* comm) {
   return YM_OK;
 }
 
+// ---- the init-time weight broadcast: one rank's side, shared by the two transports
+// (ym_broadcast_weights: RCCL, one rank per process; ym_broadcast_weights_local: every rank's context in this process,
+// the fake backend of SURVEY §4.4) — staging buffer, the root's upload, a receiver's copy-out and load, and the
+// verdict every rank agrees on.  The transports only move the chunk between staging buffers and sum control words.
+struct BcastRank {
+  ym_ctx* c = nullptr;
+  int rank = -1;
+  bool hip_ok = true, copy_ok = true;
+  char* d = nullptr;  // kBcastChunk staging bytes on the context's device
+  std::vector<char> h;  // a receiver's copy of the blob
+  int rc = YM_OK;
+  BcastRank() = default;
+  BcastRank(const BcastRank&) = delete;
+  BcastRank& operator=(const BcastRank&) = delete;
+  ~BcastRank() {
+    if (d) (void)hipFree(d);
+  }
+  // step (1): this rank's contribution to {the root's blob size (0: the root has no weights), staging failures}
+  void open(int root, unsigned long long h1[2]) {
+    hip_ok = hipSetDevice(c->device) == hipSuccess;
+    const bool alloc_ok = hip_ok && hipMalloc(&d, kBcastChunk) == hipSuccess;
+    if (!alloc_ok) d = nullptr;
+    h1[0] += (rank == root && c->loaded) ? (unsigned long long)c->blob_host.size() : 0ull;
+    h1[1] += alloc_ok ? 0ull : 1ull;
+    copy_ok = hip_ok;
+  }
+  // step (2), per chunk: the root uploads it into its staging buffer before the transport moves it ...
+  void put(int root, unsigned long long off, size_t len, hipStream_t st) {
+    if (rank == root)
+      copy_ok = copy_ok && hipMemcpyAsync(d, c->blob_host.data() + off, len, hipMemcpyHostToDevice, st) == hipSuccess;
+  }
+  // ... and a receiver copies it out after (the staging buffer is reused by the next chunk)
+  void get(int root, unsigned long long off, size_t len, hipStream_t st) {
+    if (rank != root)
+      copy_ok = copy_ok && hipMemcpyAsync(h.data() + off, d, len, hipMemcpyDeviceToHost, st) == hipSuccess;
+    copy_ok = copy_ok && hipStreamSynchronize(st) == hipSuccess;
+  }
+  // step (3): a receiver loads what it got; returns this rank's failure count for the verdict all-reduce
+  unsigned long long load(int root, unsigned long long nbytes) {
+    rc = copy_ok ? YM_OK : fail(YM_EHIP, "blob staging copy failed");
+    if (rc == YM_OK && rank != root) rc = ym_load_weights(c, h.data(), nbytes);
+    return rc == YM_OK ? 0ull : 1ull;
+  }
+};
+
+// The identical-on-every-rank verdict on step (1)'s sums: YM_OK or the error every rank returns before step (2).
+static int bcast_check(const unsigned long long h1[2], bool is_root, int root) {
+  if (h1[0] == 0)
+    return fail(YM_ESTATE, is_root ? "the root context has no weights to broadcast"
+                                   : "the root rank %d has no weights to broadcast", root);
+  if (h1[0] < kHdr * 4 || h1[0] > (1ull << 34)) return fail(YM_EBLOB, "broadcast blob size %llu", h1[0]);
+  if (h1[1]) return fail(YM_ENOMEM, "%llu rank(s) could not allocate the %zu-byte staging buffer", h1[1], kBcastChunk);
+  return YM_OK;
+}
+
 // The root rank's loaded blob (plan + weights, exactly the bytes its ym_load_weights received) goes to every rank
 // of `comm` over RCCL (xGMI) and each non-root rank loads it into `c` (ym_load_weights), so every rank ends with an
 // identical model without touching the file system.  Synchronous.
@@ -1370,57 +1425,77 @@ int ym_broadcast_weights(ym_ctx* c, void* comm, int root, void* stream) {
   RCCLCK(R->count(comm, &n));
   if (root < 0 || root >= n) return fail(YM_EINVAL, "root %d out of range (%d ranks)", root, n);
   const hipStream_t st = static_cast<hipStream_t>(stream);
-  bool hip_ok = hipSetDevice(c->device) == hipSuccess;
+  BcastRank me;
+  me.c = c;
+  me.rank = rank;
   // control words: the context's 4 KB scratch (allocated by ym_create, so nothing can fail before step 1)
   unsigned long long* dctl = reinterpret_cast<unsigned long long*>(c->d_misc + 2048);
   auto allreduce_sum = [&](unsigned long long* h, int cnt) -> int {
-    hip_ok = hip_ok && hipMemcpyAsync(dctl, h, 8 * cnt, hipMemcpyHostToDevice, st) == hipSuccess;
+    me.hip_ok = me.hip_ok && hipMemcpyAsync(dctl, h, 8 * cnt, hipMemcpyHostToDevice, st) == hipSuccess;
     const int r = R->allreduce(dctl, dctl, cnt, kNcclUint64, kNcclSum, comm, st);
     if (r) return r;
-    hip_ok = hip_ok && hipMemcpyAsync(h, dctl, 8 * cnt, hipMemcpyDeviceToHost, st) == hipSuccess &&
-             hipStreamSynchronize(st) == hipSuccess;
+    me.hip_ok = me.hip_ok && hipMemcpyAsync(h, dctl, 8 * cnt, hipMemcpyDeviceToHost, st) == hipSuccess &&
+                hipStreamSynchronize(st) == hipSuccess;
     return 0;
   };
-  const unsigned long long mine = (rank == root && c->loaded) ? (unsigned long long)c->blob_host.size() : 0ull;
-  const size_t chunk_cap = kBcastChunk;
-  char* d = nullptr;
-  const bool alloc_ok = hip_ok && hipMalloc(&d, chunk_cap) == hipSuccess;
-  unsigned long long h1[2] = {mine, alloc_ok ? 0ull : 1ull};
+  unsigned long long h1[2] = {0ull, 0ull};
+  me.open(root, h1);
   int r = allreduce_sum(h1, 2);  // (1)
-  auto done = [&](int code) {
-    if (d) (void)hipFree(d);
-    return code;
-  };
-  if (r) return done(fail(YM_EHIP, "ncclAllReduce(size): %s", R->err(r)));
+  if (r) return fail(YM_EHIP, "ncclAllReduce(size): %s", R->err(r));
+  if (int e = bcast_check(h1, rank == root, root)) return e;
   const unsigned long long nbytes = h1[0];
-  if (nbytes == 0)
-    return done(fail(YM_ESTATE, rank == root ? "the root context has no weights to broadcast"
-                                             : "the root rank %d has no weights to broadcast", root));
-  if (nbytes < kHdr * 4 || nbytes > (1ull << 34)) return done(fail(YM_EBLOB, "broadcast blob size %llu", nbytes));
-  if (h1[1]) return done(fail(YM_ENOMEM, "%llu rank(s) could not allocate the %zu-byte staging buffer", h1[1], chunk_cap));
-  // (2) the blob, chunk by chunk through the staging buffer
-  std::vector<char> h;
-  if (rank != root) h.resize(nbytes);
-  bool copy_ok = hip_ok;
-  for (unsigned long long off = 0; off < nbytes; off += chunk_cap) {
-    const size_t len = (size_t)std::min<unsigned long long>(chunk_cap, nbytes - off);
-    if (rank == root)
-      copy_ok = copy_ok && hipMemcpyAsync(d, c->blob_host.data() + off, len, hipMemcpyHostToDevice, st) == hipSuccess;
-    r = R->bcast(d, d, len, kNcclUint8, root, comm, st);
-    if (r) return done(fail(YM_EHIP, "ncclBroadcast(blob): %s", R->err(r)));
-    if (rank != root)
-      copy_ok = copy_ok && hipMemcpyAsync(h.data() + off, d, len, hipMemcpyDeviceToHost, st) == hipSuccess;
-    copy_ok = copy_ok && hipStreamSynchronize(st) == hipSuccess;  // the staging buffer is reused
+  if (rank != root) me.h.resize(nbytes);
+  for (unsigned long long off = 0; off < nbytes; off += kBcastChunk) {  // (2)
+    const size_t len = (size_t)std::min<unsigned long long>(kBcastChunk, nbytes - off);
+    me.put(root, off, len, st);
+    r = R->bcast(me.d, me.d, len, kNcclUint8, root, comm, st);
+    if (r) return fail(YM_EHIP, "ncclBroadcast(blob): %s", R->err(r));
+    me.get(root, off, len, st);
   }
-  // (3) load on the receivers, then agree on the outcome
-  int rc = copy_ok ? YM_OK : fail(YM_EHIP, "blob staging copy failed");
-  if (rc == YM_OK && rank != root) rc = ym_load_weights(c, h.data(), nbytes);
-  unsigned long long h3[1] = {rc == YM_OK ? 0ull : 1ull};
+  unsigned long long h3[1] = {me.load(root, nbytes)};  // (3)
   r = allreduce_sum(h3, 1);
-  if (r) return done(fail(YM_EHIP, "ncclAllReduce(status): %s", R->err(r)));
-  if (rc != YM_OK) return done(rc);
-  if (h3[0]) return done(fail(YM_EBLOB, "the weight broadcast failed on %llu other rank(s)", h3[0]));
-  return done(YM_OK);
+  if (r) return fail(YM_EHIP, "ncclAllReduce(status): %s", R->err(r));
+  if (me.rc != YM_OK) return me.rc;
+  if (h3[0]) return fail(YM_EBLOB, "the weight broadcast failed on %llu other rank(s)", h3[0]);
+  return YM_OK;
+}
+
+// The fake backend of the same broadcast (N ranks as N contexts of this process, e.g. on one GPU):
+// rank i is ctxs[i]; the all-reduces are host sums and the chunk moves from the root's staging buffer to every
+// other rank's by a device-to-device copy on `stream`, between the same BcastRank put / get / load steps the RCCL
+// transport runs.  Returns the status of the first failing rank (every rank's context is left loaded or not as in
+// the RCCL path); on success every context holds the root's blob.
+int ym_broadcast_weights_local(ym_ctx* const* ctxs, int n, int root, void* stream) {
+  if (!ctxs || n < 1) return fail(YM_EINVAL, "null / empty context list");
+  if (root < 0 || root >= n) return fail(YM_EINVAL, "root %d out of range (%d ranks)", root, n);
+  for (int i = 0; i < n; ++i)
+    if (!ctxs[i]) return fail(YM_EINVAL, "null context for rank %d", i);
+  const hipStream_t st = static_cast<hipStream_t>(stream);
+  std::vector<BcastRank> ranks(n);
+  unsigned long long h1[2] = {0ull, 0ull};
+  for (int i = 0; i < n; ++i) {  // (1)
+    ranks[i].c = ctxs[i];
+    ranks[i].rank = i;
+    ranks[i].open(root, h1);
+  }
+  if (int e = bcast_check(h1, true, root)) return e;
+  const unsigned long long nbytes = h1[0];
+  for (int i = 0; i < n; ++i)
+    if (i != root) ranks[i].h.resize(nbytes);
+  for (unsigned long long off = 0; off < nbytes; off += kBcastChunk) {  // (2)
+    const size_t len = (size_t)std::min<unsigned long long>(kBcastChunk, nbytes - off);
+    ranks[root].put(root, off, len, st);
+    for (int i = 0; i < n; ++i)
+      if (i != root)
+        ranks[i].copy_ok = ranks[i].copy_ok && ranks[root].copy_ok &&
+                           hipMemcpyAsync(ranks[i].d, ranks[root].d, len, hipMemcpyDeviceToDevice, st) == hipSuccess;
+    for (int i = 0; i < n; ++i) ranks[i].get(root, off, len, st);
+  }
+  unsigned long long h3 = 0;  // (3)
+  for (int i = 0; i < n; ++i) h3 += ranks[i].load(root, nbytes);
+  for (int i = 0; i < n; ++i)
+    if (ranks[i].rc != YM_OK) return ranks[i].rc;
+  return h3 ? fail(YM_EBLOB, "the weight broadcast failed on %llu rank(s)", h3) : YM_OK;
 }
 
 int ym_sync(ym_ctx* c) {

@@ -3,9 +3,10 @@
 One process per GPU.  At init rank 0 packs the model blob (BN-folded, NHWC packed weights + plan) and broadcasts it
 over RCCL (xGMI) through the C-ABI (`rccl_broadcast_model` → ym_broadcast_weights; `broadcast_blob` is the same
 exchange as one torch.distributed uint8 tensor, used by the gloo CPU tests).  Per batch,
-rank r runs images [r*B_local, (r+1)*B_local) of the global batch on its own stream/graph; the only exchange is one
-fp32 all-reduce (MAX) so that LoadTensor's /255 rule — a whole-batch decision in the reference — is taken over the
-global batch, not per shard (`GlobalBatchMax`).  The reference itself is single-device for inference
+rank r runs images [r*B_local, (r+1)*B_local) of the global batch on its own stream/graph.  LoadTensor's /255 rule
+— a whole-batch decision in the reference — is taken over the global batch, not per shard: once where the batch is
+split (`split_batch_max`, what the bench does: no per-step collective), or per call by one fp32 all-reduce (MAX,
+`GlobalBatchMax`) for callers without a splitter.  The reference itself is single-device for inference
 (/root/reference/core/model.py:111-112).
 """
 from __future__ import annotations
@@ -35,29 +36,68 @@ def broadcast_blob(blob: Optional[bytes], device: torch.device, src: int = 0) ->
     return blob if rank == src else bytes(buf.cpu().numpy())
 
 
-def rccl_broadcast_model(make_model, blob: Optional[bytes], device: torch.device, root: int = 0):
+def rccl_broadcast_model(make_model, blob: Optional[bytes], device: torch.device, root: int = 0,
+                         scale: str = None, task: str = None, dtype: str = None):
     """The C-ABI path of the init-time weight broadcast (include/yolomi.h ym_broadcast_weights): the root's packed
-    blob goes to every rank over RCCL (xGMI) straight into each rank's context.  The RCCL unique id travels over the
-    default torch.distributed group; `make_model(**kw)` builds the rank's YOLO11Model (root: weights_blob=blob,
-    others: weights_from=(comm, root)).  Collective: every rank calls it."""
+    blob goes to every rank over RCCL (xGMI) straight into each rank's context.  `make_model(**kw)` builds the rank's
+    YOLO11Model (root: weights_blob=blob, others: weights_from=<the received Runtime>); scale / task / dtype describe
+    the model the receivers' empty contexts must accept.  Collective: every rank calls it.
+
+    No rank is left inside a collective its peers never reach: every rank first builds what needs no peer (the
+    root its whole model, the others an empty context) and the ranks agree on that over the torch group; only if all
+    succeeded do they create the RCCL communicator and enter ym_broadcast_weights (whose own steps return one verdict
+    on every rank).  A local failure raises on every rank."""
     from . import lib as L
     rank, world = dist.get_rank(), dist.get_world_size()
-    if rank == root and blob is None:
-        raise ValueError("the root rank must provide the blob")
-    uid = [L.rccl_unique_id() if rank == root else None]
-    dist.broadcast_object_list(uid, src=root)
-    comm = L.rccl_comm_init(device.index if device.index is not None else torch.cuda.current_device(), world, uid[0],
-                            rank)
+    dev_index = device.index if device.index is not None else torch.cuda.current_device()
+    model, rt, err = None, None, None
     try:
         if rank == root:
+            if blob is None:
+                raise ValueError("the root rank must provide the blob")
             model = make_model(weights_blob=blob)
-            model.model.engine.broadcast_weights(comm, root)
         else:
-            model = make_model(weights_from=(comm, root))
+            rt = L.Runtime(dev_index, None, scale=scale, task=task, dtype=dtype)
+    except Exception as e:  # reported to the peers below, re-raised here
+        err = e
+    if all_ranks_failed(err is not None, device):
+        raise err if err is not None else RuntimeError("weight broadcast: another rank failed to build its context")
+    uid = [L.rccl_unique_id() if rank == root else None]
+    dist.broadcast_object_list(uid, src=root)
+    comm = L.rccl_comm_init(dev_index, world, uid[0], rank)
+    try:
+        stream = torch.cuda.current_stream(device).cuda_stream
+        if rank == root:
+            model.model.engine.rt.broadcast_weights(comm, root, stream)
+        else:
+            rt.broadcast_weights(comm, root, stream)
         torch.cuda.synchronize(device)
     finally:
         L.rccl_comm_destroy(comm)
-    return model
+    return model if rank == root else make_model(weights_from=rt)
+
+
+def all_ranks_failed(failed: bool, device: torch.device) -> bool:
+    """True on every rank when any rank reports failure (one int all-reduce over the default group)."""
+    flag = torch.tensor([1 if failed else 0], dtype=torch.int32,
+                        device=device if dist.get_backend() == "nccl" else torch.device("cpu"))
+    dist.all_reduce(flag)
+    return bool(flag.item())
+
+
+def local_broadcast_models(make_model, blob: bytes, n: int, device: torch.device, root: int = 0,
+                           scale: str = None, task: str = None, dtype: str = None):
+    """SURVEY §4.4's fake backend: n "ranks" as n models in this process (e.g. on one GPU).  The root model is built
+    from `blob`; the others start as empty contexts and receive it through ym_broadcast_weights_local — the
+    receive / ym_load_weights / verdict steps of the RCCL broadcast, with device-to-device copies for RCCL."""
+    from . import lib as L
+    dev_index = device.index if device.index is not None else torch.cuda.current_device()
+    models = [None] * n
+    models[root] = make_model(weights_blob=blob)
+    rts = [models[root].model.engine.rt if i == root else L.Runtime(dev_index, None, scale=scale, task=task,
+                                                                     dtype=dtype) for i in range(n)]
+    L.Runtime.broadcast_weights_local(rts, root, torch.cuda.current_stream(device).cuda_stream)
+    return [models[i] if i == root else make_model(weights_from=rts[i]) for i in range(n)]
 
 
 def shard(global_batch: int, rank: int, world: int) -> Tuple[int, int]:
@@ -92,10 +132,22 @@ class GlobalBatchMax:
 
 
 def enable_global_rule(model, group=None) -> GlobalBatchMax:
-    """Make `model.predict` take the /255 decision over the global batch of this process group."""
+    """Make `model.predict` take the /255 decision over the global batch of this process group: one fp32
+    all-reduce per call (every rank's step waits for the slowest rank's input statistic)."""
     rule = GlobalBatchMax(model.model.engine, group=group)
     model.global_batch_max = rule
     return rule
+
+
+def split_batch_max(model, x: torch.Tensor, group=None) -> torch.Tensor:
+    """The /255 decision taken where the global batch is split, not per step: each rank's shard max, all-reduced
+    ONCE, pinned as the model's global statistic for this batch (a (1,) device tensor).  For a rank that runs the
+    same shard repeatedly (the bench's timed loop) this is the reference's whole-batch LoadTensor rule with no
+    per-step collective; a serving splitter would ship the max with each shard instead."""
+    rule = GlobalBatchMax(model.model.engine, group=group)
+    m = rule(x).clone()
+    model.global_batch_max = lambda _x: m
+    return m
 
 
 def digest(blob: bytes) -> str:

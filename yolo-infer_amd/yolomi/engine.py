@@ -41,7 +41,12 @@ class Engine:
         self.graph = GraphBuilder(scale, task, nc=nc, quant=dtype in QUANT_DTYPES,
                                   fuse=fuse_default(dtype))
         dev_index = device.index if device.index is not None else torch.cuda.current_device()
-        if receive is not None:  # a non-root rank: the model arrives over RCCL from the root's context
+        if isinstance(receive, Runtime):  # a context that already received the root's blob (yolomi.dist)
+            if receive.n_ops != len(self.graph.ops) or receive.device_index != dev_index:
+                raise ValueError("the received context does not hold this plan on this device")
+            self.blob = None
+            self.rt = receive
+        elif receive is not None:  # a non-root rank: the model arrives over RCCL from the root's context
             self.blob = None
             self.rt = Runtime(dev_index, None, scale=scale, task=task, dtype=dtype)
             self.rt.broadcast_weights(receive[0], receive[1], torch.cuda.current_stream(device).cuda_stream)

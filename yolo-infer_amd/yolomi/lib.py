@@ -72,6 +72,7 @@ def load_library(path: os.PathLike = LIB_PATH):
         "ym_read_buffer": (I, [P, I, P, C.c_size_t]),
         "ym_input_max": (I, [P, P, C.c_size_t, P, P]),
         "ym_broadcast_weights": (I, [P, P, I, P]),
+        "ym_broadcast_weights_local": (I, [C.POINTER(P), I, I, P]),
         "ym_rccl_get_unique_id": (I, [C.POINTER(RcclId)]),
         "ym_rccl_comm_init": (I, [I, I, C.POINTER(RcclId), I, C.POINTER(P)]),
         "ym_rccl_comm_destroy": (I, [P]),
@@ -89,7 +90,7 @@ def load_library(path: os.PathLike = LIB_PATH):
     return lib
 
 
-EXPORTED = ("ym_create", "ym_load_weights", "ym_broadcast_weights", "ym_rccl_get_unique_id", "ym_rccl_comm_init",
+EXPORTED = ("ym_create", "ym_load_weights", "ym_broadcast_weights", "ym_broadcast_weights_local", "ym_rccl_get_unique_id", "ym_rccl_comm_init",
             "ym_rccl_comm_destroy", "ym_infer", "ym_input_max", "ym_calibrate", "ym_masks", "ym_masks_slots", "ym_letterbox",
             "ym_profile", "ym_profile_replay", "ym_tune", "ym_get_op_cfg", "ym_set_op_cfg", "ym_num_ops", "ym_op_name",
             "ym_num_buffers", "ym_buffer_info", "ym_read_buffer", "ym_sync", "ym_last_error", "ym_destroy",
@@ -156,6 +157,16 @@ class Runtime:
         _check(self.lib.ym_broadcast_weights(self.ctx, C.c_void_p(comm), root, C.c_void_p(stream)))
         self.n_ops = self.lib.ym_num_ops(self.ctx)
         self.op_names = [self.lib.ym_op_name(self.ctx, i).decode() for i in range(self.n_ops)]
+
+    @staticmethod
+    def broadcast_weights_local(runtimes, root: int, stream: int):
+        """ym_broadcast_weights_local: runtimes[root]'s model to every other Runtime of this process (the fake
+        backend of the RCCL broadcast; the receivers are empty contexts, Runtime(dev, None))."""
+        arr = (C.c_void_p * len(runtimes))(*[r.ctx.value for r in runtimes])
+        _check(runtimes[0].lib.ym_broadcast_weights_local(arr, len(runtimes), root, C.c_void_p(stream)))
+        for r in runtimes:
+            r.n_ops = r.lib.ym_num_ops(r.ctx)
+            r.op_names = [r.lib.ym_op_name(r.ctx, i).decode() for i in range(r.n_ops)]
 
     @staticmethod
     def make_args(conf=0.25, iou=0.7, max_det=300, max_nms=30000, agnostic=False, max_wh=7680.0, in_eps=1.1920929e-07,
