@@ -183,7 +183,7 @@ def pmc_family_bytes(workload):
 
 # op kind (yolomi/arch.py) → the rocprof kernel family of tools/rocprof_summary.py
 KIND_FAMILY = {"stem": "stem", "dwconv": "dwconv3x3", "sppf": "sppf", "attn": "attn_psa", "decode": "decode_anchors",
-               "input": "max_reduce", "nms": "nms_image"}
+               "input": "input_stats", "nms": "nms_image"}
 
 
 def kernel_table(model, x, dtype, workload):

@@ -31,7 +31,7 @@ def dispatches(d):
         e = disp.setdefault(k, {"kernel": r["Kernel_Name"]})
         e[r["Counter_Name"]] = e.get(r["Counter_Name"], 0.0) + float(r["Counter_Value"])
     seq = [disp[k] for k in sorted(disp)]
-    starts = [i for i, e in enumerate(seq) if "init_ctl" in e["kernel"]]
+    starts = [i for i, e in enumerate(seq) if "input_stats" in e["kernel"]]
     return seq[starts[-1]:]
 
 

@@ -4,7 +4,7 @@
     rocprofv3 --pmc FETCH_SIZE -d gpurun_out/pmc_fetch -o run --output-format csv -- python3 tools/pmc_forward.py
 
 Uses the same tuned conv tables as bench.py (YM_TUNE_DIR / yolomi/tuned), so the dispatch sequence of the last
-`--reps` forwards is exactly one bench forward each; tools/rocprof_summary.py splits them at the init_ctl kernel.
+`--reps` forwards is exactly one bench forward each; tools/rocprof_summary.py splits them at the input_stats kernel.
 """
 import argparse
 import os

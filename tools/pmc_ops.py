@@ -1,6 +1,6 @@
 #!/usr/bin/env python3
 """Per-op PMC counters of one eager forward: joins rocprofv3 --pmc counter_collection.csv dispatches (last forward,
-split at init_ctl) with the op list written by `tools/pmc_forward.py --ops-out`.
+split at input_stats) with the op list written by `tools/pmc_forward.py --ops-out`.
 
     python tools/pmc_ops.py <ops.txt> <pmc_dir> [<pmc_dir> ...] [--ops regex]
 
@@ -21,7 +21,7 @@ def last_forward(d):
         e = disp.setdefault(k, {"name": r["Kernel_Name"]})
         e[r["Counter_Name"]] = e.get(r["Counter_Name"], 0.0) + float(r["Counter_Value"])
     seq = [disp[k] for k in sorted(disp)]
-    starts = [i for i, e in enumerate(seq) if "init_ctl" in e["name"]]
+    starts = [i for i, e in enumerate(seq) if "input_stats" in e["name"]]
     return seq[starts[-1]:]
 
 
@@ -34,7 +34,7 @@ def main():
     ops = [o for o in ops if o[1] != "input"]
     fwd = None
     for d in args[1:]:
-        seq = last_forward(d)[2:]  # init_ctl, max_reduce = the input op
+        seq = last_forward(d)[1:]  # input_stats = the input op
         if fwd is None:
             fwd = seq
         else:

@@ -34,7 +34,7 @@ def family(name):
         return "stem"
     if CONV.search(name):
         return "conv"
-    for k in ("dwconv3x3", "sppf", "attn_psa", "decode_anchors", "nms_image", "init_ctl", "max_reduce", "spin_wait", "requant_copy",
+    for k in ("dwconv3x3", "sppf", "attn_psa", "decode_anchors", "nms_image", "input_stats", "spin_wait", "requant_copy",
               "copyBuffer"):
         if k in name:
             return k
@@ -79,7 +79,7 @@ def pmc_per_forward(d, counter, reps):
         e = disp.setdefault(k, [r["Kernel_Name"], 0.0])
         e[1] += float(r["Counter_Value"])
     seq = [disp[k] for k in sorted(disp)]
-    starts = [i for i, (n, _) in enumerate(seq) if "init_ctl" in n]
+    starts = [i for i, (n, _) in enumerate(seq) if "input_stats" in n]
     if len(starts) < reps:
         raise SystemExit(f"{d}: found {len(starts)} forwards, need {reps}")
     fwd = []

@@ -3,7 +3,7 @@
 
     python tools/trace_timeline.py <rocprof_dir> [forwards] [skip]
 
-Forwards are split at the init_ctl kernel (the first op of every forward).  Per forward: wall span (first start to
+Forwards are split at the input_stats kernel (the first op of every forward).  Per forward: wall span (first start to
 last end), the union of kernel-busy intervals (span - union = time no kernel of the forward runs: launch / dependency
 gaps), the sum of kernel durations (sum / union > 1: concurrent branches), and the largest idle gaps with the kernels
 on either side.  Averaged over the last `forwards` forwards (default 20) before the last `skip` ones (default 0; a
@@ -30,7 +30,7 @@ def main():
     for r in csv.DictReader(open(f)):
         rows.append((int(r["Start_Timestamp"]), int(r["End_Timestamp"]), r["Kernel_Name"]))
     rows.sort()
-    starts = [i for i, r in enumerate(rows) if "init_ctl" in r[2]]
+    starts = [i for i, r in enumerate(rows) if "input_stats" in r[2]]
     fwds = []
     for j in range(len(starts)):
         end = starts[j + 1] if j + 1 < len(starts) else len(rows)

@@ -13,56 +13,79 @@ namespace {
 
 // ------------------------------------------------------------------------------------------------- input stats
 // LoadTensor._single_check: `if im.max() > 1 + finfo(dtype).eps: im = im.float() / 255` over the WHOLE batch.
-// ctl[0] holds max as an order-preserving int; ctl is reset by the init kernel at the start of every forward.
+// ctl[0] holds max as an order-preserving int (ym_input_max reads the YM_CTL_SLOTS slots).
 // The division itself happens in the stem conv's loader (csrc/ym_stem.hip), which reads the NCHW batch.
-__global__ __launch_bounds__(256) void init_ctl(float* ctl, int* counts, int B, int* cnt, int cnt_len) {
-  const int t = blockIdx.x * blockDim.x + threadIdx.x;
-  if (t < YM_CTL_SLOTS) reinterpret_cast<int*>(ctl)[t * YM_CTL_STRIDE] = f2ord(-INFINITY);
-  for (int b = t; b < B; b += gridDim.x * blockDim.x) counts[b] = 0;
-  int4* c4 = reinterpret_cast<int4*>(cnt);  // split-K tile counters (csrc/ym_conv_dma.hip)
-  for (int i = t; i < cnt_len / 4; i += gridDim.x * blockDim.x) c4[i] = make_int4(0, 0, 0, 0);
-}
-
-__global__ __launch_bounds__(256) void max_reduce(const float* __restrict__ x, long n, float* ctl) {
-  float m = -INFINITY;
+//
+// input_stats: the forward's first kernel, one launch.  Every block zeroes its share of the per-image candidate
+// counts and the split-K tile counters (csrc/ym_conv_dma.hip; self-resetting, cleared here as a guard against an
+// aborted forward), reduces a contiguous chunk of the batch to its max and stores it write-through (sc1) into its
+// partial slot; after its `vmcnt(0)` one lane takes an agent-scope ticket, and the block whose ticket is last
+// reduces the partials (sc1 loads: the hand-off of MI355X_MICROARCH §inter-workgroup visibility, first table row),
+// writes the slots and resets the ticket.  No per-forward init kernel, no same-address atomicMax storm.
+// batch_max non-null (multi-GPU shard): the slots take the given global max, x is not read.
+constexpr int kStatsBlocks = 1024;  // partial slots (ym_runtime.cpp reserves them behind the ctl slots)
+__global__ __launch_bounds__(256) void input_stats(const float* __restrict__ x, long n, float* ctl, int* counts, int B,
+                                                   int* cnt, int cnt_len, const float* batch_max) {
+  const int tid = threadIdx.x;
+  const long gt = blockIdx.x * 256L + tid, gstride = (long)gridDim.x * 256;
+  for (long b = gt; b < B; b += gstride) counts[b] = 0;
+  int4* c4 = reinterpret_cast<int4*>(cnt);
+  for (long i = gt; i < cnt_len / 4; i += gstride) c4[i] = make_int4(0, 0, 0, 0);
+  int* slots = reinterpret_cast<int*>(ctl);
+  if (batch_max) {
+    if (blockIdx.x == 0 && tid < YM_CTL_SLOTS) slots[tid * YM_CTL_STRIDE] = tid == 0 ? f2ord(*batch_max) : f2ord(-INFINITY);
+    return;
+  }
+  int* part = slots + YM_CTL_SLOTS * YM_CTL_STRIDE + 64;  // [kStatsBlocks], after the ticket's 256-byte line
+  int* ticket = slots + YM_CTL_SLOTS * YM_CTL_STRIDE;
+  // contiguous chunk of whole float4s per block, eight 16-byte loads in flight per lane
   const long n4 = n >> 2;
+  const long per = (n4 + gridDim.x - 1) / gridDim.x;
+  const long lo = blockIdx.x * per, hi = lo + per < n4 ? lo + per : n4;
   const f32x4* x4 = reinterpret_cast<const f32x4*>(x);
-  const long step = (long)gridDim.x * blockDim.x;
-  long i = blockIdx.x * (long)blockDim.x + threadIdx.x;
-  for (; i + 7 * step < n4; i += 8 * step) {  // eight independent 16-byte loads in flight per lane
+  float m = -INFINITY;
+  long i = lo + tid;
+  for (; i + 7 * 256 < hi; i += 8 * 256) {
     f32x4 v[8];
 #pragma unroll
-    for (int u = 0; u < 8; ++u) v[u] = __builtin_nontemporal_load(x4 + i + u * step);
+    for (int u = 0; u < 8; ++u) v[u] = x4[i + u * 256];
 #pragma unroll
     for (int u = 0; u < 8; ++u) m = fmaxf(m, fmaxf(fmaxf(v[u][0], v[u][1]), fmaxf(v[u][2], v[u][3])));
   }
-  for (; i < n4; i += step) {
+  for (; i < hi; i += 256) {
     const f32x4 v = x4[i];
     m = fmaxf(m, fmaxf(fmaxf(v[0], v[1]), fmaxf(v[2], v[3])));
   }
-  for (long i = (n4 << 2) + blockIdx.x * (long)blockDim.x + threadIdx.x; i < n; i += (long)gridDim.x * blockDim.x)
-    m = fmaxf(m, x[i]);
+  if (blockIdx.x == 0)
+    for (long j = (n4 << 2) + tid; j < n; j += 256) m = fmaxf(m, x[j]);
 #pragma unroll
   for (int o = 32; o > 0; o >>= 1) m = fmaxf(m, __shfl_xor(m, o));
   __shared__ float wm[4];
-  if ((threadIdx.x & 63) == 0) wm[threadIdx.x >> 6] = m;
+  __shared__ int last;
+  if ((tid & 63) == 0) wm[tid >> 6] = m;
   __syncthreads();
-  if (threadIdx.x == 0) {
+  if (tid == 0) {
     m = fmaxf(fmaxf(wm[0], wm[1]), fmaxf(wm[2], wm[3]));
-    atomicMax(reinterpret_cast<int*>(ctl) + (blockIdx.x % YM_CTL_SLOTS) * YM_CTL_STRIDE, f2ord(m));
+    __hip_atomic_store(part + blockIdx.x, f2ord(m), __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);  // sc1
+    asm volatile("s_waitcnt vmcnt(0)" ::: "memory");
+    const int t = __hip_atomic_fetch_add(ticket, 1, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
+    last = t == (int)gridDim.x - 1;
   }
+  __syncthreads();
+  if (!last) return;
+  int r = f2ord(-INFINITY);
+  for (int b = tid; b < (int)gridDim.x; b += 256)
+    r = max(r, __hip_atomic_load(part + b, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT));
+#pragma unroll
+  for (int o = 32; o > 0; o >>= 1) r = max(r, __shfl_xor(r, o));
+  __shared__ int wr[4];
+  if ((tid & 63) == 0) wr[tid >> 6] = r;
+  __syncthreads();
+  if (tid < YM_CTL_SLOTS)
+    slots[tid * YM_CTL_STRIDE] = tid == 0 ? max(max(wr[0], wr[1]), max(wr[2], wr[3])) : f2ord(-INFINITY);
+  if (tid == 0) __hip_atomic_store(ticket, 0, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
 }
 
-// The batch-sharded multi-GPU path: LoadTensor's rule is over the GLOBAL batch, whose max the ranks agree on with
-// one all-reduce (yolomi/dist.py); the forward then takes its /255 decision from that float instead of its shard.
-__global__ void ctl_from_max(float* ctl, const float* m) {
-  const int t = threadIdx.x;
-  if (t < YM_CTL_SLOTS) reinterpret_cast<int*>(ctl)[t * YM_CTL_STRIDE] = t == 0 ? f2ord(*m) : f2ord(-INFINITY);
-}
-__global__ void ctl_reset(float* ctl) {
-  const int t = threadIdx.x;
-  if (t < YM_CTL_SLOTS) reinterpret_cast<int*>(ctl)[t * YM_CTL_STRIDE] = f2ord(-INFINITY);
-}
 __global__ void ctl_to_max(const float* ctl, float* out) {
   if (threadIdx.x == 0) *out = ym_input_max(ctl);
 }
@@ -1436,28 +1459,21 @@ hipError_t ym_launch_spin(int usec, hipStream_t st) {
 
 hipError_t ym_launch_prep(int dtype, const PrepArgs& a, int* counts, int B, hipStream_t st) {
   (void)dtype;
-  const int ib = (a.cnt_len / 4 + 255) / 256;
-  hipLaunchKernelGGL(init_ctl, dim3(ib < 1 ? 1 : (ib > 64 ? 64 : ib)), dim3(256), 0, st, a.ctl, counts, B, a.cnt,
-                     a.cnt_len);
-  if (a.batch_max) {  // the global batch max is given (multi-GPU shard): no reduction over this rank's images
-    hipLaunchKernelGGL(ctl_from_max, dim3(1), dim3(64), 0, st, a.ctl, a.batch_max);
-    return hipGetLastError();
-  }
-  // one atomic per block: a few hundred same-address atomics, not thousands (one word takes ~90 per us)
+  // one launch: counters cleared, batch max reduced (or the given global max taken) — input_stats above
   const long n = (long)a.B * a.C * a.H * a.W;
-  long blocks = (n / 4 + 255) / 256;
-  if (blocks > 2048) blocks = 2048;
+  long blocks = a.batch_max ? 64 : (n / 4 + 2047) / 2048;  // >= 8 float4 per lane
+  if (blocks > kStatsBlocks) blocks = kStatsBlocks;
   if (blocks < 1) blocks = 1;
-  hipLaunchKernelGGL(max_reduce, dim3(blocks), dim3(256), 0, st, a.in, n, a.ctl);
+  hipLaunchKernelGGL(input_stats, dim3(blocks), dim3(256), 0, st, a.in, n, a.ctl, counts, B, a.cnt, a.cnt_len,
+                     a.batch_max);
   return hipGetLastError();
 }
 
 hipError_t ym_launch_input_max(const float* x, long n, float* ctl, float* out, hipStream_t st) {
-  hipLaunchKernelGGL(ctl_reset, dim3(1), dim3(64), 0, st, ctl);
-  long blocks = (n / 4 + 255) / 256;
-  if (blocks > 2048) blocks = 2048;
+  long blocks = (n / 4 + 2047) / 2048;
+  if (blocks > kStatsBlocks) blocks = kStatsBlocks;
   if (blocks < 1) blocks = 1;
-  hipLaunchKernelGGL(max_reduce, dim3(blocks), dim3(256), 0, st, x, n, ctl);
+  hipLaunchKernelGGL(input_stats, dim3(blocks), dim3(256), 0, st, x, n, ctl, nullptr, 0, nullptr, 0, nullptr);
   hipLaunchKernelGGL(ctl_to_max, dim3(1), dim3(64), 0, st, ctl, out);
   return hipGetLastError();
 }

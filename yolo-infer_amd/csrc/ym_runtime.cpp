@@ -129,7 +129,7 @@ struct ym_ctx {
   int strides[4] = {8, 16, 32, 0};
   int input_buf = -1, anchor_buf = -1, proto_buf = -1, no = 0;
   float* d_lowres = nullptr;  // Segment mask assembly scratch (ym_masks)
-  char* d_misc = nullptr;     // 4 KB: ym_input_max statistics slots, ym_broadcast_weights control words
+  char* d_misc = nullptr;     // 16 KB: ym_input_max statistics region, ym_broadcast_weights control words
   size_t lowres_bytes = 0;
   std::vector<BufDesc> bufs;
   std::vector<Op> ops;
@@ -266,7 +266,7 @@ int ensure_workspace(ym_ctx* c, int B, int H, int W) {
   c->off_cls = off;    off = align_up(off + BA * 4, 256);
   c->off_keys = off;   off = align_up(off + (size_t)nB * c->kstride * 8, 256);
   c->off_counts = off; off = align_up(off + (size_t)nB * 4, 256);
-  c->off_ctl = off;    off = align_up(off + YM_CTL_SLOTS * YM_CTL_STRIDE * 4, 256);
+  c->off_ctl = off;    off = align_up(off + YM_CTL_BYTES, 256);
   c->off_sboxes = off; off = align_up(off + BA * 16, 256);
   c->off_sareas = off; off = align_up(off + BA * 4, 256);
   c->off_sup = off;    off = align_up(off + BA, 256);
@@ -592,7 +592,9 @@ int ym_create(int device, const ym_model_desc* desc, ym_ctx** out) {
   hipError_t e = hipStreamCreateWithFlags(&c->cap_stream, hipStreamNonBlocking);
   for (int l = 1; l < kMaxLanes && e == hipSuccess; ++l) e = hipStreamCreateWithFlags(&c->lane_streams[l], hipStreamNonBlocking);
   if (e == hipSuccess) e = hipEventCreateWithFlags(&c->fork_ev, hipEventDisableTiming);
-  if (e == hipSuccess) e = hipMalloc(&c->d_misc, 4096);  // ym_input_max slots [0, 2048), broadcast control words
+  // ym_input_max's ctl region (slots, ticket, partials: YM_CTL_BYTES) at 0, broadcast control words at 8 KB
+  if (e == hipSuccess) e = hipMalloc(&c->d_misc, 16384);
+  if (e == hipSuccess) e = hipMemset(c->d_misc, 0, 16384);
   for (int l = 1; l < kMaxLanes && e == hipSuccess; ++l) e = hipEventCreateWithFlags(&c->join_ev[l], hipEventDisableTiming);
   if (e != hipSuccess) {
     delete c;
@@ -1429,7 +1431,7 @@ int ym_broadcast_weights(ym_ctx* c, void* comm, int root, void* stream) {
   me.c = c;
   me.rank = rank;
   // control words: the context's 4 KB scratch (allocated by ym_create, so nothing can fail before step 1)
-  unsigned long long* dctl = reinterpret_cast<unsigned long long*>(c->d_misc + 2048);
+  unsigned long long* dctl = reinterpret_cast<unsigned long long*>(c->d_misc + 8192);
   auto allreduce_sum = [&](unsigned long long* h, int cnt) -> int {
     me.hip_ok = me.hip_ok && hipMemcpyAsync(dctl, h, 8 * cnt, hipMemcpyHostToDevice, st) == hipSuccess;
     const int r = R->allreduce(dctl, dctl, cnt, kNcclUint64, kNcclSum, comm, st);

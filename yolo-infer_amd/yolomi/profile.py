@@ -12,18 +12,18 @@ import numpy as np
 import torch
 
 
-KERNELS_PER_OP = {"input": 2}
+KERNELS_PER_OP = {"input": 1}
 
 
 def trace_times(csv_path: str, n_ops_kernels: int, kinds):
     """Kernel durations (ms) per plan op from a rocprofv3 --kernel-trace CSV: the LAST complete forward's dispatches
-    in order (input = 2 kernels: init, max-reduce; every other op = 1 kernel)."""
+    in order (every op = 1 kernel: the input op is input_stats)."""
     import csv
     rows = list(csv.DictReader(open(csv_path)))
     rows.sort(key=lambda r: int(r["Start_Timestamp"]))
     names = [r["Kernel_Name"] for r in rows]
     # forwards start with the init kernel of the input op
-    starts = [i for i, n in enumerate(names) if "init_ctl" in n]
+    starts = [i for i, n in enumerate(names) if "input_stats" in n]
     s = starts[-1]
     seg = rows[s:s + n_ops_kernels]
     durs = [(int(r["End_Timestamp"]) - int(r["Start_Timestamp"])) * 1e-6 for r in seg]
