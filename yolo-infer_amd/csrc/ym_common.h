@@ -321,6 +321,9 @@ struct ConvArgs {
   // 7.6e-4 px, the fp32 oracle's own distance from float64 being 8.2e-4).  wsc / wsc2 = 2^-s undo it exactly in the
   // epilogue: fmaf(acc, wsc, bias) rounds once, as acc + bias did (ym_x3_pre).  1 for every other plan.
   float wsc, wsc2;
+  // LDS-DMA kernels (csrc/ym_conv_dma.hip): request every line of the workgroup's K range into L2 before the ring
+  // starts (latency-bound small-M layers; YM_DMA_PF = the largest M it is used for, 0 = never)
+  int pf;
 };
 
 // x3 epilogue pre-activation: the weight scale (exact: a power of two) and the bias in one rounding

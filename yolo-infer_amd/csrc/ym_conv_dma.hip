@@ -103,7 +103,7 @@ __global__ __launch_bounds__(256 * KG) void conv_dma(const ConvArgs a) {
   constexpr int NREG = TM * TN * 16;
   constexpr int SPW = 4 / KG;                        // 16-deep k sub-steps per wave per stage
   constexpr int NACC = TM * TN == 1 && SPW >= 2 ? 2 : 1;  // one 32x32 block per wave: alternate two accumulators
-  __shared__ __attribute__((aligned(16))) char smem[NSTAGE * SB + 16];
+  __shared__ __attribute__((aligned(16))) char smem[NSTAGE * SB + 16 + 256];  // + split-K flag, L2 warm-up scratch
 
   YM_STAMP(0);
   const int tid = threadIdx.x, lane = tid & 63, wid = tid >> 6;
@@ -295,6 +295,58 @@ __global__ __launch_bounds__(256 * KG) void conv_dma(const ConvArgs a) {
 #pragma unroll
     for (int u = 0; u < SUB; ++u) issue_sub(smem + slot * SB + u * SBS);
   };
+  // L2 warm-up (ConvArgs::pf, the latency-bound small-M layers): every line this workgroup's K range will stage is
+  // requested ONCE up front by a 4-byte LDS-DMA into a scratch slot (the same per-lane addresses as the ring, so the
+  // same zero-fill rules; no VGPR destination, so no compiler waits), all in flight together; the ring's stages then
+  // find their lines in L2.  The counted vmcnt waits stay exact: these requests are older than every ring stage.
+  if (a.pf) {
+    const int s_tap = tap, s_cb = cb, s_ky = ky, s_kx = kx, s_k = kcur;
+    char* scratch = smem + NSTAGE * SB + 16;
+    for (int st = 0; st < nk * SUB; ++st) {
+      const int chunk = kcur * 8 + c;
+      if constexpr (KIND == 1) {
+        const bool second = a.src1 && kcur * DK >= C0s;
+#pragma unroll
+        for (int gi = 0; gi < GB; ++gi) {
+          const int pb = second ? pbase1[gi] : pbase0[gi];
+          const unsigned off = pb >= 0 ? (unsigned)(pb + chunk * 8 - (second ? C0s : 0)) * 2u : OOB;
+          __builtin_amdgcn_raw_ptr_buffer_load_lds(second ? rs1 : rs0, (lds_void_t*)scratch, 4, off, 0, 0, 0);
+        }
+      } else if constexpr (KIND == 3) {
+        const int ty = tap / 3, tx = tap - (tap / 3) * 3;
+#pragma unroll
+        for (int gi = 0; gi < GB; ++gi) {
+          const int iy = piy[gi] + ty, ix = pix[gi] + tx;
+          const bool ok = pbase0[gi] >= 0 && (unsigned)iy < (unsigned)a.Hin && (unsigned)ix < (unsigned)a.Win;
+          const unsigned off =
+              ok ? (unsigned)((pbase0[gi] + iy * a.Win + ix) * s0_ctot + s0_coff + cb * 8) * 2u : OOB;
+          __builtin_amdgcn_raw_ptr_buffer_load_lds(rs0, (lds_void_t*)scratch, 4, off, 0, 0, 0);
+        }
+        cb += 8;
+        while (cb >= a.Cin8) { cb -= a.Cin8; ++tap; }
+      } else {
+        const int S = (ky * a.Win + kx) * s0_ctot + cb * 8;
+#pragma unroll
+        for (int gi = 0; gi < GB; ++gi) {
+          const unsigned off = (tmask[gi] >> tap) & 1u ? (unsigned)(pbase0[gi] + S) * 2u : OOB;
+          __builtin_amdgcn_raw_ptr_buffer_load_lds(rs0, (lds_void_t*)scratch, 4, off, 0, 0, 0);
+        }
+        cb += 8;
+        if (cb == a.Cin8) {
+          cb = 0;
+          ++tap;
+          if (++kx == 3) { kx = 0; ++ky; }
+        }
+      }
+#pragma unroll
+      for (int gi = 0; gi < GA; ++gi) {
+        const unsigned off = wbase[gi] >= 0 ? (unsigned)(wbase[gi] + kcur * DK) * 2u : OOB;
+        __builtin_amdgcn_raw_ptr_buffer_load_lds(rw, (lds_void_t*)scratch, 4, off, 0, 0, 0);
+      }
+      ++kcur;
+    }
+    tap = s_tap; cb = s_cb; ky = s_ky; kx = s_kx; kcur = s_k;
+  }
 
   f32x16 acc[NACC][TM][TN];
 #pragma unroll

@@ -381,6 +381,8 @@ int conv_args(ym_ctx* c, const Op& op, int B, const float* d_in, float in_eps, C
       a.slab_cap = (long)c->slab_bytes;
       a.cnt = reinterpret_cast<int*>(c->d_arena + c->off_cnt) + (size_t)c->lane * kSplitCounters;
       a.cnt_cap = kSplitCounters;
+      static const int pf_max = [] { const char* e = getenv("YM_DMA_PF"); return e ? atoi(e) : 0; }();
+      a.pf = a.M <= pf_max;
       return YM_OK;
 }
 
