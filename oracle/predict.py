@@ -30,6 +30,25 @@ class OracleModel:
         return im, y, dict(saved=saved, feats=feats)
 
     @torch.no_grad()
+    def predict_exact(self, im: torch.Tensor, conf: float = 0.25, iou: float = 0.7, max_det: int = 300) -> List:
+        """The same graph and weights evaluated in float64 (the reference's arithmetic without its
+        fp32 rounding), the same NMS and clip; (n, 6) float64 rows per image.  Measures how far the fp32 reference
+        itself is from the exact answer (tests/matching.py ref_f64_slack)."""
+        import copy
+        if getattr(self, "_net64", None) is None:
+            self._net64 = copy.deepcopy(self.net).double()
+        x = pp.load_tensor_check(im.float().cpu() if im.dtype != torch.float32 else im.cpu()).double()
+        y, _ = self._net64(x)[0]
+        shape = x.shape[2:]
+        out = []
+        nc = 80 if self.task == "segment" else 0
+        for d in pp.non_max_suppression(y, conf, iou, None, False, max_det, nc=nc):
+            d = d.clone()
+            d[:, :4] = pp.scale_boxes(shape, d[:, :4], shape)
+            out.append(d[:, :6])
+        return out
+
+    @torch.no_grad()
     def predict(self, im: torch.Tensor, conf: float = 0.25, iou: float = 0.7, classes: Optional[Sequence] = None,
                 agnostic_nms: bool = False, max_det: int = 300) -> List[Dict]:
         im, y, ex = self.raw(im)

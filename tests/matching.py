@@ -60,13 +60,14 @@ def _exempt(d: np.ndarray, same: np.ndarray, conf: float, iou_thr: float, conf_m
     return ex
 
 
-def match_image(ref: np.ndarray, got: np.ndarray, conf: float, iou_thr: float, tol_xy: float, tol_score: float,
+def match_image(ref: np.ndarray, got: np.ndarray, conf: float, iou_thr: float, tol_xy, tol_score: float,
                 conf_margin: float = 2e-3, iou_margin: float = 1e-3, rep: MatchReport = None,
                 max_det: int = 300) -> MatchReport:
     """When a list is truncated at max_det, detections scoring within conf_margin of the last kept score are
     exempt too (which of several near-equal candidates make the cut is an ulp-level decision).  iou_margin is
-    SURVEY §8(c)'s 1e-3."""
+    SURVEY §8(c)'s 1e-3.  tol_xy: one bound, or one per reference row (in `ref`'s order; ref_f64_slack)."""
     rep = rep or MatchReport()
+    tol_row = np.broadcast_to(np.asarray(tol_xy, np.float64), (len(ref),))
     oref = np.argsort(-ref[:, 4], kind="stable") if len(ref) else np.zeros(0, np.int64)
     ogot = np.argsort(-got[:, 4], kind="stable") if len(got) else np.zeros(0, np.int64)
     ref = ref[oref] if len(ref) else ref.reshape(0, ref.shape[1] if ref.ndim == 2 else 6)
@@ -91,7 +92,7 @@ def match_image(ref: np.ndarray, got: np.ndarray, conf: float, iou_thr: float, t
         for j in cand:
             dxy = float(np.abs(got[j, :4] - ref[i, :4]).max())
             ds = float(abs(got[j, 4] - ref[i, 4]))
-            if dxy <= tol_xy and ds <= tol_score:
+            if dxy <= tol_row[oref[i]] and ds <= tol_score:
                 used[j] = True
                 rep.matched += 1
                 rep.pairs.append((int(oref[i]), int(ogot[j])))
@@ -113,3 +114,21 @@ def match_image(ref: np.ndarray, got: np.ndarray, conf: float, iou_thr: float, t
         for r in rest[~ex_b]:
             rep.failures.append(f"build det {r.tolist()} unmatched")
     return rep
+
+
+def ref_f64_slack(ref: np.ndarray, exact: np.ndarray, tol_xy: float = 1e-3) -> np.ndarray:
+    """Per-row coordinate bound for matching against an fp32 reference `ref` whose own rounding error is known:
+    tol_xy plus that row's distance from the same detection computed in float64 (`exact`: the reference graph run in
+    float64, same NMS; matched by class and IoU >= 0.99; a row with no float64 counterpart keeps tol_xy).  The bar
+    then reads "within tol_xy of the reference, beyond the reference's own fp32 rounding": on yolo11s the fp32 path
+    itself sits up to 8e-4 px from the float64 answer (tools/x3_emulate.py), so two faithful fp32 evaluations of the
+    same graph can differ by more than 1e-3 px on the largest stride-32 boxes."""
+    out = np.full(len(ref), tol_xy, np.float64)
+    if not len(ref) or not len(exact):
+        return out
+    ious = iou_matrix(ref[:, :4], exact[:, :4])
+    for i in range(len(ref)):
+        cand = np.where((exact[:, 5] == ref[i, 5]) & (ious[i] >= 0.99))[0]
+        if len(cand):
+            out[i] = tol_xy + float(np.abs(exact[cand, :4] - ref[i, :4]).max(1).min())
+    return out
