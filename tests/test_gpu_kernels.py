@@ -3,6 +3,8 @@ buffer (read back from the plan's arena), so each variant is judged on its own a
 
 Tolerances (written here): fp32-storage plans (f32, x3) within 2e-6 of the output's max magnitude — the kernels
 accumulate in fp32 with fmaf, the reference in float64; f16 within 2e-3 (one fp16 rounding of the output)."""
+import os
+
 import numpy as np
 import pytest
 import torch
@@ -32,7 +34,12 @@ def test_dwconv_variants_match_float64(scale, B, dtype, mode):
     import os
     sd = synth_weights(scale, "detect", 0)
     if (scale, dtype) not in _models:
-        _models[(scale, dtype)] = YOLO11Model(task="detect", size=scale, device="cuda:0", dtype=dtype, verbose=False)
+        os.environ["YM_FUSE_DW"] = "0"  # x3 plans fuse the depthwise ops into their 1x1 convs by default
+        try:
+            _models[(scale, dtype)] = YOLO11Model(task="detect", size=scale, device="cuda:0", dtype=dtype,
+                                                  verbose=False)
+        finally:
+            del os.environ["YM_FUSE_DW"]
     eng = _models[(scale, dtype)].model.engine
     x = synthetic_batch(B, 640, 77, DEV)
     os.environ["YM_DW_MODE"] = mode
@@ -58,6 +65,48 @@ def test_dwconv_variants_match_float64(scale, B, dtype, mode):
         assert err < TOL[dtype], (op.name, err)
         n += 1
     assert n == 6
+
+
+@pytest.mark.parametrize("cfg", [-1, 0, 1, 2])
+@pytest.mark.parametrize("scale,B", [("s", 8), ("n", 2)])
+def test_fused_depthwise_1x1_matches_float64(scale, B, cfg):
+    """csrc/ym_conv_dwpw.hip (x3 plans: every Detect-head DWConv fused into the 1x1 conv it feeds) in each
+    configuration (-1: the heuristic; 0/1/2: 1, 2 or 4 waves splitting K), eager forwards: the stored 1x1 output =
+    SiLU(b + W · SiLU(b_dw + Σ_taps w_dw·x)) of the stored depthwise input, against float64 with the same fp32
+    weights, within 2e-6 of the output's max magnitude (the x3 GEMM's split products miss only lo·lo, ~2^-22)."""
+    from core.model import YOLO11Model
+    from yolomi.plan import _conv_weights
+    sd = synth_weights(scale, "detect", 0)
+    if (scale, "x3dw") not in _models:
+        _models[(scale, "x3dw")] = YOLO11Model(task="detect", size=scale, device="cuda:0", dtype="x3", verbose=False)
+    eng = _models[(scale, "x3dw")].model.engine
+    x = synthetic_batch(B, 640, 78, DEV)
+    eng.run(x, use_graph=False)  # tables for this shape
+    try:
+        eng.rt.set_op_cfg(B, 640, 640, [cfg if op.args.get("dw") else -1 for op in eng.graph.ops])
+        eng.run(x, use_graph=False)
+        n = 0
+        for op in eng.graph.ops:
+            a = op.args
+            if not a.get("dw"):
+                continue
+            C, N = a["c1"], a["c2"]
+            src = eng.read_buffer(a["src0"].buf.id, B)[..., a["src0"].coff:a["src0"].coff + C].double()
+            got = eng.read_buffer(a["dst"].buf.id, B)[..., a["dst"].coff:a["dst"].coff + N].double()
+            w9, bd = _dw_weights(a["dw"]["wkey"], sd)
+            wd = torch.from_numpy(np.ascontiguousarray(w9.T)).double().reshape(C, 1, 3, 3)
+            h = F.silu(F.conv2d(src.permute(0, 3, 1, 2), wd, torch.from_numpy(bd).double(), padding=1, groups=C))
+            w, b = _conv_weights(a, sd)  # (N, 1, 1, C)
+            ref = F.conv2d(h, torch.from_numpy(w).double().permute(0, 3, 1, 2), torch.from_numpy(b).double())
+            if a["act"]:
+                ref = F.silu(ref)
+            ref = ref.permute(0, 2, 3, 1)
+            err = (got - ref).abs().max().item() / ref.abs().max().item()
+            assert err < 2e-6, (op.name, cfg, err)
+            n += 1
+        assert n == 6
+    finally:
+        eng._tuned.discard((B, 640, 640))
 
 
 def test_predict_rows_are_per_call():

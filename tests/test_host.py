@@ -140,7 +140,7 @@ def test_x3_fused_pairs_pack_w2(scale):
     g = GraphBuilder(scale, "detect", fuse="x3")
     pairs = [op for op in g.ops if op.args.get("pair")]
     assert pairs and any(op.args["pair"]["k"] == 3 for op in pairs) and any(op.args["pair"]["k"] == 1 for op in pairs)
-    assert any(op.name.startswith("model.23.cv3.0.1.1") for op in pairs)
+    assert any(op.name == "model.1+cv1" for op in pairs)
     blob = pack_model(scale, "detect", sd, "x3")
     h = struct.unpack("<32i", blob[:128])
     nb, nop = h[11], h[12]
@@ -161,6 +161,40 @@ def test_x3_fused_pairs_pack_w2(scale):
         rebuilt = (pr[:, :, 0] + pr[:, :, 1]).reshape(N2, K2) * 2.0 ** -r[23]
         rel = np.abs(rebuilt - ref) / np.maximum(np.abs(ref), 2 ** -17 * np.abs(ref).max())
         assert rel.max() < 2 ** -21, op.name
+
+@pytest.mark.parametrize("scale", ["n", "s"])
+def test_x3_fused_depthwise_pack(scale, monkeypatch):
+    """x3 plans merge every Detect-head DWConv into the 1x1 conv that consumes it (GraphBuilder.fuse_dw): no
+    depthwise op is left, the fused conv reads the depthwise INPUT, keeps the 1x1's weights and carries the depthwise
+    [9][C] weights ‖ bias at record slot 24 (1 + offset); YM_FUSE_DW=0 keeps the six depthwise launches."""
+    from yolomi.plan import _dw_weights
+    sd = synth_weights(scale, "detect", 0)
+    g0 = GraphBuilder(scale, "detect", fuse=False)
+    g = GraphBuilder(scale, "detect", fuse="x3")
+    assert not [op for op in g.ops if op.kind == "dwconv"]
+    fused = [op for op in g.ops if op.args.get("dw")]
+    assert len(fused) == 6 == len([op for op in g0.ops if op.kind == "dwconv"])
+    assert g.macs_per_image() == g0.macs_per_image()
+    dws = {op.name: op for op in g0.ops if op.kind == "dwconv"}
+    for op in fused:
+        d = dws[op.name.split("+")[0]]
+        assert op.args["src0"].buf.name == d.args["src"].buf.name and op.args["c1"] == d.args["C"]
+        assert op.args["k"] == 1 and not op.args.get("pair")
+    blob = pack_model(scale, "detect", sd, "x3")
+    h = struct.unpack("<32i", blob[:128])
+    nb, nop = h[11], h[12]
+    base = (128 + 32 * nb + 176 * nop + 255) // 256 * 256
+    for i, op in enumerate(g.ops):
+        r = struct.unpack("<32i", blob[128 + 32 * nb + 128 * i: 128 + 32 * nb + 128 * (i + 1)])
+        assert (r[24] > 0) == bool(op.args.get("dw")), op.name
+        if r[24] > 0:
+            C = op.args["c1"]
+            w9, b = _dw_weights(op.args["dw"]["wkey"], sd)
+            got = np.frombuffer(blob, np.float32, 10 * C, base + r[24] - 1)
+            assert np.array_equal(got[:9 * C], w9.reshape(-1)) and np.array_equal(got[9 * C:], b.astype(np.float32))
+    monkeypatch.setenv("YM_FUSE_DW", "0")
+    assert len([op for op in GraphBuilder(scale, "detect", fuse="x3").ops if op.kind == "dwconv"]) == 6
+
 
 def test_facade_contract_without_gpu():
     from core.model import YOLO11Model

@@ -59,6 +59,10 @@ int main(int argc, char** argv) {
   a.s0_elems = (long)nin; a.s1_elems = 0;
   a.fd_hw = ym_fdiv(Ho * Wo); a.fd_w = ym_fdiv(Wo);
   a.slab = slab; a.slab_cap = 64 << 20; a.cnt = cnt; a.cnt_cap = 65536;
+  void* zeros;
+  CK(hipMalloc(&zeros, 4096));
+  CK(hipMemset(zeros, 0, 4096));
+  a.zeros = zeros;
   hipStream_t st;
   CK(hipStreamCreate(&st));
   for (int i = 0; i < 5; ++i) CK(ym_launch_conv_dma(0, a, cfg, st));
@@ -86,7 +90,7 @@ int main(int argc, char** argv) {
          "%.2f us/launch (stream, eager)\n", B, H, W, C, N, k, S, x3, cfg, dc.bm, dc.bn, dc.split, dc.kg, dc.ns, dc.sub,
          nk, ms * 1e3 / reps);
   const unsigned long long t0 = hs[0];
-  printf("  prologue (indices + first stages issued): %llu cyc\n", hs[1] - t0);
+  printf("  prologue: index setup %llu cyc, first stages issued %llu cyc\n", hs[4] - t0, hs[1] - hs[4]);
   const int per = nk / dc.split / dc.sub;
   for (int it = 0; it < per && it < 64; ++it) {
     const unsigned long long* q = &hs[8 + 4 * it];
@@ -94,7 +98,8 @@ int main(int argc, char** argv) {
     printf("  stage %3d at %6llu: wait %5lld  barrier %5lld  issue %5lld  compute %5lld\n", it, q[0] - t0,
            (long long)(q[0] - prev), (long long)(q[1] - q[0]), (long long)(q[2] - q[1]), (long long)(q[3] - q[2]));
   }
-  printf("  loop end %llu, epilogue end %llu (epilogue %lld cyc)\n", hs[2] - t0, hs[3] - t0,
-         (long long)(hs[3] - hs[2]));
+  printf("  loop end %llu, epilogue end %llu (epilogue %lld cyc: wave-group reduction %lld, split-K hand-off %lld, "
+         "bias / act / stores %lld)\n", hs[2] - t0, hs[3] - t0, (long long)(hs[3] - hs[2]), (long long)(hs[5] - hs[2]),
+         (long long)(hs[6] - hs[5]), (long long)(hs[3] - hs[6]));
   return 0;
 }

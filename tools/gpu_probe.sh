@@ -17,4 +17,6 @@ run PROBE_X3=1 $P 8 20 20 256 256 1 12
 run PROBE_X3=0 $P 8 20 20 256 256 1 12
 # 3x3 256->256 at 40x40 s2 from 80x80 (model.5 is 128->256 s2: 80->40)
 run PROBE_X3=1 $P 8 80 80 128 256 3 15 2
+# cold-read layouts of the input max (csrc/ym_misc.hip input_stats)
+echo "== read_probe" >> $o; timeout -k 5 60 tools/probe_bin/read_probe >> $o 2>&1 || { echo "rc=$?" >> $o; exit 1; }
 echo done >> $o

@@ -164,6 +164,20 @@ __device__ __forceinline__ void ym_p2_store4_pair(P2* p, const float* v, bool od
     *reinterpret_cast<f16x8*>((u & ~(uintptr_t)31) + (odd ? 16 : 0)) = o;
   }
 }
+// v_permlane32_swap on a whole 8 x fp16 fragment: lanes 32-63 of a trade places with lanes 0-31 of b, so
+// a = [a.lower | b.lower], b = [a.upper | b.upper] (per lane half; cdna_hip_programming.md T21 semantics).
+__device__ __forceinline__ void ym_swap32(f16x8& a, f16x8& b) {
+  typedef unsigned u32x4_t __attribute__((ext_vector_type(4)));
+  u32x4_t x = __builtin_bit_cast(u32x4_t, a), y = __builtin_bit_cast(u32x4_t, b);
+#pragma unroll
+  for (int k = 0; k < 4; ++k) {
+    const auto r = __builtin_amdgcn_permlane32_swap(x[k], y[k], false, false);
+    x[k] = r[0];
+    y[k] = r[1];
+  }
+  a = __builtin_bit_cast(f16x8, x);
+  b = __builtin_bit_cast(f16x8, y);
+}
 __device__ __forceinline__ void ym_p2_load4(const P2* p, float* v) {  // v[e] = hi + lo
   const f16* q = ym_p2_hi4(p);
   const f16x4 h = *reinterpret_cast<const f16x4*>(q), l = *reinterpret_cast<const f16x4*>(q + 8);
@@ -324,7 +338,39 @@ struct ConvArgs {
   // LDS-DMA kernels (csrc/ym_conv_dma.hip): request every line of the workgroup's K range into L2 before the ring
   // starts (latency-bound small-M layers; YM_DMA_PF = the largest M it is used for, 0 = never)
   int pf;
+  // 256+ zero bytes of device memory: the residual source of a conv without one, so the epilogue-operand loads are
+  // unconditional (a load under a per-lane or per-kernel condition made the compiler wait for it on the spot)
+  const void* zeros;
+  // fused depthwise (yolomi/arch.py GraphBuilder.fuse_dw; csrc/ym_conv_dwpw.hip): src0 is the DEPTHWISE input and this
+  // 1x1 conv consumes act(dw3x3(src0) + dw_b) computed in registers.  dw_w [9][C0] fp32, dw_b [C0]; null: no depthwise
+  const float* dw_w; const float* dw_b; int dw_act;
 };
+
+// Warm the scalar cache with every line of a kernel's argument block in ONE round trip: the compiler loads kernel
+// arguments lazily at first use, and each batch of s_loads ends in an lgkmcnt(0) wait for a line that is not yet in
+// the scalar cache (the argument block is freshly written per launch: a memory round trip each).  A ConvArgs-sized
+// block took ~6 such waits, ~3k cycles before the first DMA issue (tools/dma_probe.hip); after this the lazy loads
+// hit the cache.
+template <int BYTES>
+__device__ __forceinline__ void ym_warm_kernargs() {
+  const __attribute__((address_space(4))) char* kp =
+      (const __attribute__((address_space(4))) char*)__builtin_amdgcn_kernarg_segment_ptr();
+  static_assert(BYTES <= 16 * 64, "argument block too large");
+  int v[16];
+#pragma unroll
+  for (int i = 0; i < 16; ++i)
+    if (i * 64 < BYTES) v[i] = *(const __attribute__((address_space(4))) int*)(kp + i * 64);
+#pragma unroll
+  for (int i = 0; i < 16; ++i)
+    if (i * 64 < BYTES) asm volatile("" ::"s"(v[i]));
+}
+
+// A load through the global address space (global_load, vmcnt only; a generic pointer makes the compiler emit a
+// flat load, which also counts in lgkmcnt and so is waited for together with the scalar/LDS traffic).
+template <typename T>
+__device__ __forceinline__ T ym_gld(const void* p) {
+  return *(const __attribute__((address_space(1))) T*)(p);
+}
 
 // x3 epilogue pre-activation: the weight scale (exact: a power of two) and the bias in one rounding
 __device__ __forceinline__ float ym_x3_pre(float acc, float wsc, float bias) { return fmaf(acc, wsc, bias); }
@@ -435,6 +481,8 @@ int ym_conv_bneck_x3_num_cfgs();  // x3-only Bottleneck variants (launch indices
 hipError_t ym_launch_conv_stream(int out_f32, const ConvArgs& a, int i, hipStream_t st);  // f16 1x1 only
 int ym_conv_stream_num_cfgs();
 hipError_t ym_launch_conv_halo(int out_f32, const ConvArgs& a, int i, hipStream_t st);  // f16 3x3 halo tiles
+hipError_t ym_launch_conv_dwpw(int dtype, int out_f32, const ConvArgs& a, int cfg, hipStream_t st, bool strict);
+int ym_conv_dwpw_num_cfgs();  // fused depthwise → 1x1 (ConvArgs::dw_w): its own cfg id space 0 .. n-1
 int ym_conv_halo_num_cfgs();
 hipError_t ym_launch_masks(const MaskArgs& a, hipStream_t st);
 bool ym_masks_fused(const MaskArgs& a);  // the one-launch path (no (total, MH, MW) scratch)  // Segment: process_mask(upsample=True)

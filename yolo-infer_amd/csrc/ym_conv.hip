@@ -713,6 +713,8 @@ int ym_conv_num_cfgs_dt(int dtype) {
 }
 
 hipError_t ym_launch_conv(int dtype, int out_f32, const ConvArgs& a, int cfg, hipStream_t st, bool strict) {
+  // a depthwise-fused 1x1 (csrc/ym_conv_dwpw.hip) runs on its own kernel only: no other family computes the depthwise
+  if (a.dw_w) return ym_launch_conv_dwpw(dtype, out_f32, a, cfg, st, strict);
   int kind;
   if (a.nchw) kind = (a.k == 3 && a.Cin8 == 1) ? 0 : -1;
   else if (a.k == 1 && a.s == 1) kind = 1;

@@ -24,6 +24,7 @@ namespace {
 // writes the slots and resets the ticket.  No per-forward init kernel, no same-address atomicMax storm.
 // batch_max non-null (multi-GPU shard): the slots take the given global max, x is not read.
 constexpr int kStatsBlocks = 1024;  // partial slots (ym_runtime.cpp reserves them behind the ctl slots)
+constexpr int kStatsU = 10;         // float4 loads in flight per lane and round
 __global__ __launch_bounds__(256) void input_stats(const float* __restrict__ x, long n, float* ctl, int* counts, int B,
                                                    int* cnt, int cnt_len, const float* batch_max) {
   const int tid = threadIdx.x;
@@ -38,23 +39,23 @@ __global__ __launch_bounds__(256) void input_stats(const float* __restrict__ x, 
   }
   int* part = slots + YM_CTL_SLOTS * YM_CTL_STRIDE + 64;  // [kStatsBlocks], after the ticket's 256-byte line
   int* ticket = slots + YM_CTL_SLOTS * YM_CTL_STRIDE;
-  // contiguous chunk of whole float4s per block, eight 16-byte loads in flight per lane
+  // contiguous chunk of whole float4s per block; every round issues kStatsU 16-byte loads per lane at once, the
+  // indices past the chunk clamped onto its last float4 (a duplicate cannot change a max), so there is no
+  // predicated or remainder load: at B = 8, 640² (2400 float4 per block) the whole chunk is ONE round trip
   const long n4 = n >> 2;
   const long per = (n4 + gridDim.x - 1) / gridDim.x;
   const long lo = blockIdx.x * per, hi = lo + per < n4 ? lo + per : n4;
   const f32x4* x4 = reinterpret_cast<const f32x4*>(x);
   float m = -INFINITY;
-  long i = lo + tid;
-  for (; i + 7 * 256 < hi; i += 8 * 256) {
-    f32x4 v[8];
+  for (long i = lo + tid; lo < hi && i - tid < hi; i += kStatsU * 256) {
+    f32x4 v[kStatsU];
 #pragma unroll
-    for (int u = 0; u < 8; ++u) v[u] = x4[i + u * 256];
+    for (int u = 0; u < kStatsU; ++u) {
+      const long j = i + u * 256;
+      v[u] = x4[j < hi ? j : hi - 1];  // (plain loads: the stem reads the batch next)
+    }
 #pragma unroll
-    for (int u = 0; u < 8; ++u) m = fmaxf(m, fmaxf(fmaxf(v[u][0], v[u][1]), fmaxf(v[u][2], v[u][3])));
-  }
-  for (; i < hi; i += 256) {
-    const f32x4 v = x4[i];
-    m = fmaxf(m, fmaxf(fmaxf(v[0], v[1]), fmaxf(v[2], v[3])));
+    for (int u = 0; u < kStatsU; ++u) m = fmaxf(m, fmaxf(fmaxf(v[u][0], v[u][1]), fmaxf(v[u][2], v[u][3])));
   }
   if (blockIdx.x == 0)
     for (long j = (n4 << 2) + tid; j < n; j += 256) m = fmaxf(m, x[j]);

@@ -351,6 +351,13 @@ int conv_args(ym_ctx* c, const Op& op, int B, const float* d_in, float in_eps, C
           return fail(YM_EBLOB, "op %s: bad fused-pair geometry", op.name);
         if (ym_conv_num_cfgs_dt(c->dtype) > 127) return fail(YM_EBLOB, "split cfg encoding needs < 128 conv configs");
       }
+      if (r[24] > 0 && !ym_dt_q8(c->dtype)) {  // fused depthwise (yolomi/arch.py fuse_dw): 1 + offset of [9][C] ‖ [C]
+        if ((c->dtype != YM_DT_F16 && c->dtype != YM_DT_X3) || k != 1 || s != 1 || b1 >= 0 || up0 || r[30])
+          return fail(YM_EBLOB, "op %s: a fused depthwise needs a single-source 1x1 conv of an f16 / x3 plan", op.name);
+        a.dw_w = reinterpret_cast<const float*>(c->d_weights + (size_t)(uint32_t)(r[24] - 1));
+        a.dw_b = a.dw_w + 9 * (size_t)cin;
+        a.dw_act = 1;
+      }
       a.shuffle = r[16];
       a.npr = a.shuffle ? cout / 4 : cout;
       a.dst = c->bptr(bd); a.d_ctot = c->bufs[bd].C; a.d_coff = r[14]; a.d_P = c->buf_P(bd);
@@ -383,6 +390,7 @@ int conv_args(ym_ctx* c, const Op& op, int B, const float* d_in, float in_eps, C
       a.cnt_cap = kSplitCounters;
       static const int pf_max = [] { const char* e = getenv("YM_DMA_PF"); return e ? atoi(e) : 0; }();
       a.pf = a.M <= pf_max;
+      a.zeros = c->d_misc + 12288;  // zeroed at ym_create, never written
       return YM_OK;
 }
 
@@ -594,7 +602,8 @@ int ym_create(int device, const ym_model_desc* desc, ym_ctx** out) {
   hipError_t e = hipStreamCreateWithFlags(&c->cap_stream, hipStreamNonBlocking);
   for (int l = 1; l < kMaxLanes && e == hipSuccess; ++l) e = hipStreamCreateWithFlags(&c->lane_streams[l], hipStreamNonBlocking);
   if (e == hipSuccess) e = hipEventCreateWithFlags(&c->fork_ev, hipEventDisableTiming);
-  // ym_input_max's ctl region (slots, ticket, partials: YM_CTL_BYTES) at 0, broadcast control words at 8 KB
+  // ym_input_max's ctl region (slots, ticket, partials: YM_CTL_BYTES) at 0, broadcast control words at 8 KB, a zero
+  // page at 12 KB (ConvArgs::zeros)
   if (e == hipSuccess) e = hipMalloc(&c->d_misc, 16384);
   if (e == hipSuccess) e = hipMemset(c->d_misc, 0, 16384);
   for (int l = 1; l < kMaxLanes && e == hipSuccess; ++l) e = hipEventCreateWithFlags(&c->join_ev[l], hipEventDisableTiming);
@@ -728,6 +737,7 @@ static int validate_plan(const std::vector<BufDesc>& bufs, const std::vector<Op>
              view_ok(r[17], r[18], Nout, true) && (r[6] != input_buf || (r[7] == 0 && r[10] == -1)) &&
              w_ok(r[19], (size_t)N * Kpad * esz) && w_ok(r[20], (size_t)N * 4);
         if (ok && ym_dt_q8(dtype)) ok = w_ok(r[22], qrec) && w_ok(r[23], (size_t)N * 4) && w_ok(r[24], (size_t)N * 4);
+        else if (ok && r[24] > 0) ok = w_ok(r[24] - 1, (size_t)10 * r[3] * 4);  // fused depthwise weights + bias
         if (ok && fused) {
           const int N2 = r[27], K2 = r[29];
           ok = N2 > 0 && K2 > 0 && K2 <= (1 << 16) && buf_ok(r[31], false) && w_ok(r[25], (size_t)N2 * K2 * 2) &&

@@ -108,6 +108,9 @@ class GraphBuilder:
         if fuse is True or fuse == "x3":
             if quant:
                 raise ValueError("fused conv pairs are f16-only (int8 plans requantise every conv output)")
+            import os
+            if self.x3 and os.environ.get("YM_FUSE_DW", "1") != "0":
+                self.fuse_dw()
             self.fuse_pairs()
 
     # ------------------------------------------------------------------ helpers
@@ -396,6 +399,41 @@ class GraphBuilder:
             i += 1
         self.ops = out
 
+    DW_MAX_C, DW_MAX_N = 512, 128  # csrc/ym_conv_dwpw.hip kDwpwMaxC, 16 * kDwpwNB
+
+    def fuse_dw(self):
+        """Merge each depthwise op D into the 1x1 conv B that immediately follows it and is the only reader of D's
+        whole output (the Detect head's cv3.l.0 / cv3.l.1 pairs): B reads D's input and computes act(dw3x3 + bias)
+        in registers as its B operand (csrc/ym_conv_dwpw.hip); D's output buffer is never written.  The depthwise
+        arithmetic is the unfused op's (same fmaf order, same x3 split), so the 1x1 sees the same operands."""
+        out: List[Op] = []
+        i = 0
+        while i < len(self.ops):
+            op = self.ops[i]
+            nxt = self.ops[i + 1] if i + 1 < len(self.ops) else None
+            if op.kind == "dwconv" and nxt is not None and self._dw_fusable(op, nxt):
+                d = op.args
+                args = dict(nxt.args)
+                args.update(src0=d["src"], dw=dict(wkey=d["wkey"], act=d["act"], C=d["C"]))
+                out.append(Op("conv", args, f"{op.name}+{nxt.name.rsplit('.', 1)[-1]}"))
+                i += 2
+                continue
+            out.append(op)
+            i += 1
+        self.ops = out
+
+    def _dw_fusable(self, D: Op, B: Op) -> bool:
+        d = D.args
+        if B.kind != "conv" or not d["act"]:
+            return False
+        b = B.args
+        mid = d["dst"]
+        return (b["k"] == 1 and b["s"] == 1 and b["src1"] is None and not b["up0"] and not b["shuffle2x2"]
+                and not b.get("convT") and b["res"] is None and b["anchor_level"] < 0 and not b.get("pair")
+                and b["src0"].buf is mid.buf and mid.coff == 0 and mid.C == mid.buf.C and b["src0"].C == mid.C
+                and self._readers(mid.buf) == 1 and d["C"] % 8 == 0 and d["C"] <= self.DW_MAX_C
+                and b["c2"] % 4 == 0 and b["c2"] <= self.DW_MAX_N)
+
     # csrc/ym_conv_bneck.hip: the (C, C_mid, C_out) Bottleneck shapes with a fused kernel
     BNECK_SHAPES = {(16, 8, 16), (32, 16, 32), (64, 32, 64), (32, 32, 32), (64, 64, 64)}
 
@@ -404,6 +442,8 @@ class GraphBuilder:
             return False
         a, b = A.args, B.args
         if a.get("pair") or a.get("convT") or a["shuffle2x2"] or a["res"] is not None or a["anchor_level"] >= 0:
+            return False
+        if a.get("dw") or b.get("dw"):  # a depthwise-fused 1x1 runs on its own kernel (csrc/ym_conv_dwpw.hip)
             return False
         if b["k"] == 3:  # a Bottleneck (3x3 -> 3x3 + shortcut) on the fused kernel of csrc/ym_conv_bneck.hip
             mid = a["dst"]
@@ -455,6 +495,9 @@ class GraphBuilder:
                     f1 = a["src1"].buf.f
                     by += B * (H // f1) * (W // f1) * a["src1"].C * act_bytes
                 by += a["k"] * a["k"] * cin * a["c2"] * act_bytes + a["c2"] * 4
+                if a.get("dw"):  # the fused depthwise: its taps, weights and bias (its output never reaches HBM)
+                    fl += 2 * npx * 9 * a["c1"]
+                    by += 10 * a["c1"] * 4
                 c_out = a["c2"]
                 if a.get("pair"):  # + the second conv; its input (this conv's output) never reaches HBM
                     c_out, k2 = a["pair"]["c2"], a["pair"]["k"]
@@ -500,6 +543,8 @@ class GraphBuilder:
                 fo = self.out_factor(op)
                 npx = (H // fo) * (W // fo)
                 tot += npx * a["k"] * a["k"] * (a["c1"] if op.name != "model.0" else 3) * a["c2"]
+                if a.get("dw"):
+                    tot += npx * 9 * a["c1"]
                 if a.get("pair"):
                     tot += npx * a["pair"]["k"] ** 2 * a["c2"] * a["pair"]["c2"]
             elif op.kind == "dwconv":

@@ -22,7 +22,8 @@ Blob layout (int32 little-endian; parsed by `csrc/ym_runtime.cpp:ym_load_weights
   header[32] | buffers[nbuf][8] | ops[nop][32] | names[nop][48 bytes] | pad to 256 | weights
 Conv op record: [1..5] k, s, Cin, N, act | [6..9] src0 buf, coff, C, up0 | [10..12] src1 | [13..16] dst buf, coff,
 anchor level, pixel shuffle | [17..18] residual | [19..21] weight / bias offsets, Kpad | [22..24] int8 QRec, s_in·s_w,
-int32 bias | [25..31] fused successor conv (f16 plans, GraphBuilder.fuse_pairs): W2 / bias2 offsets, N2, act2, Kpad2,
+int32 bias (f16 / x3 plans: r[24] = 1 + offset of a fused depthwise's [9][C] weights ‖ [C] bias, GraphBuilder.fuse_dw;
+0: none) | [25..31] fused successor conv (f16 plans, GraphBuilder.fuse_pairs): W2 / bias2 offsets, N2, act2, Kpad2,
 its kernel size k2 (1: streaming FUSE; 3: Bottleneck kernel), intermediate buffer (used when the tuner runs the pair as
 two launches).
 """
@@ -236,6 +237,12 @@ def pack_graph(g: GraphBuilder, sd: Dict[str, np.ndarray], dtype: str = "f16", q
             r[19] = arena.add(wp if quant or wp.dtype == np.float16 else wp.astype(np_dt))  # (x3 stem: fp32)
             r[20] = arena.add(b.astype(np.float32))
             r[21] = Kpad
+            if a.get("dw") is not None:  # fused depthwise (GraphBuilder.fuse_dw): r[24] = 1 + offset of [9][C] ‖ bias [C]
+                if dtype not in ("f16", "x3"):
+                    raise ValueError(f"op {op.name}: fused depthwise convs are f16 / x3 only")
+                w9, bdw = _dw_weights(a["dw"]["wkey"], sd)
+                assert w9.shape == (9, C0)
+                r[24] = 1 + arena.add(np.concatenate([w9.reshape(-1), np.asarray(bdw, np.float32)]).astype(np.float32))
             pair = a.get("pair")
             if pair is not None:  # fused successor (GraphBuilder.fuse_pairs): W2 [N2][Kpad2], K = (ky, kx, this conv's N)
                 if dtype not in ("f16", "x3"):
