@@ -39,11 +39,18 @@ def oracle(scale="n", task="detect"):
     return _cache[k]
 
 
-def model(scale="n", task="detect"):
+def model(scale="n", task="detect", fuse_dw=True):
+    """fuse_dw=False: the plan with the Detect-head depthwise convs as their own ops (YM_FUSE_DW=0), whose cv3
+    1x1 → 1x1 pairs then run on the streaming kernel's x3 FUSE mode."""
     from core.model import YOLO11Model
-    k = ("m", scale, task)
+    k = ("m", scale, task, fuse_dw)
     if k not in _cache:
-        _cache[k] = YOLO11Model(task=task, size=scale, device="cuda:0", dtype="x3", verbose=False)
+        if not fuse_dw:
+            os.environ["YM_FUSE_DW"] = "0"
+        try:
+            _cache[k] = YOLO11Model(task=task, size=scale, device="cuda:0", dtype="x3", verbose=False)
+        finally:
+            os.environ.pop("YM_FUSE_DW", None)
     return _cache[k]
 
 
@@ -191,8 +198,9 @@ def test_x3_fused_pairs_match_split(scale):
         three 16x16x16 MFMAs per K block of the second GEMM) on every streaming configuration;
       * Bottlenecks (csrc/ym_conv_bneck.hip in the x3 mode: hi / lo LDS planes, three MFMAs per K step) on every
         tile variant, the x3-only 2 x 32 tiles included (the ones whose doubled LDS does not fit fall back to the
-        split pair)."""
-    eng = model(scale).model.engine
+        split pair).
+    (On the plan without the depthwise fusion: with it the head's cv3 1x1s are depthwise-fused, not paired.)"""
+    eng = model(scale, fuse_dw=False).model.engine
     x = make_input("uniform", (21, 22), 640).to(DEV)
     B, _, H, W = x.shape
     ops = eng.graph.ops

@@ -27,26 +27,13 @@ typedef float f32x16 __attribute__((ext_vector_type(16)));
 typedef __attribute__((address_space(3))) void lds_void_t;
 typedef unsigned u32x4 __attribute__((ext_vector_type(4)));
 
-#ifdef YM_DMA_STAMPS  // tools/dma_probe.hip: cycle stamps of workgroup 0, wave 0 (never built into the library).
-// Kept in LDS (ds_write: no vmcnt wait, so the probe does not drain the wave's in-flight DMA) and copied to
-// ym_dma_stamps by YM_STAMP_FLUSH at the end.
+#ifdef YM_DMA_STAMPS  // tools/dma_probe.hip: cycle stamps of workgroup 0, wave 0 (never built into the library)
 __device__ unsigned long long* ym_dma_stamps;
 #define YM_STAMP(i)                                                                          \
   do {                                                                                       \
-    if (blockIdx.x == 0 && threadIdx.x == 0) ym_stamp_lds[(i)] = __builtin_readcyclecounter(); \
-  } while (0)
-#define YM_STAMP_DECL __shared__ unsigned long long ym_stamp_lds[264];
-#define YM_STAMP_FLUSH(i)                                                            \
-  do {                                                                               \
-    YM_STAMP(i);                                                                     \
-    if (blockIdx.x == 0 && threadIdx.x == 0)                                         \
-      for (int q_ = 0; q_ < 264; ++q_) ym_dma_stamps[q_] = ym_stamp_lds[q_];         \
+    if (blockIdx.x == 0 && threadIdx.x == 0) ym_dma_stamps[(i)] = __builtin_readcyclecounter(); \
   } while (0)
 #else
-#define YM_STAMP_DECL
-#define YM_STAMP_FLUSH(i) \
-  do {                    \
-  } while (0)
 #define YM_STAMP(i) \
   do {              \
   } while (0)
@@ -117,12 +104,10 @@ __global__ __launch_bounds__(256 * KG) void conv_dma(const ConvArgs a) {
   constexpr int SPW = 4 / KG;                        // 16-deep k sub-steps per wave per stage
   constexpr int NACC = TM * TN == 1 && SPW >= 2 ? 2 : 1;  // one 32x32 block per wave: alternate two accumulators
   __shared__ __attribute__((aligned(16))) char smem[NSTAGE * SB + 16 + 256];  // + split-K flag, L2 warm-up scratch
-  YM_STAMP_DECL
 
   YM_STAMP(0);
-  ym_warm_kernargs<sizeof(ConvArgs)>();
   const int tid = threadIdx.x, lane = tid & 63, wid = tid >> 6;
-  const int kg = __builtin_amdgcn_readfirstlane(wid >> 2), wq = wid & 3;  // (wave-uniform: scalar branches on kg)
+  const int kg = wid >> 2, wq = wid & 3;
   const int wm = wq & 1, wn = wq >> 1;
   const int l32 = lane & 31, h = lane >> 5;
   // tile map: every N tile and every K split of pixel tile tm share bid % 8 = one XCD (its L2 holds the pixels and
@@ -138,32 +123,24 @@ __global__ __launch_bounds__(256 * KG) void conv_dma(const ConvArgs a) {
 
   // ---- epilogue operands first (bias, residual; wave group 0 runs the epilogue): their latency hides behind the
   // K loop.  They are older than every DMA, so the counted vmcnt waits below stay exact (loads retire in order).
-  // Every load is unconditional (an out-of-range lane reads a clamped valid address, a conv without residual reads
-  // the zero page) and its registers are not touched before the epilogue: a conditional load, or arithmetic on the
-  // loaded value here, made the compiler wait for each load in turn (tools/dma_probe.hip: ~3k of the prologue's
-  // cycles were four serial bias-load round trips).
   int ep_m[TM];
   size_t ep_obase[TM];
   f32x4 bias4[TN][4];
-  struct RV {  // residual of 4 channels as loaded (x3: hi and lo halves, summed at use), zero without residual
-    f16x4 hi, lo;
-    __device__ __forceinline__ float at(int e) const { return X3 ? (float)hi[e] + (float)lo[e] : (float)hi[e]; }
-  };
+  typedef typename std::conditional<X3, f32x4, f16x4>::type RV;  // residual (x3: hi + lo)
   RV res4[TM][TN][4];
+  const f16* res = static_cast<const f16*>(a.res);
+  const P2* resp = static_cast<const P2*>(a.res);
   constexpr int XS = X3 ? 2 : 1;  // fp16 storage elements per logical channel
   const int s0_ctot = XS * a.s0_ctot, s0_coff = XS * a.s0_coff, s1_ctot = XS * a.s1_ctot, s1_coff = XS * a.s1_coff;
   const int C0s = XS * a.C0;
-  {  // (every wave, although only wave group 0 runs the epilogue: under `kg == 0` the merge after the block copied
-     // the loaded registers, which waited for the loads)
+  if (kg == 0) {
 #pragma unroll
     for (int j = 0; j < TN; ++j)
 #pragma unroll
       for (int q = 0; q < 4; ++q) {
         const int n = tn * BN + wn * (BN / 2) + 32 * j + 8 * q + 4 * h;
-        bias4[j][q] = ym_gld<f32x4>(a.bias + (n < a.N ? n : 0));
+        bias4[j][q] = n < a.N ? *reinterpret_cast<const f32x4*>(a.bias + n) : f32x4{0.f, 0.f, 0.f, 0.f};
       }
-    const bool has_res = a.res != nullptr;
-    const f16* rsrc = static_cast<const f16*>(has_res ? a.res : a.zeros);
 #pragma unroll
     for (int i = 0; i < TM; ++i) {
       const int m = tm * BM + wm * (BM / 2) + 32 * i + l32;
@@ -173,21 +150,19 @@ __global__ __launch_bounds__(256 * KG) void conv_dma(const ConvArgs a) {
       const int oy = ym_div(rem, a.fd_w), ox = rem - oy * a.Wo;
       const int pix = a.shuffle ? (2 * oy) * a.d_W + 2 * ox : oy * a.d_W + ox;
       ep_obase[i] = (size_t)(b * a.d_P + a.d_pixoff + pix) * a.d_ctot + a.d_coff;
-      const size_t rbase = (size_t)(b * a.r_P + oy * a.Wo + ox) * a.r_ctot + a.r_coff;
+      const size_t rbase = res ? (size_t)(b * a.r_P + oy * a.Wo + ox) * a.r_ctot + a.r_coff : 0;
 #pragma unroll
       for (int j = 0; j < TN; ++j)
 #pragma unroll
         for (int q = 0; q < 4; ++q) {
           const int n = tn * BN + wn * (BN / 2) + 32 * j + 8 * q + 4 * h;
-          // logical element index of the 4 channels (x3: a P2 index; its hi halves at fp16 2 (e & ~7) + (e & 7),
-          // the lo halves 8 further — ym_p2_hi4)
-          const size_t e = has_res ? rbase + (n < a.N ? n : 0) : 0;
           if constexpr (X3) {
-            const f16* hp = rsrc + 2 * (e & ~(size_t)7) + (e & 7);
-            res4[i][j][q].hi = ym_gld<f16x4>(hp);
-            res4[i][j][q].lo = ym_gld<f16x4>(hp + 8);
+            float rv[4] = {0.f, 0.f, 0.f, 0.f};
+            if (res && m < a.M && n < a.N) ym_p2_load4(resp + rbase + n, rv);
+            res4[i][j][q] = f32x4{rv[0], rv[1], rv[2], rv[3]};
           } else {
-            res4[i][j][q].hi = ym_gld<f16x4>(rsrc + e);
+            res4[i][j][q] = (res && m < a.M && n < a.N) ? *reinterpret_cast<const f16x4*>(res + rbase + n)
+                                                         : f16x4{0, 0, 0, 0};
           }
         }
     }
@@ -385,20 +360,12 @@ __global__ __launch_bounds__(256 * KG) void conv_dma(const ConvArgs a) {
 
   const int key = (l32 >> 1) & 7;
   // this wave's k sub-steps of the stage: fragment reads first, then the MFMAs (one LDS latency per stage)
-  // islot >= 0: the next stage's DMA is issued INSIDE the compute, one 64-deep sub-stage after each sub-stage's
-  // first MFMAs, so the issue (bound by the CU's ~64 B/clk request path, ~750 cycles per 48 KB stage) overlaps the
-  // MFMAs instead of preceding them (tools/dma_probe.hip: issue then compute was ~1.8k cycles per x3 stage)
-  auto compute = [&](int slot, int islot) {
+  auto compute = [&](int slot) {
     if constexpr (X3) {
       static_assert(SPW % 2 == 0, "x3: a wave's k sub-steps come in pairs");
-      // per sub-step pair (s, s+1) the NATURAL fragments only (lane half h reads storage chunk 2s + h: hi / lo of
-      // logical chunk s) — two LDS reads per operand instead of three — and the three split-product operands are
-      // made in registers with v_permlane32_swap:
-      //   A_s = [w_hi_s | w_lo_s] · B'_s = [x_lo_s | x_hi_s]         → w_hi_s·x_lo_s + w_lo_s·x_hi_s
-      //   A_s+1 · B'_s+1                                             → the same for s+1
-      //   [w_hi_s | w_hi_s+1] · [x_hi_s | x_hi_s+1]                 → w_hi·x_hi of both chunks
-      // (the LDS reads were the compute phase's bound: tools/dma_probe.hip; same products, another summation order)
-      f16x8 fb[SUB][SPW / 2][2][TM], fa[SUB][SPW / 2][2][TN];
+      // per sub-step pair (s, s+1): A'_s = w_hi_s on both lane halves, B_s natural; the same for s+1; A'' =
+      // [w_lo_s | w_lo_s+1], B'' = [x_hi_s | x_hi_s+1]
+      f16x8 fb[SUB][SPW / 2][3][TM], fa[SUB][SPW / 2][3][TN];
 #pragma unroll
       for (int su = 0; su < SUB; ++su) {
         const char* sb = smem + slot * SB + su * SBS;
@@ -406,49 +373,31 @@ __global__ __launch_bounds__(256 * KG) void conv_dma(const ConvArgs a) {
 #pragma unroll
         for (int u = 0; u < SPW / 2; ++u) {
           const int s = kg * SPW + 2 * u;
+          const int ca[3] = {2 * s, 2 * s + 2, 2 * (s + h) + 1}, cbx[3] = {2 * s + h, 2 * s + 2 + h, 2 * (s + h)};
 #pragma unroll
-          for (int v = 0; v < 2; ++v) {
-            const int off = (((2 * (s + v) + h) ^ key) << 4) + l32 * 128;
+          for (int v = 0; v < 3; ++v) {
+            const int offa = ((ca[v] ^ key) << 4) + l32 * 128, offb = ((cbx[v] ^ key) << 4) + l32 * 128;
 #pragma unroll
             for (int i = 0; i < TM; ++i)
-              fb[su][u][v][i] = *reinterpret_cast<const f16x8*>(sb + (wm * (BM / 2) + 32 * i) * 128 + off);
+              fb[su][u][v][i] = *reinterpret_cast<const f16x8*>(sb + (wm * (BM / 2) + 32 * i) * 128 + offb);
 #pragma unroll
             for (int j = 0; j < TN; ++j)
-              fa[su][u][v][j] = *reinterpret_cast<const f16x8*>(sa + (wn * (BN / 2) + 32 * j) * 128 + off);
+              fa[su][u][v][j] = *reinterpret_cast<const f16x8*>(sa + (wn * (BN / 2) + 32 * j) * 128 + offa);
           }
         }
       }
 #pragma unroll
       for (int su = 0; su < SUB; ++su)
 #pragma unroll
-        for (int u = 0; u < SPW / 2; ++u) {
-          f16x8 bhh[TM], bsw0[TM], bsw1[TM], ahh[TN];
+        for (int u = 0; u < SPW / 2; ++u)
 #pragma unroll
-          for (int i = 0; i < TM; ++i) {
-            f16x8 x = fb[su][u][0][i], y = fb[su][u][1][i];
-            ym_swap32(x, y);  // x = [x_hi_s | x_hi_s+1], y = [x_lo_s | x_lo_s+1]
-            bhh[i] = x;
-            ym_swap32(y, x);  // y = [x_lo_s | x_hi_s], x = [x_lo_s+1 | x_hi_s+1]
-            bsw0[i] = y;
-            bsw1[i] = x;
-          }
+          for (int v = 0; v < 3; ++v)
 #pragma unroll
-          for (int j = 0; j < TN; ++j) {
-            f16x8 x = fa[su][u][0][j], y = fa[su][u][1][j];
-            ym_swap32(x, y);  // x = [w_hi_s | w_hi_s+1]
-            ahh[j] = x;
-          }
+            for (int i = 0; i < TM; ++i)
 #pragma unroll
-          for (int i = 0; i < TM; ++i)
-#pragma unroll
-            for (int j = 0; j < TN; ++j) {
-              acc[0][i][j] = __builtin_amdgcn_mfma_f32_32x32x16_f16(fa[su][u][0][j], bsw0[i], acc[0][i][j], 0, 0, 0);
-              acc[1 % NACC][i][j] =
-                  __builtin_amdgcn_mfma_f32_32x32x16_f16(fa[su][u][1][j], bsw1[i], acc[1 % NACC][i][j], 0, 0, 0);
-              acc[0][i][j] = __builtin_amdgcn_mfma_f32_32x32x16_f16(ahh[j], bhh[i], acc[0][i][j], 0, 0, 0);
-            }
-          if (u == 0 && islot >= 0) issue_sub(smem + islot * SB + su * SBS);
-        }
+              for (int j = 0; j < TN; ++j)
+                acc[v % NACC][i][j] = __builtin_amdgcn_mfma_f32_32x32x16_f16(fa[su][u][v][j], fb[su][u][v][i],
+                                                                             acc[v % NACC][i][j], 0, 0, 0);
     } else {
       f16x8 fb[SUB][SPW][TM], fa[SUB][SPW][TN];
 #pragma unroll
@@ -470,20 +419,17 @@ __global__ __launch_bounds__(256 * KG) void conv_dma(const ConvArgs a) {
 #pragma unroll
       for (int su = 0; su < SUB; ++su)
 #pragma unroll
-        for (int u = 0; u < SPW; ++u) {
+        for (int u = 0; u < SPW; ++u)
 #pragma unroll
           for (int i = 0; i < TM; ++i)
 #pragma unroll
             for (int j = 0; j < TN; ++j)
               acc[u % NACC][i][j] =
                   __builtin_amdgcn_mfma_f32_32x32x16_f16(fa[su][u][j], fb[su][u][i], acc[u % NACC][i][j], 0, 0, 0);
-          if (u == 0 && islot >= 0) issue_sub(smem + islot * SB + su * SBS);
-        }
     }
   };
 
   static_assert(NSTAGE >= 2 && NSTAGE <= 4, "ring depth");
-  YM_STAMP(4);
 #pragma unroll
   for (int s0 = 0; s0 < NSTAGE - 1; ++s0)
     if (nk > s0) issue(s0);
@@ -496,9 +442,9 @@ __global__ __launch_bounds__(256 * KG) void conv_dma(const ConvArgs a) {
     YM_STAMP(8 + 4 * (it & 63));
     raw_barrier();  // stage it is in LDS for every wave; every wave is done reading stage it-1's slot
     YM_STAMP(9 + 4 * (it & 63));
-    // (the slot the in-compute issue fills was last read in iteration it - 1, before this barrier)
+    if (it + NSTAGE - 1 < nk) issue((it + NSTAGE - 1) % NSTAGE);
     YM_STAMP(10 + 4 * (it & 63));
-    compute(it % NSTAGE, it + NSTAGE - 1 < nk ? (it + NSTAGE - 1) % NSTAGE : -1);
+    compute(it % NSTAGE);
     YM_STAMP(11 + 4 * (it & 63));
   }
   YM_STAMP(2);
@@ -537,7 +483,6 @@ __global__ __launch_bounds__(256 * KG) void conv_dma(const ConvArgs a) {
     }
   }
 
-  YM_STAMP(5);
   // ---- split-K: publish the partial tile write-through, the last arriver reduces (wave group 0 only holds the
   // tile; every thread still takes part in the workgroup barriers)
   if constexpr (SPLIT > 1) {
@@ -571,7 +516,6 @@ __global__ __launch_bounds__(256 * KG) void conv_dma(const ConvArgs a) {
       *flag = last;
     }
     __syncthreads();
-    if (!*flag) YM_STAMP_FLUSH(7);  // (probe builds: a workgroup that is not the last arriver ends here)
     if (!*flag || kg != 0) return;
     __builtin_amdgcn_fence(__ATOMIC_ACQUIRE, "wavefront");  // no instruction: keeps the sc1 loads below the ticket
     // sum every slab (this workgroup's own included) in split order — bitwise-reproducible whichever split arrived
@@ -600,61 +544,59 @@ __global__ __launch_bounds__(256 * KG) void conv_dma(const ConvArgs a) {
         }
   }
   if (kg != 0) return;
-  YM_STAMP(6);
 
   // ---- epilogue: lane owns channels nb + 32j + 8q + 4h + {0..3} of pixel pbm + 32i + l32
   OutT* dst = static_cast<OutT*>(a.dst);
   // x3 pair-layout outputs: lanes l and l ^ 32 (h = 0 / 1: channels +0..3 / +4..7 of one chunk of one pixel) write
-  // the chunk as one 32-byte run (ym_p2_store4_pair, v_permlane32_swap exchange) where the slice, the channel count
-  // and the pixel-shuffle sub-pixel width keep every chunk whole (uniform)
+  // the chunk as one 32-byte run (ym_p2_store4_pair) where the slice, the channel count and the pixel-shuffle
+  // sub-pixel width keep every chunk whole (uniform)
   constexpr bool PAIRST = X3 && std::is_same<OutT, P2>::value;
   const bool pairst = PAIRST && (a.pst & 1) && ((a.N | a.d_coff | a.d_ctot) & 7) == 0 && (!a.shuffle || (a.npr & 7) == 0);
-  // The uniform choices (SiLU or not, pair stores, Proto's pixel shuffle) are taken ONCE, outside the element loops:
-  // decided per element they made every SiLU its own branch-guarded block, a serial chain of transcendental latencies
-  // (tools/dma_probe.hip: ~2.4k cycles for the 16 outputs of a lane of a 64 x 64 x3 tile; now straight-line code).
-  auto epilogue = [&](auto act_t, auto pair_t, auto shuf_t) {
-    constexpr bool ACT = decltype(act_t)::value, PAIR = decltype(pair_t)::value, SHUF = decltype(shuf_t)::value;
 #pragma unroll
-    for (int i = 0; i < TM; ++i) {
-      if (ep_m[i] >= a.M) continue;  // both lanes of a pair alike (same pixel)
+  for (int i = 0; i < TM; ++i) {
+    if (ep_m[i] >= a.M) continue;
 #pragma unroll
-      for (int j = 0; j < TN; ++j)
+    for (int j = 0; j < TN; ++j)
 #pragma unroll
-        for (int q = 0; q < 4; ++q) {
-          const int n = tn * BN + wn * (BN / 2) + 32 * j + 8 * q + 4 * h;
-          float v[4];
+      for (int q = 0; q < 4; ++q) {
+        const int n = tn * BN + wn * (BN / 2) + 32 * j + 8 * q + 4 * h;
+        if constexpr (PAIRST) {
+          if (pairst) {  // both lanes of a pair take this branch together (same pixel, n < N alike)
+            const bool okn = n < a.N;
+            float v[4];
 #pragma unroll
-          for (int e = 0; e < 4; ++e) {
-            float x = X3 ? ym_x3_pre(acc[0][i][j][4 * q + e], a.wsc, bias4[j][q][e])
-                         : acc[0][i][j][4 * q + e] + bias4[j][q][e];
-            if constexpr (ACT) x = X3 ? ym_silu_x3(x) : ym_silu_fast(x);
-            v[e] = x + res4[i][j][q].at(e);
-          }
-          size_t o = ep_obase[i] + n;
-          if constexpr (SHUF) {
-            const int sub = n / a.npr;
-            const int ch = n - sub * a.npr;
-            o = ep_obase[i] + (size_t)((sub >> 1) * a.d_W + (sub & 1)) * a.d_ctot + ch;
-          }
-          if constexpr (PAIR) {
-            const bool okn = n < a.N;  // both lanes of a pair alike
-            if constexpr (PAIRST) ym_p2_store4_pair<32>(dst + (okn ? o : 0), v, h, okn, true);
-          } else {
-            if (n < a.N) Store4<OutT>::st(dst + o, v);
+            for (int e = 0; e < 4; ++e) {
+              const float x = ym_x3_pre(acc[0][i][j][4 * q + e], a.wsc, bias4[j][q][e]);
+              v[e] = (a.act ? ym_silu_x3(x) : x) + (float)res4[i][j][q][e];
+            }
+            size_t o = ep_obase[i] + n;
+            if (a.shuffle) {
+              const int sub = n / a.npr;
+              const int ch = n - sub * a.npr;
+              o = ep_obase[i] + (size_t)((sub >> 1) * a.d_W + (sub & 1)) * a.d_ctot + ch;
+            }
+            ym_p2_store4_pair<32>(dst + (okn ? o : 0), v, h, okn, a.pst & 16);
+            continue;
           }
         }
-    }
-  };
-  using T_ = std::true_type;
-  using F_ = std::false_type;
-  if (a.shuffle) {
-    if (pairst) a.act ? epilogue(T_{}, T_{}, T_{}) : epilogue(F_{}, T_{}, T_{});
-    else a.act ? epilogue(T_{}, F_{}, T_{}) : epilogue(F_{}, F_{}, T_{});
-  } else {
-    if (pairst) a.act ? epilogue(T_{}, T_{}, F_{}) : epilogue(F_{}, T_{}, F_{});
-    else a.act ? epilogue(T_{}, F_{}, F_{}) : epilogue(F_{}, F_{}, F_{});
+        if (n >= a.N) continue;
+        float v[4];
+#pragma unroll
+        for (int e = 0; e < 4; ++e) {
+          const float x = X3 ? ym_x3_pre(acc[0][i][j][4 * q + e], a.wsc, bias4[j][q][e])
+                             : acc[0][i][j][4 * q + e] + bias4[j][q][e];
+          v[e] = (a.act ? (X3 ? ym_silu_x3(x) : ym_silu_fast(x)) : x) + (float)res4[i][j][q][e];
+        }
+        if (a.shuffle) {
+          const int sub = n / a.npr;
+          const int ch = n - sub * a.npr;
+          Store4<OutT>::st(dst + ep_obase[i] + (size_t)((sub >> 1) * a.d_W + (sub & 1)) * a.d_ctot + ch, v);
+        } else {
+          Store4<OutT>::st(dst + ep_obase[i] + n, v);
+        }
+      }
   }
-  YM_STAMP_FLUSH(3);
+  YM_STAMP(3);
 }
 
 struct DmaCfg {

@@ -3,23 +3,22 @@
 // Sequential(DWConv(c3, c3, 3), Conv(c3, c3, 1)), Conv2d(c3, nc, 1))).  yolomi/arch.py GraphBuilder.fuse_dw merges a
 // depthwise op into the 1x1 conv that is the only reader of its output; the depthwise output never reaches HBM.
 //
-// A wave owns 16 consecutive output pixels and every output channel (N <= 128: 8 blocks of 16).  Per K block of 32
-// logical channels, lane (g, col) computes the depthwise output of pixel col, channels 32 kb + 8 g .. + 7 — exactly its
-// B operand of v_mfma_f32_16x16x32_f16 (k = 8 g .. 8 g + 7 of pixel col), so the depthwise result goes from VALU
-// registers straight into the MFMAs: no LDS tile, no barrier inside the K loop.
-//   * taps: 9 16-byte loads per lane (x3: 18, the hi and lo halves of the pair layout) through a buffer resource, an
-//     out-of-image tap or a channel chunk past C at an out-of-range offset (the hardware returns zeros): no branch;
-//   * depthwise arithmetic exactly as csrc/ym_misc.hip dwconv3x3*: acc = bias, then fmaf over taps 0..8 on the values
-//     as stored (x3: hi + lo in fp32), SiLU (x3: ym_silu_x3, f16: ym_silu_fast), then x3: hi = fp16(v),
-//     lo = fp16(v - hi) — the same B operands the unfused 1x1 reads back from the stored depthwise tensor;
-//   * the 1x1: A = weight rows from global (L2-resident; x3 pair-chunk rows give w_hi and w_lo of the lane's chunk in
-//     one 32-byte run), issued with the taps so their latency hides under the depthwise VALU work; x3 takes three MFMAs
-//     per block (w_lo·x_hi + w_hi·x_lo + w_hi·x_hi), f16 one;
-//   * KW > 1: the KW waves of a workgroup split the K blocks of one pixel group (the 20² / 40² maps have too few pixel
-//     groups to fill the GPU), their partial sums meet in LDS in wave order (deterministic);
+// A workgroup owns a TH x TW tile of output pixels of one image (TH·TW = 64: four 16-pixel groups, one per wave) and
+// every output channel (N <= 128: 8 blocks of 16).  Per K block of 32 logical channels:
+//   * staging: the (TH+2) x (TW+2) input window of the block's 4 channel chunks (zeros outside the image: buffer
+//     loads at an out-of-range offset), the 1x1 weight rows of the block and its depthwise taps / bias go to LDS —
+//     loaded into registers one block AHEAD, so the memory latency hides under the previous block's compute; each
+//     window pixel is fetched once per workgroup instead of 9 times per output pixel;
+//   * depthwise: lane (g, col) of wave w computes pixel 16 w + col (tile row-major), channels 32 kb + 8 g .. + 7 —
+//     exactly its B operand of v_mfma_f32_16x16x32_f16 (k = 8 g .. 8 g + 7 of pixel col), in the arithmetic of
+//     csrc/ym_misc.hip dwconv3x3* (acc = bias, fmaf over taps 0..8 on the stored values — x3: hi + lo in fp32 —,
+//     SiLU (x3: ym_silu_x3, f16: ym_silu_fast), then x3: hi = fp16(v), lo = fp16(v - hi)): the same B operands the
+//     unfused 1x1 would read back from the stored depthwise tensor;
+//   * the 1x1: A fragments from the LDS weight rows (pitch 32·XS + 16 halves, conflict-free for the 16-row reads as
+//     in csrc/ym_conv_stream.hip); x3 takes three MFMAs per block (w_lo·x_hi + w_hi·x_lo + w_hi·x_hi), f16 one;
 //   * epilogue as the other x3 convs: fmaf(acc, 2^-s, bias), SiLU, lane-pair whole-chunk stores (x3) / fp16x4.
-// The depthwise weights ([9][C] fp32 then the bias [C]) are staged in LDS once per workgroup; lanes of one g read the
-// same address (broadcast).
+// The window is kept in two planes of 4 channels ([chunk][pixel] f32x4 for x3, f16x8 for f16), so the 16-byte reads of
+// consecutive lanes (consecutive pixels) are consecutive in LDS.
 #include <type_traits>
 
 #include "ym_common.h"
@@ -29,144 +28,180 @@ namespace {
 typedef _Float16 h8 __attribute__((ext_vector_type(8)));
 typedef unsigned u32x4 __attribute__((ext_vector_type(4)));
 
-#define YM_DWPW_CFGS(X) X(0, 1) X(1, 2) X(2, 4)
+#define YM_DWPW_CFGS(X) X(0, 16) X(1, 8) X(2, 4)
 struct DwpwCfg {
-  int kw;  // waves of a workgroup splitting the K blocks of one 16-pixel group (4 / kw pixel groups per workgroup)
+  int tw;  // tile width (the tile is 64 / tw rows high): 16 for 80² maps, 8 for 40², 4 or 8 for 20²
 };
 constexpr DwpwCfg kDwpw[] = {
-#define YM_X(id, kw) {kw},
+#define YM_X(id, tw) {tw},
     YM_DWPW_CFGS(YM_X)
 #undef YM_X
 };
 constexpr int kNumDwpw = sizeof(kDwpw) / sizeof(kDwpw[0]);
-constexpr int kDwpwMaxC = 512;  // depthwise channels staged in LDS (10 x C fp32)
-constexpr int kDwpwNB = 8;      // output-channel blocks of 16 per wave (N <= 128)
+constexpr int kDwpwMaxC = 512;  // depthwise channels (the head's widest input)
+constexpr int kDwpwNB = 8;      // output-channel blocks of 16 (N <= 128)
 constexpr unsigned OOBX = 0x80000000u;
 
-__device__ __forceinline__ h8 bld(__amdgpu_buffer_rsrc_t r, unsigned off) {
-  return __builtin_bit_cast(h8, __builtin_amdgcn_raw_buffer_load_b128(r, off, 0, 0));
+__device__ __forceinline__ u32x4 bld(__amdgpu_buffer_rsrc_t r, unsigned off) {
+  return __builtin_amdgcn_raw_buffer_load_b128(r, off, 0, 0);
 }
 
-template <typename T, int KW>
-__global__ __launch_bounds__(256) void conv_dwpw(const ConvArgs a) {
+template <typename T, int TW>
+__global__ __launch_bounds__(256, 2) void conv_dwpw(const ConvArgs a) {
   constexpr bool X3 = std::is_same<T, P2>::value;
-  constexpr int XS = X3 ? 2 : 1;  // fp16 storage elements per logical channel
-  constexpr int PXG = 4 / KW;     // 16-pixel groups per workgroup
-  __shared__ __attribute__((aligned(16))) float wl[10 * kDwpwMaxC];  // depthwise taps [9][C], then bias [C]
-  __shared__ __attribute__((aligned(16))) f32x4 red[KW > 1 ? (KW - 1) * PXG * kDwpwNB * 64 : 1];
+  constexpr int XS = X3 ? 2 : 1;            // fp16 storage elements per logical channel
+  constexpr int TH = 64 / TW, IH = TH + 2, IW = TW + 2, NPIX = IH * IW;
+  constexpr int NWIN = NPIX * 4;            // window items (pixel, 8-channel chunk)
+  constexpr int WPT = (NWIN + 255) / 256;   // window items per thread
+  constexpr int LDW = 32 * XS + 16;         // LDS pitch of a 1x1 weight row (halves)
+  constexpr int WQ = 128 * 32 * XS / 8 / 256;  // 16-byte weight pieces per thread and block (x3 4, f16 2)
+  // window planes: x3 [2][4 chunks][NPIX] f32x4 (channels 0-3 / 4-7 of each chunk as fp32 hi + lo); f16 [4][NPIX] f16x8
+  __shared__ __attribute__((aligned(16))) u32x4 win[(X3 ? 2 : 1) * 4 * NPIX];
+  __shared__ __attribute__((aligned(16))) f16 w1[128 * LDW];
+  __shared__ __attribute__((aligned(16))) float dwk[10 * 32];  // the block's taps [9][32], then bias [32]
   const int tid = threadIdx.x, lane = tid & 63, wave = tid >> 6;
   const int g = lane >> 4, col = lane & 15;
-  const int kw = __builtin_amdgcn_readfirstlane(wave % KW), pg = wave / KW;
   const int C = a.C0;
-  for (int i = tid; i < 10 * C / 4; i += 256) {
-    const int t = (4 * i) / C, c = 4 * i - t * C;
-    *reinterpret_cast<f32x4*>(wl + 4 * i) =
-        ym_gld<f32x4>(t < 9 ? a.dw_w + t * C + c : a.dw_b + c);
-  }
-
-  // this lane's pixel and its 3x3 window (bit t: tap t inside the image; none for a pixel past M)
-  const int vb = ym_xcd_block(blockIdx.x, gridDim.x);
-  const int m = (vb * PXG + pg) * 16 + col;
-  const bool okm = m < a.M;
-  const int mm = okm ? m : 0;
-  const int b = ym_div(mm, a.fd_hw), rem = mm - b * (a.Ho * a.Wo);
-  const int y = ym_div(rem, a.fd_w), x = rem - y * a.Wo;
-  unsigned tmask = 0;
-#pragma unroll
-  for (int t = 0; t < 9; ++t) {
-    const int iy = y - 1 + t / 3, ix = x - 1 + t % 3;
-    tmask |= ((unsigned)iy < (unsigned)a.Hin && (unsigned)ix < (unsigned)a.Win) ? (1u << t) : 0u;
-  }
-  if (!okm) tmask = 0;
-  // byte offset of the lane's window origin (pixel (y-1, x-1), channel 0) in the source; only in-image taps are used
-  const int pix0 = (b * a.s0_P + (y - 1) * a.s0_W + (x - 1)) * a.s0_ctot + a.s0_coff;  // logical elements
+  const int ntx = (a.Wo + TW - 1) / TW, nty = (a.Ho + TH - 1) / TH;
+  int vb = ym_xcd_block(blockIdx.x, gridDim.x);  // neighbouring tiles (shared window rows) on one XCD
+  const int tx = vb % ntx;
+  vb /= ntx;
+  const int ty = vb % nty, b = vb / nty;
+  const int y0 = ty * TH, x0 = tx * TW;
   const __amdgpu_buffer_rsrc_t rs = __builtin_amdgcn_make_buffer_rsrc(const_cast<void*>(a.src0), 0,
                                                                       (int)(a.s0_elems * 2), 0x00020000);
   const __amdgpu_buffer_rsrc_t rw = __builtin_amdgcn_make_buffer_rsrc(const_cast<void*>(a.w), 0,
                                                                       (int)((long)a.N * a.Kpad * 2), 0x00020000);
-  const int NB = (a.N + 15) >> 4;
-  const int nkb = (C + 31) >> 5;  // K blocks of 32 logical channels
-  const int kb0 = nkb * kw / KW, kb1 = nkb * (kw + 1) / KW;
+  const __amdgpu_buffer_rsrc_t rd = __builtin_amdgcn_make_buffer_rsrc(const_cast<float*>(a.dw_w), 0, 40 * C, 0x00020000);
+  // per thread, fixed over the K loop: its window items' pixel offsets (logical elements; -1 outside the image)
+  int woff[WPT];
+#pragma unroll
+  for (int u = 0; u < WPT; ++u) {
+    const int i = tid + 256 * u, q = i >> 2;
+    const int iy = y0 - 1 + q / IW, ix = x0 - 1 + q % IW;
+    woff[u] = (i < NWIN && (unsigned)iy < (unsigned)a.Hin && (unsigned)ix < (unsigned)a.Win)
+                  ? (b * a.s0_P + iy * a.s0_W + ix) * a.s0_ctot + a.s0_coff + 8 * (i & 3)
+                  : -1;
+  }
+  // registers of the next block: window items (x3: hi and lo), weight pieces, one dw-weight float4
+  u32x4 rwin[WPT][XS], rw1[WQ], rdk;
+  auto load = [&](int kb) {
+    const int c0 = 32 * kb;
+#pragma unroll
+    for (int u = 0; u < WPT; ++u) {
+      const bool ok = woff[u] >= 0 && c0 + 8 * ((tid + 256 * u) & 3) < C;
+      const unsigned off = (unsigned)(woff[u] + c0) * (2u * XS);
+      rwin[u][0] = bld(rs, ok ? off : OOBX);
+      if constexpr (X3) rwin[u][1] = bld(rs, ok ? off + 16u : OOBX);
+    }
+#pragma unroll
+    for (int q = 0; q < WQ; ++q) {  // piece i: row n = i / (4 XS), 16-byte piece j of the row's block
+      const int i = tid + 256 * q, n = i / (4 * XS), j = i % (4 * XS);
+      const bool ok = n < a.N && c0 * XS + 8 * j < a.Kpad;
+      rw1[q] = bld(rw, ok ? (unsigned)(n * a.Kpad + c0 * XS + 8 * j) * 2u : OOBX);
+    }
+    if (tid < 80) {  // taps t < 9: dw_w[t][c0 + 4 v]; t == 9: the bias (dw_b follows dw_w: one buffer)
+      const int t = tid >> 3, v = tid & 7;
+      const bool ok = c0 + 4 * v < C;
+      rdk = __builtin_bit_cast(u32x4, __builtin_amdgcn_raw_buffer_load_b128(rd, ok ? (unsigned)((t * C + c0 + 4 * v) * 4) : OOBX, 0, 0));
+    }
+  };
+  auto store = [&]() {
+#pragma unroll
+    for (int u = 0; u < WPT; ++u) {
+      const int i = tid + 256 * u;
+      if (i >= NWIN) continue;
+      const int pix = i >> 2, ch = i & 3;
+      if constexpr (X3) {
+        const f16x8 hv = __builtin_bit_cast(f16x8, rwin[u][0]), lv = __builtin_bit_cast(f16x8, rwin[u][1]);
+        f32x4 p0, p1;
+#pragma unroll
+        for (int e = 0; e < 4; ++e) {
+          p0[e] = (float)hv[e] + (float)lv[e];
+          p1[e] = (float)hv[4 + e] + (float)lv[4 + e];
+        }
+        win[ch * NPIX + pix] = __builtin_bit_cast(u32x4, p0);
+        win[(4 + ch) * NPIX + pix] = __builtin_bit_cast(u32x4, p1);
+      } else {
+        win[ch * NPIX + pix] = rwin[u][0];
+      }
+    }
+#pragma unroll
+    for (int q = 0; q < WQ; ++q) {
+      const int i = tid + 256 * q, n = i / (4 * XS), j = i % (4 * XS);
+      *reinterpret_cast<u32x4*>(w1 + n * LDW + 8 * j) = rw1[q];
+    }
+    if (tid < 80) *reinterpret_cast<u32x4*>(dwk + 4 * tid) = rdk;
+  };
 
+  // this lane's output pixel
+  const int p = 16 * wave + col, py = p / TW, px = p % TW;
+  const int y = y0 + py, x = x0 + px;
+  const bool okm = y < a.Ho && x < a.Wo;
+  const int NB = (a.N + 15) >> 4;
+  const int nkb = (C + 31) >> 5;
   f32x4 acc[kDwpwNB];
 #pragma unroll
   for (int nb = 0; nb < kDwpwNB; ++nb) acc[nb] = f32x4{0.f, 0.f, 0.f, 0.f};
-  __syncthreads();  // depthwise weights in LDS
-
-  for (int kb = kb0; kb < kb1; ++kb) {
-    const int c = 32 * kb + 8 * g;  // the lane's first logical channel
-    const bool kc = c < C;
-    // the 9 taps of the lane's chunk
-    h8 th[9], tl[X3 ? 9 : 1];
-#pragma unroll
-    for (int t = 0; t < 9; ++t) {
-      const bool ok = kc && ((tmask >> t) & 1u);
-      const unsigned off = (unsigned)(pix0 + ((t / 3) * a.s0_W + t % 3) * a.s0_ctot + c) * (2u * XS);
-      th[t] = bld(rs, ok ? off : OOBX);
-      if constexpr (X3) tl[t] = bld(rs, ok ? off + 16u : OOBX);
-    }
-    // depthwise: bias, taps 0..8 (csrc/ym_misc.hip dwconv3x3_lds order), SiLU
-    const int cc = kc ? c : 0;
+  load(0);
+  for (int kb = 0; kb < nkb; ++kb) {
+    store();
+    __syncthreads();
+    if (kb + 1 < nkb) load(kb + 1);
+    const bool kc = 32 * kb + 8 * g < C;
+    // depthwise of (pixel p, chunk g): bias, taps 0..8
     float v[8];
     {
-      const f32x4 b0 = *reinterpret_cast<const f32x4*>(wl + 9 * C + cc), b1 = *reinterpret_cast<const f32x4*>(wl + 9 * C + cc + 4);
+      const f32x4 b0 = *reinterpret_cast<const f32x4*>(dwk + 9 * 32 + 8 * g),
+                  b1 = *reinterpret_cast<const f32x4*>(dwk + 9 * 32 + 8 * g + 4);
 #pragma unroll
       for (int e = 0; e < 4; ++e) { v[e] = b0[e]; v[4 + e] = b1[e]; }
     }
 #pragma unroll
     for (int t = 0; t < 9; ++t) {
-      const f32x4 w0 = *reinterpret_cast<const f32x4*>(wl + t * C + cc), w1 = *reinterpret_cast<const f32x4*>(wl + t * C + cc + 4);
+      const int q = (py + t / 3) * IW + px + t % 3;
+      const f32x4 w0 = *reinterpret_cast<const f32x4*>(dwk + t * 32 + 8 * g),
+                  w1v = *reinterpret_cast<const f32x4*>(dwk + t * 32 + 8 * g + 4);
+      if constexpr (X3) {
+        const f32x4 x0v = __builtin_bit_cast(f32x4, win[g * NPIX + q]), x1v = __builtin_bit_cast(f32x4, win[(4 + g) * NPIX + q]);
 #pragma unroll
-      for (int e = 0; e < 8; ++e) {
-        const float xv = X3 ? (float)th[t][e] + (float)tl[t][e] : (float)th[t][e];
-        v[e] = fmaf(xv, e < 4 ? w0[e] : w1[e - 4], v[e]);
+        for (int e = 0; e < 4; ++e) {
+          v[e] = fmaf(x0v[e], w0[e], v[e]);
+          v[4 + e] = fmaf(x1v[e], w1v[e], v[4 + e]);
+        }
+      } else {
+        const f16x8 xv = __builtin_bit_cast(f16x8, win[g * NPIX + q]);
+#pragma unroll
+        for (int e = 0; e < 4; ++e) {
+          v[e] = fmaf((float)xv[e], w0[e], v[e]);
+          v[4 + e] = fmaf((float)xv[4 + e], w1v[e], v[4 + e]);
+        }
       }
     }
     h8 xh, xl;
 #pragma unroll
     for (int e = 0; e < 8; ++e) {
-      float s = a.dw_act ? (X3 ? ym_silu_x3(v[e]) : ym_silu_fast(v[e])) : v[e];
-      s = kc ? s : 0.f;  // channels past C: a zero operand (their weights are zero-padded too)
-      xh[e] = (f16)s;
-      if constexpr (X3) xl[e] = (f16)(s - (float)xh[e]);
-    }
-    // 1x1 weight fragments of the block: row 16 nb + col, the lane's 8 channels (x3: hi then lo, one 32-byte run)
-    h8 wa[kDwpwNB], wb[X3 ? kDwpwNB : 1];
-#pragma unroll
-    for (int nb = 0; nb < kDwpwNB; ++nb) {
-      const int n = 16 * nb + col;
-      const bool ok = nb < NB && n < a.N;
-      const unsigned off = (unsigned)(n * a.Kpad + XS * c) * 2u;
-      wa[nb] = bld(rw, ok ? off : OOBX);
-      if constexpr (X3) wb[nb] = bld(rw, ok ? off + 16u : OOBX);
+      float sv = a.dw_act ? (X3 ? ym_silu_x3(v[e]) : ym_silu_fast(v[e])) : v[e];
+      sv = kc ? sv : 0.f;  // channels past C: a zero operand (their weights are zero-padded too)
+      xh[e] = (f16)sv;
+      if constexpr (X3) xl[e] = (f16)(sv - (float)xh[e]);
     }
 #pragma unroll
     for (int nb = 0; nb < kDwpwNB; ++nb) {
       if (nb >= NB) break;
+      const f16* wr = w1 + (16 * nb + col) * LDW + 8 * XS * g;  // x3: [hi x8 | lo x8] of the lane's chunk
+      const h8 wa = *reinterpret_cast<const h8*>(wr);
       if constexpr (X3) {
-        acc[nb] = __builtin_amdgcn_mfma_f32_16x16x32_f16(wb[nb], xh, acc[nb], 0, 0, 0);
-        acc[nb] = __builtin_amdgcn_mfma_f32_16x16x32_f16(wa[nb], xl, acc[nb], 0, 0, 0);
+        const h8 wb = *reinterpret_cast<const h8*>(wr + 8);
+        acc[nb] = __builtin_amdgcn_mfma_f32_16x16x32_f16(wb, xh, acc[nb], 0, 0, 0);
+        acc[nb] = __builtin_amdgcn_mfma_f32_16x16x32_f16(wa, xl, acc[nb], 0, 0, 0);
       }
-      acc[nb] = __builtin_amdgcn_mfma_f32_16x16x32_f16(wa[nb], xh, acc[nb], 0, 0, 0);
+      acc[nb] = __builtin_amdgcn_mfma_f32_16x16x32_f16(wa, xh, acc[nb], 0, 0, 0);
     }
+    __syncthreads();  // every wave is done with the block's LDS before the next store
   }
 
-  if constexpr (KW > 1) {  // partial sums of waves kw > 0 → wave kw = 0 of the pixel group, added in wave order
-    if (kw > 0) {
-#pragma unroll
-      for (int nb = 0; nb < kDwpwNB; ++nb)
-        if (nb < NB) red[(((kw - 1) * PXG + pg) * kDwpwNB + nb) * 64 + lane] = acc[nb];
-    }
-    __syncthreads();
-    if (kw > 0) return;
-#pragma unroll
-    for (int q = 1; q < KW; ++q)
-#pragma unroll
-      for (int nb = 0; nb < kDwpwNB; ++nb)
-        if (nb < NB) acc[nb] += red[(((q - 1) * PXG + pg) * kDwpwNB + nb) * 64 + lane];
-  }
-
-  // epilogue: lane (g, col) holds channels 16 nb + 4 g .. + 3 of pixel m
+  // epilogue: lane (g, col) holds channels 16 nb + 4 g .. + 3 of pixel (y, x)
   const int ob = b * a.d_P + a.d_pixoff + y * a.d_W + x;
   T* dst = static_cast<T*>(a.dst);
   const bool pair = X3 && ((a.N | a.d_coff | a.d_ctot) & 7) == 0;
@@ -197,10 +232,11 @@ __global__ __launch_bounds__(256) void conv_dwpw(const ConvArgs a) {
   }
 }
 
-template <typename T, int KW>
+template <typename T, int TW>
 hipError_t launch(const ConvArgs& a, hipStream_t st) {
-  const int groups = (a.M + 15) / 16, pxg = 4 / KW;
-  hipLaunchKernelGGL((conv_dwpw<T, KW>), dim3((groups + pxg - 1) / pxg), dim3(256), 0, st, a);
+  constexpr int TH = 64 / TW;
+  const int tiles = (a.M / (a.Ho * a.Wo)) * ((a.Ho + TH - 1) / TH) * ((a.Wo + TW - 1) / TW);
+  hipLaunchKernelGGL((conv_dwpw<T, TW>), dim3(tiles), dim3(256), 0, st, a);
   return hipGetLastError();
 }
 
@@ -219,22 +255,19 @@ hipError_t ym_launch_conv_dwpw(int dtype, int out_f32, const ConvArgs& a, int cf
   if (a.s0_elems * 2 >= 0x7FFFFFF0L || (long)a.N * a.Kpad * 2 >= 0x7FFFFFF0L) return hipErrorInvalidValue;
   if (cfg < 0 || cfg >= kNumDwpw) {
     if (strict) return hipErrorInvalidValue;
-    // enough waves for the GPU (~2k), each K range at least two blocks
-    const int groups = (a.M + 15) / 16, nkb = (a.C0 + 31) / 32;
-    cfg = 0;
-    while (cfg + 1 < kNumDwpw && groups * kDwpw[cfg].kw < 2048 && nkb >= 2 * kDwpw[cfg + 1].kw) ++cfg;
+    cfg = a.Wo % 16 == 0 ? 0 : (a.Wo % 8 == 0 ? 1 : 2);  // a tile width that divides the map
   }
-  const int kw = kDwpw[cfg].kw;
+  const int tw = kDwpw[cfg].tw;
   if (dtype == YM_DT_X3) {
-    switch (kw) {
-      case 1: return launch<P2, 1>(a, st);
-      case 2: return launch<P2, 2>(a, st);
+    switch (tw) {
+      case 16: return launch<P2, 16>(a, st);
+      case 8: return launch<P2, 8>(a, st);
       default: return launch<P2, 4>(a, st);
     }
   }
-  switch (kw) {
-    case 1: return launch<f16, 1>(a, st);
-    case 2: return launch<f16, 2>(a, st);
+  switch (tw) {
+    case 16: return launch<f16, 16>(a, st);
+    case 8: return launch<f16, 8>(a, st);
     default: return launch<f16, 4>(a, st);
   }
 }

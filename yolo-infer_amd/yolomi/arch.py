@@ -400,6 +400,11 @@ class GraphBuilder:
         self.ops = out
 
     DW_MAX_C, DW_MAX_N = 512, 128  # csrc/ym_conv_dwpw.hip kDwpwMaxC, 16 * kDwpwNB
+    # map strides whose depthwise ops are fused: measured (yolo11s B=8 x3 replay, r04) the fused kernel beats the
+    # depthwise + 1x1 launches on the P3 maps only (80²: 32.6 vs 35.5 us per pair); on P4 / P5 (40², 20²) the few
+    # workgroups run their K blocks' load → depthwise → MFMA chains at ~2-4 us each and lose (21.8 vs 18.5 us,
+    # 35.7 vs 14.9 us for the 512-channel P5 input)
+    DW_FUSE_STRIDES = (8,)
 
     def fuse_dw(self):
         """Merge each depthwise op D into the 1x1 conv B that immediately follows it and is the only reader of D's
@@ -424,7 +429,7 @@ class GraphBuilder:
 
     def _dw_fusable(self, D: Op, B: Op) -> bool:
         d = D.args
-        if B.kind != "conv" or not d["act"]:
+        if B.kind != "conv" or not d["act"] or d["src"].buf.f not in self.DW_FUSE_STRIDES:
             return False
         b = B.args
         mid = d["dst"]

@@ -9,7 +9,8 @@ import os
 from pathlib import Path
 from typing import Optional
 
-LIB_PATH = Path(__file__).resolve().parent / "libyolomi.so"
+# YM_LIB: another build of the library (same-box A/B of kernel variants: tools/gpu_ab_libs.sh); default in-tree
+LIB_PATH = Path(os.environ.get("YM_LIB") or Path(__file__).resolve().parent / "libyolomi.so")
 
 YM_ERRORS = {-1: "EINVAL", -2: "EBLOB", -3: "EHIP", -4: "ENOMEM", -5: "ESTATE"}
 
