@@ -217,8 +217,11 @@ def test_x3_fused_pairs_match_split(scale):
         eng.rt.set_op_cfg(B, H, W, split)
         eng.run(x, use_graph=False)
         ref = eng.read_buffer(eng.graph.anchor_buf.id, B)
-        for cfgs, ids in ((range(STREAM_BASE, STREAM_BASE + N_STREAM), [i for i in pairs if i not in bneck]),
-                          (list(range(BNECK_BASE, BNECK_BASE + N_BNECK)) + list(range(*X3_BNECK)), bneck)):
+        band = list(range(BNECK_BASE, BNECK_BASE + N_BNECK)) + list(range(*X3_BNECK))
+        # conv -> 1x1 pairs: the streaming FUSE mode, and the band kernel's x3 stride-2 "down" mode (model.1+cv1:
+        # the tiles whose doubled LDS fits)
+        for cfgs, ids in ((list(range(STREAM_BASE, STREAM_BASE + N_STREAM)) + band, [i for i in pairs if i not in bneck]),
+                          (band, bneck)):
             for c in cfgs:
                 cfg = list(split)
                 for i in ids:

@@ -3,7 +3,8 @@
 an op whose name survives keeps its committed (in-context refined) cfg, an op the old table does not name takes the
 pick of a fresh ym_tune on this GPU.  Writes gpurun_out/tuned/<table>.json (copy into yolomi/tuned/ to commit).
 
-    python tools/retable.py [scale:task:dtype:B ...]     (default: the committed x3 tables)"""
+    python tools/retable.py [scale:task:dtype:B ...]     (default: the committed x3 tables)
+YM_RETABLE_OPS=a,b: ops whose committed cfg is replaced by the fresh tune's pick too."""
 import json
 import os
 import sys
@@ -32,7 +33,9 @@ for spec in specs:
         old = json.load(open(os.path.join(TUNED_DIR, name)))
     except OSError:
         old = {"ops": [], "cfg": []}
-    keep = dict(zip(old["ops"], old["cfg"]))
+    # YM_RETABLE_OPS: op names to re-tune as well (a kernel family gained a configuration for them)
+    retune = set(filter(None, os.environ.get("YM_RETABLE_OPS", "").split(",")))
+    keep = {n: c for n, c in zip(old["ops"], old["cfg"]) if n not in retune}
     eng.run(synthetic_batch(B, 640, 1000, dev))  # tunes (no table)
     torch.cuda.synchronize()
     tuned = eng.rt.get_op_cfg(B, 640, 640)

@@ -458,8 +458,12 @@ hipError_t ym_launch_conv_bneck(int out_f32, const ConvArgs& a, int i, hipStream
   const int xs = a.x3 ? 2 : 1;
   if (xs * C != 8 * a.Cin8 || a.Kpad < xs * 32 * ((9 * C + 31) / 32) || a.Kpad2 < xs * 32 * ((K2 * K2 * CM + 31) / 32))
     return hipErrorInvalidValue;
-  if (a.x3) {  // the Bottleneck shapes (the stride-2 "down" pairs do not fit twice the LDS)
-    if (!bneck) return hipErrorInvalidValue;
+  if (a.x3) {
+    if (down) {  // the stride-2 "down" pairs: only the narrow tiles fit the doubled LDS (2 x 32 px: 136 KB for s model.1)
+      if (C == 32 && CM == 64 && N2 == 64) return dispatch_cfg<32, 64, 64, 2, 1, true>(a, i, st);
+      if (C == 16 && CM == 32 && N2 == 32) return dispatch_cfg<16, 32, 32, 2, 1, true>(a, i, st);
+      return hipErrorInvalidValue;
+    }
     if (C == 16 && CM == 8 && N2 == 16) return dispatch_cfg<16, 8, 16, 1, 3, true>(a, i, st);
     if (C == 32 && CM == 16 && N2 == 32) return dispatch_cfg<32, 16, 32, 1, 3, true>(a, i, st);
     if (C == 64 && CM == 32 && N2 == 64) return dispatch_cfg<64, 32, 64, 1, 3, true>(a, i, st);
