@@ -22,7 +22,7 @@ import sys
 
 ROOT = os.path.dirname(os.path.dirname(os.path.abspath(__file__)))
 PROF = os.path.join(ROOT, "profiles")
-CONV = re.compile(r"conv_igemm|conv_lds|conv_dma|conv_i8|conv_stream|conv_small|conv_halo|conv_bneck")
+CONV = re.compile(r"conv_igemm|conv_lds|conv_dma|conv_i8|conv_stream|conv_small|conv_halo|conv_bneck|conv_dwpw")
 STEM = re.compile(r"stem_conv3x3s2|stem_i8|stem_mfma|stem_valu")
 CALIB = re.compile(r"conv_igemm<float, float|conv_igemmIffL")  # the f32 calibration forwards of an int8 run
 
