@@ -195,7 +195,8 @@ def test_x3_fused_pairs_match_split(scale):
     """x3 fused pairs against the same plan with its pairs run as two launches, Detect rows within 2e-6 relative (the
     same split products summed in another order; the plan's own per-layer parity is test_x3_layers_match_oracle):
       * conv -> 1x1 pairs (csrc/ym_conv_stream.hip FUSE in the x3 mode: the intermediate split hi/lo in registers,
-        three 16x16x16 MFMAs per K block of the second GEMM) on every streaming configuration;
+        three 16x16x16 MFMAs per K block of the second GEMM) on every streaming configuration, and on the LDS-DMA
+        kernel's fused-epilogue GEMM (csrc/ym_conv_dma.hip FUSE: the intermediate split into the idle stage ring);
       * Bottlenecks (csrc/ym_conv_bneck.hip in the x3 mode: hi / lo LDS planes, three MFMAs per K step) on every
         tile variant, the x3-only 2 x 32 tiles included (the ones whose doubled LDS does not fit fall back to the
         split pair).
@@ -218,9 +219,12 @@ def test_x3_fused_pairs_match_split(scale):
         eng.run(x, use_graph=False)
         ref = eng.read_buffer(eng.graph.anchor_buf.id, B)
         band = list(range(BNECK_BASE, BNECK_BASE + N_BNECK)) + list(range(*X3_BNECK))
-        # conv -> 1x1 pairs: the streaming FUSE mode, and the band kernel's x3 stride-2 "down" mode (model.1+cv1:
-        # the tiles whose doubled LDS fits)
-        for cfgs, ids in ((list(range(STREAM_BASE, STREAM_BASE + N_STREAM)) + band, [i for i in pairs if i not in bneck]),
+        # conv -> 1x1 pairs: the streaming FUSE mode, the LDS-DMA kernel's fused-epilogue GEMM (DMA ids 17..46, those
+        # of YM_DMA_FUSE_CFGS instantiated) and the band kernel's x3 stride-2 "down" mode (model.1+cv1: the tiles
+        # whose doubled LDS fits)
+        dma = list(range(17, 17 + 30))
+        for cfgs, ids in ((list(range(STREAM_BASE, STREAM_BASE + N_STREAM)) + dma + band,
+                           [i for i in pairs if i not in bneck]),
                           (band, bneck)):
             for c in cfgs:
                 cfg = list(split)

@@ -473,6 +473,7 @@ hipError_t ym_launch_letterbox(const LetterboxArgs& a, hipStream_t st);
 hipError_t ym_launch_spin(int usec, hipStream_t st);  // profiling: park the stream for usec (wall clock)
 hipError_t ym_launch_conv_dma(int out_f32, const ConvArgs& a, int i, hipStream_t st);  // f16 plans only
 int ym_conv_dma_num_cfgs();
+hipError_t ym_launch_conv_dma_fuse(int out_f32, const ConvArgs& a, int i, hipStream_t st);  // x3 conv -> 1x1 pairs
 int ym_conv_dma_x3_num_cfgs();  // x3-only LDS-DMA configurations (op cfg ids from ym_conv_num_cfgs() on)
 int ym_conv_num_cfgs_dt(int dtype);  // conv-config catalogue size of a plan dtype (YM_DT_*)
 hipError_t ym_launch_conv_bneck(int out_f32, const ConvArgs& a, int i, hipStream_t st);  // fused Bottleneck

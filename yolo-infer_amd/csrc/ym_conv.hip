@@ -753,6 +753,10 @@ hipError_t ym_launch_conv(int dtype, int out_f32, const ConvArgs& a, int cfg, hi
       if (e != hipErrorInvalidValue || strict) return e;
     }
     const int sbase = kNumAllCfg + ym_conv_dma_num_cfgs(), ns = ym_conv_stream_num_cfgs();
+    if (dtype == YM_DT_X3 && a.k2 == 1 && cfg >= kNumAllCfg && cfg < sbase) {  // LDS-DMA ids: the fused-epilogue GEMM
+      const hipError_t e = ym_launch_conv_dma_fuse(out_f32, a, cfg - kNumAllCfg, st);
+      if (e != hipErrorInvalidValue || strict) return e;
+    }
     if (cfg >= sbase && cfg < sbase + ns) {
       const hipError_t e = ym_launch_conv_stream(out_f32, a, cfg - sbase, st);
       if (e != hipErrorInvalidValue || strict) return e;

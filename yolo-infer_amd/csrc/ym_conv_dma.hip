@@ -91,7 +91,15 @@ template <> struct Store4<P2> {
 // form the split product hi·hi + hi·lo + lo·hi of both chunks: A = [w_hi_s | w_hi_s] with the natural B (w_hi·x_hi +
 // w_hi·x_lo), the same for s+1, and A = [w_lo_s | w_lo_s+1] with B = [x_hi_s | x_hi_s+1] (w_lo·x_hi of both) — only
 // the chunk each lane half reads from LDS changes, the swizzle stays conflict-free.
-template <typename OutT, int BM, int BN, int KIND, int SPLIT, int KG, int NSTAGE, int SUB, bool X3 = false>
+// FUSE (x3 plans; a fused conv -> 1x1 pair, ConvArgs::w2 with k2 == 1, yolomi/arch.py fuse_pairs): the tile holds
+// every output channel of the first conv (N <= BN), so after its K loop the activated tile is split hi / lo exactly as
+// its stored pair-layout tensor would be and written into the idle stage ring in the staging layout of the pixel
+// operand; W2 (prefetched into registers at the start, its latency hidden by the K loop) goes into an LDS slot in the
+// weight-operand layout, and the second GEMM (K = the first conv's N) runs as extra ring stages — the same fragment
+// reads and split MFMAs — before the epilogue stores the second conv's output.  The intermediate never reaches HBM and
+// the pair is one launch (the split pair wrote and read it back: model.1+cv1, the Detect cv2.l.1 -> cv2.l.2 chains).
+template <typename OutT, int BM, int BN, int KIND, int SPLIT, int KG, int NSTAGE, int SUB, bool X3 = false,
+          bool FUSE = false>
 __global__ __launch_bounds__(256 * KG) void conv_dma(const ConvArgs a) {
   constexpr int NW = 4 * KG;
   constexpr int TM = BM / 64, TN = BN / 64;
@@ -104,6 +112,12 @@ __global__ __launch_bounds__(256 * KG) void conv_dma(const ConvArgs a) {
   constexpr int SPW = 4 / KG;                        // 16-deep k sub-steps per wave per stage
   constexpr int NACC = TM * TN == 1 && SPW >= 2 ? 2 : 1;  // one 32x32 block per wave: alternate two accumulators
   __shared__ __attribute__((aligned(16))) char smem[NSTAGE * SB + 16 + 256];  // + split-K flag, L2 warm-up scratch
+  // FUSE: the second GEMM's K (the first conv's BN channels) in 64-deep storage sub-stages, W2 [KS2][BN rows][128 B]
+  constexpr int KS2 = FUSE ? (X3 ? 2 : 1) * BN / 64 : 0;
+  static_assert(!FUSE || (SPLIT == 1 && NSTAGE * SB >= KS2 * BM * 128), "fused pair: whole-K tiles, T fits the ring");
+  __shared__ __attribute__((aligned(16))) char w2s[FUSE ? KS2 * BN * 128 : 16];
+  constexpr int W2P = FUSE ? KS2 * BN * 8 / (256 * KG) : 1;  // 16-byte W2 pieces per thread
+  static_assert(!FUSE || (KS2 * BN * 8) % (256 * KG) == 0, "W2 pieces divide over the threads");
 
   YM_STAMP(0);
   const int tid = threadIdx.x, lane = tid & 63, wid = tid >> 6;
@@ -133,13 +147,30 @@ __global__ __launch_bounds__(256 * KG) void conv_dma(const ConvArgs a) {
   constexpr int XS = X3 ? 2 : 1;  // fp16 storage elements per logical channel
   const int s0_ctot = XS * a.s0_ctot, s0_coff = XS * a.s0_coff, s1_ctot = XS * a.s1_ctot, s1_coff = XS * a.s1_coff;
   const int C0s = XS * a.C0;
+  // FUSE: the epilogue writes the SECOND conv (N2 channels, bias2); bias4a holds the first conv's bias for the tile T
+  const int NOUT = FUSE ? a.N2 : a.N;
+  f32x4 bias4a[FUSE ? TN : 1][4];
+  u32x4 w2r[W2P];
+  if constexpr (FUSE) {
+#pragma unroll
+    for (int u = 0; u < W2P; ++u) {  // piece p: row n2 = p / (8 KS2), storage chunk cs = p % (8 KS2) of W2's K
+      const int p = tid + 256 * KG * u, n2 = p / (8 * KS2), cs = p % (8 * KS2);
+      const bool ok = n2 < a.N2 && 8 * cs < a.Kpad2;
+      // (unconditional load of a clamped address; the out-of-range pieces are zeroed when they go to LDS, after the
+      // K loop: a select here would make the compiler wait for the load on the spot)
+      w2r[u] = ym_gld<u32x4>(static_cast<const f16*>(a.w2) + (ok ? (size_t)n2 * a.Kpad2 + 8 * cs : 0));
+    }
+  }
   if (kg == 0) {
 #pragma unroll
     for (int j = 0; j < TN; ++j)
 #pragma unroll
       for (int q = 0; q < 4; ++q) {
         const int n = tn * BN + wn * (BN / 2) + 32 * j + 8 * q + 4 * h;
-        bias4[j][q] = n < a.N ? *reinterpret_cast<const f32x4*>(a.bias + n) : f32x4{0.f, 0.f, 0.f, 0.f};
+        const float* bsrc = FUSE ? a.bias2 : a.bias;
+        bias4[j][q] = n < NOUT ? *reinterpret_cast<const f32x4*>(bsrc + n) : f32x4{0.f, 0.f, 0.f, 0.f};
+        if constexpr (FUSE)
+          bias4a[j][q] = n < a.N ? *reinterpret_cast<const f32x4*>(a.bias + n) : f32x4{0.f, 0.f, 0.f, 0.f};
       }
 #pragma unroll
     for (int i = 0; i < TM; ++i) {
@@ -543,6 +574,110 @@ __global__ __launch_bounds__(256 * KG) void conv_dma(const ConvArgs a) {
           for (int e = 0; e < 4; ++e) acc[0][i][j][4 * q + e] = v[e];
         }
   }
+  if constexpr (FUSE) {
+    // ---- fused 1x1: T = the first conv's activated tile (exactly its stored split) in the ring, W2 in w2s, then
+    // the second GEMM (all of its K sub-steps in wave group 0) into acc[0]
+    __syncthreads();  // every wave is past its last read of the ring (and of the wave-group reduction area)
+    char* T = smem;
+    const int key = (l32 >> 1) & 7;
+    if (kg == 0) {
+#pragma unroll
+      for (int i = 0; i < TM; ++i)
+#pragma unroll
+        for (int j = 0; j < TN; ++j)
+#pragma unroll
+          for (int q = 0; q < 4; ++q) {
+            f16x4 hv, lv;
+#pragma unroll
+            for (int e = 0; e < 4; ++e) {
+              const float x = X3 ? ym_x3_pre(acc[0][i][j][4 * q + e], a.wsc, bias4a[j][q][e])
+                                 : acc[0][i][j][4 * q + e] + bias4a[j][q][e];
+              const float v = a.act ? (X3 ? ym_silu_x3(x) : ym_silu_fast(x)) : x;
+              hv[e] = (f16)v;
+              lv[e] = (f16)(v - (float)hv[e]);
+            }
+            const int row = wm * (BM / 2) + 32 * i + l32;
+            const int jc = (wn * (BN / 2) + 32 * j + 8 * q) >> 3;  // tile-local logical chunk
+            auto put = [&](int sc, f16x4 val) {                    // storage chunk sc of the second GEMM's K
+              *reinterpret_cast<f16x4*>(T + (sc >> 3) * BM * 128 + row * 128 + (((sc & 7) ^ key) << 4) + 8 * h) = val;
+            };
+            if constexpr (X3) {
+              put(2 * jc, hv);
+              put(2 * jc + 1, lv);
+            } else {
+              put(jc, hv);
+            }
+          }
+    }
+#pragma unroll
+    for (int u = 0; u < W2P; ++u) {
+      const int p = tid + 256 * KG * u, n2 = p / (8 * KS2), cs = p % (8 * KS2);
+      const bool ok = n2 < a.N2 && 8 * cs < a.Kpad2;
+      *reinterpret_cast<u32x4*>(w2s + (cs >> 3) * BN * 128 + n2 * 128 + (((cs & 7) ^ ((n2 >> 1) & 7)) << 4)) =
+          ok ? w2r[u] : u32x4{0u, 0u, 0u, 0u};
+    }
+    __syncthreads();
+    if (kg != 0) return;
+    f32x16 acc2[NACC][TM][TN];
+#pragma unroll
+    for (int u = 0; u < NACC; ++u)
+#pragma unroll
+      for (int i = 0; i < TM; ++i)
+#pragma unroll
+        for (int j = 0; j < TN; ++j)
+#pragma unroll
+          for (int r = 0; r < 16; ++r) acc2[u][i][j][r] = 0.f;
+#pragma unroll
+    for (int ks = 0; ks < KS2; ++ks) {
+      const char* sb = T + ks * BM * 128;
+      const char* sa = w2s + ks * BN * 128;
+      if constexpr (X3) {
+#pragma unroll
+        for (int s = 0; s < 4; s += 2) {  // sub-step pairs (0, 1), (2, 3): the main loop's three split MFMAs
+          const int ca[3] = {2 * s, 2 * s + 2, 2 * (s + h) + 1}, cbx[3] = {2 * s + h, 2 * s + 2 + h, 2 * (s + h)};
+          f16x8 fb[3][TM], fa[3][TN];
+#pragma unroll
+          for (int v = 0; v < 3; ++v) {
+            const int offa = ((ca[v] ^ key) << 4) + l32 * 128, offb = ((cbx[v] ^ key) << 4) + l32 * 128;
+#pragma unroll
+            for (int i = 0; i < TM; ++i)
+              fb[v][i] = *reinterpret_cast<const f16x8*>(sb + (wm * (BM / 2) + 32 * i) * 128 + offb);
+#pragma unroll
+            for (int j = 0; j < TN; ++j)
+              fa[v][j] = *reinterpret_cast<const f16x8*>(sa + (wn * (BN / 2) + 32 * j) * 128 + offa);
+          }
+#pragma unroll
+          for (int v = 0; v < 3; ++v)
+#pragma unroll
+            for (int i = 0; i < TM; ++i)
+#pragma unroll
+              for (int j = 0; j < TN; ++j)
+                acc2[v % NACC][i][j] =
+                    __builtin_amdgcn_mfma_f32_32x32x16_f16(fa[v][j], fb[v][i], acc2[v % NACC][i][j], 0, 0, 0);
+        }
+      } else {
+#pragma unroll
+        for (int s = 0; s < 4; ++s) {
+          const int off = (((2 * s + h) ^ key) << 4) + l32 * 128;
+#pragma unroll
+          for (int i = 0; i < TM; ++i)
+#pragma unroll
+            for (int j = 0; j < TN; ++j)
+              acc2[s % NACC][i][j] = __builtin_amdgcn_mfma_f32_32x32x16_f16(
+                  *reinterpret_cast<const f16x8*>(sa + (wn * (BN / 2) + 32 * j) * 128 + off),
+                  *reinterpret_cast<const f16x8*>(sb + (wm * (BM / 2) + 32 * i) * 128 + off), acc2[s % NACC][i][j], 0,
+                  0, 0);
+        }
+      }
+    }
+#pragma unroll
+    for (int i = 0; i < TM; ++i)
+#pragma unroll
+      for (int j = 0; j < TN; ++j) {
+        acc[0][i][j] = acc2[0][i][j];
+        if constexpr (NACC == 2) acc[0][i][j] += acc2[1][i][j];
+      }
+  }
   if (kg != 0) return;
 
   // ---- epilogue: lane owns channels nb + 32j + 8q + 4h + {0..3} of pixel pbm + 32i + l32
@@ -551,7 +686,7 @@ __global__ __launch_bounds__(256 * KG) void conv_dma(const ConvArgs a) {
   // the chunk as one 32-byte run (ym_p2_store4_pair) where the slice, the channel count and the pixel-shuffle
   // sub-pixel width keep every chunk whole (uniform)
   constexpr bool PAIRST = X3 && std::is_same<OutT, P2>::value;
-  const bool pairst = PAIRST && (a.pst & 1) && ((a.N | a.d_coff | a.d_ctot) & 7) == 0 && (!a.shuffle || (a.npr & 7) == 0);
+  const bool pairst = PAIRST && (a.pst & 1) && ((NOUT | a.d_coff | a.d_ctot) & 7) == 0 && (!a.shuffle || (a.npr & 7) == 0);
 #pragma unroll
   for (int i = 0; i < TM; ++i) {
     if (ep_m[i] >= a.M) continue;
@@ -562,12 +697,12 @@ __global__ __launch_bounds__(256 * KG) void conv_dma(const ConvArgs a) {
         const int n = tn * BN + wn * (BN / 2) + 32 * j + 8 * q + 4 * h;
         if constexpr (PAIRST) {
           if (pairst) {  // both lanes of a pair take this branch together (same pixel, n < N alike)
-            const bool okn = n < a.N;
+            const bool okn = n < NOUT;
             float v[4];
 #pragma unroll
             for (int e = 0; e < 4; ++e) {
-              const float x = ym_x3_pre(acc[0][i][j][4 * q + e], a.wsc, bias4[j][q][e]);
-              v[e] = (a.act ? ym_silu_x3(x) : x) + (float)res4[i][j][q][e];
+              const float x = ym_x3_pre(acc[0][i][j][4 * q + e], FUSE ? a.wsc2 : a.wsc, bias4[j][q][e]);
+              v[e] = ((FUSE ? a.act2 : a.act) ? ym_silu_x3(x) : x) + (float)res4[i][j][q][e];
             }
             size_t o = ep_obase[i] + n;
             if (a.shuffle) {
@@ -579,13 +714,13 @@ __global__ __launch_bounds__(256 * KG) void conv_dma(const ConvArgs a) {
             continue;
           }
         }
-        if (n >= a.N) continue;
+        if (n >= NOUT) continue;
         float v[4];
 #pragma unroll
         for (int e = 0; e < 4; ++e) {
-          const float x = X3 ? ym_x3_pre(acc[0][i][j][4 * q + e], a.wsc, bias4[j][q][e])
+          const float x = X3 ? ym_x3_pre(acc[0][i][j][4 * q + e], FUSE ? a.wsc2 : a.wsc, bias4[j][q][e])
                              : acc[0][i][j][4 * q + e] + bias4[j][q][e];
-          v[e] = (a.act ? (X3 ? ym_silu_x3(x) : ym_silu_fast(x)) : x) + (float)res4[i][j][q][e];
+          v[e] = ((FUSE ? a.act2 : a.act) ? (X3 ? ym_silu_x3(x) : ym_silu_fast(x)) : x) + (float)res4[i][j][q][e];
         }
         if (a.shuffle) {
           const int sub = n / a.npr;
@@ -679,7 +814,56 @@ hipError_t dispatch(const ConvArgs& a, int kind, int i, hipStream_t st) {
   return hipErrorInvalidValue;
 }
 
+// Fused conv -> 1x1 pairs (FUSE, x3): the DMA configurations (ids as in YM_DMA_CFGS) instantiated with the second GEMM
+// — whole-K tiles (no split) of BN 64, the first conv's N <= 64: s model.1+cv1 (3x3 s2 32 -> 64, 1x1 64 -> 64), the
+// Detect cv2.l.1 -> cv2.l.2 chains (3x3 64 -> 64, 1x1 64 -> 64 fp32 rows), s-seg cv4.l.1 -> cv4.l.2
+// (the 144-KB rings of ids 11 / 16 leave no room for W2)
+#define YM_DMA_FUSE_CFGS(X) \
+  X(7, 64, 64, 1, 2, 4, 2) X(18, 128, 64, 1, 1, 2, 1) X(21, 64, 64, 1, 1, 2, 2) X(24, 64, 64, 1, 1, 2, 1) \
+  X(26, 64, 64, 1, 2, 2, 2)
+
+template <typename OutT, int BM, int BN, int KG, int NS, int SUB>
+hipError_t launch_fuse(ConvArgs a, int kind, hipStream_t st) {
+  if ((4 / KG) % 2) return hipErrorInvalidValue;
+  if (a.N > BN || a.N2 > BN) return hipErrorInvalidValue;
+  if (SUB > 1 && (a.Kpad / DK) % SUB) return hipErrorInvalidValue;  // whole stages
+  const int tiles_m8 = ((a.M + BM - 1) / BM + 7) / 8 * 8;
+  a.tiles_n = 1;
+  const dim3 grid(tiles_m8), block(256 * KG);
+  if (kind == 4)
+    hipLaunchKernelGGL((conv_dma<OutT, BM, BN, 4, 1, KG, NS, SUB, true, true>), grid, block, 0, st, a);
+  else if (kind == 3)
+    hipLaunchKernelGGL((conv_dma<OutT, BM, BN, 3, 1, KG, NS, SUB, true, true>), grid, block, 0, st, a);
+  else
+    return hipErrorInvalidValue;
+  return hipGetLastError();
+}
+
+template <typename OutT>
+hipError_t dispatch_fuse(const ConvArgs& a, int kind, int i, hipStream_t st) {
+  switch (i) {
+#define YM_X(id, bm, bn, sp, kg, ns, sub) \
+  case id: return launch_fuse<OutT, bm, bn, kg, ns, sub>(a, kind, st);
+    YM_DMA_FUSE_CFGS(YM_X)
+#undef YM_X
+  }
+  return hipErrorInvalidValue;
+}
+
 }  // namespace
+
+// A fused conv -> 1x1 pair (ConvArgs::w2, k2 == 1) on the LDS-DMA kernel with the second GEMM in its epilogue (x3
+// plans; i: a DMA configuration id, only YM_DMA_FUSE_CFGS are instantiated)
+hipError_t ym_launch_conv_dma_fuse(int out_f32, const ConvArgs& a, int i, hipStream_t st) {
+  if (!a.x3 || !a.w2 || a.k2 != 1 || a.k != 3 || a.res || a.shuffle || a.src1 || a.up0 || !a.src0 || a.nchw)
+    return hipErrorInvalidValue;
+  if (a.Kpad % DK || (a.N & 7) || (a.N2 & 7) || a.Kpad2 < 2 * a.N || (a.d_ctot & 3) || (a.d_coff & 3))
+    return hipErrorInvalidValue;
+  const long lim = 0x7FFFFFF0L / 2;  // elements
+  if ((long)a.N * a.Kpad > lim || a.s0_elems > lim) return hipErrorInvalidValue;
+  const int kind = a.Cin8 % 8 == 0 ? 4 : 3;
+  return out_f32 ? dispatch_fuse<float>(a, kind, i, st) : dispatch_fuse<P2>(a, kind, i, st);
+}
 
 int ym_conv_dma_num_cfgs() { return kNumDma; }
 int ym_conv_dma_x3_num_cfgs() { return kNumDmaX3; }

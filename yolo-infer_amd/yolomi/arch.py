@@ -362,6 +362,7 @@ class GraphBuilder:
 
     # ------------------------------------------------------------------ fused pairs (f16 plans)
     STREAM_KS = {1: (2, 4, 6, 8), 3: (4, 6, 10, 18)}  # csrc/ym_conv_stream.hip K steps of 32 per kind
+    DMA_FUSE_MAX = 64                                # csrc/ym_conv_dma.hip YM_DMA_FUSE_CFGS: BN 64 (x3 plans)
     FUSE_MAX_N = 128                                 # csrc/ym_conv_stream.hip kFuseMaxN
     FUSE_MAX_LDS = 112 * 1024                        # csrc/ym_conv_stream.hip kMaxFusedBytes
 
@@ -469,6 +470,9 @@ class GraphBuilder:
         if a["k"] == 3 and (a["src1"] is not None or a["up0"]):
             return False
         N, N2 = a["c2"], b["c2"]
+        if (self.x3 and a["k"] == 3 and N <= self.DMA_FUSE_MAX and N2 <= self.DMA_FUSE_MAX and N % 8 == 0
+                and N2 % 8 == 0 and b["res"] is None):
+            return True  # the LDS-DMA kernel's fused-epilogue GEMM (csrc/ym_conv_dma.hip FUSE) takes any K
         xs = 2 if self.x3 else 1  # x3: fp16 storage K of the pair-chunk rows, W2 in hi and lo planes
         kpad = -(-xs * a["k"] * a["k"] * a["c1"] // 64) * 64
         if N > self.FUSE_MAX_N or N % 4 or N2 % 4 or kpad // 32 not in self.STREAM_KS[a["k"]]:
