@@ -10,9 +10,9 @@ run() {  # name limit cmd...
   if [ $rc -ge 124 ] || [ $rc -eq 134 ] || [ $rc -eq 139 ]; then exit $rc; fi
   return 0
 }
-run fpairs 600 python -u -m pytest tests/test_gpu_x3.py -q -x --timeout 500 --timeout-method thread -k "fused_pairs or layers_match or b8_matches"
+run fpairs 700 python -u -m pytest tests/test_gpu_x3.py -q -x --timeout 600 --timeout-method thread -k "fused_pairs or layers_match or b8_matches or segment or golden"
 rm -rf gpurun_out/tuned
-YM_TUNE_LOG=1 YM_RETABLE_OPS=model.1+cv1 run retable 400 python -u tools/retable.py
+run retable 400 python -u tools/retable.py
 cp gpurun_out/tuned/*.json yolo-infer_amd/yolomi/tuned/ 2>/dev/null
 run optable 200 python -u tools/op_table.py --model s --dtype x3
 run bench 400 python -u bench.py --steps 50 --warmup 10 --no-cpu

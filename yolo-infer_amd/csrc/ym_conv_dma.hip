@@ -118,6 +118,8 @@ __global__ __launch_bounds__(256 * KG) void conv_dma(const ConvArgs a) {
   __shared__ __attribute__((aligned(16))) char w2s[FUSE ? KS2 * BN * 128 : 16];
   constexpr int W2P = FUSE ? KS2 * BN * 8 / (256 * KG) : 1;  // 16-byte W2 pieces per thread
   static_assert(!FUSE || (KS2 * BN * 8) % (256 * KG) == 0, "W2 pieces divide over the threads");
+  // BN 128: W2 is 64 KB, 16 pieces per thread — too many registers to hold through the K loop; loaded after it
+  constexpr bool W2LATE = W2P > 8;
 
   YM_STAMP(0);
   const int tid = threadIdx.x, lane = tid & 63, wid = tid >> 6;
@@ -150,8 +152,8 @@ __global__ __launch_bounds__(256 * KG) void conv_dma(const ConvArgs a) {
   // FUSE: the epilogue writes the SECOND conv (N2 channels, bias2); bias4a holds the first conv's bias for the tile T
   const int NOUT = FUSE ? a.N2 : a.N;
   f32x4 bias4a[FUSE ? TN : 1][4];
-  u32x4 w2r[W2P];
-  if constexpr (FUSE) {
+  u32x4 w2r[W2LATE ? 1 : W2P];
+  if constexpr (FUSE && !W2LATE) {
 #pragma unroll
     for (int u = 0; u < W2P; ++u) {  // piece p: row n2 = p / (8 KS2), storage chunk cs = p % (8 KS2) of W2's K
       const int p = tid + 256 * KG * u, n2 = p / (8 * KS2), cs = p % (8 * KS2);
@@ -613,8 +615,13 @@ __global__ __launch_bounds__(256 * KG) void conv_dma(const ConvArgs a) {
     for (int u = 0; u < W2P; ++u) {
       const int p = tid + 256 * KG * u, n2 = p / (8 * KS2), cs = p % (8 * KS2);
       const bool ok = n2 < a.N2 && 8 * cs < a.Kpad2;
+      u32x4 v;
+      if constexpr (W2LATE)
+        v = ym_gld<u32x4>(static_cast<const f16*>(a.w2) + (ok ? (size_t)n2 * a.Kpad2 + 8 * cs : 0));
+      else
+        v = w2r[u];
       *reinterpret_cast<u32x4*>(w2s + (cs >> 3) * BN * 128 + n2 * 128 + (((cs & 7) ^ ((n2 >> 1) & 7)) << 4)) =
-          ok ? w2r[u] : u32x4{0u, 0u, 0u, 0u};
+          ok ? v : u32x4{0u, 0u, 0u, 0u};
     }
     __syncthreads();
     if (kg != 0) return;
@@ -815,12 +822,13 @@ hipError_t dispatch(const ConvArgs& a, int kind, int i, hipStream_t st) {
 }
 
 // Fused conv -> 1x1 pairs (FUSE, x3): the DMA configurations (ids as in YM_DMA_CFGS) instantiated with the second GEMM
-// — whole-K tiles (no split) of BN 64, the first conv's N <= 64: s model.1+cv1 (3x3 s2 32 -> 64, 1x1 64 -> 64), the
-// Detect cv2.l.1 -> cv2.l.2 chains (3x3 64 -> 64, 1x1 64 -> 64 fp32 rows), s-seg cv4.l.1 -> cv4.l.2
+// — whole-K tiles (no split) of BN 64 / 128 holding the first conv's N: s model.1+cv1 (3x3 s2 32 -> 64, 1x1 64 -> 64),
+// model.3+cv1 (3x3 s2 64 -> 128, 1x1 128 -> 128), the Detect cv2.l.1 -> cv2.l.2 chains (3x3 64 -> 64, 1x1 64 -> 64 fp32
+// rows), s-seg cv4.l.1 -> cv4.l.2
 // (the 144-KB rings of ids 11 / 16 leave no room for W2)
 #define YM_DMA_FUSE_CFGS(X) \
   X(7, 64, 64, 1, 2, 4, 2) X(18, 128, 64, 1, 1, 2, 1) X(21, 64, 64, 1, 1, 2, 2) X(24, 64, 64, 1, 1, 2, 1) \
-  X(26, 64, 64, 1, 2, 2, 2)
+  X(26, 64, 64, 1, 2, 2, 2) X(17, 128, 128, 1, 1, 2, 1) X(19, 64, 128, 1, 1, 2, 1)
 
 template <typename OutT, int BM, int BN, int KG, int NS, int SUB>
 hipError_t launch_fuse(ConvArgs a, int kind, hipStream_t st) {

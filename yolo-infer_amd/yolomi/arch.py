@@ -362,7 +362,7 @@ class GraphBuilder:
 
     # ------------------------------------------------------------------ fused pairs (f16 plans)
     STREAM_KS = {1: (2, 4, 6, 8), 3: (4, 6, 10, 18)}  # csrc/ym_conv_stream.hip K steps of 32 per kind
-    DMA_FUSE_MAX = 64                                # csrc/ym_conv_dma.hip YM_DMA_FUSE_CFGS: BN 64 (x3 plans)
+    DMA_FUSE_MAX = 128                               # csrc/ym_conv_dma.hip YM_DMA_FUSE_CFGS: BN <= 128 (x3 plans)
     FUSE_MAX_N = 128                                 # csrc/ym_conv_stream.hip kFuseMaxN
     FUSE_MAX_LDS = 112 * 1024                        # csrc/ym_conv_stream.hip kMaxFusedBytes
 
