@@ -1236,10 +1236,13 @@ __global__ __launch_bounds__(NMS_T) void nms_image(const NmsArgs a) {
   const int b = blockIdx.x;
   const int tid = threadIdx.x;
   if (a.dbg == 6) return;
+  unsigned long long* gk = a.keys + (size_t)b * a.kstride;
+  // the first NMS_BM keys are loaded before the count is known (the key rows hold kstride >= A entries): the count
+  // and the keys are ONE memory round trip instead of two dependent ones; entries past the count are ignored
+  const unsigned long long kpre = tid < NMS_BM && tid < a.kstride ? gk[tid] : 0ull;
   int n = a.counts[b];
   if (n > a.A) n = a.A;
   if (a.dbg == 7) return;
-  unsigned long long* gk = a.keys + (size_t)b * a.kstride;
   const size_t ib = (size_t)b * a.A;
   const int rowlen = 6 + a.nm;
   float* out = a.dets + (size_t)b * a.max_det * rowlen;
@@ -1248,7 +1251,7 @@ __global__ __launch_bounds__(NMS_T) void nms_image(const NmsArgs a) {
     // lane i holds candidate i; bitonic sort by key across lanes, then the greedy scan with shuffles.
     if (tid >= 64) return;
     const int lane = tid;
-    unsigned long long key = lane < n ? gk[lane] : 0ull;
+    unsigned long long key = lane < n ? kpre : 0ull;
 #pragma unroll
     for (int size = 2; size <= 64; size <<= 1) {
 #pragma unroll
@@ -1297,7 +1300,7 @@ __global__ __launch_bounds__(NMS_T) void nms_image(const NmsArgs a) {
     unsigned long long* sorted = sk + NMS_BM;
     unsigned long long* mask = reinterpret_cast<unsigned long long*>(sbx + NMS_BM);  // [ne][W]
     unsigned long long ki = 0;
-    if (tid < n) sk[tid] = ki = gk[tid];
+    if (tid < n) sk[tid] = ki = kpre;
     if (tid == n) sk[n] = 0ull;  // pad to an even count (keys are > 0: the score bits of a candidate are)
     __syncthreads();
     if (a.dbg == 1) return;
