@@ -21,3 +21,23 @@ def pytest_collection_modifyitems(config, items):
     for it in items:
         if "gpu" in it.keywords:
             it.add_marker(skip)
+
+
+@pytest.fixture(autouse=True, scope="module")
+def _release_module_models(request):
+    """GPU test modules cache their models (contexts, arenas, captured graphs) in module-level dicts; release them when
+    the module is done, so the whole `-m gpu` suite does not keep every earlier module's contexts alive."""
+    yield
+    for name in ("_models", "_cache"):
+        d = getattr(request.module, name, None)
+        if isinstance(d, dict):
+            d.clear()
+    import gc
+    gc.collect()
+    try:
+        import torch
+        if torch.cuda.is_available():
+            torch.cuda.synchronize()
+            torch.cuda.empty_cache()
+    except Exception:
+        pass
