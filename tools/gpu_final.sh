@@ -14,7 +14,7 @@ run() {  # name limit cmd...
   return 0
 }
 run smoke 300 python -u -c "import __graft_entry__ as g; g.smoke(); print('smoke ok')"
-run suite 1200 python -u -m pytest tests -m gpu -q -p no:cacheprovider --timeout 300 --timeout-method thread
+run suite 1200 python -u -X faulthandler -m pytest tests -m gpu -q -p no:cacheprovider --timeout 300 --timeout-method thread
 run bench_s 400 python -u bench.py
 run bench_n 400 python -u bench.py --model n --no-f16
 run bench_seg 400 python -u bench.py --task segment --batch 4 --no-f16
