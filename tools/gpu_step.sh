@@ -10,9 +10,9 @@ run() {  # name limit cmd...
   if [ $rc -ge 124 ] || [ $rc -eq 134 ] || [ $rc -eq 139 ]; then exit $rc; fi
   return 0
 }
-run tests 900 python -u -m pytest tests/test_gpu_x3.py tests/test_gpu_parity.py -q -x --timeout 300 --timeout-method thread
-: > gpurun_out/nms_phases.log
-for d in 0 1 6; do
-  YM_NMS_DBG=$d timeout -k 10 120 python -u tools/nms_phases.py >> gpurun_out/nms_phases.log 2>&1 || { echo "nms rc=$?" >> gpurun_out/steps.log; exit 1; }
-done
-run bench 400 python -u bench.py --steps 50 --warmup 10 --no-cpu --no-f16
+run fpairs 700 python -u -m pytest tests/test_gpu_x3.py -q -x --timeout 600 --timeout-method thread -k "fused_pairs"
+rm -rf gpurun_out/tuned
+YM_RETABLE_OPS=model.1+cv1,model.3+cv1,model.5+cv1,model.23.cv2.0.1+2,model.23.cv2.1.1+2,model.23.cv2.2.1+2,model.23.proto.cv2+cv3,model.23.cv4.0.1+2,model.23.cv4.1.1+2,model.23.cv4.2.1+2 run retable 400 python -u tools/retable.py
+cp gpurun_out/tuned/*.json yolo-infer_amd/yolomi/tuned/ 2>/dev/null
+run optable 200 python -u tools/op_table.py --model s --dtype x3
+run bench 400 python -u bench.py --steps 100 --warmup 10 --no-cpu

@@ -828,7 +828,8 @@ hipError_t dispatch(const ConvArgs& a, int kind, int i, hipStream_t st) {
 // (the 144-KB rings of ids 11 / 16 leave no room for W2)
 #define YM_DMA_FUSE_CFGS(X) \
   X(7, 64, 64, 1, 2, 4, 2) X(18, 128, 64, 1, 1, 2, 1) X(21, 64, 64, 1, 1, 2, 2) X(24, 64, 64, 1, 1, 2, 1) \
-  X(26, 64, 64, 1, 2, 2, 2) X(17, 128, 128, 1, 1, 2, 1) X(19, 64, 128, 1, 1, 2, 1)
+  X(26, 64, 64, 1, 2, 2, 2) X(17, 128, 128, 1, 1, 2, 1) X(19, 64, 128, 1, 1, 2, 1) X(3, 64, 64, 1, 2, 4, 1)     \
+  X(5, 128, 64, 1, 2, 4, 1) X(25, 128, 64, 1, 1, 3, 1)
 
 template <typename OutT, int BM, int BN, int KG, int NS, int SUB>
 hipError_t launch_fuse(ConvArgs a, int kind, hipStream_t st) {
