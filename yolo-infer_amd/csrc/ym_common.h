@@ -164,20 +164,6 @@ __device__ __forceinline__ void ym_p2_store4_pair(P2* p, const float* v, bool od
     *reinterpret_cast<f16x8*>((u & ~(uintptr_t)31) + (odd ? 16 : 0)) = o;
   }
 }
-// v_permlane32_swap on a whole 8 x fp16 fragment: lanes 32-63 of a trade places with lanes 0-31 of b, so
-// a = [a.lower | b.lower], b = [a.upper | b.upper] (per lane half; cdna_hip_programming.md T21 semantics).
-__device__ __forceinline__ void ym_swap32(f16x8& a, f16x8& b) {
-  typedef unsigned u32x4_t __attribute__((ext_vector_type(4)));
-  u32x4_t x = __builtin_bit_cast(u32x4_t, a), y = __builtin_bit_cast(u32x4_t, b);
-#pragma unroll
-  for (int k = 0; k < 4; ++k) {
-    const auto r = __builtin_amdgcn_permlane32_swap(x[k], y[k], false, false);
-    x[k] = r[0];
-    y[k] = r[1];
-  }
-  a = __builtin_bit_cast(f16x8, x);
-  b = __builtin_bit_cast(f16x8, y);
-}
 __device__ __forceinline__ void ym_p2_load4(const P2* p, float* v) {  // v[e] = hi + lo
   const f16* q = ym_p2_hi4(p);
   const f16x4 h = *reinterpret_cast<const f16x4*>(q), l = *reinterpret_cast<const f16x4*>(q + 8);
