@@ -658,6 +658,23 @@ static void build_schedule(ym_ctx* c) {
   const char* env = getenv("YM_BRANCHES");
   const int def = (c->dtype == YM_DT_F16 || c->dtype == YM_DT_X3) && c->task == 0 ? S : 1;
   const int maxs = env && *env ? (atoi(env) < 1 ? 1 : (atoi(env) > S ? S : atoi(env))) : def;
+  // YM_SCHED=crit: continue the stream of the dependency expected to finish LAST (a per-op time estimate at
+  // 640², B = 8: ~6 us per launch plus MACs at ~40 TMAC/s), instead of the latest dependency in program order — a
+  // join then waits on the other streams' earlier producers, and the slowest chain flows straight into its consumer
+  // without a cross-queue wait (the kernel trace shows ~10 us idle at such joins, e.g. before decode)
+  const char* sched = getenv("YM_SCHED");
+  const bool crit = sched && !strcmp(sched, "crit");
+  std::vector<double> fin(nop, 0.0), sfin(S, 0.0);
+  auto est_us = [&](const Op& o) {
+    const int32_t* r = o.r;
+    double macs = 0;
+    if (r[0] == OP_CONV && r[13] >= 0 && r[13] < nbuf) {
+      const int f = c->bufs[r[13]].f > 0 ? c->bufs[r[13]].f : 8;  // output stride (head rows: level stride unknown)
+      const double px = 8.0 * (640.0 / f) * (640.0 / f);
+      macs = px * r[1] * r[1] * (double)r[3] * r[4] * (r[30] ? 2 : 1);
+    }
+    return 6.0 + macs / 40e6;
+  };
   for (int i = 0; i < nop; ++i) {
     rw(c->ops[i], rd, wr);
     std::vector<int> deps;
@@ -670,7 +687,12 @@ static void build_schedule(ym_ctx* c) {
     int jmax = -1;
     for (int j : deps) jmax = j > jmax ? j : jmax;
     int s = -1;
-    if (jmax >= 0 && tail[c->br_of[jmax]] == jmax) s = c->br_of[jmax];
+    if (crit) {  // the stream tail among the dependencies with the latest estimated finish
+      double best = -1;
+      for (int j : deps)
+        if (tail[c->br_of[j]] == j && fin[j] > best) { best = fin[j]; s = c->br_of[j]; }
+    }
+    if (s < 0 && jmax >= 0 && tail[c->br_of[jmax]] == jmax) s = c->br_of[jmax];
     if (s < 0 && jmax >= 0 && used < maxs) s = used++;
     if (s < 0) {  // the stream whose tail is oldest
       s = 0;
@@ -685,6 +707,9 @@ static void build_schedule(ym_ctx* c) {
       known[s][t] = j;
       for (int u = 0; u < S; ++u) if (snap[j][u] > known[s][u]) known[s][u] = snap[j][u];
     }
+    double start = sfin[s];
+    for (int j : deps) start = fin[j] > start ? fin[j] : start;
+    fin[i] = sfin[s] = start + est_us(c->ops[i]);
     c->br_of[i] = s;
     tail[s] = i;
     known[s][s] = i;
