@@ -4,6 +4,8 @@ import sys
 import pytest
 
 ROOT = os.path.dirname(os.path.dirname(os.path.abspath(__file__)))
+# a host crash inside libyolomi prints its native backtrace before faulthandler's Python stack (csrc/ym_runtime.cpp)
+os.environ.setdefault("YM_SEGV_TRACE", "1")
 for p in (os.path.join(ROOT, "yolo-infer_amd"), ROOT):
     if p not in sys.path:
         sys.path.insert(0, p)

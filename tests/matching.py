@@ -132,3 +132,25 @@ def ref_f64_slack(ref: np.ndarray, exact: np.ndarray, tol_xy: float = 1e-3) -> n
         if len(cand):
             out[i] = tol_xy + float(np.abs(exact[cand, :4] - ref[i, :4]).max(1).min())
     return out
+
+
+def dist_to_exact(exact: np.ndarray, got: np.ndarray):
+    """The build's own distance from the exact answer: for every build detection with a same-class float64 detection
+    at IoU >= 0.99 (`exact`: oracle predict_exact rows), the coordinate and score distance to the nearest one.
+    Returns (max |dxy| px, max |dscore|, detections compared, detections without a float64 counterpart)."""
+    dxy = ds = 0.0
+    n = miss = 0
+    if not len(got):
+        return dxy, ds, n, miss
+    ious = iou_matrix(got[:, :4], exact[:, :4]) if len(exact) else np.zeros((len(got), 0))
+    for i in range(len(got)):
+        c = np.where((exact[:, 5] == got[i, 5]) & (ious[i] >= 0.99))[0] if len(exact) else []
+        if not len(c):
+            miss += 1
+            continue
+        d = np.abs(exact[c, :4] - got[i, :4]).max(1)
+        k = c[int(np.argmin(d))]
+        dxy = max(dxy, float(d.min()))
+        ds = max(ds, float(abs(exact[k, 4] - got[i, 4])))
+        n += 1
+    return dxy, ds, n, miss

@@ -405,3 +405,14 @@ def test_resource_monitor_contract():
     assert {"timestamp", "cpu_percent", "memory_percent", "memory_used", "memory_total", "gpu_usage"} <= set(p)
     avg = m.get_average_usage()
     assert "avg_cpu_percent" in avg and "avg_memory_percent" in avg
+
+
+def test_x3_weight_exp_is_clamped_to_the_loader_range():
+    """a nearly pruned conv (max |w| < 2^-50) must still pack into a blob ym_load_weights accepts
+    (|s| <= 64, csrc/ym_runtime.cpp conv_args), and a huge one too; ordinary matrices keep max |w·2^s| in (2^13, 2^14]."""
+    from yolomi.plan import X3_WEXP_MAX
+    assert x3_weight_exp(np.full((8, 8), 2.0 ** -60, np.float32)) == X3_WEXP_MAX
+    assert x3_weight_exp(np.full((8, 8), 2.0 ** 90, np.float32)) == -X3_WEXP_MAX
+    w = np.full((8, 8), 0.03, np.float32)
+    assert 2 ** 13 < 0.03 * 2.0 ** x3_weight_exp(w) <= 2 ** 14
+    assert x3_weight_exp(np.zeros((8, 8), np.float32)) == 0

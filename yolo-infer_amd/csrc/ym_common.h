@@ -324,32 +324,10 @@ struct ConvArgs {
   // LDS-DMA kernels (csrc/ym_conv_dma.hip): request every line of the workgroup's K range into L2 before the ring
   // starts (latency-bound small-M layers; YM_DMA_PF = the largest M it is used for, 0 = never)
   int pf;
-  // 256+ zero bytes of device memory: the residual source of a conv without one, so the epilogue-operand loads are
-  // unconditional (a load under a per-lane or per-kernel condition made the compiler wait for it on the spot)
-  const void* zeros;
   // fused depthwise (yolomi/arch.py GraphBuilder.fuse_dw; csrc/ym_conv_dwpw.hip): src0 is the DEPTHWISE input and this
   // 1x1 conv consumes act(dw3x3(src0) + dw_b) computed in registers.  dw_w [9][C0] fp32, dw_b [C0]; null: no depthwise
   const float* dw_w; const float* dw_b; int dw_act;
 };
-
-// Warm the scalar cache with every line of a kernel's argument block in ONE round trip: the compiler loads kernel
-// arguments lazily at first use, and each batch of s_loads ends in an lgkmcnt(0) wait for a line that is not yet in
-// the scalar cache (the argument block is freshly written per launch: a memory round trip each).  A ConvArgs-sized
-// block took ~6 such waits, ~3k cycles before the first DMA issue (tools/dma_probe.hip); after this the lazy loads
-// hit the cache.
-template <int BYTES>
-__device__ __forceinline__ void ym_warm_kernargs() {
-  const __attribute__((address_space(4))) char* kp =
-      (const __attribute__((address_space(4))) char*)__builtin_amdgcn_kernarg_segment_ptr();
-  static_assert(BYTES <= 16 * 64, "argument block too large");
-  int v[16];
-#pragma unroll
-  for (int i = 0; i < 16; ++i)
-    if (i * 64 < BYTES) v[i] = *(const __attribute__((address_space(4))) int*)(kp + i * 64);
-#pragma unroll
-  for (int i = 0; i < 16; ++i)
-    if (i * 64 < BYTES) asm volatile("" ::"s"(v[i]));
-}
 
 // A load through the global address space (global_load, vmcnt only; a generic pointer makes the compiler emit a
 // flat load, which also counts in lgkmcnt and so is waited for together with the scalar/LDS traffic).

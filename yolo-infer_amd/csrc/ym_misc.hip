@@ -68,12 +68,14 @@ __global__ __launch_bounds__(256) void input_stats(const float* __restrict__ x, 
   if (tid == 0) {
     m = fmaxf(fmaxf(wm[0], wm[1]), fmaxf(wm[2], wm[3]));
     __hip_atomic_store(part + blockIdx.x, f2ord(m), __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);  // sc1
-    asm volatile("s_waitcnt vmcnt(0)" ::: "memory");
-    const int t = __hip_atomic_fetch_add(ticket, 1, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
+    // release: the partial is visible at agent scope before the ticket moves; acquire: the last block sees every
+    // partial released before its ticket
+    const int t = __hip_atomic_fetch_add(ticket, 1, __ATOMIC_ACQ_REL, __HIP_MEMORY_SCOPE_AGENT);
     last = t == (int)gridDim.x - 1;
   }
   __syncthreads();
   if (!last) return;
+  __builtin_amdgcn_fence(__ATOMIC_ACQUIRE, "agent");
   int r = f2ord(-INFINITY);
   for (int b = tid; b < (int)gridDim.x; b += 256)
     r = max(r, __hip_atomic_load(part + b, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT));

@@ -6,6 +6,9 @@
 #include <hip/hip_runtime.h>
 
 #include <dlfcn.h>
+#include <execinfo.h>
+#include <signal.h>
+#include <unistd.h>
 
 #include <algorithm>
 #include <cmath>
@@ -21,6 +24,36 @@
 namespace {
 
 thread_local std::string g_err;
+
+// YM_SEGV_TRACE=1: on SIGSEGV / SIGBUS print the native backtrace (library + offset per frame) to stderr, then hand
+// the signal to the handler installed before ours (Python's faulthandler under pytest, which prints the Python
+// stack), so a host crash inside the runtime leaves a trace that names the frame.
+struct sigaction g_prev_sig[2];
+void segv_trace(int sig, siginfo_t* si, void* uc) {
+  static const char msg[] = "[yolomi] fatal signal, native backtrace:\n";
+  void* fr[64];
+  const int n = backtrace(fr, 64);
+  if (write(2, msg, sizeof msg - 1) < 0) {}
+  backtrace_symbols_fd(fr, n, 2);
+  const struct sigaction& p = g_prev_sig[sig == SIGBUS];
+  if ((p.sa_flags & SA_SIGINFO) && p.sa_sigaction) return p.sa_sigaction(sig, si, uc);
+  if (!(p.sa_flags & SA_SIGINFO) && p.sa_handler != SIG_DFL && p.sa_handler != SIG_IGN) return p.sa_handler(sig);
+  signal(sig, SIG_DFL);
+  raise(sig);
+}
+__attribute__((constructor)) void install_segv_trace() {
+  const char* e = getenv("YM_SEGV_TRACE");
+  if (!e || !*e || *e == '0') return;
+  void* warm[2];
+  (void)backtrace(warm, 2);  // loads the unwinder now, not inside the handler
+  struct sigaction sa;
+  memset(&sa, 0, sizeof(sa));
+  sa.sa_sigaction = segv_trace;
+  sa.sa_flags = SA_SIGINFO | SA_ONSTACK;
+  sigemptyset(&sa.sa_mask);
+  sigaction(SIGSEGV, &sa, &g_prev_sig[0]);
+  sigaction(SIGBUS, &sa, &g_prev_sig[1]);
+}
 
 int fail(int code, const char* fmt, ...) {
   char buf[512];
@@ -42,6 +75,8 @@ constexpr int32_t kMagic = 0x4C504D59;  // 'YMPL'
 constexpr int kHdr = 32, kBufRec = 8, kOpRec = 32, kNameLen = 48;
 constexpr int kSplitCounters = 16384;  // split-K tiles per conv launch (csrc/ym_conv_dma.hip)
 constexpr int kMaxLanes = 4;           // concurrent batch slices in one forward graph (<= GPU_MAX_HW_QUEUES)
+constexpr size_t kMaxGraphs = 16;
+constexpr size_t kMiscBytes = 16384;  // ym_ctx::d_misc      // captured forwards cached per context (the oldest is retired first)
 
 enum OpKind { OP_INPUT = 1, OP_CONV = 2, OP_DW = 3, OP_SPPF = 4, OP_ATTN = 5, OP_DECODE = 6, OP_NMS = 7, OP_REQ = 8 };
 
@@ -72,6 +107,7 @@ struct GraphEntry {
   hipGraph_t graph;
   hipGraphExec_t exec;
   float* dets = nullptr;                 // the rows the exec's NMS nodes write now
+  hipEvent_t done = nullptr;             // recorded behind every launch of `exec` (retire_graph waits on it)
   std::vector<hipGraphNode_t> nms_nodes;  // empty: dets is part of the key
   std::vector<NmsArgs> nms_args;
 };
@@ -116,6 +152,20 @@ int repoint_dets(GraphEntry& ge, float* d_dets) {
   }
   ge.dets = d_dets;
   return YM_OK;
+}
+
+// Destroy a captured forward only after its last launch has finished on whatever stream it was replayed on: the
+// HIP runtime may still hold the exec's launch state (kernel arguments, the packet chain) while it is in flight.
+void retire_graph(GraphEntry& g) {
+  if (g.done) {
+    (void)hipEventSynchronize(g.done);
+    (void)hipEventDestroy(g.done);
+    g.done = nullptr;
+  }
+  if (g.exec) (void)hipGraphExecDestroy(g.exec);
+  if (g.graph) (void)hipGraphDestroy(g.graph);
+  g.exec = nullptr;
+  g.graph = nullptr;
 }
 
 }  // namespace
@@ -203,10 +253,7 @@ struct ym_ctx {
     for (hipEvent_t e : op_ev) (void)hipEventDestroy(e);
   }
   void clear_graphs() {
-    for (auto& g : graphs) {
-      (void)hipGraphExecDestroy(g.exec);
-      (void)hipGraphDestroy(g.graph);
-    }
+    for (auto& g : graphs) retire_graph(g);
     graphs.clear();
   }
   int buf_P(int b) const {
@@ -239,6 +286,7 @@ int ensure_workspace(ym_ctx* c, int B, int H, int W) {
   const int nB = (H == c->cH && W == c->cW && B < c->cB) ? c->cB : B;
   c->clear_graphs();
   if (c->d_arena) {
+    HIPCK(hipDeviceSynchronize());  // eager forwards on any stream may still read or write the old arena
     HIPCK(hipFree(c->d_arena));
     c->d_arena = nullptr;
   }
@@ -390,7 +438,6 @@ int conv_args(ym_ctx* c, const Op& op, int B, const float* d_in, float in_eps, C
       a.cnt_cap = kSplitCounters;
       static const int pf_max = [] { const char* e = getenv("YM_DMA_PF"); return e ? atoi(e) : 0; }();
       a.pf = a.M <= pf_max;
-      a.zeros = c->d_misc + 12288;  // zeroed at ym_create, never written
       return YM_OK;
 }
 
@@ -602,10 +649,9 @@ int ym_create(int device, const ym_model_desc* desc, ym_ctx** out) {
   hipError_t e = hipStreamCreateWithFlags(&c->cap_stream, hipStreamNonBlocking);
   for (int l = 1; l < kMaxLanes && e == hipSuccess; ++l) e = hipStreamCreateWithFlags(&c->lane_streams[l], hipStreamNonBlocking);
   if (e == hipSuccess) e = hipEventCreateWithFlags(&c->fork_ev, hipEventDisableTiming);
-  // ym_input_max's ctl region (slots, ticket, partials: YM_CTL_BYTES) at 0, broadcast control words at 8 KB, a zero
-  // page at 12 KB (ConvArgs::zeros)
-  if (e == hipSuccess) e = hipMalloc(&c->d_misc, 16384);
-  if (e == hipSuccess) e = hipMemset(c->d_misc, 0, 16384);
+  // ym_input_max's ctl region (slots, ticket, partials: YM_CTL_BYTES) at 0, broadcast control words at 8 KB
+  if (e == hipSuccess) e = hipMalloc(&c->d_misc, kMiscBytes);
+  if (e == hipSuccess) e = hipMemset(c->d_misc, 0, kMiscBytes);
   for (int l = 1; l < kMaxLanes && e == hipSuccess; ++l) e = hipEventCreateWithFlags(&c->join_ev[l], hipEventDisableTiming);
   if (e != hipSuccess) {
     delete c;
@@ -839,6 +885,7 @@ int ym_load_weights(ym_ctx* c, const void* blob, size_t bytes) {
   // buffers); the weights are replaced below
   c->loaded = false;
   c->clear_graphs();
+  if (c->d_arena || c->d_weights) HIPCK(hipDeviceSynchronize());  // no launch may still use the old plan's memory
   if (c->d_arena) HIPCK(hipFree(c->d_arena));
   c->d_arena = nullptr;
   c->arena_bytes = 0;
@@ -976,19 +1023,20 @@ int ym_infer(ym_ctx* c, const float* d_in, int B, int H, int W, const ym_infer_a
   GraphKey key_d = key;  // the key of a graph whose NMS nodes could not be re-pointed
   key_d.dets = d_dets;
   for (auto& g : c->graphs) {
-    if (g.key == key) {  // re-pointable: new rows through the NMS nodes' parameters
-      if (g.dets != d_dets && (rc = repoint_dets(g, d_dets))) return rc;
+    if (g.key == key || g.key == key_d) {
+      // re-pointable: new rows through the NMS nodes' parameters (the exec's previous launch must have finished:
+      // the parameters of a launch still queued are not ours to change)
+      if (g.key == key && g.dets != d_dets) {
+        HIPCK(hipEventSynchronize(g.done));
+        if ((rc = repoint_dets(g, d_dets))) return rc;
+      }
       HIPCK(hipGraphLaunch(g.exec, st));
-      return YM_OK;
-    }
-    if (g.key == key_d) {
-      HIPCK(hipGraphLaunch(g.exec, st));
+      HIPCK(hipEventRecord(g.done, st));
       return YM_OK;
     }
   }
-  if (c->graphs.size() >= 16) {
-    (void)hipGraphExecDestroy(c->graphs.front().exec);
-    (void)hipGraphDestroy(c->graphs.front().graph);
+  if (c->graphs.size() >= kMaxGraphs) {  // evict the oldest capture once its last replay has drained
+    retire_graph(c->graphs.front());
     c->graphs.erase(c->graphs.begin());
   }
   // capture on the private stream (lane streams join through the fork event), replay on the caller's stream
@@ -1001,12 +1049,18 @@ int ym_infer(ym_ctx* c, const float* d_in, int B, int H, int W, const ym_infer_a
   }
   GraphEntry ge;
   HIPCK(hipStreamEndCapture(c->cap_stream, &ge.graph));
-  HIPCK(hipGraphInstantiate(&ge.exec, ge.graph, nullptr, nullptr, 0));
+  hipError_t e = hipGraphInstantiate(&ge.exec, ge.graph, nullptr, nullptr, 0);
+  if (e == hipSuccess) e = hipEventCreateWithFlags(&ge.done, hipEventDisableTiming);
+  if (e != hipSuccess) {
+    retire_graph(ge);
+    return fail(YM_EHIP, "graph instantiate: %s", hipGetErrorString(e));
+  }
   ge.dets = d_dets;
-  static const bool no_repoint = [] { const char* e = getenv("YM_GRAPH_REPOINT"); return e && *e == '0'; }();
+  static const bool no_repoint = [] { const char* v = getenv("YM_GRAPH_REPOINT"); return v && *v == '0'; }();
   ge.key = (!no_repoint && find_nms_nodes(ge)) ? key : key_d;
   c->graphs.push_back(ge);
   HIPCK(hipGraphLaunch(ge.exec, st));
+  HIPCK(hipEventRecord(ge.done, st));
   return YM_OK;
 }
 

@@ -146,8 +146,30 @@ def split_batch_max(model, x: torch.Tensor, group=None) -> torch.Tensor:
     per-step collective; a serving splitter would ship the max with each shard instead."""
     rule = GlobalBatchMax(model.model.engine, group=group)
     m = rule(x).clone()
-    model.global_batch_max = lambda _x: m
+    model.global_batch_max = PinnedBatchMax(x, m)
     return m
+
+
+class PinnedBatchMax:
+    """The global statistic split_batch_max took for ONE shard tensor.  It answers only for that tensor, unmodified
+    (same storage, shape and version counter): any other input raises instead of silently reusing the old /255
+    decision — a rank cannot re-run the all-reduce alone (the other ranks would not join it), so the caller must
+    take the decision again where the new batch is split (split_batch_max) or use enable_global_rule."""
+
+    def __init__(self, x: torch.Tensor, m: torch.Tensor):
+        self.key = self._key(x)
+        self.m = m
+
+    @staticmethod
+    def _key(x: torch.Tensor):
+        return (x.data_ptr(), tuple(x.shape), x._version)
+
+    def __call__(self, x: torch.Tensor) -> torch.Tensor:
+        if self._key(x) != self.key:
+            raise RuntimeError("split_batch_max pinned LoadTensor's /255 decision for another input tensor (or this "
+                               "one was modified since): call split_batch_max for the new shard, or enable_global_rule "
+                               "for a per-call all-reduce")
+        return self.m
 
 
 def digest(blob: bytes) -> str:

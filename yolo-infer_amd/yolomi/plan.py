@@ -98,6 +98,7 @@ def _dw_weights(key: str, sd):
     return np.ascontiguousarray(w.reshape(C, 9).T).astype(np.float32), b  # [9][C]
 
 
+X3_WEXP_MAX = 64  # |s| the runtime accepts for an x3 weight scale 2^s (csrc/ym_runtime.cpp conv_args)
 X3_WMAX_LOG2 = 14  # x3 weight scaling: max |w|·2^s in (2^13, 2^14] (fp16 max 65504; csrc/ym_common.h ConvArgs::wsc)
 
 
@@ -111,7 +112,9 @@ def x3_weight_exp(w: np.ndarray) -> int:
         raise ValueError("non-finite conv weight")
     if m == 0.0:
         return 0
-    return int(X3_WMAX_LOG2 - np.ceil(np.log2(m)))
+    # clamped to the range ym_load_weights accepts (conv_args: |s| <= X3_WEXP_MAX): a nearly pruned matrix (max |w|
+    # below 2^-50) keeps s = 64 and with it subnormal lo parts, instead of a blob the loader rejects
+    return int(min(max(X3_WMAX_LOG2 - np.ceil(np.log2(m)), -X3_WEXP_MAX), X3_WEXP_MAX))
 
 
 def x3_pair_rows(w: np.ndarray, s: int) -> np.ndarray:
