@@ -72,7 +72,9 @@ typedef struct {
   int use_graph;       /* 1: capture/replay a HIP graph per (shape, pointers, args); 0: eager launches */
   int lanes;           /* 1..4 image slices run as concurrent graph branches (0 = 1); conv tile tables are looked
                           up at the slice batch ceil(B / lanes) */
-  int reserved0;
+  int counts_after_dets; /* 1: the detection counts are also written, as B int32 words, right after the B x max_det
+                            rows of d_dets (d_dets must hold B*max_det*(6+nm) + B floats): a caller that hands in
+                            fresh rows per call gets that call's counts with them, and may read them later */
   const float* d_batch_max; /* NULL: LoadTensor's /255 rule reduces over d_input (the whole batch).  Else a device
                                pointer to ONE float, the max over the GLOBAL batch (batch-sharded multi-GPU: every
                                rank's ym_input_max, all-reduced MAX), read by the forward instead of its shard */

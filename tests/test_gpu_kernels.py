@@ -177,3 +177,24 @@ def test_graph_cache_eviction_with_queued_replays():
         torch.cuda.synchronize()
         for o in outs:
             assert torch.equal(o[0, :n], ref[0, :n])
+
+
+def test_async_predict_counts_behind_rows():
+    """predict() on a tensor batch does not synchronise: the NMS kernel writes each call's B counts behind its fresh
+    rows (ym_infer_args.counts_after_dets) and the Results read them on first access.  Several calls on different
+    inputs queued back to back (graph replays, lanes 1 and 2, a side stream current when they are read) give the
+    detections of the synchronous calls (sync=True), bit for bit."""
+    from core.model import YOLO11Model
+    for dtype, lanes in (("x3", 1), ("f16", 2)):
+        m = YOLO11Model(task="detect", size="n", device="cuda:0", dtype=dtype, verbose=False)
+        m.model.engine.lanes = lanes
+        xs = [synthetic_batch(3, 320, 40 + i, DEV) for i in range(4)]
+        ref = [[r.boxes.data.clone() for r in m.predict(x, conf=0.05, sync=True)] for x in xs]
+        torch.cuda.synchronize()
+        got = [m.predict(x, conf=0.05) for x in xs for _ in range(2)]
+        with torch.cuda.stream(torch.cuda.Stream()):
+            for k, res in enumerate(got):
+                assert len(res) == 3
+                for r, d in zip(res, ref[k // 2]):
+                    assert torch.equal(r.boxes.data, d)
+        assert sum(len(d) for d in ref[0]) > 0

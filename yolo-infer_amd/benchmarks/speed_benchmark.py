@@ -111,12 +111,12 @@ class SpeedBenchmark:
         monitor = ResourceMonitor(interval=1.0)  # reference :243-244
         monitor.start_monitoring()
         for _ in range(self.warmup_runs):
-            model.predict(test_input, verbose=False)
+            model.predict(test_input, verbose=False, sync=True)
         start = time.time()
         count, times = 0, []
         while time.time() - start < duration_seconds:
             t0 = time.time()
-            model.predict(test_input, verbose=False)
+            model.predict(test_input, verbose=False, sync=True)
             times.append(time.time() - t0)
             count += 1
         total = time.time() - start
@@ -134,12 +134,12 @@ class SpeedBenchmark:
         model.model.eval()
         with torch.no_grad():
             for _ in range(self.warmup_runs):
-                model.predict(test_input, verbose=False)
+                model.predict(test_input, verbose=False, sync=True)
         times = []
         with torch.no_grad():
             for _ in range(self.benchmark_runs):
                 t0 = time.time()
-                model.predict(test_input, verbose=False)
+                model.predict(test_input, verbose=False, sync=True)
                 times.append(time.time() - t0)
         avg = statistics.mean(times)
         return {"avg_inference_time": avg, "min_inference_time": min(times), "max_inference_time": max(times),

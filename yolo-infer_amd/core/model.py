@@ -21,7 +21,7 @@ import torch
 from yolomi.engine import Engine
 from yolomi.synth import synth_weights
 
-from .results import Results
+from .results import LazyCounts, Results
 
 logger = logging.getLogger(__name__)
 
@@ -217,11 +217,25 @@ class YOLO11Model:
         eng = self.model.engine
         bm = self.global_batch_max(im) if self.global_batch_max is not None and imsrc is None else None
         B = im.shape[0]
+        names = self.model.names
+        if self.task != "segment" and imsrc is None:
+            # Asynchronous call: the NMS kernel writes this call's rows AND its B detection counts (the int32 words
+            # behind the rows) into a fresh buffer, so no host sync is needed here: the Results read the counts on
+            # first access (one device->host read shared by the call's B Results), and back-to-back predict() calls
+            # queue their forwards with no host gap between them.
+            out, cnt = eng.rows_buffer(B, max_det)
+            eng.run(im, conf=conf, iou=iou, max_det=max_det, classes=classes, agnostic=agnostic, in_eps=eps,
+                    batch_max=bm, dets_out=out, counts_after=True)
+            lazy = LazyCounts(cnt, torch.cuda.current_stream(im.device))
+            if kwargs.get("sync", False):  # per-call latency loops: return only once the forward is done
+                lazy[0]
+            speed = {"preprocess": (t1 - t0) * 1e3, "inference": (time.perf_counter() - t1) * 1e3,
+                     "postprocess": 0.0}  # host time of the calls (the forward itself runs asynchronously)
+            return [Results.from_batch(im, b, names, out, lazy, path=f"image{b}.jpg", speed=speed) for b in range(B)]
         # the NMS kernel writes this call's rows straight into a fresh tensor (the Results keep views into it)
         out = torch.empty((B, max_det, 6 + eng.nm), dtype=torch.float32, device=im.device)
         dets, counts = eng.run(im, conf=conf, iou=iou, max_det=max_det, classes=classes, agnostic=agnostic,
                                in_eps=eps, batch_max=bm, dets_out=out)
-        names = self.model.names
         masks = None
         if self.task == "segment":  # process_mask(upsample=True) on the GPU, in letterboxed coordinates
             # the masks of the first `cap` detections per image are enqueued behind the forward, reading the device
@@ -317,11 +331,11 @@ class YOLO11Model:
     def benchmark(self, data_source, num_runs: int = 100, warmup_runs: int = 10) -> Dict[str, float]:
         """Same protocol as the reference (core/model.py:253-291): warm-up, then wall-clock per predict()."""
         for _ in range(warmup_runs):
-            _ = self.predict(data_source, verbose=False)
+            _ = self.predict(data_source, verbose=False, sync=True)
         times = []
-        for _ in range(num_runs):
+        for _ in range(num_runs):  # sync=True: each call's wall clock covers its whole forward (predict is async)
             start = time.time()
-            _ = self.predict(data_source, verbose=False)
+            _ = self.predict(data_source, verbose=False, sync=True)
             times.append(time.time() - start)
         avg = sum(times) / len(times)
         return {"avg_inference_time": avg, "min_inference_time": min(times), "max_inference_time": max(times),

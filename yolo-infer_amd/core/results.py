@@ -116,6 +116,26 @@ class Masks(_TensorView):
         return (self.orig_shape,)
 
 
+class LazyCounts:
+    """The B detection counts of one asynchronous predict() call, still on the device (the words the NMS kernel
+    writes behind the call's rows): read to the host once, on the first access by any of the call's Results."""
+
+    def __init__(self, dev_counts: torch.Tensor, stream=None):
+        self._dev = dev_counts
+        self._host = None
+        self._ev = None
+        if stream is not None:  # the launch stream's point: the read may happen under another current stream
+            self._ev = torch.cuda.Event()
+            self._ev.record(stream)
+
+    def __getitem__(self, b: int) -> int:
+        if self._host is None:
+            if self._ev is not None:
+                self._ev.synchronize()
+            self._host = self._dev.tolist()  # the device->host read of this call
+        return self._host[b]
+
+
 class Results:
     def __init__(self, orig_tensor: Optional[torch.Tensor], names: Dict[int, str], boxes: torch.Tensor,
                  masks: Optional[torch.Tensor] = None, path: str = "image0.jpg", speed=None):
@@ -132,12 +152,12 @@ class Results:
         self.obb = None
 
     @classmethod
-    def from_batch(cls, batch: torch.Tensor, b: int, names: Dict[int, str], dets: torch.Tensor, n: int,
+    def from_batch(cls, batch: torch.Tensor, b: int, names: Dict[int, str], dets: torch.Tensor, n,
                    path: str = "image0.jpg", speed=None, masks: Optional[torch.Tensor] = None,
                    moff: int = 0) -> "Results":
         """Image b of a predict() batch: boxes = dets[b, :n, :6], the input slice batch[b] and (Segment) the masks
         masks[moff : moff + n], all taken (as tensor views) on first access, so building the B Results of a call
-        costs no tensor operations."""
+        costs no tensor operations.  n: the count, or the call's LazyCounts (read from the device on first access)."""
         r = cls.__new__(cls)
         r._batch, r._b, r._dets, r._n = batch, b, dets, n
         r._orig_tensor_v = None
@@ -177,9 +197,13 @@ class Results:
         self._batch = None
 
     @property
+    def _count(self) -> int:
+        return self._n if isinstance(self._n, int) else self._n[self._b]
+
+    @property
     def boxes(self) -> "Boxes":
         if self._boxes is None:
-            self._boxes = Boxes(self._dets[self._b, : self._n, :6], self.orig_shape)
+            self._boxes = Boxes(self._dets[self._b, : self._count, :6], self.orig_shape)
         return self._boxes
 
     @boxes.setter
@@ -190,7 +214,7 @@ class Results:
     def masks(self) -> Optional["Masks"]:
         if self._masks is None and getattr(self, "_msrc", None) is not None:
             mb, moff = self._msrc
-            self._masks = Masks(mb[moff:moff + self._n], self.orig_shape)
+            self._masks = Masks(mb[moff:moff + self._count], self.orig_shape)
         return self._masks
 
     @masks.setter

@@ -386,6 +386,7 @@ struct NmsArgs {
   unsigned long long* keys; const int* counts;
   float4* sboxes; float* sareas; unsigned char* sup;  // per image scratch (A each)
   float* dets; int* out_counts;                       // (B, max_det, 6 + nm), (B)
+  int* counts2;  // non-null (ym_infer_args.counts_after_dets): the counts again, in the words after the batch's rows
   int A, kstride, nm, max_det, max_nms, agnostic, B;
   float max_wh, img_h, img_w;
   double iou;

@@ -1292,7 +1292,10 @@ __global__ __launch_bounds__(NMS_T) void nms_image(const NmsArgs a) {
       const int pos = __popcll(km & ((1ull << lane) - 1ull));
       write_det(a, out + (size_t)pos * rowlen, ib + ai);
     }
-    if (lane == 0) a.out_counts[b] = kept;
+    if (lane == 0) {
+      a.out_counts[b] = kept;
+      if (a.counts2) a.counts2[b] = kept;
+    }
     return;
   }
   if (n <= NMS_BM) {
@@ -1392,7 +1395,10 @@ __global__ __launch_bounds__(NMS_T) void nms_image(const NmsArgs a) {
       const unsigned ai = 0xFFFFFFFFu - (unsigned)(sorted[keep_bm[q]] & 0xFFFFFFFFull);
       write_det(a, out + (size_t)q * rowlen, ib + ai);
     }
-    if (tid == 0) a.out_counts[b] = kept;
+    if (tid == 0) {
+      a.out_counts[b] = kept;
+      if (a.counts2) a.counts2[b] = kept;
+    }
     return;
   }
   int n2 = 1;
@@ -1441,7 +1447,10 @@ __global__ __launch_bounds__(NMS_T) void nms_image(const NmsArgs a) {
     const unsigned ai = 0xFFFFFFFFu - (unsigned)(k[i] & 0xFFFFFFFFull);
     write_det(a, out + (size_t)q * rowlen, ib + ai);
   }
-  if (tid == 0) a.out_counts[b] = kept;
+  if (tid == 0) {
+    a.out_counts[b] = kept;
+    if (a.counts2) a.counts2[b] = kept;
+  }
 }
 
 // ------------------------------------------------------------------------------------------------- profiling aid

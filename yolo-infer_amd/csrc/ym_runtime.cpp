@@ -142,6 +142,9 @@ int repoint_dets(GraphEntry& ge, float* d_dets) {
   for (size_t j = 0; j < ge.nms_nodes.size(); ++j) {
     NmsArgs na = ge.nms_args[j];
     na.dets = d_dets + (na.dets - ge.dets);
+    if (na.counts2)  // the counts behind the rows move with them
+      na.counts2 = reinterpret_cast<int*>(reinterpret_cast<char*>(na.counts2) +
+                                          (reinterpret_cast<char*>(d_dets) - reinterpret_cast<char*>(ge.dets)));
     hipKernelNodeParams p{};
     HIPCK(hipGraphKernelNodeGetParams(ge.nms_nodes[j], &p));
     void* args[] = {&na};
@@ -208,6 +211,7 @@ struct ym_ctx {
   hipStream_t lane_streams[kMaxLanes] = {};
   hipEvent_t fork_ev = nullptr, join_ev[kMaxLanes] = {};
   int lane = 0, lane_img0 = 0;  // lane / first image of the ops being launched
+  int call_B = 0;               // images of the forward being launched (all lanes)
   std::vector<GraphEntry> graphs;
   std::vector<hipEvent_t> prof_events;
   float* const* calib_raw = nullptr;  // ym_calibrate: per-op pre-activation output buffers (f32 plans)
@@ -598,6 +602,11 @@ int launch_op(ym_ctx* c, const Op& op, int B, const float* d_in, const ym_infer_
       a.sup = c->scratch<unsigned char>(c->off_sup, (size_t)c->A);
       a.dets = d_dets;
       a.out_counts = d_counts;
+      // counts_after_dets: this lane's images' words behind the WHOLE batch's rows (lane_img0: d_dets is the lane's)
+      a.counts2 = args->counts_after_dets
+                      ? reinterpret_cast<int*>(d_dets + (size_t)(c->call_B - c->lane_img0) * args->max_det * (6 + c->nm)) +
+                            c->lane_img0
+                      : nullptr;
       a.A = c->A; a.kstride = c->kstride; a.nm = c->nm; a.max_det = args->max_det; a.max_nms = args->max_nms;
       a.agnostic = args->agnostic; a.B = B;
       a.max_wh = args->max_wh; a.img_h = (float)c->cH; a.img_w = (float)c->cW;
@@ -621,6 +630,8 @@ int check_call(ym_ctx* c, const float* d_in, int B, int H, int W, const ym_infer
     return fail(YM_EINVAL, "input shape (%d,3,%d,%d): H and W must be positive multiples of 32", B, H, W);
   if (args->max_det < 1 || args->max_nms < 1) return fail(YM_EINVAL, "max_det/max_nms must be >= 1");
   if (args->max_det > 1024) return fail(YM_EINVAL, "max_det %d > 1024 is not supported", args->max_det);
+  if (args->counts_after_dets != 0 && args->counts_after_dets != 1) return fail(YM_EINVAL, "counts_after_dets is 0 or 1");
+  c->call_B = B;  // (launch_forward sets it again; eager per-op paths launch the NMS op directly)
   return YM_OK;
 }
 
@@ -960,6 +971,7 @@ static int launch_forward(ym_ctx* c, const float* d_in, int B, const ym_infer_ar
                           int* d_counts, hipStream_t st) {
   int L, Bl, rc;
   lane_split(args, B, L, Bl);
+  c->call_B = B;
   c->lane = 0;
   c->lane_img0 = 0;
   if (L == 1 && c->nbr > 1) {  // one lane: the branch schedule (build_schedule)

@@ -133,6 +133,13 @@ class Engine:
             self._out[key] = (dets, counts)
         return self._out[key]
 
+    def rows_buffer(self, B: int, max_det: int):
+        """A fresh flat fp32 device buffer for one call: (rows (B, max_det, 6 + nm) view, counts (B,) int32 view of the
+        words behind the rows) — for run(..., dets_out=rows, counts_after=True)."""
+        no = 6 + self.nm
+        flat = torch.empty((B * max_det * no + B,), dtype=torch.float32, device=self.device)
+        return flat[: B * max_det * no].view(B, max_det, no), flat[B * max_det * no:].view(torch.int32)
+
     def lane_batch(self, B: int, lanes: Optional[int] = None) -> int:
         """Images per lane (the batch every kernel sees) for a B-image call: ceil(B / clamp(lanes, 1, 4, B))."""
         L = max(1, min(self.lanes if lanes is None else lanes, 4, B))
@@ -140,12 +147,16 @@ class Engine:
 
     def run(self, x: torch.Tensor, conf=0.25, iou=0.7, max_det=300, classes: Optional[Sequence[int]] = None,
             agnostic=False, in_eps=None, use_graph=True, max_nms=30000, max_wh=7680.0, lanes=None,
-            batch_max: Optional[torch.Tensor] = None, dets_out: Optional[torch.Tensor] = None):
+            batch_max: Optional[torch.Tensor] = None, dets_out: Optional[torch.Tensor] = None,
+            counts_after: bool = False):
         """x: (B,3,H,W) float32 contiguous on this device. Returns the engine-owned (dets, counts) tensors, or
         (dets_out, counts) when the caller hands in its own (>= B, max_det, 6 + nm) fp32 rows (predict(): a fresh
         tensor per call, written by the NMS kernel directly — a cached graph re-points its NMS nodes, no copy).
         batch_max: optional (1,) fp32 device tensor, the max over the GLOBAL batch (yolomi.dist: a batch-sharded
-        rank takes LoadTensor's /255 decision from it instead of from its own shard)."""
+        rank takes LoadTensor's /255 decision from it instead of from its own shard).
+        counts_after (with dets_out = the first B*max_det rows of a flat buffer, see rows_buffer): the NMS also writes
+        this call's B detection counts as int32 words right behind those rows, so the caller can read them later
+        (predict() reads them lazily: no host sync per call)."""
         assert x.is_cuda and x.dtype == torch.float32 and x.is_contiguous() and x.dim() == 4 and x.shape[1] == 3
         B, _, H, W = x.shape
         if in_eps is None:
@@ -157,18 +168,22 @@ class Engine:
             assert batch_max.is_cuda and batch_max.dtype == torch.float32 and batch_max.numel() >= 1
             bm = batch_max.data_ptr()
         akey = (conf, iou, max_det, max_nms, agnostic, max_wh, in_eps, tuple(classes) if classes is not None else None,
-                use_graph, lanes, bm)
+                use_graph, lanes, bm, counts_after)
         args = self._args_cache.get(akey)
         if args is None:
             if len(self._args_cache) > 64:
                 self._args_cache.clear()
             args = self._args_cache[akey] = Runtime.make_args(conf, iou, max_det, max_nms, agnostic, max_wh, in_eps,
-                                                              classes, use_graph, lanes, bm)
+                                                              classes, use_graph, lanes, bm, counts_after)
         dets, counts = self.outputs(B, max_det)
         if dets_out is not None:
             assert (dets_out.is_cuda and dets_out.dtype == torch.float32 and dets_out.is_contiguous()
                     and dets_out.dim() == 3 and dets_out.shape[0] >= B and tuple(dets_out.shape[1:]) == tuple(dets.shape[1:]))
             dets = dets_out
+        if counts_after:  # room for the B count words behind the rows, in dets_out's own storage
+            need = dets_out.storage_offset() * 4 + B * max_det * (6 + self.nm) * 4 + 4 * B if dets_out is not None else -1
+            if dets_out is None or dets_out.untyped_storage().nbytes() < need:
+                raise ValueError("counts_after needs dets_out from Engine.rows_buffer (rows followed by B int32 words)")
         stream = torch.cuda.current_stream(self.device).cuda_stream
         Bl = self.lane_batch(B, lanes)
         if (Bl, H, W) not in self._tuned:

@@ -35,7 +35,7 @@ class RcclId(C.Structure):
 class InferArgs(C.Structure):
     _fields_ = [("conf", C.c_float), ("max_wh", C.c_float), ("iou", C.c_double), ("max_det", C.c_int),
                 ("max_nms", C.c_int), ("agnostic", C.c_int), ("in_eps", C.c_float), ("has_classes", C.c_int),
-                ("classes", C.c_uint32 * 4), ("use_graph", C.c_int), ("lanes", C.c_int), ("reserved0", C.c_int),
+                ("classes", C.c_uint32 * 4), ("use_graph", C.c_int), ("lanes", C.c_int), ("counts_after_dets", C.c_int),
                 ("d_batch_max", C.c_void_p), ("reserved", C.c_int * 4)]
 
 
@@ -171,8 +171,9 @@ class Runtime:
 
     @staticmethod
     def make_args(conf=0.25, iou=0.7, max_det=300, max_nms=30000, agnostic=False, max_wh=7680.0, in_eps=1.1920929e-07,
-                  classes=None, use_graph=True, lanes=1, batch_max_ptr=0) -> InferArgs:
+                  classes=None, use_graph=True, lanes=1, batch_max_ptr=0, counts_after_dets=False) -> InferArgs:
         a = InferArgs()
+        a.counts_after_dets = int(bool(counts_after_dets))
         a.d_batch_max = batch_max_ptr or None
         a.conf, a.iou, a.max_det, a.max_nms = float(conf), float(iou), int(max_det), int(max_nms)
         a.agnostic, a.max_wh, a.in_eps, a.use_graph = int(bool(agnostic)), float(max_wh), float(in_eps), int(use_graph)
