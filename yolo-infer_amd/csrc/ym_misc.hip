@@ -747,15 +747,27 @@ __global__ __launch_bounds__(256) void attn_psa_x3(const AttnArgs a) {
   const int hq = a.q_coff + h * 128;  // per head: q 32, k 32, v 64 logical channels
   for (int i = tid; i < 640; i += 256)
     pw[i] = i < 576 ? a.pe_w[(i >> 6) * a.C + h * 64 + (i & 63)] : a.pe_b[h * 64 + i - 576];
-  // 1. V^T hi / lo planes (keys >= N zero): 8 chunks of 8 v channels per key
-  for (int i = tid; i < 16 * NKT * 8; i += 256) {
-    const int key = i >> 3, ch = i & 7;
-    HL v{Vec8<f16>::zero(), Vec8<f16>::zero()};
-    if (key < N) v = ym_load_hl(qkv + (img + key) * a.q_ctot + hq + 64 + 8 * ch);
+  // 1. V^T hi / lo planes (keys >= N zero): 8 chunks of 8 v channels per key.  Every chunk load is in flight
+  // before the first LDS store (one memory latency, not NIT of them: the loop form waited for each load in turn)
+  {
+    constexpr int NIT = 16 * NKT * 8 / 256;
+    static_assert(16 * NKT * 8 % 256 == 0, "V chunks divide over the threads");
+    HL v[NIT];
 #pragma unroll
-    for (int e = 0; e < 8; ++e) {
-      vt[(8 * ch + e) * LDV + key] = v.hi[e];
-      vtl[(8 * ch + e) * LDV + key] = v.lo[e];
+    for (int it = 0; it < NIT; ++it) {
+      const int i = tid + 256 * it, key = i >> 3, ch = i & 7;
+      // (an unconditional load of a clamped key, zeroed below: a load under a condition is waited for on the spot)
+      v[it] = ym_load_hl(qkv + (img + (key < N ? key : N - 1)) * a.q_ctot + hq + 64 + 8 * ch);
+    }
+#pragma unroll
+    for (int it = 0; it < NIT; ++it) {
+      const int i = tid + 256 * it, key = i >> 3, ch = i & 7;
+      const bool ok = key < N;
+#pragma unroll
+      for (int e = 0; e < 8; ++e) {
+        vt[(8 * ch + e) * LDV + key] = ok ? v[it].hi[e] : (f16)0;
+        vtl[(8 * ch + e) * LDV + key] = ok ? v[it].lo[e] : (f16)0;
+      }
     }
   }
   const int q = qb * 64 + wave * 16 + c;
