@@ -329,6 +329,25 @@ struct ConvArgs {
   const float* dw_w; const float* dw_b; int dw_act;
 };
 
+// Warm the scalar cache with every 64-byte line of a kernel's argument block in ONE round trip: the compiler loads
+// kernel arguments lazily at first use, each batch of s_loads ending in an lgkmcnt(0) wait for a line that is not in
+// the scalar cache yet (a graph replay's argument block is cold): ~6 dependent round trips for a ConvArgs block
+// before the first DMA issue (tools/dma_probe.hip prologue stamps: "index setup" 3.2k cycles).  After this the lazy
+// loads hit the cache.
+template <int BYTES>
+__device__ __forceinline__ void ym_warm_kernargs() {
+  const __attribute__((address_space(4))) char* kp =
+      (const __attribute__((address_space(4))) char*)__builtin_amdgcn_kernarg_segment_ptr();
+  static_assert(BYTES <= 16 * 64, "argument block too large");
+  int v[16];
+#pragma unroll
+  for (int i = 0; i < 16; ++i)
+    if (i * 64 < BYTES) v[i] = *(const __attribute__((address_space(4))) int*)(kp + i * 64);
+#pragma unroll
+  for (int i = 0; i < 16; ++i)
+    if (i * 64 < BYTES) asm volatile("" ::"s"(v[i]));
+}
+
 // A load through the global address space (global_load, vmcnt only; a generic pointer makes the compiler emit a
 // flat load, which also counts in lgkmcnt and so is waited for together with the scalar/LDS traffic).
 template <typename T>
