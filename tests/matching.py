@@ -148,9 +148,12 @@ def dist_to_exact(exact: np.ndarray, got: np.ndarray):
         if not len(c):
             miss += 1
             continue
+        # the counterpart is the candidate nearest in coordinates AND score (each against its own bar): boxes that NMS
+        # kept apart can coincide after the clip to the image (two whole-image boxes of one class), told apart by score
         d = np.abs(exact[c, :4] - got[i, :4]).max(1)
-        k = c[int(np.argmin(d))]
-        dxy = max(dxy, float(d.min()))
-        ds = max(ds, float(abs(exact[k, 4] - got[i, 4])))
+        e = np.abs(exact[c, 4] - got[i, 4])
+        k = int(np.argmin(np.maximum(d / 5e-4, e / 5e-5)))
+        dxy = max(dxy, float(d[k]))
+        ds = max(ds, float(e[k]))
         n += 1
     return dxy, ds, n, miss

@@ -30,12 +30,7 @@ def kernel_dma_counts(asm: str):
             int, re.search(r"Li(\d+)ELi(\d+)ELi(\d)ELi(\d)ELi(\d)ELi(\d)ELi(\d)E", m.group(1)).groups())
         nl = sub * (bm // 8 + bn // 8) // (4 * kg)  # DMA instructions per wave per stage
         n = len(re.findall(r"buffer_load_dwordx4 .*\blds\b", body))
-        # (NSTAGE-1) prologue + 1 loop stage; staggered wave groups (last template flag STG, `...ELb1EEEv`): the
-        # compiler may unswitch the K loop on the wave group (wave-uniform), so the loop's stage appears twice —
-        # each wave still runs exactly one copy per iteration
-        stg = bool(re.search(r"Lb[01]ELb[01]ELb1EEEv", m.group(1)))
-        ok = (nstage * nl, (nstage + 1) * nl) if stg else (nstage * nl,)
-        out.append((m.group(1), bm, bn, kind, split, n, n if n in ok else ok[0]))
+        out.append((m.group(1), bm, bn, kind, split, n, nstage * nl))  # (NSTAGE-1) prologue + 1 loop stage
     return out
 
 

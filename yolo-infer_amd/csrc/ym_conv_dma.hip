@@ -19,8 +19,6 @@
 //    workgroup, and no L1 invalidate.
 // Epilogue as in ym_conv.hip: + folded-BN bias, SiLU, + residual, channel-slice store (zero-copy concat), fp32
 // anchor-major Detect rows, 2x2 pixel shuffle (Proto ConvTranspose2d).
-#include <stdlib.h>
-
 #include <type_traits>
 
 #include "ym_common.h"
@@ -100,17 +98,9 @@ template <> struct Store4<P2> {
 // weight-operand layout, and the second GEMM (K = the first conv's N) runs as extra ring stages — the same fragment
 // reads and split MFMAs — before the epilogue stores the second conv's output.  The intermediate never reaches HBM and
 // the pair is one launch (the split pair wrote and read it back: model.1+cv1, the Detect cv2.l.1 -> cv2.l.2 chains).
-// STG (x3, KG == 2): the two wave groups run half a stage apart, so one group's LDS fragment reads overlap the other
-// group's MFMAs.  Per stage two barriers: after the first (stage it landed) group 0 reads stage it while group 1 runs
-// the MFMAs of stage it-1 from its registers; after the second group 0 runs stage it's MFMAs while group 1 reads
-// stage it.  (Unstaggered, both groups read the stage at once — every ds_read of the CU queued on the LDS — then both
-// run their MFMAs with the LDS idle: the stage took the SUM of the two, tools/dma_probe.hip stamps.)  Ring reuse
-// is unchanged: the DMA issued after a stage's first barrier overwrites stage it-1's slot, which group 1 finished
-// reading before that barrier (its lgkmcnt(0)).
 template <typename OutT, int BM, int BN, int KIND, int SPLIT, int KG, int NSTAGE, int SUB, bool X3 = false,
-          bool FUSE = false, bool STG = false>
+          bool FUSE = false>
 __global__ __launch_bounds__(256 * KG) void conv_dma(const ConvArgs a) {
-  static_assert(!STG || (X3 && KG == 2 && !FUSE), "staggered wave groups: x3, two groups, no fused epilogue GEMM");
   constexpr int NW = 4 * KG;
   constexpr int TM = BM / 64, TN = BN / 64;
   static_assert((BM / 8) % NW == 0 && (BN / 8) % NW == 0, "DMA groups must divide over the waves");
@@ -405,50 +395,6 @@ __global__ __launch_bounds__(256 * KG) void conv_dma(const ConvArgs a) {
         for (int r = 0; r < 16; ++r) acc[u][i][j][r] = 0.f;
 
   const int key = (l32 >> 1) & 7;
-  // x3 fragment registers of this wave's k sub-steps of one stage (filled by xread, consumed by xmma; staggered
-  // groups hold them across a barrier)
-  f16x8 xfb[X3 ? SUB : 1][X3 ? SPW / 2 : 1][3][TM], xfa[X3 ? SUB : 1][X3 ? SPW / 2 : 1][3][TN];
-  auto xread = [&](int slot) {
-    if constexpr (X3) {
-      static_assert(SPW % 2 == 0, "x3: a wave's k sub-steps come in pairs");
-#pragma unroll
-      for (int su = 0; su < SUB; ++su) {
-        const char* sb = smem + slot * SB + su * SBS;
-        const char* sa = sb + BM * 128;
-#pragma unroll
-        for (int u = 0; u < SPW / 2; ++u) {
-          const int s = kg * SPW + 2 * u;
-          const int ca[3] = {2 * s, 2 * s + 2, 2 * (s + h) + 1}, cbx[3] = {2 * s + h, 2 * s + 2 + h, 2 * (s + h)};
-#pragma unroll
-          for (int v = 0; v < 3; ++v) {
-            const int offa = ((ca[v] ^ key) << 4) + l32 * 128, offb = ((cbx[v] ^ key) << 4) + l32 * 128;
-#pragma unroll
-            for (int i = 0; i < TM; ++i)
-              xfb[su][u][v][i] = *reinterpret_cast<const f16x8*>(sb + (wm * (BM / 2) + 32 * i) * 128 + offb);
-#pragma unroll
-            for (int j = 0; j < TN; ++j)
-              xfa[su][u][v][j] = *reinterpret_cast<const f16x8*>(sa + (wn * (BN / 2) + 32 * j) * 128 + offa);
-          }
-        }
-      }
-    }
-  };
-  auto xmma = [&]() {
-    if constexpr (X3) {
-#pragma unroll
-      for (int su = 0; su < SUB; ++su)
-#pragma unroll
-        for (int u = 0; u < SPW / 2; ++u)
-#pragma unroll
-          for (int v = 0; v < 3; ++v)
-#pragma unroll
-            for (int i = 0; i < TM; ++i)
-#pragma unroll
-              for (int j = 0; j < TN; ++j)
-                acc[v % NACC][i][j] = __builtin_amdgcn_mfma_f32_32x32x16_f16(xfa[su][u][v][j], xfb[su][u][v][i],
-                                                                             acc[v % NACC][i][j], 0, 0, 0);
-    }
-  };
   // this wave's k sub-steps of the stage: fragment reads first, then the MFMAs (one LDS latency per stage)
   auto compute = [&](int slot) {
     if constexpr (X3) {
@@ -534,19 +480,8 @@ __global__ __launch_bounds__(256 * KG) void conv_dma(const ConvArgs a) {
     YM_STAMP(9 + 4 * (it & 63));
     if (it + NSTAGE - 1 < nk) issue((it + NSTAGE - 1) % NSTAGE);
     YM_STAMP(10 + 4 * (it & 63));
-    if constexpr (STG) {
-      if (kg == 0) xread(it % NSTAGE);
-      else if (it > 0) xmma();  // stage it-1, read after the previous iteration's second barrier
-      raw_barrier();
-      if (kg == 0) xmma();
-      else xread(it % NSTAGE);
-    } else {
-      compute(it % NSTAGE);
-    }
+    compute(it % NSTAGE);
     YM_STAMP(11 + 4 * (it & 63));
-  }
-  if constexpr (STG) {
-    if (kg != 0 && nk > 0) xmma();  // group 1's last stage
   }
   YM_STAMP(2);
   if constexpr (NACC == 2) {
@@ -809,13 +744,6 @@ __global__ __launch_bounds__(256 * KG) void conv_dma(const ConvArgs a) {
   YM_STAMP(3);
 }
 
-// x3 two-group configurations run with staggered wave groups (conv_dma STG) unless YM_DMA_STG=0; read at every launch,
-// i.e. at graph capture (same-box A/B)
-bool ym_dma_stagger() {
-  const char* e = getenv("YM_DMA_STG");
-  return !(e && *e == '0');
-}
-
 struct DmaCfg {
   int bm, bn, split, kg, ns, sub;
 };
@@ -852,21 +780,6 @@ hipError_t launch_dma(ConvArgs a, int kind, hipStream_t st) {
   }
   if (SUB > 1 && (a.Kpad / DK) % (SPLIT * SUB)) return hipErrorInvalidValue;  // whole stages in every split
   const dim3 grid(tiles_m8 * a.tiles_n * SPLIT), block(256 * KG);
-  if constexpr (X3 && KG == 2) {
-    if (ym_dma_stagger()) {  // staggered wave groups (conv_dma STG)
-      if (kind == 1) {
-        hipLaunchKernelGGL((conv_dma<OutT, BM, BN, 1, SPLIT, KG, NS, SUB, X3, false, true>), grid, block, 0, st, a);
-      } else if constexpr (!std::is_same<OutT, float>::value) {
-        if (kind == 4)
-          hipLaunchKernelGGL((conv_dma<OutT, BM, BN, 4, SPLIT, KG, NS, SUB, X3, false, true>), grid, block, 0, st, a);
-        else
-          hipLaunchKernelGGL((conv_dma<OutT, BM, BN, 3, SPLIT, KG, NS, SUB, X3, false, true>), grid, block, 0, st, a);
-      } else {
-        return hipErrorInvalidValue;
-      }
-      return hipGetLastError();
-    }
-  }
   if (kind == 1) {
     hipLaunchKernelGGL((conv_dma<OutT, BM, BN, 1, SPLIT, KG, NS, SUB, X3>), grid, block, 0, st, a);
   } else if constexpr (!std::is_same<OutT, float>::value) {  // fp32 outputs: only the Detect head's 1x1 convs
