@@ -133,27 +133,3 @@ def ref_f64_slack(ref: np.ndarray, exact: np.ndarray, tol_xy: float = 1e-3) -> n
             out[i] = tol_xy + float(np.abs(exact[cand, :4] - ref[i, :4]).max(1).min())
     return out
 
-
-def dist_to_exact(exact: np.ndarray, got: np.ndarray):
-    """The build's own distance from the exact answer: for every build detection with a same-class float64 detection
-    at IoU >= 0.99 (`exact`: oracle predict_exact rows), the coordinate and score distance to the nearest one.
-    Returns (max |dxy| px, max |dscore|, detections compared, detections without a float64 counterpart)."""
-    dxy = ds = 0.0
-    n = miss = 0
-    if not len(got):
-        return dxy, ds, n, miss
-    ious = iou_matrix(got[:, :4], exact[:, :4]) if len(exact) else np.zeros((len(got), 0))
-    for i in range(len(got)):
-        c = np.where((exact[:, 5] == got[i, 5]) & (ious[i] >= 0.99))[0] if len(exact) else []
-        if not len(c):
-            miss += 1
-            continue
-        # the counterpart is the candidate nearest in coordinates AND score (each against its own bar): boxes that NMS
-        # kept apart can coincide after the clip to the image (two whole-image boxes of one class), told apart by score
-        d = np.abs(exact[c, :4] - got[i, :4]).max(1)
-        e = np.abs(exact[c, 4] - got[i, 4])
-        k = int(np.argmin(np.maximum(d / 5e-4, e / 5e-5)))
-        dxy = max(dxy, float(d[k]))
-        ds = max(ds, float(e[k]))
-        n += 1
-    return dxy, ds, n, miss

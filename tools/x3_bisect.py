@@ -56,9 +56,12 @@ def forward_from(net64, k, inj):
     return x[0] if isinstance(x, tuple) else x
 
 
-def dets_of(y, conf=0.25, iou=0.7):
+def dets_of(y, conf=0.25, iou=0.7, shape=(640, 640)):
+    """NMS then the clip of predict()'s scale_boxes (oracle/predict.py), as predict_exact."""
     out = []
     for d in pp.non_max_suppression(y.double(), conf, iou, None, False, 300):
+        d = d.clone()
+        d[:, :4] = pp.scale_boxes(shape, d[:, :4], shape)
         out.append(d[:, :6].numpy())
     return out
 

@@ -771,21 +771,32 @@ __global__ __launch_bounds__(256) void attn_psa_x3(const AttnArgs a) {
     }
   }
   const int q = qb * 64 + wave * 16 + c;
-  HL qf{Vec8<f16>::zero(), Vec8<f16>::zero()};
-  if (q < N) qf = ym_load_hl(qkv + (img + q) * a.q_ctot + hq + 8 * g);
-  // 2. scores S^T = K·Q^T (log2 units): lane (g, c) supplies key 16t + c, logical chunk g of K
+  // (queries past N: a clamped row; their outputs are never stored)
+  const HL qf = ym_load_hl(qkv + (img + (q < N ? q : N - 1)) * a.q_ctot + hq + 8 * g);
+  // 2. scores S^T = K·Q^T (log2 units): lane (g, c) supplies key 16t + c, logical chunk g of K.  The K fragments
+  // of KB key tiles are loaded together (unconditional loads of clamped keys: rows past N only feed scores that are
+  // masked to -inf), then their MFMAs run: NKT / KB memory round trips instead of one per tile
   const float sl2 = a.scale * 1.4426950408889634f;
   float s[NKT][4];
+  constexpr int KB = 8;
 #pragma unroll
-  for (int t = 0; t < NKT; ++t) {
-    const int key = 16 * t + c;
-    HL kf{Vec8<f16>::zero(), Vec8<f16>::zero()};
-    if (key < N) kf = ym_load_hl(qkv + (img + key) * a.q_ctot + hq + 32 + 8 * g);
-    f32x4 d = __builtin_amdgcn_mfma_f32_16x16x32_f16(kf.lo, qf.hi, f32x4{0.f, 0.f, 0.f, 0.f}, 0, 0, 0);
-    d = __builtin_amdgcn_mfma_f32_16x16x32_f16(kf.hi, qf.lo, d, 0, 0, 0);
-    d = __builtin_amdgcn_mfma_f32_16x16x32_f16(kf.hi, qf.hi, d, 0, 0, 0);
+  for (int t0 = 0; t0 < NKT; t0 += KB) {
+    HL kf[KB];
 #pragma unroll
-    for (int r = 0; r < 4; ++r) s[t][r] = 16 * t + 4 * g + r < N ? d[r] * sl2 : -INFINITY;
+    for (int u = 0; u < KB; ++u) {
+      const int key = 16 * (t0 + u) + c;
+      if (t0 + u < NKT) kf[u] = ym_load_hl(qkv + (img + (key < N ? key : N - 1)) * a.q_ctot + hq + 32 + 8 * g);
+    }
+#pragma unroll
+    for (int u = 0; u < KB; ++u) {
+      const int t = t0 + u;
+      if (t >= NKT) break;
+      f32x4 d = __builtin_amdgcn_mfma_f32_16x16x32_f16(kf[u].lo, qf.hi, f32x4{0.f, 0.f, 0.f, 0.f}, 0, 0, 0);
+      d = __builtin_amdgcn_mfma_f32_16x16x32_f16(kf[u].hi, qf.lo, d, 0, 0, 0);
+      d = __builtin_amdgcn_mfma_f32_16x16x32_f16(kf[u].hi, qf.hi, d, 0, 0, 0);
+#pragma unroll
+      for (int r = 0; r < 4; ++r) s[t][r] = 16 * t + 4 * g + r < N ? d[r] * sl2 : -INFINITY;
+    }
   }
   __syncthreads();
   // 3. softmax over the keys of query l&15 (fp32, exact exp2)
