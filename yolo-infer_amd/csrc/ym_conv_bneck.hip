@@ -76,6 +76,7 @@ __device__ __forceinline__ int xpix(int row, int xc, int XC, int XE) {
 // Bottleneck's cv2 with its 1-pixel halo on the mid image; 1: a following 1x1 such as C3k2.cv1, no halo).
 template <int C, int CM, int N2, int PX, int NW, int S1, int K2, bool X3>
 __global__ __launch_bounds__(64 * NW) void conv_bneck(const ConvArgs a, const BneckGeom g) {
+  ym_warm_kernargs<sizeof(ConvArgs)>();  // one round trip for the whole argument block (ym_common.h)
   constexpr int NT = 64 * NW;
   constexpr int XS = X3 ? 2 : 1;  // fp16 storage elements per logical channel (global pair layout)
   constexpr int CH = C / 8, CHM = CM / 8;

@@ -48,6 +48,7 @@ __device__ __forceinline__ u32x4 bld(__amdgpu_buffer_rsrc_t r, unsigned off) {
 
 template <typename T, int TW>
 __global__ __launch_bounds__(256, 2) void conv_dwpw(const ConvArgs a) {
+  ym_warm_kernargs<sizeof(ConvArgs)>();  // one round trip for the whole argument block (ym_common.h)
   constexpr bool X3 = std::is_same<T, P2>::value;
   constexpr int XS = X3 ? 2 : 1;            // fp16 storage elements per logical channel
   constexpr int TH = 64 / TW, IH = TH + 2, IW = TW + 2, NPIX = IH * IW;

@@ -95,6 +95,7 @@ template <> struct SRes<true> {
 
 template <typename OutT, int KIND, int KS, int PX, bool FUSE, int NWV, bool X3 = false>
 __global__ __launch_bounds__(64 * NWV) void conv_stream(const ConvArgs a) {
+  ym_warm_kernargs<sizeof(ConvArgs)>();  // one round trip for the whole argument block (ym_common.h)
   static_assert(!X3 || KS % 2 == 0, "x3: K steps in pairs");
   constexpr int XS = X3 ? 2 : 1;       // fp16 storage elements per logical channel
   constexpr int KX = X3 ? KS / 2 : 0;  // x3: the extra x_hi gather per step pair
@@ -426,6 +427,7 @@ constexpr int kNumSmall = sizeof(kSmall) / sizeof(kSmall[0]);
 
 template <typename OutT, int KIND, int KSW, int PXG>
 __global__ __launch_bounds__(256) void conv_small(const ConvArgs a) {
+  ym_warm_kernargs<sizeof(ConvArgs)>();  // one round trip for the whole argument block (ym_common.h)
   __shared__ f32x4 red[3][PXG][64];
   const int tid = threadIdx.x, lane = tid & 63, wave = tid >> 6;
   const int g = lane >> 4, col = lane & 15;

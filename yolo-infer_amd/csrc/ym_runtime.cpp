@@ -1036,12 +1036,11 @@ int ym_infer(ym_ctx* c, const float* d_in, int B, int H, int W, const ym_infer_a
   key_d.dets = d_dets;
   for (auto& g : c->graphs) {
     if (g.key == key || g.key == key_d) {
-      // re-pointable: new rows through the NMS nodes' parameters (the exec's previous launch must have finished:
-      // the parameters of a launch still queued are not ours to change)
-      if (g.key == key && g.dets != d_dets) {
-        HIPCK(hipEventSynchronize(g.done));
-        if ((rc = repoint_dets(g, d_dets))) return rc;
-      }
+      // re-pointable: new rows through the NMS nodes' parameters.  A launch already queued keeps the parameters it
+      // was launched with (hipGraphExecKernelNodeSetParams changes later launches only:
+      // tests/test_gpu_kernels.py test_repointed_graph_rows_with_no_sync_between_calls), so no wait here — an
+      // asynchronous predict() loop enqueues the next forward while the previous one runs
+      if (g.key == key && g.dets != d_dets && (rc = repoint_dets(g, d_dets))) return rc;
       HIPCK(hipGraphLaunch(g.exec, st));
       HIPCK(hipEventRecord(g.done, st));
       return YM_OK;

@@ -52,6 +52,7 @@ constexpr int MTH = 16;  // MFMA path: 16 output rows per workgroup (32 groups o
 // product (w_lo·x_hi + w_hi·x_lo + w_hi·x_hi), the output is stored in the pair layout with the exact SiLU
 template <typename T, int NT, bool F8 = false>
 __global__ __launch_bounds__(256) void stem_mfma(const ConvArgs a) {
+  ym_warm_kernargs<sizeof(ConvArgs)>();  // one round trip for the whole argument block (ym_common.h)
   constexpr bool QUANT = sizeof(T) == 1;
   constexpr bool X3 = std::is_same<T, P2>::value;
   constexpr int TH = MTH, PH = 2 * TH + 1;
