@@ -67,15 +67,19 @@ __global__ __launch_bounds__(256) void input_stats(const float* __restrict__ x, 
   __syncthreads();
   if (tid == 0) {
     m = fmaxf(fmaxf(wm[0], wm[1]), fmaxf(wm[2], wm[3]));
-    __hip_atomic_store(part + blockIdx.x, f2ord(m), __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);  // sc1
-    // release: the partial is visible at agent scope before the ticket moves; acquire: the last block sees every
-    // partial released before its ticket
-    const int t = __hip_atomic_fetch_add(ticket, 1, __ATOMIC_ACQ_REL, __HIP_MEMORY_SCOPE_AGENT);
+    // the sc1 hand-off (cdna_hip_programming.md Guideline 16, MI355X_MICROARCH.md § visibility, the counter row):
+    // the partial is stored write-through (an agent-scope relaxed store is sc1) and drained before the agent-scope
+    // ticket; the last block reads every partial with sc1 loads (agent-scope relaxed loads), so neither side needs a
+    // fence instruction.  (An acquire-release ticket puts an L2 write-back in every one of the 1,024 blocks: the
+    // kernel went 21.8 -> 52.8 us per call under rocprofv3: profiles/r04d_s_b8_x3_summary.json vs r05c.)
+    __hip_atomic_store(part + blockIdx.x, f2ord(m), __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
+    asm volatile("s_waitcnt vmcnt(0)" ::: "memory");
+    const int t = __hip_atomic_fetch_add(ticket, 1, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
     last = t == (int)gridDim.x - 1;
   }
   __syncthreads();
   if (!last) return;
-  __builtin_amdgcn_fence(__ATOMIC_ACQUIRE, "agent");
+  __builtin_amdgcn_fence(__ATOMIC_ACQUIRE, "wavefront");  // no instruction: keeps the sc1 loads below the ticket
   int r = f2ord(-INFINITY);
   for (int b = tid; b < (int)gridDim.x; b += 256)
     r = max(r, __hip_atomic_load(part + b, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT));
@@ -1403,9 +1407,18 @@ __global__ __launch_bounds__(NMS_T) void nms_image(const NmsArgs a) {
           avail &= ~remk & ~((2ull << j) - 1ull);
         }
         const bool mine = (keepbits >> lane) & 1ull;
-        if (mine) {
-          keep_bm[kept + __popcll(keepbits & ((1ull << lane) - 1ull))] = row;
-          for (int w = k + 1; w < W; ++w) atomicOr(&rem_w[w], mask[row * W + w]);
+        if (mine) keep_bm[kept + __popcll(keepbits & ((1ull << lane) - 1ull))] = row;
+        // the block's kept rows OR their later mask words into the removed words: an OR across the wave (shuffles),
+        // one LDS write per word (per-lane LDS atomics on one address serialised, ~35 per block)
+        for (int w = k + 1; w < W; ++w) {
+          const unsigned long long v = mine ? mask[row * W + w] : 0ull;
+          unsigned vlo = (unsigned)v, vhi = (unsigned)(v >> 32);
+#pragma unroll
+          for (int o = 32; o > 0; o >>= 1) {
+            vlo |= (unsigned)__shfl_xor((int)vlo, o);
+            vhi |= (unsigned)__shfl_xor((int)vhi, o);
+          }
+          if (lane == 0) rem_w[w] |= ((unsigned long long)vhi << 32) | vlo;
         }
         kept = kk;
       }
