@@ -1,17 +1,19 @@
-"""GPU tests of the fp8 (e4m3) PTQ plan through the C-ABI (csrc/ym_quant.h Q8<true>: v_mfma_f32_*_fp8_fp8 convs,
-e4m3 storage) against the fp8 oracle (oracle/quant.py backend "fp8") and its committed fixture.
+"""GPU tests of the fp8 (e4m3) PTQ plan through the C-ABI (csrc/ym_quant.h Q8<true>: e4m3 storage, the codes widened
+exactly to fp16 and multiplied on the f16 MFMA) against the fp8 oracle (oracle/quant.py backend "fp8") and its
+committed fixture.
 
-Parity bar (a tolerance, written here).  The oracle sums e4m3 products exactly (float64); the fp8 MFMA accumulates
-in fp32 with its own internal precision, and on gfx950 a conv's output code differs from the exact one in ~0.1 % of
-the elements (measured layer-locally, tools/f8_diag.py: the same rate whether the reference sums in float64 or in
-sequential fp32, so it is the instruction's accumulation, not the order).  One such flip moves a value by an e4m3
-step (6-12 %), and through 20+ quantized layers the flips cascade (an e4m3 network is chaotic under perturbations of
-that size), so end-to-end codes cannot be compared.  The bar is therefore:
+Parity bar (a tolerance, written here).  The oracle sums e4m3 products exactly (float64) and rounds the sum once to
+fp32; the GPU's products are exact and it sums them in fp32 (the f16 MFMA's accumulation: within ~1 fp32 ulp of the
+exact sum per instruction, tools/f8_mfma_probe.hip), so a conv's output code can differ from the oracle's only
+where the requantisation lands within a few fp32 ulps of an e4m3 rounding boundary.  Until round 5 the plan used
+the fp8 MFMA (v_mfma_f32_*_fp8_fp8), whose accumulation is not fp32-exact (outputs a median 505 ulps from the exact
+sum on the probe): ~0.1 % of codes flipped per layer, the flips cascaded through 20+ quantized layers, and the
+plan scored mAP50-95 0.23 against the fp8 oracle.  The bar is:
   * the stem (image quantisation + f16 MFMA on exact e4m3 values + the e4m3 epilogue): every code exact;
-  * every plain Conv layer fed the GPU's own stored input: >= 99.8 % of the output codes exact, none more than two
-    e4m3 steps away (the requantisation to the conv's observer, then the stored tensor's: one flip, two roundings);
-  * detections: the GPU plan's quality against the float oracle within 0.7x of the fp8 oracle's own (mAP50-95 on
-    the fixture images), i.e. the quantisation loss is the fp8 scheme's, not a kernel defect.
+  * every plain Conv layer fed the GPU's own stored input: >= 99.99 % of the output codes exact, none more than one
+    e4m3 step away;
+  * detections end to end: the GPU plan against the fp8 oracle's detections at mAP50-95 >= 0.95 (measured 0.995
+    on the fixture images), and its quality against the float oracle no worse than 0.9x the fp8 oracle's own.
 The e4m3 codec itself (clamp, round to nearest even) is pinned on the CPU against an independent restatement of the
 format (tests/test_fp8_oracle.py).
 """
@@ -107,11 +109,11 @@ def test_f8_conv_layers_match_oracle_locally(name):
     rep = _layer_local(name, (1, 3, 5, 7, 17, 20))
     print("fp8 layer-local (layer, exact codes, max step distance):", rep)
     for i, same, dmax in rep:
-        assert same >= 0.998 and dmax <= 2, rep
+        assert same >= 0.9999 and dmax <= 1, rep
 
 
 @pytest.mark.parametrize("name", list(F8_FIXTURES))
-def test_f8_detection_quality_is_the_schemes(name):
+def test_f8_detections_match_the_fp8_oracle(name):
     from oracle.predict import OracleModel
     from yolomi.metrics import evaluate
     g = fixture(name)
@@ -119,10 +121,10 @@ def test_f8_detection_quality_is_the_schemes(name):
     fl = [r["boxes"].numpy() for r in OracleModel(g["scale"], "detect", synth_weights(g["scale"], "detect", 0)).predict(x)]
     o8 = [np.array(d, np.float32).reshape(-1, 6) for d in g["dets"]]
     g8 = [r.boxes.data.cpu().numpy() for r in f8_model(name).predict(x.to(DEV), conf=g["conf"], iou=g["iou"])]
-    m_o8, m_g8 = evaluate(o8, fl)["map"], evaluate(g8, fl)["map"]
-    print(f"fp8 mAP50-95 vs float oracle: fp8 oracle {m_o8:.3f}, GPU fp8 plan {m_g8:.3f}; GPU vs fp8 oracle "
-          f"{evaluate(g8, o8)['map']:.3f}")
-    assert m_g8 >= 0.7 * m_o8
+    m_o8, m_g8, m_go = evaluate(o8, fl)["map"], evaluate(g8, fl)["map"], evaluate(g8, o8)["map"]
+    print(f"fp8 mAP50-95 vs float oracle: fp8 oracle {m_o8:.3f}, GPU fp8 plan {m_g8:.3f}; GPU vs fp8 oracle {m_go:.3f}")
+    assert m_go >= 0.95
+    assert m_g8 >= 0.9 * m_o8
 
 
 def test_f8_graph_replay_bitwise_equals_eager():

@@ -1,0 +1,124 @@
+#!/usr/bin/env python3
+"""Fit rounding models of the gfx950 fp8 MFMA accumulation to tools/f8_mfma_probe.hip's data.
+
+    python tools/f8_mfma_model.py gpurun_out/.../f8probe.bin
+
+For every output D = C + sum_k A[row][k]·B[k][col] of every instance, the match rate (bitwise, fp32) of:
+  exact      fl32(C + exact sum)                                (one rounding)
+  seq        acc = C; acc = fl32(acc + p_k) for k = 0 .. K-1     (per-product fp32 RNE)
+  prodfirst  fl32(fl32(exact sum) + C)
+  groups g   exact sums of g consecutive products, each rounded to fp32, accumulated in fp32 after C
+  trunc N    every term (C and the products) truncated toward zero to N bits below the largest term's leading bit,
+             summed exactly, rounded to fp32 (RNE) — an aligned fixed-point adder of finite width
+e4m3 products are exact in fp32 (8-bit significands), so any difference is the adder's.  Kind 2 (the same values on
+the f16 MFMA, scaled by 2^-8 each) is the candidate replacement datapath for the fp8 plan.
+"""
+import sys
+
+import numpy as np
+
+
+def e4m3_table():
+    v = np.zeros(256, np.float64)
+    for c in range(256):
+        e, m = (c >> 3) & 15, c & 7
+        x = m * 2.0 ** -9 if e == 0 else (8 + m) * 2.0 ** (e - 10)
+        v[c] = -x if c & 0x80 else x
+    v[0x7F] = v[0xFF] = np.nan
+    return v
+
+
+def load(path):
+    raw = open(path, "rb").read()
+    magic, n, nkinds, ndist = np.frombuffer(raw[:16], np.int32)
+    assert magic == 0x38465059
+    off, out = 16, []
+    for kind in range(nkinds):
+        KL = 32 if kind == 1 else 8
+        na = n * 64 * KL
+        A = np.frombuffer(raw[off:off + na], np.uint8).reshape(n, 64, KL); off += na
+        B = np.frombuffer(raw[off:off + na], np.uint8).reshape(n, 64, KL); off += na
+        C = np.frombuffer(raw[off:off + n * 4096], np.float32).reshape(n, 32, 32); off += n * 4096
+        D = np.frombuffer(raw[off:off + n * 4096], np.float32).reshape(n, 32, 32); off += n * 4096
+        out.append((KL, A, B, C, D))
+    return n, ndist, out
+
+
+def terms(KL, A, B, tab):
+    """Products p[inst][row][col][k] (float64, exact) under the probe's lane map: lane h*32 + r holds
+    A[row r][k = KL h + j] and B[k = KL h + j][col r]."""
+    n = A.shape[0]
+    K = 2 * KL
+    Am = np.zeros((n, 32, K)); Bm = np.zeros((n, K, 32))
+    for h in range(2):
+        Am[:, :, KL * h:KL * (h + 1)] = tab[A[:, 32 * h:32 * (h + 1), :]]
+        Bm[:, KL * h:KL * (h + 1), :] = tab[B[:, 32 * h:32 * (h + 1), :]].transpose(0, 2, 1)
+    return Am[:, :, None, :] * Bm.transpose(0, 2, 1)[:, None, :, :]  # (n, row, col, k)
+
+
+def f32(x):
+    return np.asarray(x, np.float64).astype(np.float32)
+
+
+def main():
+    n, ndist, kinds = load(sys.argv[1])
+    tab = e4m3_table()
+    for kind, (KL, A, B, C, D) in enumerate(kinds):
+        P = terms(KL, A, B, tab)  # exact in float64 (8-bit significands)
+        if kind == 2:  # the f16 MFMA on e4m3 values scaled by 2^-8 each
+            P = P * 2.0 ** -16
+        K = P.shape[-1]
+        Cd = C.astype(np.float64)
+        L = P.astype(np.longdouble).sum(-1) + Cd.astype(np.longdouble)  # exact: the spans fit 64 bits here
+        models = {}
+        models["exact"] = L.astype(np.float32)
+        acc = C.copy()
+        for k in range(K):
+            acc = (acc + P[..., k].astype(np.float32)).astype(np.float32)
+        models["seq"] = acc
+        acc = C.copy()
+        for k in reversed(range(K)):
+            acc = (acc + P[..., k].astype(np.float32)).astype(np.float32)
+        models["seq_rev"] = acc
+        models["prodfirst"] = (P.astype(np.longdouble).sum(-1).astype(np.float32) + C).astype(np.float32)
+        for g in (2, 4, 8, 16, 32):
+            if g > K:
+                continue
+            acc = C.copy()
+            for k0 in range(0, K, g):
+                grp = P[..., k0:k0 + g].astype(np.longdouble).sum(-1).astype(np.float32)
+                acc = (acc + grp).astype(np.float32)
+            models[f"groups{g}"] = acc
+            acc = P[..., :g].astype(np.longdouble).sum(-1).astype(np.float32)
+            for k0 in range(g, K, g):
+                acc = (acc + P[..., k0:k0 + g].astype(np.longdouble).sum(-1).astype(np.float32)).astype(np.float32)
+            models[f"groups{g}_Clast"] = (acc + C).astype(np.float32)
+        T = np.concatenate([P, Cd[..., None]], -1)  # all terms
+        absmax = np.abs(T).max(-1)
+        emax = np.floor(np.log2(np.where(absmax > 0, absmax, 1.0)))
+        for N in (24, 25, 26, 27, 28, 30, 32, 36, 40):
+            q = 2.0 ** (emax - N + 1)  # the adder's LSB
+            tt = np.trunc(T / q[..., None])  # toward zero, exact in float64 for these spans
+            s = tt.astype(np.longdouble).sum(-1) * q.astype(np.longdouble)
+            models[f"trunc{N}"] = s.astype(np.float32)
+            tr = np.floor(T / q[..., None])  # toward -inf
+            s = tr.astype(np.longdouble).sum(-1) * q.astype(np.longdouble)
+            models[f"floor{N}"] = s.astype(np.float32)
+        per = n // ndist
+        print(f"kind {kind} (K={K}): {n} instances x 1024 outputs")
+        for name, Mv in models.items():
+            eq = (Mv.view(np.uint32) == D.view(np.uint32)) | ((Mv == 0) & (D == 0))
+            rates = [eq[d * per:(d + 1) * per].mean() for d in range(ndist)]
+            print(f"  {name:16s} all {eq.mean() * 100:8.4f} %   by distribution " +
+                  " ".join(f"{r * 100:7.3f}" for r in rates), flush=True)
+        # where exact fails: how far, in fp32 ulps
+        ex = models["exact"]
+        bad = ex.view(np.uint32) != D.view(np.uint32)
+        if bad.any():
+            ulp = np.abs(ex[bad].view(np.int32).astype(np.int64) - D[bad].view(np.int32).astype(np.int64))
+            print(f"  exact vs D where they differ: ulps min {ulp.min()} median {np.median(ulp)} max {ulp.max()}, "
+                  f"D closer to zero {np.mean(np.abs(D[bad]) < np.abs(ex[bad])):.3f}")
+
+
+if __name__ == "__main__":
+    main()

@@ -26,10 +26,11 @@ __device__ __forceinline__ int pack4(const int* v) {
 // ---------------------------------------------------------------------------------------------- fp8 (e4m3) plans
 // The fp8 PTQ plan (oracle/quant.py backend "fp8") stores every quantized tensor as OCP e4m3 codes (gfx950's fp8
 // format) with a per-tensor scale and zero point 0: code = e4m3(clamp(v·(1/s), ±448)), round to nearest even, and
-// its value is e4m3(code)·s.  Weights are e4m3 with per-output-channel scales; convs accumulate on the fp8 MFMA in
-// fp32.  Everything else — requantising the conv output to its observer, the 256-entry post table indexed by that
-// code, residual adds, the stored tensor's code — is the int8 plan's structure with this codec in place of the affine
-// uint8 one (the post table still has exactly 256 entries: a code is one byte).
+// its value is e4m3(code)·s.  Weights are e4m3 with per-output-channel scales; convs multiply the e4m3 values
+// exactly on the f16 MFMA (below) and accumulate in fp32.  Everything else — requantising the conv output to its
+// observer, the 256-entry post table indexed by that code, residual adds, the stored tensor's code — is the int8
+// plan's structure with this codec in place of the affine uint8 one (the post table still has exactly 256 entries:
+// a code is one byte).
 typedef float f32x16 __attribute__((ext_vector_type(16)));
 typedef int i32x16 __attribute__((ext_vector_type(16)));
 
@@ -72,15 +73,40 @@ template <> struct Q8<true> {
 };
 
 // one 16-byte K chunk per lane: int8 = one MFMA, fp8 = two (bytes 0-7, 8-15; A and B split alike, so the pairs of
-// k indices the hardware multiplies are the same as in the int8 instruction)
+// k indices the hardware multiplies are the same as in the int8 instruction).
+//
+// The e4m3 operands are multiplied on the f16 MFMA, each code widened exactly to fp16 first
+// (v_cvt_scalef32_pk_f16_fp8, scale 1: every e4m3 value, subnormals included, is an fp16 value).  The fp8 MFMA
+// itself (v_mfma_f32_*_fp8_fp8, same cycles as the f16 form of the same M×N on gfx950) is far from the exact sum of
+// its products: on tools/f8_mfma_probe.hip's data 24 % of its outputs equal fl32(C + exact sum), the others are a
+// median 505 fp32 ulps away (up to ~2^-11 of the largest product; profiles/r05h_f8_mfma_probe.txt).  That flipped
+// ~0.1 % of a conv's e4m3 output codes against the oracle's exact sum and, cascading through 20+ quantized layers,
+// left the plan at mAP50-95 0.23 against the fp8 oracle.  The f16 MFMA on the same values: 82 % equal, the others a
+// median 1 ulp away (its two 8-product halves summed as in fp32: tools/f8_mfma_model.py "groups8", 93 %).
+// YM_F8_NATIVE_MFMA keeps the fp8 instruction for A/Bs.
+typedef _Float16 f16x2_t __attribute__((ext_vector_type(2)));
+typedef _Float16 f16x8_t __attribute__((ext_vector_type(8)));
+__device__ __forceinline__ f16x8_t f8x8_to_f16(long v) {
+  const unsigned lo = (unsigned)v, hi = (unsigned)((unsigned long)v >> 32);
+  const f16x2_t p0 = __builtin_amdgcn_cvt_scalef32_pk_f16_fp8(lo, 1.0f, false);
+  const f16x2_t p1 = __builtin_amdgcn_cvt_scalef32_pk_f16_fp8(lo, 1.0f, true);
+  const f16x2_t p2 = __builtin_amdgcn_cvt_scalef32_pk_f16_fp8(hi, 1.0f, false);
+  const f16x2_t p3 = __builtin_amdgcn_cvt_scalef32_pk_f16_fp8(hi, 1.0f, true);
+  return f16x8_t{p0[0], p0[1], p1[0], p1[1], p2[0], p2[1], p3[0], p3[1]};
+}
 __device__ __forceinline__ i32x4 mfma16(i8x16 a, i8x16 b, i32x4 c) {
   return __builtin_amdgcn_mfma_i32_16x16x64_i8(a, b, c, 0, 0, 0);
 }
 __device__ __forceinline__ f32x4 mfma16(i8x16 a, i8x16 b, f32x4 c) {
   typedef long l2 __attribute__((ext_vector_type(2)));
   const l2 la = __builtin_bit_cast(l2, a), lb = __builtin_bit_cast(l2, b);
+#ifdef YM_F8_NATIVE_MFMA
   c = __builtin_amdgcn_mfma_f32_16x16x32_fp8_fp8(la[0], lb[0], c, 0, 0, 0);
   return __builtin_amdgcn_mfma_f32_16x16x32_fp8_fp8(la[1], lb[1], c, 0, 0, 0);
+#else
+  c = __builtin_amdgcn_mfma_f32_16x16x32_f16(f8x8_to_f16(la[0]), f8x8_to_f16(lb[0]), c, 0, 0, 0);
+  return __builtin_amdgcn_mfma_f32_16x16x32_f16(f8x8_to_f16(la[1]), f8x8_to_f16(lb[1]), c, 0, 0, 0);
+#endif
 }
 __device__ __forceinline__ i32x16 mfma32(i8x16 a, i8x16 b, i32x16 c) {
   return __builtin_amdgcn_mfma_i32_32x32x32_i8(a, b, c, 0, 0, 0);
@@ -88,6 +114,11 @@ __device__ __forceinline__ i32x16 mfma32(i8x16 a, i8x16 b, i32x16 c) {
 __device__ __forceinline__ f32x16 mfma32(i8x16 a, i8x16 b, f32x16 c) {
   typedef long l2 __attribute__((ext_vector_type(2)));
   const l2 la = __builtin_bit_cast(l2, a), lb = __builtin_bit_cast(l2, b);
+#ifdef YM_F8_NATIVE_MFMA
   c = __builtin_amdgcn_mfma_f32_32x32x16_fp8_fp8(la[0], lb[0], c, 0, 0, 0);
   return __builtin_amdgcn_mfma_f32_32x32x16_fp8_fp8(la[1], lb[1], c, 0, 0, 0);
+#else
+  c = __builtin_amdgcn_mfma_f32_32x32x16_f16(f8x8_to_f16(la[0]), f8x8_to_f16(lb[0]), c, 0, 0, 0);
+  return __builtin_amdgcn_mfma_f32_32x32x16_f16(f8x8_to_f16(la[1]), f8x8_to_f16(lb[1]), c, 0, 0, 0);
+#endif
 }
