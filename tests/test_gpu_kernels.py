@@ -67,20 +67,31 @@ def test_dwconv_variants_match_float64(scale, B, dtype, mode):
     assert n == 6
 
 
-@pytest.mark.parametrize("cfg", [-1, 0, 1, 2])
-@pytest.mark.parametrize("scale,B", [("s", 8), ("n", 2)])
-def test_fused_depthwise_1x1_matches_float64(scale, B, cfg):
-    """csrc/ym_conv_dwpw.hip (x3 plans: the Detect-head DWConvs on the stride-8 maps fused into the 1x1 conv they
-    feed, yolomi/arch.py DW_FUSE_STRIDES) in each configuration (-1: the heuristic; 0/1/2: tiles 16, 8 or 4 pixels
-    wide, YM_DWPW_CFGS), eager forwards: the stored 1x1 output =
+@pytest.mark.parametrize("cfg", [-1, 0, 1, 2, 3, 4, 5, 6, 7])
+@pytest.mark.parametrize("scale,B,strides", [("s", 8, ""), ("n", 2, ""), ("s", 8, "8,16,32"), ("n", 2, "8,16,32")])
+def test_fused_depthwise_1x1_matches_float64(scale, B, strides, cfg):
+    """csrc/ym_conv_dwpw.hip (x3 plans: the Detect-head DWConvs fused into the 1x1 conv they feed, yolomi/arch.py
+    DW_FUSE_STRIDES; strides "8,16,32" = every level, YM_DW_FUSE_STRIDES) in each configuration (-1: the heuristic;
+    0/1/2: tiles 16, 8 or 4 pixels wide; 3-7: the K split over 2-8 workgroups, YM_DWPW_CFGS — a split the op's K
+    blocks cannot take falls back to the heuristic), eager forwards: the stored 1x1 output =
     SiLU(b + W · SiLU(b_dw + Σ_taps w_dw·x)) of the stored depthwise input, against float64 with the same fp32
     weights, within 2e-6 of the output's max magnitude (the x3 GEMM's split products miss only lo·lo, ~2^-22)."""
     from core.model import YOLO11Model
     from yolomi.plan import _conv_weights
+    import os
     sd = synth_weights(scale, "detect", 0)
-    if (scale, "x3dw") not in _models:
-        _models[(scale, "x3dw")] = YOLO11Model(task="detect", size=scale, device="cuda:0", dtype="x3", verbose=False)
-    eng = _models[(scale, "x3dw")].model.engine
+    key = (scale, "x3dw", strides)
+    if key not in _models:
+        if strides:  # (a plan with no committed table: heuristic tiles, no ym_tune here — the test sets the cfgs)
+            os.environ["YM_DW_FUSE_STRIDES"] = strides
+            os.environ["YM_AUTOTUNE"] = "0"
+        try:
+            _models[key] = YOLO11Model(task="detect", size=scale, device="cuda:0", dtype="x3", verbose=False)
+        finally:
+            os.environ.pop("YM_DW_FUSE_STRIDES", None)
+            if strides:
+                os.environ.pop("YM_AUTOTUNE", None)
+    eng = _models[key].model.engine
     x = synthetic_batch(B, 640, 78, DEV)
     eng.run(x, use_graph=False)  # tables for this shape
     try:
@@ -105,7 +116,7 @@ def test_fused_depthwise_1x1_matches_float64(scale, B, cfg):
             err = (got - ref).abs().max().item() / ref.abs().max().item()
             assert err < 2e-6, (op.name, cfg, err)
             n += 1
-        assert n == 2
+        assert n == (6 if strides else 2)
     finally:
         eng._tuned.discard((B, 640, 640))
 

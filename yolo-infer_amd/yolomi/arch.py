@@ -404,7 +404,9 @@ class GraphBuilder:
     # map strides whose depthwise ops are fused: measured (yolo11s B=8 x3 replay, r04) the fused kernel beats the
     # depthwise + 1x1 launches on the P3 maps only (80²: 32.6 vs 35.5 us per pair); on P4 / P5 (40², 20²) the few
     # workgroups run their K blocks' load → depthwise → MFMA chains at ~2-4 us each and lose (21.8 vs 18.5 us,
-    # 35.7 vs 14.9 us for the 512-channel P5 input)
+    # 35.7 vs 14.9 us for the 512-channel P5 input).  Round 5 split those K blocks over 2-8 workgroups (SPLIT
+    # configs): still behind the split pairs (level 1 chain 40.1 vs 38.1 us, level 2 37.1 vs 28.6;
+    # profiles/r05i_dwpw_split_ab.txt)
     DW_FUSE_STRIDES = (8,)
 
     def fuse_dw(self):
@@ -428,9 +430,14 @@ class GraphBuilder:
             i += 1
         self.ops = out
 
+    def _dw_fuse_strides(self):
+        import os
+        e = os.environ.get("YM_DW_FUSE_STRIDES")  # A/B override, e.g. "8,16,32"
+        return tuple(int(v) for v in e.split(",") if v) if e else self.DW_FUSE_STRIDES
+
     def _dw_fusable(self, D: Op, B: Op) -> bool:
         d = D.args
-        if B.kind != "conv" or not d["act"] or d["src"].buf.f not in self.DW_FUSE_STRIDES:
+        if B.kind != "conv" or not d["act"] or d["src"].buf.f not in self._dw_fuse_strides():
             return False
         b = B.args
         mid = d["dst"]
