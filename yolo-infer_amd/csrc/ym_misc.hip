@@ -21,7 +21,9 @@ namespace {
 // aborted forward), reduces a contiguous chunk of the batch to its max and stores it write-through (sc1) into its
 // partial slot; after its `vmcnt(0)` one lane takes an agent-scope ticket, and the block whose ticket is last
 // reduces the partials (sc1 loads: the hand-off of MI355X_MICROARCH §inter-workgroup visibility, first table row),
-// writes the slots and resets the ticket.  No per-forward init kernel, no same-address atomicMax storm.
+// writes the slots and resets the ticket.  No per-forward init kernel, no same-address atomicMax storm.  The ticket
+// starts at zero (ensure_workspace zeroes the arena it lives in), and a launch can only stop part-way through a device
+// fault, which ends the context: a stale ticket cannot carry into a later forward.
 // batch_max non-null (multi-GPU shard): the slots take the given global max, x is not read.
 constexpr int kStatsBlocks = 1024;  // partial slots (ym_runtime.cpp reserves them behind the ctl slots)
 constexpr int kStatsU = 10;         // float4 loads in flight per lane and round
