@@ -502,7 +502,7 @@ def test_fused_pairs_split_equals_unfused_plan():
     ef.run(x, use_graph=False)
     fused = ef.rt.get_op_cfg(B, H, W)
     try:
-        ef.rt.set_op_cfg(B, H, W, [(SPLIT_TAG + 128 * cfg + cfg if op.args.get("pair") else cfg)
+        ef.rt.set_op_cfg(B, H, W, [(SPLIT_TAG + 256 * cfg + cfg if op.args.get("pair") else cfg)
                                    if op.kind == "conv" else -1 for op in ef.graph.ops])
         eu.run(x, use_graph=False)
         ef.run(x, use_graph=False)
@@ -550,7 +550,7 @@ def test_bneck_kernel_matches_split_pair(scale):
                 for i in bn]
 
     try:
-        ref = outputs(SPLIT_TAG + 128 * 29 + 29)  # the two convs as separate launches (LDS-DMA tiles)
+        ref = outputs(SPLIT_TAG + 256 * 29 + 29)  # the two convs as separate launches (LDS-DMA tiles)
         for v in range(N_BNECK):
             got = outputs(BNECK_BASE + v)
             for i, r, g in zip(bn, ref, got):

@@ -228,7 +228,7 @@ def test_x3_fused_pairs_match_split(scale):
     try:
         split = list(base)
         for i in pairs:
-            split[i] = SPLIT_TAG + 128 * 29 + 29  # one LDS-DMA tile for both convs (inapplicable: the heuristic)
+            split[i] = SPLIT_TAG + 256 * 29 + 29  # one LDS-DMA tile for both convs (inapplicable: the heuristic)
         eng.rt.set_op_cfg(B, H, W, split)
         eng.run(x, use_graph=False)
         ref = eng.read_buffer(eng.graph.anchor_buf.id, B)

@@ -1,24 +1,48 @@
 #!/bin/bash
-# Round-end evidence on one box: smoke, the whole GPU suite, the three bench lines, rocprofv3 stats + PMC passes of
-# the headline bench command, and the per-op replay table.  Each GPU step under its own limit; a fatal status ends it.
+# Round-end evidence on one box: smoke, the whole GPU suite, the bench lines (headline yolo11s x3, yolo11n x3,
+# yolo11s-seg, the yolo11n PTQ int8 / fp8 lines and f16 beside them), the per-op replay table, rocprofv3 stats and
+# PMC passes of the headline bench command.  Each GPU step under its own limit; a fatal status ends it.
+#   TAG=r05z STEPS="smoke suite" bash tools/gpu_final.sh        (default: every step; output gpurun_out/$TAG)
 cd "$(dirname "$0")/.." || exit 1
-mkdir -p gpurun_out/final
+OUT=gpurun_out/${TAG:-final}
+mkdir -p "$OUT"
 export TMPDIR=/tmp
-: > gpurun_out/final/steps.log
+: > "$OUT/steps.log"
 run() {  # name limit cmd...
   local name=$1 lim=$2; shift 2
-  timeout -k 10 "$lim" "$@" > "gpurun_out/final/$name.log" 2>&1
+  timeout -k 10 "$lim" "$@" > "$OUT/$name.log" 2>&1
   local rc=$?
-  echo "[$name] rc=$rc $(date +%T)" | tee -a gpurun_out/final/steps.log
+  echo "[$name] rc=$rc $(date +%T)" | tee -a "$OUT/steps.log"
   if [ $rc -ge 124 ] || [ $rc -eq 134 ] || [ $rc -eq 139 ]; then exit $rc; fi
   return 0
 }
-run smoke 300 python -u -c "import __graft_entry__ as g; g.smoke(); print('smoke ok')"
-run suite 1200 python -u -X faulthandler -m pytest tests -m gpu -q -p no:cacheprovider --timeout 300 --timeout-method thread
-run bench_s 400 python -u bench.py
-run bench_n 400 python -u bench.py --model n --no-f16
-run bench_seg 400 python -u bench.py --task segment --batch 4 --no-f16
-run optable 200 python -u tools/op_table.py --model s --dtype x3
-bash tools/gpu_round.sh prof > gpurun_out/final/prof_step.log 2>&1 || exit 1
-PMC_ARGS="--model s --dtype x3" bash tools/gpu_round.sh pmc > gpurun_out/final/pmc_step.log 2>&1 || exit 1
-echo done >> gpurun_out/final/steps.log
+for step in ${STEPS:-smoke suite bench_s bench_n bench_seg bench_ptq optable prof pmc}; do
+  case $step in
+    smoke) run smoke 300 python -u -c "import __graft_entry__ as g; g.smoke(); print('smoke ok')" ;;
+    suite) run suite 1100 python -u -X faulthandler -m pytest tests -m gpu -q -p no:cacheprovider --timeout 300 --timeout-method thread ;;
+    bench_s) run bench_s 400 python -u bench.py ;;
+    bench_n) run bench_n 400 python -u bench.py --model n --no-f16 ;;
+    bench_seg) run bench_seg 400 python -u bench.py --task segment --batch 4 --no-f16 ;;
+    bench_ptq) run bench_n_i8 400 python -u bench.py --model n --dtype i8
+               run bench_n_f8 400 python -u bench.py --model n --dtype f8
+               run bench_n_f16 400 python -u bench.py --model n --dtype f16 --no-cpu ;;
+    optable) run optable 200 python -u tools/op_table.py --model s --dtype x3 ;;
+    prof) (cd /tmp && timeout -k 10 400 rocprofv3 --kernel-trace --stats --output-format csv \
+             -d "$GRAFT_REPO_ROOT/$OUT/prof" -o run -- python3 "$GRAFT_REPO_ROOT/bench.py" --steps 50 \
+             --warmup 10 --no-cpu --no-f16 > "$GRAFT_REPO_ROOT/$OUT/prof_bench.log" 2>&1); rc=$?
+          echo "[prof] rc=$rc $(date +%T)" | tee -a "$OUT/steps.log"
+          if [ $rc -ne 0 ]; then exit $rc; fi
+          python3 tools/trace_timeline.py "$OUT/prof" 20 55 > "$OUT/timeline.txt" 2>&1 ;;
+    pmc) (cd /tmp && timeout -s KILL 300 rocprofv3 --pmc FETCH_SIZE --output-format csv \
+             -d "$GRAFT_REPO_ROOT/$OUT/pmc_fetch" -o run -- python3 "$GRAFT_REPO_ROOT/tools/pmc_forward.py" --model s --dtype x3 \
+             > "$GRAFT_REPO_ROOT/$OUT/pmc_fetch.log" 2>&1); rc=$?
+         echo "[pmc_fetch] rc=$rc $(date +%T)" | tee -a "$OUT/steps.log"
+         if [ $rc -ne 0 ]; then exit $rc; fi
+         (cd /tmp && timeout -s KILL 300 rocprofv3 --pmc WRITE_SIZE --output-format csv \
+             -d "$GRAFT_REPO_ROOT/$OUT/pmc_write" -o run -- python3 "$GRAFT_REPO_ROOT/tools/pmc_forward.py" --model s --dtype x3 \
+             > "$GRAFT_REPO_ROOT/$OUT/pmc_write.log" 2>&1); rc=$?
+         echo "[pmc_write] rc=$rc $(date +%T)" | tee -a "$OUT/steps.log"
+         if [ $rc -ne 0 ]; then exit $rc; fi ;;
+  esac
+done
+echo done >> "$OUT/steps.log"

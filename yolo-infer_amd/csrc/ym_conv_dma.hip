@@ -795,7 +795,10 @@ hipError_t launch_dma(ConvArgs a, int kind, hipStream_t st) {
 
 // x3-only configurations (op cfg ids appended after the whole f16 catalogue, so the f16 tables keep their ids): the
 // pair layout doubles a conv's storage K, and with it the chain of K stages of the latency-bound 20² / 40² layers —
-// split K 3-8 ways over workgroups with 128-192-deep stages to shorten it.
+// split K 3-8 ways over workgroups with 128-192-deep stages to shorten it.  (Round 5 tried the same splits on 128-wide
+// tiles, whose waves own 64 x 64 blocks and so read each LDS fragment for 2 MFMAs instead of 1: slower on every 20² /
+// 40² op, e.g. 16.3 vs 12.3 us for a 20² 3x3 128 -> 128 — fewer workgroups and one wave per SIMD;
+// profiles/r05l_x3_wide_tiles.txt.)
 #define YM_DMA_X3_CFGS(X)                                                                                      \
   X(0, 64, 64, 4, 2, 2, 3) X(1, 64, 64, 4, 2, 2, 2) X(2, 64, 64, 3, 2, 2, 2) X(3, 64, 64, 6, 2, 2, 2)          \
   X(4, 64, 64, 8, 2, 2, 2) X(5, 64, 64, 4, 1, 2, 2) X(6, 64, 128, 4, 2, 2, 2) X(7, 64, 64, 2, 2, 2, 4)         \

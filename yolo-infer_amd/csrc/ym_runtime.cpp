@@ -401,7 +401,7 @@ int conv_args(ym_ctx* c, const Op& op, int B, const float* d_in, float in_eps, C
         if ((a.k2 != 1 && a.k2 != 3) || a.N2 <= 0 || a.Kpad2 < a.k2 * a.k2 * cout * (a.x3 ? 2 : 1) || r[31] < 0 || r[31] >= (int)c->bufs.size() || cout % 8 ||
             c->buf_H(r[31]) != a.Ho || c->buf_Wd(r[31]) != a.Wo || c->bufs[r[31]].C != cout || c->bufs[r[31]].f32)
           return fail(YM_EBLOB, "op %s: bad fused-pair geometry", op.name);
-        if (ym_conv_num_cfgs_dt(c->dtype) > 127) return fail(YM_EBLOB, "split cfg encoding needs < 128 conv configs");
+        if (ym_conv_num_cfgs_dt(c->dtype) > 255) return fail(YM_EBLOB, "split cfg encoding needs < 256 conv configs");
       }
       if (r[24] > 0 && !ym_dt_q8(c->dtype)) {  // fused depthwise (yolomi/arch.py fuse_dw): 1 + offset of [9][C] ‖ [C]
         if ((c->dtype != YM_DT_F16 && c->dtype != YM_DT_X3) || k != 1 || s != 1 || b1 >= 0 || up0 || r[30])
@@ -447,7 +447,7 @@ int conv_args(ym_ctx* c, const Op& op, int B, const float* d_in, float in_eps, C
 
 // A fused pair (ConvArgs::w2) run as its two convs: A writes the intermediate buffer (record r[31]), B reads it.
 // The tuner picks this when the two tuned single launches beat every fused variant (op cfg kSplitTag + ...).
-constexpr int kSplitTag = 1 << 20;  // op cfg = kSplitTag + 128 * cfg(A) + cfg(B)
+constexpr int kSplitTag = 1 << 20;  // op cfg = kSplitTag + 256 * cfg(A) + cfg(B)
 void split_args(ym_ctx* c, const Op& op, const ConvArgs& a, ConvArgs& A, ConvArgs& Bc) {
   const int mid = op.r[31];
   A = a;
@@ -470,12 +470,12 @@ hipError_t launch_fused(ym_ctx* c, const Op& op, const ConvArgs& a, int out_f32,
   if (cfg < kSplitTag) {
     const hipError_t e = ym_launch_conv(c->dtype, out_f32, a, cfg, st);
     if (e != hipErrorInvalidValue) return e;
-    cfg = kSplitTag + 128 * 127 + 127;  // no fused kernel takes this shape (e.g. a map width the Bottleneck kernel
+    cfg = kSplitTag + 256 * 255 + 255;  // no fused kernel takes this shape (e.g. a map width the Bottleneck kernel
   }                                     // does not tile): the two convs with their heuristic tiles
   ConvArgs A, Bc;
   split_args(c, op, a, A, Bc);
-  const hipError_t e = ym_launch_conv(c->dtype, 0, A, ((cfg - kSplitTag) >> 7) & 127, st);
-  return e != hipSuccess ? e : ym_launch_conv(c->dtype, out_f32, Bc, (cfg - kSplitTag) & 127, st);
+  const hipError_t e = ym_launch_conv(c->dtype, 0, A, ((cfg - kSplitTag) >> 8) & 255, st);
+  return e != hipSuccess ? e : ym_launch_conv(c->dtype, out_f32, Bc, (cfg - kSplitTag) & 255, st);
 }
 
 int launch_op(ym_ctx* c, const Op& op, int B, const float* d_in, const ym_infer_args* args, float* d_dets,
@@ -1243,7 +1243,7 @@ int ym_tune(ym_ctx* c, const float* d_in, int B, int H, int W, const ym_infer_ar
       split_args(c, op, a, A, Bc);
       int ca = -1, cb = -1;
       const float ta = tune_one(A, 0, ca), tb = tune_one(Bc, out_f32, cb);
-      if (ca >= 0 && cb >= 0 && ta + tb < tf) best[i] = kSplitTag + 128 * ca + cb;
+      if (ca >= 0 && cb >= 0 && ta + tb < tf) best[i] = kSplitTag + 256 * ca + cb;
     }
   }
   (void)hipEventDestroy(e0);
@@ -1264,8 +1264,8 @@ int ym_set_op_cfg(ym_ctx* c, int B, int H, int W, const int* cfg, int n) {
   if (!c || !cfg || n != (int)c->ops.size()) return fail(YM_EINVAL, "cfg array must hold %zu entries", c ? c->ops.size() : 0);
   for (int i = 0; i < n; ++i) {
     if (cfg[i] >= kSplitTag && c->ops[i].r[0] == OP_CONV && c->ops[i].r[30] &&
-        ((cfg[i] - kSplitTag) >> 7) < ym_conv_num_cfgs_dt(c->dtype) &&
-        ((cfg[i] - kSplitTag) & 127) < ym_conv_num_cfgs_dt(c->dtype))
+        ((cfg[i] - kSplitTag) >> 8) < ym_conv_num_cfgs_dt(c->dtype) &&
+        ((cfg[i] - kSplitTag) & 255) < ym_conv_num_cfgs_dt(c->dtype))
       continue;  // a fused pair run as two launches
     if (cfg[i] >= ym_conv_num_cfgs_dt(c->dtype)) return fail(YM_EINVAL, "cfg[%d] = %d out of range", i, cfg[i]);
   }

@@ -17,7 +17,7 @@ from .lib import Runtime
 from .plan import QUANT_DTYPES, fuse_default, pack_graph
 
 # Bump when the meaning of a conv config index (csrc/ym_conv.hip kCfgs) changes: stale tables are then ignored.
-TUNE_VERSION = 10
+TUNE_VERSION = 11  # 11: split-pair cfgs encoded kSplitTag + 256·a + b (8 bits per config)
 TUNED_DIR = os.path.join(os.path.dirname(os.path.abspath(__file__)), "tuned")  # committed tables
 
 
