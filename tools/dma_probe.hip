@@ -59,10 +59,6 @@ int main(int argc, char** argv) {
   a.s0_elems = (long)nin; a.s1_elems = 0;
   a.fd_hw = ym_fdiv(Ho * Wo); a.fd_w = ym_fdiv(Wo);
   a.slab = slab; a.slab_cap = 64 << 20; a.cnt = cnt; a.cnt_cap = 65536;
-  void* zeros;
-  CK(hipMalloc(&zeros, 4096));
-  CK(hipMemset(zeros, 0, 4096));
-  a.zeros = zeros;
   hipStream_t st;
   CK(hipStreamCreate(&st));
   for (int i = 0; i < 5; ++i) CK(ym_launch_conv_dma(0, a, cfg, st));

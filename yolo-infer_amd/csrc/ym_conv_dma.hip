@@ -50,6 +50,13 @@ __device__ __forceinline__ void wait_vm() {
   __builtin_amdgcn_s_waitcnt((N & 0xF) | ((N >> 4) << 14) | (0x7 << 4) | (0xF << 8));
 }
 
+// a DMA byte offset, or OOB (the DMA deposits zeros) where !ok: branch-free bit select — a ?: here compiled to an
+// exec-mask branch around the address arithmetic before every DMA instruction
+__device__ __forceinline__ unsigned oob_sel(bool ok, unsigned off) {
+  const unsigned m = 0u - (unsigned)ok;
+  return (off & m) | (OOB & ~m);
+}
+
 __device__ __forceinline__ void raw_barrier() { asm volatile("s_waitcnt lgkmcnt(0)\n\ts_barrier" ::: "memory"); }
 
 __device__ __forceinline__ void dma16(__amdgpu_buffer_rsrc_t r, void* lds, unsigned voff) {
@@ -125,7 +132,9 @@ __global__ __launch_bounds__(256 * KG) void conv_dma(const ConvArgs a) {
 #ifndef YM_NO_WARM
   ym_warm_kernargs<sizeof(ConvArgs)>();
 #endif
-  const int tid = threadIdx.x, lane = tid & 63, wid = tid >> 6;
+  // wid in an SGPR (uniform per wave): every LDS-DMA destination (M0) derived from it is then scalar arithmetic,
+  // not a VALU address moved to M0 by v_readfirstlane before each DMA instruction
+  const int tid = threadIdx.x, lane = tid & 63, wid = __builtin_amdgcn_readfirstlane(tid >> 6);
   const int kg = wid >> 2, wq = wid & 3;
   const int wm = wq & 1, wn = wq >> 1;
   const int l32 = lane & 31, h = lane >> 5;
@@ -290,7 +299,7 @@ __global__ __launch_bounds__(256 * KG) void conv_dma(const ConvArgs a) {
 #pragma unroll
       for (int gi = 0; gi < GB; ++gi) {
         const int pb = second ? pbase1[gi] : pbase0[gi];
-        const unsigned off = pb >= 0 ? (unsigned)(pb + chunk * 8 - (second ? C0s : 0)) * 2u : OOB;
+        const unsigned off = oob_sel(pb >= 0, (unsigned)(pb + chunk * 8 - (second ? C0s : 0)) * 2u);
         dma16(second ? rs1 : rs0, sbase + (wid + NW * gi) * 1024, off);
       }
     } else if constexpr (KIND == 3) {
@@ -299,8 +308,7 @@ __global__ __launch_bounds__(256 * KG) void conv_dma(const ConvArgs a) {
       for (int gi = 0; gi < GB; ++gi) {
         const int iy = piy[gi] + ty, ix = pix[gi] + tx;
         const bool ok = pbase0[gi] >= 0 && (unsigned)iy < (unsigned)a.Hin && (unsigned)ix < (unsigned)a.Win;
-        const unsigned off =
-            ok ? (unsigned)((pbase0[gi] + iy * a.Win + ix) * s0_ctot + s0_coff + cb * 8) * 2u : OOB;
+        const unsigned off = oob_sel(ok, (unsigned)((pbase0[gi] + iy * a.Win + ix) * s0_ctot + s0_coff + cb * 8) * 2u);
         dma16(rs0, sbase + (wid + NW * gi) * 1024, off);
       }
       cb += 8;
@@ -309,7 +317,7 @@ __global__ __launch_bounds__(256 * KG) void conv_dma(const ConvArgs a) {
       const int S = (ky * a.Win + kx) * s0_ctot + cb * 8;  // uniform
 #pragma unroll
       for (int gi = 0; gi < GB; ++gi) {
-        const unsigned off = (tmask[gi] >> tap) & 1u ? (unsigned)(pbase0[gi] + S) * 2u : OOB;
+        const unsigned off = oob_sel((tmask[gi] >> tap) & 1u, (unsigned)(pbase0[gi] + S) * 2u);
         dma16(rs0, sbase + (wid + NW * gi) * 1024, off);
       }
       cb += 8;
@@ -322,7 +330,7 @@ __global__ __launch_bounds__(256 * KG) void conv_dma(const ConvArgs a) {
     // A: weights
 #pragma unroll
     for (int gi = 0; gi < GA; ++gi) {
-      const unsigned off = wbase[gi] >= 0 ? (unsigned)(wbase[gi] + kcur * DK) * 2u : OOB;
+      const unsigned off = oob_sel(wbase[gi] >= 0, (unsigned)(wbase[gi] + kcur * DK) * 2u);
       dma16(rw, sbase + BM * 128 + (wid + NW * gi) * 1024, off);
     }
     ++kcur;
