@@ -109,10 +109,11 @@ def test_predict_kwargs_f32(kw):
         assert len(res[0]) <= kw["max_det"]
 
 
-@pytest.mark.parametrize("conf", [0.5, 0.3, 0.15, 0.06, 0.02, 0.004])
+@pytest.mark.parametrize("conf", [0.5, 0.3, 0.15, 0.06, 0.02, 0.004, 0.001])
 def test_nms_paths_f32(conf):
     """Candidate counts from a few dozen to thousands per image: the one-wave (<= 64), bit-matrix (<= 512) and
-    LDS / global-scratch (> 512) NMS paths of csrc/ym_misc.hip nms_image all reproduce torchvision's greedy order."""
+    blocked (> 512; the validator's conf 0.001) NMS paths of csrc/ym_misc.hip nms_image all reproduce torchvision's
+    greedy order."""
     x = make_input("uniform", (31, 32), 640)
     ref = oracle().predict(x, conf=conf)
     res = model("n", "f32").predict(x.to(DEV), conf=conf)
@@ -834,3 +835,26 @@ def test_max_nms_truncation_1280_conf0001(dtype):
         check(ref, res, 0.001, 0.7, 1e-3, 1e-3)
     else:
         check(ref, res, 0.001, 0.7, 1.0, 1e-2, min_frac=0.9)
+
+
+@pytest.mark.parametrize("dtype,B", [("f32", 2), ("x3", 8)])
+def test_nms_blocked_path_equals_per_box_path(dtype, B):
+    """csrc/ym_misc.hip nms_image's blocked path (512 < candidates <= 8,960 after max_nms: sort in LDS, then blocks
+    of 512 filtered against the kept list and scanned through their own IoU bit matrix) against the one-box-per-
+    barrier path it replaced (YM_NMS_DBG=9), on the same forward's candidates at the validator's conf 0.001 and at
+    0.02 / 0.004: bit-identical rows and counts (greedy NMS is a function of the sorted candidates alone)."""
+    import os
+    eng = model("n", dtype).model.engine
+    x = make_input("uniform", tuple(range(71, 71 + B)), 640).to(DEV)
+    for conf in (0.001, 0.004, 0.02):
+        d0, c0 = (t.clone() for t in eng.run(x, conf=conf, use_graph=False))
+        os.environ["YM_NMS_DBG"] = "9"
+        try:
+            d1, c1 = (t.clone() for t in eng.run(x, conf=conf, use_graph=False))
+        finally:
+            del os.environ["YM_NMS_DBG"]
+        assert torch.equal(c0, c1), (conf, c0.tolist(), c1.tolist())
+        for b in range(B):
+            n = int(c0[b])
+            assert torch.equal(d0[b, :n], d1[b, :n]), (conf, b)
+        assert int(c0[:B].max()) > 64  # candidates past the one-wave path

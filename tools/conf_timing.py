@@ -2,7 +2,7 @@
 """Forward time vs confidence threshold (the validator's conf 0.001 vs predict's 0.25): graph-replayed forwards of
 yolo11s x3 B=8 on the bench batch, events around 20 replays per threshold; the detections kept per image.  GPU only.
 
-    python tools/conf_timing.py [scale] [B]"""
+    CONFS=0.001 python tools/conf_timing.py [scale] [B]     (CONFS: the thresholds, default 0.25,0.05,0.01,0.001)"""
 import os
 import sys
 
@@ -21,7 +21,7 @@ def main():
     m = YOLO11Model(task="detect", size=scale, device="cuda:0", dtype="x3", verbose=False)
     eng = m.model.engine
     x = synthetic_batch(B, 640, 1000, torch.device("cuda", 0))
-    for conf in (0.25, 0.05, 0.01, 0.001):
+    for conf in [float(c) for c in os.environ.get("CONFS", "0.25,0.05,0.01,0.001").split(",")]:
         for _ in range(3):
             eng.run(x, conf=conf)
         torch.cuda.synchronize()

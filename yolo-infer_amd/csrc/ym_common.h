@@ -409,7 +409,7 @@ struct NmsArgs {
   int A, kstride, nm, max_det, max_nms, agnostic, B;
   float max_wh, img_h, img_w;
   double iou;
-  int dbg;  // phase ablation (YM_NMS_DBG, timing only): exit after phase dbg of the bit-matrix path
+  int dbg;  // YM_NMS_DBG: 1-7 phase ablations of the bit-matrix path (timing only); 9 disables the blocked path
 };
 
 struct LetterboxArgs {

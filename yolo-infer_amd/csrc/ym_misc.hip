@@ -1201,6 +1201,17 @@ __global__ __launch_bounds__(256) void decode_anchors(const DecodeArgs a) {
 constexpr int NMS_T = 1024;
 constexpr int NMS_LDS = 4096;
 constexpr int NMS_BM = 512;  // bit-matrix path: 512 x 8 words of 64 bits (32 KB) behind the first 512 boxes
+// blocked path (NMS_BM < n <= NMS_SORT, e.g. the validator's conf 0.001 at 640²: up to A = 8,400 candidates): the keys
+// sorted in LDS, then the greedy scan in blocks of NMS_BLK candidates in score order — a block's candidates are first
+// tested against every box kept by earlier blocks (all threads, the kept list in LDS), the survivors' intra-block IoU
+// bit matrix is built by all waves, and one wave scans it in order (as the bit-matrix path).  Candidate j is kept iff
+// no kept i < j has IoU > iou: torchvision's greedy result, with a few barriers per block instead of one per kept box.
+constexpr int NMS_SORT = 16384;  // keys sorted in LDS (128 KB: the whole LDS arena)
+constexpr int NMS_BLK = 512;     // candidates per block (bit matrix 512 x 8 words, 32 KB)
+constexpr int NMS_KEEP = 512;    // kept boxes held in LDS: max_det up to this on the blocked path
+// the block / kept-list regions (u64 units) sit at the end of the arena, behind the sorted keys they leave in place
+constexpr int NMS_REG = 4 * NMS_BLK + NMS_BLK * (NMS_BLK / 64) + 2 * NMS_KEEP + NMS_KEEP / 2;
+constexpr int NMS_BLK_MAX = NMS_SORT - NMS_REG;  // candidates (after max_nms) the blocked path takes: 8,960
 
 __device__ void bitonic_sort_desc(unsigned long long* k, int n2, int tid) {
   for (int size = 2; size <= n2; size <<= 1) {
@@ -1260,10 +1271,13 @@ __device__ __forceinline__ bool iou_gt(const float4 bi, float ai_area, const flo
 }
 
 __global__ __launch_bounds__(NMS_T) void nms_image(const NmsArgs a) {
-  __shared__ unsigned long long sk[NMS_LDS];
-  __shared__ float4 sbx[NMS_LDS];
-  __shared__ float sar[NMS_LDS];
-  __shared__ unsigned char ssup[NMS_LDS];
+  // one LDS arena (128 KB), carved per path: keys [NMS_LDS], boxes [NMS_LDS], areas [NMS_LDS], flags [NMS_LDS] for the
+  // paths up to NMS_LDS candidates; the sort buffer, then the block / kept-list regions for the blocked path
+  __shared__ __attribute__((aligned(16))) unsigned long long arena[NMS_SORT];
+  unsigned long long* sk = arena;
+  float4* sbx = reinterpret_cast<float4*>(arena + NMS_LDS);
+  float* sar = reinterpret_cast<float*>(arena + 3 * NMS_LDS);
+  unsigned char* ssup = reinterpret_cast<unsigned char*>(arena + 3 * NMS_LDS + NMS_LDS / 2);
   const int b = blockIdx.x;
   const int tid = threadIdx.x;
   if (a.dbg == 6) return;
@@ -1432,6 +1446,122 @@ __global__ __launch_bounds__(NMS_T) void nms_image(const NmsArgs a) {
     for (int q = tid; q < kept; q += NMS_T) {
       const unsigned ai = 0xFFFFFFFFu - (unsigned)(sorted[keep_bm[q]] & 0xFFFFFFFFull);
       write_det(a, out + (size_t)q * rowlen, ib + ai);
+    }
+    if (tid == 0) {
+      a.out_counts[b] = kept;
+      if (a.counts2) a.counts2[b] = kept;
+    }
+    return;
+  }
+  if (n <= NMS_SORT && (n < a.max_nms ? n : a.max_nms) <= NMS_BLK_MAX && a.max_det <= NMS_KEEP && a.dbg != 9) {
+    // the blocked path (YM_NMS_DBG=9: off, for the A/B test against the one-box-per-barrier path below)
+    int n2 = 1;
+    while (n2 < n) n2 <<= 1;
+    for (int i = tid; i < n2; i += NMS_T) arena[i] = i < n ? gk[i] : 0ull;
+    __syncthreads();
+    bitonic_sort_desc(arena, n2, tid);
+    const int ne = n < a.max_nms ? n : a.max_nms;  // the sorted keys stay in arena[0, ne); the regions follow them
+    constexpr int W = NMS_BLK / 64;
+    unsigned long long* reg = arena + NMS_BLK_MAX;
+    float4* bb = reinterpret_cast<float4*>(reg);                                  // [NMS_BLK] class-offset boxes
+    float* ba = reinterpret_cast<float*>(reg + 2 * NMS_BLK);                      // [NMS_BLK] areas
+    int* bai = reinterpret_cast<int*>(reg + 2 * NMS_BLK + NMS_BLK / 2);           // [NMS_BLK] anchor indices
+    unsigned* bsup = reinterpret_cast<unsigned*>(reg + 3 * NMS_BLK);              // [NMS_BLK] removed flags
+    unsigned long long* bmask = reg + 4 * NMS_BLK;                                // [NMS_BLK][W]
+    float4* kb = reinterpret_cast<float4*>(reg + 4 * NMS_BLK + NMS_BLK * W);      // [NMS_KEEP] kept boxes
+    float* ka = reinterpret_cast<float*>(kb + NMS_KEEP);                          // [NMS_KEEP] their areas
+    __shared__ int blk_keep[NMS_BLK], blk_kept;
+    __shared__ unsigned long long blk_rem[W];
+    const int cap = a.max_det < NMS_KEEP ? a.max_det : NMS_KEEP;
+    int kept = 0;  // uniform: every thread reads blk_kept after the block's barrier
+    for (int b0 = 0; b0 < ne && kept < cap; b0 += NMS_BLK) {
+      const int nb = ne - b0 < NMS_BLK ? ne - b0 : NMS_BLK;
+      if (tid < nb) {
+        const unsigned ai = 0xFFFFFFFFu - (unsigned)(arena[b0 + tid] & 0xFFFFFFFFull);
+        const float4 v = a.boxes[ib + ai];
+        const float off = a.agnostic ? 0.0f : (float)a.cls[ib + ai] * a.max_wh;
+        const float4 o = make_float4(v.x + off, v.y + off, v.z + off, v.w + off);
+        bb[tid] = o;
+        ba[tid] = __fmul_rn(__fsub_rn(o.z, o.x), __fsub_rn(o.w, o.y));
+        bai[tid] = (int)ai;
+      }
+      if (tid < NMS_BLK) bsup[tid] = tid >= nb;
+      __syncthreads();
+      {  // suppression by the boxes kept in earlier blocks: threads j and j + NMS_BLK take alternate kept boxes
+        const int j = tid & (NMS_BLK - 1), half = tid / NMS_BLK;
+        if (j < nb) {
+          bool sj = false;
+          for (int i = half; i < kept && !sj; i += NMS_T / NMS_BLK) sj = iou_gt(kb[i], ka[i], bb[j], ba[j], a.iou);
+          if (sj) bsup[j] = 1u;
+        }
+      }
+      __syncthreads();
+      {  // the survivors' bit matrix: wave item (i, w) tests row i against boxes 64 w .. 64 w + 63 (ballot = word w)
+        const int wv = tid >> 6, ln = tid & 63;
+        for (int pq = wv; pq < nb * W; pq += NMS_T / 64) {
+          const int i = pq / W, w = pq - i * W;
+          const int j = 64 * w + ln;
+          const bool sij = !bsup[i] && 64 * w + 63 > i && j > i && j < nb && !bsup[j] &&
+                           iou_gt(bb[i], ba[i], bb[j], ba[j], a.iou);
+          const unsigned long long bits = __ballot(sij);
+          if (ln == 0) bmask[pq] = bits;
+        }
+      }
+      __syncthreads();
+      if (tid < 64) {  // one wave: the block's greedy scan (the bit-matrix path's), removed words seeded by bsup
+        const int lane = tid;
+#pragma unroll
+        for (int w = 0; w < W; ++w) {
+          const unsigned long long r = __ballot(bsup[64 * w + lane] != 0u);
+          if (lane == 0) blk_rem[w] = r;
+        }
+        int kk = kept;
+        for (int k2 = 0; k2 < W && kk < cap; ++k2) {
+          const int jn = nb - 64 * k2 < 64 ? nb - 64 * k2 : 64;
+          if (jn <= 0) break;
+          const int row = 64 * k2 + lane;
+          const unsigned long long diag = row < nb ? bmask[row * W + k2] : 0ull;
+          const unsigned dlo = (unsigned)diag, dhi = (unsigned)(diag >> 32);
+          const unsigned long long remv = blk_rem[k2];
+          unsigned long long remk =
+              ((unsigned long long)(unsigned)__builtin_amdgcn_readfirstlane((unsigned)(remv >> 32)) << 32) |
+              (unsigned long long)(unsigned)__builtin_amdgcn_readfirstlane((unsigned)remv);
+          unsigned long long keepbits = 0;
+          const int q0 = kk - kept;
+          unsigned long long avail = ~remk & (jn == 64 ? ~0ull : ((1ull << jn) - 1ull));
+          while (avail && kk < cap) {
+            const int j = __builtin_ctzll(avail);
+            keepbits |= 1ull << j;
+            ++kk;
+            remk |= ((unsigned long long)(unsigned)__builtin_amdgcn_readlane(dhi, j) << 32) |
+                    (unsigned long long)(unsigned)__builtin_amdgcn_readlane(dlo, j);
+            avail &= ~remk & ~((2ull << j) - 1ull);
+          }
+          const bool mine = (keepbits >> lane) & 1ull;
+          if (mine) blk_keep[q0 + __popcll(keepbits & ((1ull << lane) - 1ull))] = row;
+          for (int w = k2 + 1; w < W; ++w) {
+            const unsigned long long v = mine ? bmask[row * W + w] : 0ull;
+            unsigned vlo = (unsigned)v, vhi = (unsigned)(v >> 32);
+#pragma unroll
+            for (int o = 32; o > 0; o >>= 1) {
+              vlo |= (unsigned)__shfl_xor((int)vlo, o);
+              vhi |= (unsigned)__shfl_xor((int)vhi, o);
+            }
+            if (lane == 0) blk_rem[w] |= ((unsigned long long)vhi << 32) | vlo;
+          }
+        }
+        if (lane == 0) blk_kept = kk;
+      }
+      __syncthreads();
+      const int kept2 = blk_kept;
+      for (int q = tid; q < kept2 - kept; q += NMS_T) {  // the block's kept boxes join the list; their rows are written
+        const int r = blk_keep[q];
+        kb[kept + q] = bb[r];
+        ka[kept + q] = ba[r];
+        write_det(a, out + (size_t)(kept + q) * rowlen, ib + (size_t)bai[r]);
+      }
+      kept = kept2;
+      __syncthreads();  // the kept list is complete before the next block reads it; the block regions are free again
     }
     if (tid == 0) {
       a.out_counts[b] = kept;
@@ -1703,7 +1833,8 @@ hipError_t ym_launch_decode(const DecodeArgs& a, hipStream_t st) {
 }
 
 hipError_t ym_launch_nms(const NmsArgs& a0, hipStream_t st) {
-  static const int dbg = [] { const char* e = getenv("YM_NMS_DBG"); return e ? atoi(e) : 0; }();
+  const char* e = getenv("YM_NMS_DBG");  // read per launch (a test switches the blocked path off between eager runs)
+  const int dbg = e ? atoi(e) : 0;
   NmsArgs a = a0;
   a.dbg = dbg;
   hipLaunchKernelGGL(nms_image, dim3(a.B), dim3(NMS_T), 0, st, a);
