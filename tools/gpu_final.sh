@@ -27,6 +27,7 @@ for step in ${STEPS:-smoke suite bench_s bench_n bench_seg bench_ptq optable pro
                run bench_n_f8 400 python -u bench.py --model n --dtype f8
                run bench_n_f16 400 python -u bench.py --model n --dtype f16 --no-cpu ;;
     optable) run optable 200 python -u tools/op_table.py --model s --dtype x3 ;;
+    conf) run conf_timing 300 python -u tools/conf_timing.py s 8 ;;
     prof) (cd /tmp && timeout -k 10 400 rocprofv3 --kernel-trace --stats --output-format csv \
              -d "$GRAFT_REPO_ROOT/$OUT/prof" -o run -- python3 "$GRAFT_REPO_ROOT/bench.py" --steps 50 \
              --warmup 10 --no-cpu --no-f16 > "$GRAFT_REPO_ROOT/$OUT/prof_bench.log" 2>&1); rc=$?

@@ -407,9 +407,11 @@ struct NmsArgs {
   float* dets; int* out_counts;                       // (B, max_det, 6 + nm), (B)
   int* counts2;  // non-null (ym_infer_args.counts_after_dets): the counts again, in the words after the batch's rows
   int A, kstride, nm, max_det, max_nms, agnostic, B;
+  int nc;  // classes (the blocked path's class filter takes nc <= NMS_NC)
   float max_wh, img_h, img_w;
   double iou;
-  int dbg;  // YM_NMS_DBG: 1-7 phase ablations of the bit-matrix path (timing only); 9 disables the blocked path
+  int dbg;  // YM_NMS_DBG: 1-7 phase ablations of the bit-matrix path, 10 the blocked path's sort alone (timing only);
+            // 9 disables the blocked path
 };
 
 struct LetterboxArgs {

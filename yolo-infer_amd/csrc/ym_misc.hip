@@ -1201,29 +1201,49 @@ __global__ __launch_bounds__(256) void decode_anchors(const DecodeArgs a) {
 constexpr int NMS_T = 1024;
 constexpr int NMS_LDS = 4096;
 constexpr int NMS_BM = 512;  // bit-matrix path: 512 x 8 words of 64 bits (32 KB) behind the first 512 boxes
-// blocked path (NMS_BM < n <= NMS_SORT, e.g. the validator's conf 0.001 at 640²: up to A = 8,400 candidates): the keys
-// sorted in LDS, then the greedy scan in blocks of NMS_BLK candidates in score order — a block's candidates are first
-// tested against every box kept by earlier blocks (all threads, the kept list in LDS), the survivors' intra-block IoU
-// bit matrix is built by all waves, and one wave scans it in order (as the bit-matrix path).  Candidate j is kept iff
-// no kept i < j has IoU > iou: torchvision's greedy result, with a few barriers per block instead of one per kept box.
+// blocked path (NMS_BM < n, up to NMS_BLK_MAX candidates after max_nms, e.g. the validator's conf 0.001 at 640²: up to
+// A = 8,400): the keys sorted in LDS, then the greedy scan in blocks of NMS_BLK candidates in score order — a block's
+// candidates are first tested against every box kept by earlier blocks (the kept list in LDS), the survivors'
+// intra-block IoU bit matrix is built by all waves, and one wave scans it in order (as the bit-matrix path).
+// Candidate j is kept iff no kept i < j has IoU > iou: torchvision's greedy result, with a few barriers per block
+// instead of one per kept box.  Class filter (not agnostic, iou >= 0, max_wh above the boxes' coordinate range, nc <=
+// NMS_NC): boxes of different classes are offset cls * max_wh apart and cannot intersect (IoU 0, never > iou), so a
+// candidate is tested only against kept boxes of its class (per-class lists) and a bit-matrix word only where the
+// word holds a box of row i's class (per-word class masks).
 constexpr int NMS_SORT = 16384;  // keys sorted in LDS (128 KB: the whole LDS arena)
-constexpr int NMS_BLK = 512;     // candidates per block (bit matrix 512 x 8 words, 32 KB)
+constexpr int NMS_BLK = 256;     // candidates per block (bit matrix 256 x 4 words)
 constexpr int NMS_KEEP = 512;    // kept boxes held in LDS: max_det up to this on the blocked path
+constexpr int NMS_NC = 128;      // classes of the class filter
+constexpr int NMS_W = NMS_BLK / 64;
 // the block / kept-list regions (u64 units) sit at the end of the arena, behind the sorted keys they leave in place
-constexpr int NMS_REG = 4 * NMS_BLK + NMS_BLK * (NMS_BLK / 64) + 2 * NMS_KEEP + NMS_KEEP / 2;
-constexpr int NMS_BLK_MAX = NMS_SORT - NMS_REG;  // candidates (after max_nms) the blocked path takes: 8,960
+constexpr int NR_BB = 0, NR_BA = NR_BB + 2 * NMS_BLK, NR_BAI = NR_BA + NMS_BLK / 2, NR_BSUP = NR_BAI + NMS_BLK / 2,
+              NR_BCLS = NR_BSUP + NMS_BLK / 2, NR_BMASK = NR_BCLS + NMS_BLK / 2, NR_CCM = NR_BMASK + NMS_BLK * NMS_W,
+              NR_KB = NR_CCM + NMS_W * NMS_NC, NR_KA = NR_KB + 2 * NMS_KEEP, NR_KNEXT = NR_KA + NMS_KEEP / 2,
+              NR_KHEAD = NR_KNEXT + NMS_KEEP / 2, NMS_REG = NR_KHEAD + NMS_NC / 2;
+constexpr int NMS_BLK_MAX = NMS_SORT - NMS_REG;  // candidates (after max_nms) the blocked path takes: 12,224
 
-__device__ void bitonic_sort_desc(unsigned long long* k, int n2, int tid) {
+// A step whose stride is <= 64 only pairs elements inside the 128-element run a wave's 64 consecutive i cover (i =
+// tid + NMS_T m), so consecutive such steps need no workgroup barrier: the wave's own LDS operations are in order.
+// A barrier is taken after a step whose stride, or the next step's, is above 64 (LDS layout-independent; n2 a power
+// of two >= 2).
+__device__ __forceinline__ void bitonic_sort_desc(unsigned long long* k, int n2, int tid) {
   for (int size = 2; size <= n2; size <<= 1) {
     for (int stride = size >> 1; stride > 0; stride >>= 1) {
       for (int i = tid; i < (n2 >> 1); i += NMS_T) {
-        const int lo = (i / stride) * stride * 2 + (i % stride);
+        const int lo = ((i & ~(stride - 1)) << 1) | (i & (stride - 1));  // (i / stride) * 2 stride + i % stride
         const int hi = lo + stride;
         const bool desc = ((lo & size) == 0);
         const unsigned long long x = k[lo], y = k[hi];
         if ((x < y) == desc) { k[lo] = y; k[hi] = x; }
       }
-      __syncthreads();
+      const int next = stride > 1 ? stride >> 1 : (size < n2 ? size : 0);  // the next step's stride (0: done)
+      if (stride > 64 || next > 64 || next == 0) {
+        __syncthreads();
+      } else {
+        __builtin_amdgcn_fence(__ATOMIC_RELEASE, "wavefront");
+        __builtin_amdgcn_wave_barrier();
+        __builtin_amdgcn_fence(__ATOMIC_ACQUIRE, "wavefront");
+      }
     }
   }
 }
@@ -1457,53 +1477,76 @@ __global__ __launch_bounds__(NMS_T) void nms_image(const NmsArgs a) {
     // the blocked path (YM_NMS_DBG=9: off, for the A/B test against the one-box-per-barrier path below)
     int n2 = 1;
     while (n2 < n) n2 <<= 1;
+    if (a.dbg == 12) return;  // timing only: the kernel up to the blocked path
     for (int i = tid; i < n2; i += NMS_T) arena[i] = i < n ? gk[i] : 0ull;
     __syncthreads();
+    if (a.dbg == 11) return;  // timing only: + the key loads
     bitonic_sort_desc(arena, n2, tid);
+    if (a.dbg == 10) return;  // timing only: + the sort
     const int ne = n < a.max_nms ? n : a.max_nms;  // the sorted keys stay in arena[0, ne); the regions follow them
-    constexpr int W = NMS_BLK / 64;
+    constexpr int W = NMS_W;
     unsigned long long* reg = arena + NMS_BLK_MAX;
-    float4* bb = reinterpret_cast<float4*>(reg);                                  // [NMS_BLK] class-offset boxes
-    float* ba = reinterpret_cast<float*>(reg + 2 * NMS_BLK);                      // [NMS_BLK] areas
-    int* bai = reinterpret_cast<int*>(reg + 2 * NMS_BLK + NMS_BLK / 2);           // [NMS_BLK] anchor indices
-    unsigned* bsup = reinterpret_cast<unsigned*>(reg + 3 * NMS_BLK);              // [NMS_BLK] removed flags
-    unsigned long long* bmask = reg + 4 * NMS_BLK;                                // [NMS_BLK][W]
-    float4* kb = reinterpret_cast<float4*>(reg + 4 * NMS_BLK + NMS_BLK * W);      // [NMS_KEEP] kept boxes
-    float* ka = reinterpret_cast<float*>(kb + NMS_KEEP);                          // [NMS_KEEP] their areas
+    float4* bb = reinterpret_cast<float4*>(reg + NR_BB);          // [NMS_BLK] class-offset boxes
+    float* ba = reinterpret_cast<float*>(reg + NR_BA);            // [NMS_BLK] areas
+    int* bai = reinterpret_cast<int*>(reg + NR_BAI);              // [NMS_BLK] anchor indices
+    unsigned* bsup = reinterpret_cast<unsigned*>(reg + NR_BSUP);  // [NMS_BLK] removed flags
+    int* bcls = reinterpret_cast<int*>(reg + NR_BCLS);            // [NMS_BLK] the class list each joins
+    unsigned long long* bmask = reg + NR_BMASK;                   // [NMS_BLK][W]
+    unsigned long long* ccm = reg + NR_CCM;                       // [W][NMS_NC] lanes of word w holding class c
+    float4* kb = reinterpret_cast<float4*>(reg + NR_KB);          // [NMS_KEEP] kept boxes
+    float* ka = reinterpret_cast<float*>(reg + NR_KA);            // [NMS_KEEP] their areas
+    int* knext = reinterpret_cast<int*>(reg + NR_KNEXT);          // [NMS_KEEP] per-class kept lists
+    int* khead = reinterpret_cast<int*>(reg + NR_KHEAD);          // [NMS_NC]
     __shared__ int blk_keep[NMS_BLK], blk_kept;
     __shared__ unsigned long long blk_rem[W];
-    const int cap = a.max_det < NMS_KEEP ? a.max_det : NMS_KEEP;
+    // class filter: exact when the class offsets separate every pair of boxes (decoded coordinates lie within
+    // +-reg_max * stride of the image: the 2,048 margin covers 16 bins x 64 px)
+    const bool cf = !a.agnostic && a.iou >= 0.0 && a.nc <= NMS_NC &&
+                    (double)a.max_wh >= (double)a.img_w + (double)a.img_h + 2048.0;
+    const int cap = a.max_det;  // <= NMS_KEEP
+    for (int i = tid; i < W * NMS_NC; i += NMS_T) ccm[i] = 0ull;
+    if (tid < NMS_NC) khead[tid] = -1;
+    __syncthreads();
     int kept = 0;  // uniform: every thread reads blk_kept after the block's barrier
     for (int b0 = 0; b0 < ne && kept < cap; b0 += NMS_BLK) {
       const int nb = ne - b0 < NMS_BLK ? ne - b0 : NMS_BLK;
       if (tid < nb) {
         const unsigned ai = 0xFFFFFFFFu - (unsigned)(arena[b0 + tid] & 0xFFFFFFFFull);
         const float4 v = a.boxes[ib + ai];
-        const float off = a.agnostic ? 0.0f : (float)a.cls[ib + ai] * a.max_wh;
+        const int cl = a.cls[ib + ai];
+        const float off = a.agnostic ? 0.0f : (float)cl * a.max_wh;
         const float4 o = make_float4(v.x + off, v.y + off, v.z + off, v.w + off);
         bb[tid] = o;
         ba[tid] = __fmul_rn(__fsub_rn(o.z, o.x), __fsub_rn(o.w, o.y));
         bai[tid] = (int)ai;
+        const int c = cf ? cl : 0;
+        bcls[tid] = c;
+        if (cf) atomicOr(&ccm[(tid >> 6) * NMS_NC + c], 1ull << (tid & 63));
       }
       if (tid < NMS_BLK) bsup[tid] = tid >= nb;
       __syncthreads();
-      {  // suppression by the boxes kept in earlier blocks: threads j and j + NMS_BLK take alternate kept boxes
-        const int j = tid & (NMS_BLK - 1), half = tid / NMS_BLK;
-        if (j < nb) {
-          bool sj = false;
-          for (int i = half; i < kept && !sj; i += NMS_T / NMS_BLK) sj = iou_gt(kb[i], ka[i], bb[j], ba[j], a.iou);
-          if (sj) bsup[j] = 1u;
-        }
+      if (tid < nb) {  // suppression by the boxes kept in earlier blocks (of this candidate's class)
+        bool sj = false;
+        for (int q = khead[bcls[tid]]; q >= 0 && !sj; q = knext[q]) sj = iou_gt(kb[q], ka[q], bb[tid], ba[tid], a.iou);
+        if (sj) bsup[tid] = 1u;
       }
       __syncthreads();
-      {  // the survivors' bit matrix: wave item (i, w) tests row i against boxes 64 w .. 64 w + 63 (ballot = word w)
+      {  // the survivors' bit matrix: wave item (i, w) tests row i against boxes 64 w .. 64 w + 63 (ballot = word w);
+         // a word without a box of row i's class (or past i) is zero without a test
         const int wv = tid >> 6, ln = tid & 63;
         for (int pq = wv; pq < nb * W; pq += NMS_T / 64) {
           const int i = pq / W, w = pq - i * W;
           const int j = 64 * w + ln;
-          const bool sij = !bsup[i] && 64 * w + 63 > i && j > i && j < nb && !bsup[j] &&
-                           iou_gt(bb[i], ba[i], bb[j], ba[j], a.iou);
-          const unsigned long long bits = __ballot(sij);
+          const int lo = i + 1 - 64 * w;  // lanes >= lo lie past row i
+          const unsigned long long past = lo <= 0 ? ~0ull : (lo >= 64 ? 0ull : ~0ull << lo);
+          const int hiw = nb - 64 * w;    // lanes < hiw lie inside the block
+          const unsigned long long in = hiw >= 64 ? ~0ull : (hiw <= 0 ? 0ull : ((1ull << hiw) - 1ull));
+          const unsigned long long cand = (cf ? ccm[w * NMS_NC + bcls[i]] : ~0ull) & past & in;
+          unsigned long long bits = 0ull;
+          if (!bsup[i] && cand) {  // (uniform)
+            const bool sij = ((cand >> ln) & 1ull) && !bsup[j] && iou_gt(bb[i], ba[i], bb[j], ba[j], a.iou);
+            bits = __ballot(sij);
+          }
           if (ln == 0) bmask[pq] = bits;
         }
       }
@@ -1551,17 +1594,20 @@ __global__ __launch_bounds__(NMS_T) void nms_image(const NmsArgs a) {
           }
         }
         if (lane == 0) blk_kept = kk;
+      } else if (cf) {  // the other waves clear the class masks for the next block
+        for (int i = tid - 64; i < W * NMS_NC; i += NMS_T - 64) ccm[i] = 0ull;
       }
       __syncthreads();
       const int kept2 = blk_kept;
-      for (int q = tid; q < kept2 - kept; q += NMS_T) {  // the block's kept boxes join the list; their rows are written
-        const int r = blk_keep[q];
-        kb[kept + q] = bb[r];
-        ka[kept + q] = ba[r];
-        write_det(a, out + (size_t)(kept + q) * rowlen, ib + (size_t)bai[r]);
+      for (int q = tid; q < kept2 - kept; q += NMS_T) {  // the block's kept boxes join their class lists; rows written
+        const int r = blk_keep[q], idx = kept + q;
+        kb[idx] = bb[r];
+        ka[idx] = ba[r];
+        knext[idx] = atomicExch(&khead[bcls[r]], idx);
+        write_det(a, out + (size_t)idx * rowlen, ib + (size_t)bai[r]);
       }
       kept = kept2;
-      __syncthreads();  // the kept list is complete before the next block reads it; the block regions are free again
+      __syncthreads();  // the kept lists are complete before the next block reads them; the block regions are free
     }
     if (tid == 0) {
       a.out_counts[b] = kept;

@@ -608,7 +608,7 @@ int launch_op(ym_ctx* c, const Op& op, int B, const float* d_in, const ym_infer_
                             c->lane_img0
                       : nullptr;
       a.A = c->A; a.kstride = c->kstride; a.nm = c->nm; a.max_det = args->max_det; a.max_nms = args->max_nms;
-      a.agnostic = args->agnostic; a.B = B;
+      a.agnostic = args->agnostic; a.B = B; a.nc = c->nc;
       a.max_wh = args->max_wh; a.img_h = (float)c->cH; a.img_w = (float)c->cW;
       a.iou = args->iou;
       e = ym_launch_nms(a, st);
