@@ -327,6 +327,10 @@ struct ConvArgs {
   // fused depthwise (yolomi/arch.py GraphBuilder.fuse_dw; csrc/ym_conv_dwpw.hip): src0 is the DEPTHWISE input and this
   // 1x1 conv consumes act(dw3x3(src0) + dw_b) computed in registers.  dw_w [9][C0] fp32, dw_b [C0]; null: no depthwise
   const float* dw_w; const float* dw_b; int dw_act;
+  // LDS-DMA kernels (csrc/ym_conv_dma.hip launch_dma): the tile map's divisions, set on the host — tiles_n and Cin8 as
+  // multiply-shift divisors, the pixel tiles per XCD — instead of runtime integer divisions in every workgroup's prologue
+  FDiv fd_tn, fd_cin8;
+  int tm_per_xcd;
 };
 
 // Warm the scalar cache with every 64-byte line of a kernel's argument block in ONE round trip: the compiler loads

@@ -145,8 +145,9 @@ __global__ __launch_bounds__(256 * KG) void conv_dma(const ConvArgs a) {
   int rest = bid >> 3;
   const int sp = rest % SPLIT;
   rest /= SPLIT;
-  const int tn = rest % a.tiles_n;
-  const int tm = (bid & 7) * (int)(gridDim.x / (8u * SPLIT * a.tiles_n)) + rest / a.tiles_n;
+  const int rq = ym_div(rest, a.fd_tn);  // rest / tiles_n
+  const int tn = rest - rq * a.tiles_n;
+  const int tm = (bid & 7) * a.tm_per_xcd + rq;  // (a.tm_per_xcd = gridDim.x / (8 SPLIT tiles_n))
   if (tm * BM >= a.M) return;
 
   // ---- epilogue operands first (bias, residual; wave group 0 runs the epilogue): their latency hides behind the
@@ -281,10 +282,10 @@ __global__ __launch_bounds__(256 * KG) void conv_dma(const ConvArgs a) {
   int tap = 0, cb = 0, ky = 0, kx = 0;
   if constexpr (KIND == 3) {
     const int idx = k_lo * 8 + c;
-    tap = idx / a.Cin8;
+    tap = ym_div(idx, a.fd_cin8);
     cb = idx - tap * a.Cin8;
   } else if constexpr (KIND == 4) {
-    tap = (k_lo * 8) / a.Cin8;
+    tap = ym_div(k_lo * 8, a.fd_cin8);
     cb = k_lo * 8 - tap * a.Cin8;
     ky = tap / 3;
     kx = tap - ky * 3;
@@ -781,6 +782,9 @@ hipError_t launch_dma(ConvArgs a, int kind, hipStream_t st) {
   if (X3 && (4 / KG) % 2) return hipErrorInvalidValue;
   const int tiles_m8 = ((a.M + BM - 1) / BM + 7) / 8 * 8;
   a.tiles_n = (a.N + BN - 1) / BN;
+  a.fd_tn = ym_fdiv(a.tiles_n);
+  a.fd_cin8 = ym_fdiv(a.Cin8 > 0 ? a.Cin8 : 1);
+  a.tm_per_xcd = tiles_m8 / 8;
   if (SPLIT > 1) {
     const long tiles = (long)tiles_m8 * a.tiles_n;
     if (tiles > a.cnt_cap || tiles * SPLIT * BM * BN * 4 > a.slab_cap) return hipErrorInvalidValue;
@@ -852,6 +856,9 @@ hipError_t launch_fuse(ConvArgs a, int kind, hipStream_t st) {
   if (SUB > 1 && (a.Kpad / DK) % SUB) return hipErrorInvalidValue;  // whole stages
   const int tiles_m8 = ((a.M + BM - 1) / BM + 7) / 8 * 8;
   a.tiles_n = 1;
+  a.fd_tn = ym_fdiv(1);
+  a.fd_cin8 = ym_fdiv(a.Cin8 > 0 ? a.Cin8 : 1);
+  a.tm_per_xcd = tiles_m8 / 8;
   const dim3 grid(tiles_m8), block(256 * KG);
   if (kind == 4)
     hipLaunchKernelGGL((conv_dma<OutT, BM, BN, 4, 1, KG, NS, SUB, true, true>), grid, block, 0, st, a);
