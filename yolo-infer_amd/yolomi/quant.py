@@ -37,8 +37,8 @@ def act_observer(backend: str):
 # ----------------------------------------------------------------------------------------- fp8 (e4m3) PTQ plan
 # The same quantisation points as the int8 plan, with OCP e4m3 codes (gfx950 fp8) in place of affine uint8: a tensor
 # has a per-tensor scale s = amax / 448 (zero point 0) and code = e4m3(clamp(v * (1/s), +-448)) (round to nearest
-# even), weights per-output-channel e4m3; convs multiply the e4m3 values (widened exactly to fp16) on the f16 MFMA.  Restated in oracle/quant.py
-# (backend "fp8") with torch.float8_e4m3fn casts; kernels: csrc/ym_quant.h Q8<true>.
+# even), weights per-output-channel e4m3; convs multiply the e4m3 values (widened exactly to fp16) on the f16 MFMA.
+# Restated in oracle/quant.py (backend "fp8") with torch.float8_e4m3fn casts; kernels: csrc/ym_quant.h Q8<true>.
 def fp8_scale(amax: float) -> float:
     amax = float(amax)
     return float(F32(amax) / F32(E4M3_MAX)) if amax > 0 else float(F32(1.0) / F32(E4M3_MAX))
