@@ -49,8 +49,10 @@ def main():
     nx = eng._ncfg() - (2 if a.dtype == "x3" else 0)  # x3: the last 2 ids are x3-only Bottleneck variants
     cands_all = [c for c in range(nx) if not nb0 <= c < nb1]
     print(f"source {eng.tune_source}, {len(cands_all)} conv configs", flush=True)
-    # (ops on a fused Bottleneck id or a split pair keep it: the other families do not take a fused pair's shape)
-    conv = [i for i, op in enumerate(ops) if op.kind == "conv" and i > 1 and base[i] in cands_all]
+    # (ops on a fused Bottleneck id or a split pair keep it: the other families do not take a fused pair's shape;
+    # a depthwise-fused 1x1 runs on csrc/ym_conv_dwpw.hip, whose ids are not these)
+    conv = [i for i, op in enumerate(ops) if op.kind == "conv" and i > 1 and base[i] in cands_all
+            and not op.args.get("dw")]
 
     # isolated per-op times of every config (graph of back-to-back launches per op, as ym_tune)
     iso = {}
