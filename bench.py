@@ -17,9 +17,11 @@ rule → forward (one HIP-graph replay) → decode → NMS → per-image Results
 Multi-GPU: one process per GPU (`--gpus N` without a launcher spawns the N ranks itself through
 torch.distributed.run, as a child process); rank 0 packs the weights once and broadcasts the blob over RCCL (xGMI)
 (torch.distributed "nccl" broadcast of one uint8 tensor, yolomi.dist.broadcast_blob; `--cabi-bcast`: through the
-C-ABI, yolomi.dist.rccl_broadcast_model → ym_broadcast_weights); each rank runs its own batch shard;
-LoadTensor's /255 rule is taken over the global batch once, where it is split (one fp32 all-reduce before the timed
-loop, yolomi.dist.split_batch_max): no collective inside a step — "weak" scaling, 8 images per GPU.
+C-ABI, yolomi.dist.rccl_broadcast_model → ym_broadcast_weights); each rank runs its own batch shard ("weak" scaling,
+8 images per GPU).  LoadTensor's /255 rule reads the batch every step at every N (the same per-step work): at N = 1
+the forward's own input_stats kernel takes the batch max; at N > 1 each rank's shard max (ym_input_max) is
+all-reduced (MAX) over the ranks every step and handed to the forward (yolomi.dist.enable_global_rule), so the
+decision is the global batch's.
 
 Rank 0 prints ONE JSON line.  Extra fields: `roofline` (conv implicit-GEMM kernels, live HIP-event timing),
 `kernels` (per-kind device time and achieved HBM GB/s of the non-conv kernels), `cpu_baseline` (the oracle on host
@@ -52,6 +54,10 @@ PEAK_TFLOPS = {"f16": 2500.0, "f32": 157.3, "i8": 5000.0, "f8": 2500.0, "x3": 25
 ACT_BYTES = {"f16": 2, "f32": 4, "i8": 1, "f8": 1, "x3": 4}
 PEAK_HBM_GBS = 8000.0
 EXACT_TOL_XY, EXACT_TOL_S = 5e-4, 5e-5  # the GPU's own distance from the float64 answer (tests/test_gpu_x3.py)
+# LoadTensor's /255 rule inside the timed step, by N (verdict r5 item 7: the same per-step work at every N)
+BATCH_RULE = {False: "per step: the forward's input_stats kernel reads the batch for its max",
+              True: "per step: the shard max (ym_input_max, one read of the shard) all-reduced MAX over the ranks, "
+                    "handed to the forward"}
 
 
 def synthetic_batch(B, S, seed, device):
@@ -78,12 +84,15 @@ def pmc_traffic(workload):
     return best[1]["families"]["conv"]["bytes_corrected"], os.path.relpath(best[0], ROOT)
 
 
+PROFILE_ROUND = "r06"  # the roofline cites only profiles of this round's tree (verdict r5 item 4)
+
+
 def _newest_profile(pattern, workload):
-    """The newest committed profiles/<pattern> file whose "workload" is this bench workload (without ", predict()
-    loop"); (path relative to the repo, parsed json) or (None, None)."""
+    """The newest committed profiles/<PROFILE_ROUND><pattern> file whose "workload" is this bench workload (without
+    ", predict() loop"); (path relative to the repo, parsed json) or (None, None)."""
     import glob
     best = (None, None)
-    for p in sorted(glob.glob(os.path.join(ROOT, "profiles", pattern))):
+    for p in sorted(glob.glob(os.path.join(ROOT, "profiles", PROFILE_ROUND + pattern))):
         try:
             j = json.load(open(p))
         except (OSError, ValueError):
@@ -143,9 +152,27 @@ def conv_roofline(model, x, dtype, workload, reps=20):
     # each launch priced at whichever roof bounds it (most YOLO11 convs at B = 8 are HBM-side, not MFMA, bound)
     floor_s = sum(max(costs[i][0] / (PEAK_TFLOPS[dtype] * 1e12), costs[i][1] / (PEAK_HBM_GBS * 1e9)) for i in conv)
     traffic, tsrc = pmc_traffic(workload)
+    # in context, live: one eager forward with a HIP event pair around every op on the launch stream (ym_profile,
+    # serial order: every kernel sees the caches the previous one left), median of 5
+    ev = np.median(np.array([eng.profile(x) for _ in range(5)]), axis=0)
+    t_eager = float(ev[conv].sum()) * 1e-3
+    ach_eager = fl / t_eager / 1e12
+    ctx = concurrency_view(fl, dtype, workload)
+    # frac: the in-context figure of the bench command under rocprofv3 (4 branch streams, concurrent kernels stretch
+    # each other) when this round's profile of it is committed, else the live eager in-forward one
+    ach_main = ctx.get("achieved_rocprof", ach_eager)
     return {
-        "bound": "mfma", "achieved": round(ach, 2), "peak": PEAK_TFLOPS[dtype], "unit": "TFLOP/s",
-        "frac": round(ach / PEAK_TFLOPS[dtype], 4), "traffic": traffic,
+        "bound": "mfma", "achieved": round(ach_main, 2), "peak": PEAK_TFLOPS[dtype], "unit": "TFLOP/s",
+        "frac": round(ach_main / PEAK_TFLOPS[dtype], 4), "traffic": traffic,
+        "frac_basis": ("rocprofv3 in-context conv time per forward of this bench command (%s)" % ctx["rocprof_source"]
+                       if "achieved_rocprof" in ctx else
+                       "live: eager forward, HIP event pair per op on the launch stream (ym_profile), median of 5"),
+        "frac_live_eager_forward": round(ach_eager / PEAK_TFLOPS[dtype], 4),
+        "achieved_live_eager_forward": round(ach_eager, 2),
+        "frac_live_isolated_replay": round(ach / PEAK_TFLOPS[dtype], 4), "achieved_live_isolated_replay": round(ach, 2),
+        **({"frac_of_x3_issue_ceiling": round(ach_main / (PEAK_TFLOPS[dtype] / 3), 4),
+            "x3_issue_ceiling_note": "x3 issues three f16 MFMAs per K chunk: its MFMA-issue ceiling is peak / 3"}
+           if dtype == "x3" else {}),
         "traffic_note": (f"HBM-side bytes per forward of all conv launches (PMC FETCH_SIZE x2 + WRITE_SIZE, {tsrc}); "
                          f"algorithmic bytes per forward {int(by)}") if traffic else "no PMC summary for this workload",
         "kernel": "conv implicit GEMM (%s): all %d conv launches of one lane's forward (%d images), aggregated%s"
@@ -153,7 +180,8 @@ def conv_roofline(model, x, dtype, workload, reps=20):
                       "x3": "conv_igemm/conv_lds<x3>, 3x v_mfma_f32_32x32x16_f16 per K chunk"}.get(
                       dtype, "conv_stream/conv_small/conv_dma/conv_lds/conv_bneck/conv_halo/conv_igemm"), len(conv),
                      Bl, "; int8 ops counted as FLOPs" if dtype == "i8" else ""),
-        "timing": f"HIP events around a graph of {reps} back-to-back launches per op, on the launch stream",
+        "timing": f"isolated replay: HIP events around a graph of {reps} back-to-back launches per op, on the launch "
+                  "stream; eager: an event pair per op of one serial forward; rocprof: the bench command's own trace",
         "launches": len(conv), "avg_launch_us": round(t_conv / len(conv) * 1e6, 2),
         "flops_per_forward": fl, "bytes_per_forward_algorithmic": by,
         "hbm_algorithmic_GBps": round(by / t_conv / 1e9, 1), "hbm_frac": round(by / t_conv / 1e9 / PEAK_HBM_GBS, 4),
@@ -162,7 +190,7 @@ def conv_roofline(model, x, dtype, workload, reps=20):
                                     "divided by the sum of their measured times",
         "ms_by_kind_replay": {k: round(v, 4) for k, v in per_kind.items()},
         "top_convs": [{"op": n, "ms": round(t, 4), "tflops": round(tf, 1)} for t, n, tf in top],
-        **concurrency_view(fl, dtype, workload),
+        **ctx,
     }
 
 
@@ -356,34 +384,36 @@ def plumbing(a, world, rank):
     hs = [torch.zeros_like(h) for _ in range(world)]
     dist.all_gather(hs, h)
     rule = GlobalBatchMax(device=dev)
-    rule.local_max = lambda x: rule.buf.copy_(x.amax().reshape(1))
+    reads = [0]
+
+    def local_max(x):  # stands in for ym_input_max: one read of the shard per call
+        reads[0] += 1
+        return rule.buf.copy_(x.amax().reshape(1))
+    rule.local_max = local_max
     x = torch.rand(a.batch, 3, 32, 32) * (255.0 if rank == world - 1 else 1.0)
-    m = rule(x).clone()  # the bench's split-time decision: once, before the timed loop
 
     def step():  # a stand-in for one forward: busy for the x3 yolo11s B=8 forward's ~1.6 ms
         t = time.perf_counter()
         while time.perf_counter() - t < 1.6e-3:
             pass
-    timings = {}
-    for per_step in (False, True):  # the bench's loop, then the same loop with GlobalBatchMax's per-step all-reduce
-        for _ in range(a.warmup):
-            step()
-        dist.barrier()
-        t0 = time.perf_counter()
-        for _ in range(a.steps):
-            if per_step:
-                rule(x)
-            step()
-        dist.barrier()
-        el = torch.tensor([time.perf_counter() - t0], dtype=torch.float64)
-        dist.all_reduce(el, op=dist.ReduceOp.MAX)
-        timings[per_step] = float(el.item())
+    for _ in range(a.warmup):
+        rule(x)
+        step()
+    dist.barrier()
+    reads[0] = 0
+    t0 = time.perf_counter()
+    for _ in range(a.steps):  # the bench's step at N > 1: the shard max all-reduced, then the forward
+        m = rule(x)
+        step()
+    dist.barrier()
+    el = torch.tensor([time.perf_counter() - t0], dtype=torch.float64)
+    dist.all_reduce(el, op=dist.ReduceOp.MAX)
     if rank == 0:
         print(json.dumps({"metric": METRIC, "plumbing": True, "n_gpus": world, "steps": a.steps, "warmup": a.warmup,
-                          "value": round(world * a.batch * a.steps / timings[False], 2), "unit": "images/s",
+                          "value": round(world * a.batch * a.steps / float(el.item()), 2), "unit": "images/s",
                           "blob_bytes": len(blob), "blob_equal_on_all_ranks": all(torch.equal(hs[0], y) for y in hs),
-                          "global_batch_max": float(m.item()),
-                          "per_step_allreduce_us": round((timings[True] - timings[False]) / a.steps * 1e6, 1)}),
+                          "global_batch_max": float(m.item()), "batch_rule": BATCH_RULE[world > 1],
+                          "batch_max_reads_per_step": reads[0] / a.steps}),
               flush=True)
     dist.destroy_process_group()
 
@@ -430,7 +460,7 @@ def main():
         dist.init_process_group("nccl", device_id=dev)
 
     from core.model import YOLO11Model
-    from yolomi.dist import broadcast_blob, rccl_broadcast_model, split_batch_max
+    from yolomi.dist import broadcast_blob, enable_global_rule, rccl_broadcast_model
     from yolomi.plan import pack_model
     from yolomi.synth import synth_weights
 
@@ -460,8 +490,8 @@ def main():
 
     B = a.batch
     x = synthetic_batch(B, a.size, 1000 + rank, dev)
-    if world > 1:  # LoadTensor's /255 rule over the global batch, decided once where it is split (no per-step collective)
-        split_batch_max(model, x)
+    if world > 1:  # LoadTensor's /255 rule over the global batch: one read of the shard + an all-reduce every step
+        enable_global_rule(model)
     for _ in range(a.warmup):
         model.predict(x)
     torch.cuda.synchronize()
@@ -499,8 +529,8 @@ def main():
         "config": {"workload": f"yolo11{a.model} {a.task} {a.size}x{a.size} batch {B}/GPU {a.dtype}, predict() loop",
                    "model": f"yolo11{a.model}{'-seg' if a.task == 'segment' else ''}",
                    "batch_per_gpu": B, "global_batch": B * world, "image_size": a.size,
-                   "parallelism": f"dp{world} (batch-sharded, RCCL weight broadcast"
-                                  f"{', global /255 rule decided at the split: no per-step collective' if world > 1 else ''})"},
+                   "parallelism": f"dp{world} (batch-sharded, RCCL weight broadcast)",
+                   "batch_rule": BATCH_RULE[world > 1]},
         "device_images_per_s": round(dev_ips * world, 2),
         "init_s": round(init_s, 3),
     }

@@ -200,6 +200,16 @@ int ym_version(void);
  * by a library with the same catalogue. */
 int ym_num_conv_cfgs(int dtype);
 
+/* Process-wide debug switches for tests and A/B runs (not part of the reference interface; defaults 0), read when a
+ * kernel is launched (so at graph capture for replayed forwards): YM_DBG_NMS (9 = the NMS kernel's per-box path
+ * instead of the blocked one), YM_DBG_DW_MODE (depthwise variant: 0 LDS tiles, 1 rows, 2 column strips),
+ * YM_DBG_DW_TILE (LDS tile shape 0..3).  The environment variables of the same names set the initial values.
+ * Returns the previous value, or YM_EINVAL for an unknown key. */
+#define YM_DBG_NMS 1
+#define YM_DBG_DW_MODE 2
+#define YM_DBG_DW_TILE 3
+int ym_set_debug(int key, int value);
+
 #ifdef __cplusplus
 }
 #endif

@@ -72,7 +72,7 @@ def test_shard_ranges():
 def test_bench_spawns_its_own_ranks_plumbing_world2():
     """`bench.py --gpus 2` without a launcher starts the two ranks itself (torch.distributed.run as a child); the
     CPU/gloo rehearsal of its protocol reports n_gpus = 2, identical blobs on every rank and the /255 statistic
-    all-reduced over the global batch (only the last rank holds a 0-255 image)."""
+    all-reduced over the global batch every step (only the last rank holds a 0-255 image)."""
     import json
     import subprocess
     import sys
@@ -86,6 +86,8 @@ def test_bench_spawns_its_own_ranks_plumbing_world2():
     d = json.loads(line[0])
     assert d["n_gpus"] == 2 and d["blob_equal_on_all_ranks"] and d["blob_bytes"] > 1_000_000
     assert d["global_batch_max"] > 200.0
+    # verdict r5 item 7: the N > 1 step reads its shard for the /255 rule every step, as N = 1's forward does
+    assert d["batch_max_reads_per_step"] == 1.0 and d["batch_rule"].startswith("per step")
 
 
 def test_bench_refuses_mislabelled_world():

@@ -42,11 +42,12 @@ def test_dwconv_variants_match_float64(scale, B, dtype, mode):
             del os.environ["YM_FUSE_DW"]
     eng = _models[(scale, dtype)].model.engine
     x = synthetic_batch(B, 640, 77, DEV)
-    os.environ["YM_DW_MODE"] = mode
+    from yolomi import lib as L
+    prev = L.set_debug(L.DBG_DW_MODE, int(mode))
     try:
         eng.run(x, use_graph=False)
     finally:
-        del os.environ["YM_DW_MODE"]
+        L.set_debug(L.DBG_DW_MODE, prev)
     n = 0
     for op in eng.graph.ops:
         if op.kind != "dwconv":
@@ -194,13 +195,17 @@ def test_async_predict_counts_behind_rows():
     """predict() on a tensor batch does not synchronise: the NMS kernel writes each call's B counts behind its fresh
     rows (ym_infer_args.counts_after_dets) and the Results read them on first access.  Several calls on different
     inputs queued back to back (graph replays, lanes 1 and 2, a side stream current when they are read) give the
-    detections of the synchronous calls (sync=True), bit for bit."""
+    detections of an independent source, bit for bit: the engine's own rows and device counts of an eager forward
+    (use_graph=False, no counts-behind-rows), so a wrong counts2 offset cannot hide in the reference."""
     from core.model import YOLO11Model
     for dtype, lanes in (("x3", 1), ("f16", 2)):
         m = YOLO11Model(task="detect", size="n", device="cuda:0", dtype=dtype, verbose=False)
         m.model.engine.lanes = lanes
         xs = [synthetic_batch(3, 320, 40 + i, DEV) for i in range(4)]
-        ref = [[r.boxes.data.clone() for r in m.predict(x, conf=0.05, sync=True)] for x in xs]
+        ref = []
+        for x in xs:
+            d, c = m.model.engine.run(x, conf=0.05, use_graph=False)
+            ref.append([d[b, :int(c[b])].clone() for b in range(3)])
         torch.cuda.synchronize()
         got = [m.predict(x, conf=0.05) for x in xs for _ in range(2)]
         with torch.cuda.stream(torch.cuda.Stream()):
@@ -209,3 +214,30 @@ def test_async_predict_counts_behind_rows():
                 for r, d in zip(res, ref[k // 2]):
                     assert torch.equal(r.boxes.data, d)
         assert sum(len(d) for d in ref[0]) > 0
+
+
+def test_predict_on_alternating_streams_is_ordered():
+    """every forward of one context shares its arena, NMS scratch, split-K slabs and input_stats ticket,
+    so asynchronous predict() calls issued from different torch streams must not overlap.  ym_infer makes a forward
+    on another stream than the previous one wait for it (hipStreamWaitEvent on the previous forward's event).  Calls
+    alternating between two streams with no synchronisation between them give the same detections as eager
+    single-stream forwards of the same inputs."""
+    from core.model import YOLO11Model
+    m = YOLO11Model(task="detect", size="s", device="cuda:0", dtype="x3", verbose=False)
+    eng = m.model.engine
+    xs = [synthetic_batch(4, 640, 60 + i, DEV) for i in range(4)]
+    ref = []
+    for x in xs:
+        d, c = eng.run(x, conf=0.05, use_graph=False)
+        ref.append([d[b, :int(c[b])].clone() for b in range(4)])
+    torch.cuda.synchronize()
+    s1, s2 = torch.cuda.Stream(), torch.cuda.Stream()
+    got = []
+    for rep in range(3):
+        for k, x in enumerate(xs):
+            with torch.cuda.stream(s1 if (k + rep) % 2 == 0 else s2):
+                got.append((k, m.predict(x, conf=0.05)))
+    for k, res in got:
+        for r, d in zip(res, ref[k]):
+            assert torch.equal(r.boxes.data, d), k
+    assert sum(len(d) for d in ref[0]) > 0

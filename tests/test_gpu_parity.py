@@ -837,22 +837,37 @@ def test_max_nms_truncation_1280_conf0001(dtype):
         check(ref, res, 0.001, 0.7, 1.0, 1e-2, min_frac=0.9)
 
 
+NMS_VARIANTS = {"default": {}, "agnostic": {"agnostic": True}, "small_max_wh": {"max_wh": 64.0},
+                "classes": {"classes": [0, 2, 5, 9, 14, 27, 41, 56, 63, 79]}}
+
+
+@pytest.mark.parametrize("variant", list(NMS_VARIANTS))
 @pytest.mark.parametrize("dtype,B", [("f32", 2), ("x3", 8)])
-def test_nms_blocked_path_equals_per_box_path(dtype, B):
-    """csrc/ym_misc.hip nms_image's blocked path (512 < candidates <= 8,960 after max_nms: sort in LDS, then blocks
-    of 512 filtered against the kept list and scanned through their own IoU bit matrix) against the one-box-per-
-    barrier path it replaced (YM_NMS_DBG=9), on the same forward's candidates at the validator's conf 0.001 and at
-    0.02 / 0.004: bit-identical rows and counts (greedy NMS is a function of the sorted candidates alone)."""
-    import os
+def test_nms_blocked_path_equals_per_box_path(dtype, B, variant):
+    """csrc/ym_misc.hip nms_image's blocked path (NMS_BM = 512 < candidates <= NMS_BLK_MAX = 12,224 after max_nms:
+    keys sorted in LDS, then blocks of NMS_BLK = 256 candidates filtered against the kept list and scanned through
+    their own IoU bit matrix) against the one-box-per-barrier path it replaced (ym_set_debug(YM_DBG_NMS, 9)), on the
+    same forward's candidates at the validator's conf 0.001 and at 0.02 / 0.004: bit-identical rows and counts (greedy
+    NMS is a function of the sorted candidates alone).  Variants: the class filter (cf) applies only when
+    boxes of different classes cannot intersect — default max_wh 7680 with and without a `classes` filter (cf on),
+    agnostic NMS and max_wh 64 (cf off: every kept box is tested)."""
+    from yolomi import lib as L
+    kw = NMS_VARIANTS[variant]
     eng = model("n", dtype).model.engine
     x = make_input("uniform", tuple(range(71, 71 + B)), 640).to(DEV)
     for conf in (0.001, 0.004, 0.02):
-        d0, c0 = (t.clone() for t in eng.run(x, conf=conf, use_graph=False))
-        os.environ["YM_NMS_DBG"] = "9"
+        d0, c0 = (t.clone() for t in eng.run(x, conf=conf, use_graph=False, **kw))
+        if conf == 0.001:  # the blocked path really runs: more than NMS_BM candidates in some image
+            logits = eng.read_buffer(eng.graph.anchor_buf.id, B)[:, 0, :, 64:144]
+            if "classes" in kw:
+                logits = logits[..., kw["classes"]]
+            n_cand = int((torch.sigmoid(logits).amax(-1) > conf).sum(-1).max())
+            assert n_cand > 512, n_cand
+        prev = L.set_debug(L.DBG_NMS, 9)
         try:
-            d1, c1 = (t.clone() for t in eng.run(x, conf=conf, use_graph=False))
+            d1, c1 = (t.clone() for t in eng.run(x, conf=conf, use_graph=False, **kw))
         finally:
-            del os.environ["YM_NMS_DBG"]
+            L.set_debug(L.DBG_NMS, prev)
         assert torch.equal(c0, c1), (conf, c0.tolist(), c1.tolist())
         for b in range(B):
             n = int(c0[b])

@@ -1,7 +1,7 @@
 #!/bin/bash
 # Round-end evidence on one box: smoke, the whole GPU suite, the bench lines (headline yolo11s x3, yolo11n x3,
 # yolo11s-seg, the yolo11n PTQ int8 / fp8 lines and f16 beside them), the per-op replay table, rocprofv3 stats and
-# PMC passes of the headline bench command.  Each GPU step under its own limit; a fatal status ends it.
+# PMC passes of the headline bench command, and the per-op SQ table (MFMA busy) of one headline forward (sq).  Each GPU step under its own limit; a fatal status ends it.
 #   TAG=r05z STEPS="smoke suite" bash tools/gpu_final.sh        (default: every step; output gpurun_out/$TAG)
 cd "$(dirname "$0")/.." || exit 1
 OUT=gpurun_out/${TAG:-final}
@@ -27,6 +27,9 @@ for step in ${STEPS:-smoke suite bench_s bench_n bench_seg bench_ptq optable pro
                run bench_n_f8 400 python -u bench.py --model n --dtype f8
                run bench_n_f16 400 python -u bench.py --model n --dtype f16 --no-cpu ;;
     optable) run optable 200 python -u tools/op_table.py --model s --dtype x3 ;;
+    sq) bash tools/gpu_sq_table.sh "${TAG:-final}" --model s --dtype x3 > "$OUT/sq.log" 2>&1; rc=$?
+        echo "[sq] rc=$rc $(date +%T)" | tee -a "$OUT/steps.log"
+        if [ $rc -ne 0 ]; then exit $rc; fi ;;
     conf) run conf_timing 300 python -u tools/conf_timing.py s 8 ;;
     prof) (cd /tmp && timeout -k 10 400 rocprofv3 --kernel-trace --stats --output-format csv \
              -d "$GRAFT_REPO_ROOT/$OUT/prof" -o run -- python3 "$GRAFT_REPO_ROOT/bench.py" --steps 50 \

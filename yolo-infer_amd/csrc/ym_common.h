@@ -457,6 +457,8 @@ hipError_t ym_launch_prep(int dtype, const PrepArgs& a, int* counts, int B, hipS
 hipError_t ym_launch_input_max(const float* x, long n, float* ctl, float* out, hipStream_t st);
 hipError_t ym_launch_decode(const DecodeArgs& a, hipStream_t st);
 hipError_t ym_launch_nms(const NmsArgs& a, hipStream_t st);
+int ym_debug_get(int key);  // ym_set_debug switches (ym_misc.hip)
+int ym_debug_set(int key, int value);
 const void* ym_nms_kernel();  // the NMS kernel's function (graph replays re-point its output rows: ym_infer)
 hipError_t ym_launch_stem(int dtype, const ConvArgs& a, hipStream_t st);
 hipError_t ym_launch_letterbox(const LetterboxArgs& a, hipStream_t st);

@@ -7,6 +7,8 @@
 
 #include <type_traits>
 
+#include <atomic>
+
 #include "ym_common.h"
 
 namespace {
@@ -1707,6 +1709,31 @@ hipError_t ym_launch_input_max(const float* x, long n, float* ctl, float* out, h
   return hipGetLastError();
 }
 
+// process-wide debug switches (ym_set_debug; include/yolomi.h YM_DBG_*): set from the environment once, then only by
+// the setter — a launch reads an atomic instead of calling getenv (getenv per launch is not thread-safe
+// against setenv and costs time on every eager forward)
+namespace {
+std::atomic<int>* dbg_slots() {
+  static std::atomic<int> v[4] = {};
+  static const bool init = [] {
+    const char* names[4] = {nullptr, "YM_NMS_DBG", "YM_DW_MODE", "YM_DW_TILE"};
+    for (int k = 1; k < 4; ++k) {
+      const char* e = getenv(names[k]);
+      v[k].store(e ? atoi(e) : 0);
+    }
+    return true;
+  }();
+  (void)init;
+  return v;
+}
+}  // namespace
+
+int ym_debug_get(int key) { return key > 0 && key < 4 ? dbg_slots()[key].load(std::memory_order_relaxed) : 0; }
+int ym_debug_set(int key, int value) {
+  if (key <= 0 || key >= 4) return -1;
+  return dbg_slots()[key].exchange(value);
+}
+
 hipError_t ym_launch_dwconv(int dtype, const DwArgs& a, hipStream_t st) {
   if (ym_dt_q8(dtype)) return ym_launch_dwconv_i8(a, st, dtype == YM_DT_F8);
   const long total = (long)a.B * a.H * a.W * (a.C / 8);
@@ -1715,14 +1742,12 @@ hipError_t ym_launch_dwconv(int dtype, const DwArgs& a, hipStream_t st) {
   if (a.C % 8) return hipErrorInvalidValue;
   // pixels per thread: 4 where that still leaves >= 128 workgroups (measured best at 80²/160²), else 2 (20²/40²)
   static const int env_pxt = [] { const char* e = getenv("YM_DW_PXT"); return e ? atoi(e) : 0; }();
-  // YM_DW_MODE (A/B and tests; read at every launch, i.e. at graph capture): 0 = LDS tiles (default), 1 = row /
+  // YM_DBG_DW_MODE (A/B and tests; read at every launch, i.e. at graph capture): 0 = LDS tiles (default), 1 = row /
   // one-pixel variants, 2 = column strips
-  const char* em = getenv("YM_DW_MODE");
-  const int mode = em ? atoi(em) : 0;
+  const int mode = ym_debug_get(2);
   if (mode == 0 && !a.raw) {
-    // LDS tile shape (TH x TW pixels x CG chunks; YM_DW_TILE=0..3 for A/B, read at every launch): 0 = 8 x 16 x 4
-    const char* et = getenv("YM_DW_TILE");
-    const int ti = et ? atoi(et) : 0;
+    // LDS tile shape (TH x TW pixels x CG chunks; YM_DBG_DW_TILE 0..3 for A/B, read at every launch): 0 = 8 x 16 x 4
+    const int ti = ym_debug_get(3);
     auto go = [&](auto th, auto tw, auto cg) -> hipError_t {
       constexpr int TH = decltype(th)::value, TW = decltype(tw)::value, CG = decltype(cg)::value;
       const long tiles = (long)a.B * ((a.H + TH - 1) / TH) * ((a.W + TW - 1) / TW) * ((a.C / 8 + CG - 1) / CG);
@@ -1879,10 +1904,8 @@ hipError_t ym_launch_decode(const DecodeArgs& a, hipStream_t st) {
 }
 
 hipError_t ym_launch_nms(const NmsArgs& a0, hipStream_t st) {
-  const char* e = getenv("YM_NMS_DBG");  // read per launch (a test switches the blocked path off between eager runs)
-  const int dbg = e ? atoi(e) : 0;
   NmsArgs a = a0;
-  a.dbg = dbg;
+  a.dbg = ym_debug_get(1);  // YM_DBG_NMS (a test switches the blocked path off between eager runs)
   hipLaunchKernelGGL(nms_image, dim3(a.B), dim3(NMS_T), 0, st, a);
   return hipGetLastError();
 }

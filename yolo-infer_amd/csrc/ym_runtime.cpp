@@ -75,8 +75,8 @@ constexpr int32_t kMagic = 0x4C504D59;  // 'YMPL'
 constexpr int kHdr = 32, kBufRec = 8, kOpRec = 32, kNameLen = 48;
 constexpr int kSplitCounters = 16384;  // split-K tiles per conv launch (csrc/ym_conv_dma.hip)
 constexpr int kMaxLanes = 4;           // concurrent batch slices in one forward graph (<= GPU_MAX_HW_QUEUES)
-constexpr size_t kMaxGraphs = 16;
-constexpr size_t kMiscBytes = 16384;  // ym_ctx::d_misc      // captured forwards cached per context (the oldest is retired first)
+constexpr size_t kMaxGraphs = 16;      // captured forwards cached per context (the oldest is retired first)
+constexpr size_t kMiscBytes = 16384;  // ym_ctx::d_misc
 
 enum OpKind { OP_INPUT = 1, OP_CONV = 2, OP_DW = 3, OP_SPPF = 4, OP_ATTN = 5, OP_DECODE = 6, OP_NMS = 7, OP_REQ = 8 };
 
@@ -213,6 +213,22 @@ struct ym_ctx {
   int lane = 0, lane_img0 = 0;  // lane / first image of the ops being launched
   int call_B = 0;               // images of the forward being launched (all lanes)
   std::vector<GraphEntry> graphs;
+  // the previous forward: every forward of a context uses the same arena, NMS scratch, split-K slabs /
+  // counters and input_stats ticket, so a forward launched on another stream than the previous one first waits for
+  // it (ym_infer: hipStreamWaitEvent); last_ev is the replayed graph's `done` event or fwd_ev (eager forwards)
+  hipStream_t last_st = nullptr;
+  hipEvent_t last_ev = nullptr, fwd_ev = nullptr;
+  int order_after_last(hipStream_t st) {
+    if (last_ev && last_st != st) {
+      const hipError_t e = hipStreamWaitEvent(st, last_ev, 0);
+      if (e != hipSuccess) return fail(YM_EHIP, "stream order: %s", hipGetErrorString(e));
+    }
+    return YM_OK;
+  }
+  void retire(GraphEntry& g) {  // retire_graph, forgetting last_ev when it is that graph's event (now complete)
+    if (g.done && g.done == last_ev) last_ev = nullptr;
+    retire_graph(g);
+  }
   std::vector<hipEvent_t> prof_events;
   float* const* calib_raw = nullptr;  // ym_calibrate: per-op pre-activation output buffers (f32 plans)
   // per-shape, per-op conv tile configuration (-1 = heuristic); set by ym_tune / ym_set_op_cfg
@@ -254,10 +270,11 @@ struct ym_ctx {
       if (join_ev[l]) (void)hipEventDestroy(join_ev[l]);
     }
     if (fork_ev) (void)hipEventDestroy(fork_ev);
+    if (fwd_ev) (void)hipEventDestroy(fwd_ev);
     for (hipEvent_t e : op_ev) (void)hipEventDestroy(e);
   }
   void clear_graphs() {
-    for (auto& g : graphs) retire_graph(g);
+    for (auto& g : graphs) retire(g);
     graphs.clear();
   }
   int buf_P(int b) const {
@@ -647,6 +664,10 @@ int ym_num_conv_cfgs(int dtype) {  // public dtype codes (ym_model_desc): 1 f16,
 }
 
 const char* ym_last_error(void) { return g_err.c_str(); }
+int ym_set_debug(int key, int value) {
+  if (key < YM_DBG_NMS || key > YM_DBG_DW_TILE) return fail(YM_EINVAL, "unknown debug key %d", key);
+  return ym_debug_set(key, value);
+}
 
 int ym_create(int device, const ym_model_desc* desc, ym_ctx** out) {
   if (!out) return fail(YM_EINVAL, "null out");
@@ -1028,7 +1049,15 @@ int ym_infer(ym_ctx* c, const float* d_in, int B, int H, int W, const ym_infer_a
   hipStream_t st = static_cast<hipStream_t>(stream);
   rc = ensure_workspace(c, B, H, W);
   if (rc) return rc;
-  if (!args->use_graph) return launch_forward(c, d_in, B, args, d_dets, d_counts, st);
+  if ((rc = c->order_after_last(st))) return rc;
+  if (!args->use_graph) {
+    if (!c->fwd_ev) HIPCK(hipEventCreateWithFlags(&c->fwd_ev, hipEventDisableTiming));
+    if ((rc = launch_forward(c, d_in, B, args, d_dets, d_counts, st))) return rc;
+    HIPCK(hipEventRecord(c->fwd_ev, st));
+    c->last_ev = c->fwd_ev;
+    c->last_st = st;
+    return YM_OK;
+  }
   GraphKey key;
   memset(&key, 0, sizeof(key));
   key.B = B; key.H = H; key.W = W; key.in = d_in; key.dets = nullptr; key.counts = d_counts; key.args = *args;
@@ -1043,11 +1072,13 @@ int ym_infer(ym_ctx* c, const float* d_in, int B, int H, int W, const ym_infer_a
       if (g.key == key && g.dets != d_dets && (rc = repoint_dets(g, d_dets))) return rc;
       HIPCK(hipGraphLaunch(g.exec, st));
       HIPCK(hipEventRecord(g.done, st));
+      c->last_ev = g.done;
+      c->last_st = st;
       return YM_OK;
     }
   }
   if (c->graphs.size() >= kMaxGraphs) {  // evict the oldest capture once its last replay has drained
-    retire_graph(c->graphs.front());
+    c->retire(c->graphs.front());
     c->graphs.erase(c->graphs.begin());
   }
   // capture on the private stream (lane streams join through the fork event), replay on the caller's stream
@@ -1072,6 +1103,8 @@ int ym_infer(ym_ctx* c, const float* d_in, int B, int H, int W, const ym_infer_a
   c->graphs.push_back(ge);
   HIPCK(hipGraphLaunch(ge.exec, st));
   HIPCK(hipEventRecord(ge.done, st));
+  c->last_ev = ge.done;
+  c->last_st = st;
   return YM_OK;
 }
 
@@ -1092,6 +1125,7 @@ int ym_calibrate(ym_ctx* c, const float* d_in, int B, int H, int W, const ym_inf
   if (!d_raw || n_ops != (int)c->ops.size()) return fail(YM_EINVAL, "d_raw must hold %zu entries", c->ops.size());
   HIPCK(hipSetDevice(c->device));
   if ((rc = ensure_workspace(c, B, H, W))) return rc;
+  if ((rc = c->order_after_last(static_cast<hipStream_t>(stream)))) return rc;
   ym_infer_args one = *args;
   one.lanes = 1;
   c->calib_raw = d_raw;
@@ -1108,6 +1142,7 @@ int ym_profile(ym_ctx* c, const float* d_in, int B, int H, int W, const ym_infer
   HIPCK(hipSetDevice(c->device));
   hipStream_t st = static_cast<hipStream_t>(stream);
   if ((rc = ensure_workspace(c, B, H, W))) return rc;
+  if ((rc = c->order_after_last(st))) return rc;
   const size_t ne = c->ops.size() + 1;
   while (c->prof_events.size() < ne) {
     hipEvent_t e;
@@ -1137,6 +1172,7 @@ int ym_profile_replay(ym_ctx* c, const float* d_in, int B, int H, int W, const y
   HIPCK(hipSetDevice(c->device));
   hipStream_t st = static_cast<hipStream_t>(stream);
   if ((rc = ensure_workspace(c, B, H, W))) return rc;
+  if ((rc = c->order_after_last(st))) return rc;
   // one real forward so every buffer holds this input's activations (and the /255 flag is set)
   for (const Op& op : c->ops)
     if ((rc = launch_op(c, op, B, d_in, args, d_dets, d_counts, st))) return rc;
@@ -1183,6 +1219,7 @@ int ym_tune(ym_ctx* c, const float* d_in, int B, int H, int W, const ym_infer_ar
   HIPCK(hipSetDevice(c->device));
   hipStream_t st = static_cast<hipStream_t>(stream);
   if ((rc = ensure_workspace(c, B, H, W))) return rc;
+  if ((rc = c->order_after_last(st))) return rc;
   if (reps < 1) reps = 8;
   // one real forward first so every buffer a candidate reads holds this model's activations
   c->drop_cfg(B, H, W);

@@ -82,6 +82,7 @@ def load_library(path: os.PathLike = LIB_PATH):
         "ym_destroy": (None, [P]),
         "ym_version": (I, []),
         "ym_num_conv_cfgs": (I, [I]),
+        "ym_set_debug": (I, [I, I]),
     }
     for name, (res, args) in sig.items():
         fn = getattr(lib, name)
@@ -95,7 +96,17 @@ EXPORTED = ("ym_create", "ym_load_weights", "ym_broadcast_weights", "ym_broadcas
             "ym_rccl_comm_destroy", "ym_infer", "ym_input_max", "ym_calibrate", "ym_masks", "ym_masks_slots", "ym_letterbox",
             "ym_profile", "ym_profile_replay", "ym_tune", "ym_get_op_cfg", "ym_set_op_cfg", "ym_num_ops", "ym_op_name",
             "ym_num_buffers", "ym_buffer_info", "ym_read_buffer", "ym_sync", "ym_last_error", "ym_destroy",
-            "ym_version", "ym_num_conv_cfgs")
+            "ym_version", "ym_num_conv_cfgs", "ym_set_debug")
+
+DBG_NMS, DBG_DW_MODE, DBG_DW_TILE = 1, 2, 3  # ym_set_debug keys (include/yolomi.h)
+
+
+def set_debug(key: int, value: int) -> int:
+    """ym_set_debug: a process-wide kernel debug switch; returns the previous value."""
+    rc = load_library().ym_set_debug(key, value)
+    if rc < 0:
+        _check(rc)
+    return rc
 
 
 def _check(rc: int):
