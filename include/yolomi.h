@@ -203,11 +203,15 @@ int ym_num_conv_cfgs(int dtype);
 /* Process-wide debug switches for tests and A/B runs (not part of the reference interface; defaults 0), read when a
  * kernel is launched (so at graph capture for replayed forwards): YM_DBG_NMS (9 = the NMS kernel's per-box path
  * instead of the blocked one), YM_DBG_DW_MODE (depthwise variant: 0 LDS tiles, 1 rows, 2 column strips),
- * YM_DBG_DW_TILE (LDS tile shape 0..3).  The environment variables of the same names set the initial values.
+ * YM_DBG_DW_TILE (LDS tile shape 0..3), YM_DBG_CHAIN (1: the persistent two-conv chain kernel).
+ * The environment variables YM_NMS_DBG, YM_DW_MODE, YM_DW_TILE and YM_CHAIN set the initial values.  A forward graph
+ * already captured keeps the kernels it was captured with.
  * Returns the previous value, or YM_EINVAL for an unknown key. */
 #define YM_DBG_NMS 1
 #define YM_DBG_DW_MODE 2
 #define YM_DBG_DW_TILE 3
+#define YM_DBG_CHAIN 4 /* 1: dependent x3 3x3 pairs on one LDS-DMA configuration as one persistent launch */
+#define YM_DBG_CHAIN_LAUNCHES 5 /* chain kernels launched since it was last set (a counter) */
 int ym_set_debug(int key, int value);
 
 #ifdef __cplusplus

@@ -241,3 +241,37 @@ def test_predict_on_alternating_streams_is_ordered():
         for r, d in zip(res, ref[k]):
             assert torch.equal(r.boxes.data, d), k
     assert sum(len(d) for d in ref[0]) > 0
+
+
+def test_chain_kernel_bitwise_equals_two_launches():
+    """DESIGN.md §4.5 (verdict r5 item 1): with YM_DBG_CHAIN = 1 the dependent 20² x3 3x3 pairs that share an LDS-DMA
+    configuration (yolo11s B=8: model.8.m.0.m.0.cv1 -> cv2 and their model.22 twins) run as ONE persistent launch
+    (csrc/ym_conv_dma.hip conv_dma_chain: per-tile ready counters, write-through hand-off).  The chain launches, and
+    every plan buffer and the detections are bit-identical to the two separate launches, eager and graph-replayed."""
+    from core.model import YOLO11Model
+    from yolomi import lib as L
+    m = YOLO11Model(task="detect", size="s", device="cuda:0", dtype="x3", verbose=False)
+    eng = m.model.engine
+    x = synthetic_batch(8, 640, 5, DEV)
+    d0, c0 = (t.clone() for t in eng.run(x, conf=0.05, use_graph=False))
+    nb = len(eng.graph.buffers)
+    ref = [eng.read_buffer(b, 8, raw=True) for b in range(nb) if b != eng.graph.input.id]
+    prev = L.set_debug(L.DBG_CHAIN, 1)
+    L.set_debug(L.DBG_CHAIN_LAUNCHES, 0)
+    try:
+        d1, c1 = (t.clone() for t in eng.run(x, conf=0.05, use_graph=False))
+        got = [eng.read_buffer(b, 8, raw=True) for b in range(nb) if b != eng.graph.input.id]
+        n_chain = L.set_debug(L.DBG_CHAIN_LAUNCHES, 0)
+        xg = x.clone()  # a new graph key: captured with the chain kernels, replayed three times
+        for _ in range(3):
+            d2, c2 = (t.clone() for t in eng.run(xg, conf=0.05))
+        torch.cuda.synchronize()
+    finally:
+        L.set_debug(L.DBG_CHAIN, prev)
+    assert n_chain >= 1, "no chain kernel launched"
+    for r, g in zip(ref, got):
+        assert torch.equal(r, g)
+    for d, c in ((d1, c1), (d2, c2)):
+        assert torch.equal(c0, c)
+        for b in range(8):
+            assert torch.equal(d0[b, :int(c0[b])], d[b, :int(c0[b])])

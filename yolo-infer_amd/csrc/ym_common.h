@@ -108,6 +108,9 @@ __device__ __forceinline__ f16* ym_p2_hi4(P2* p) {
   return reinterpret_cast<f16*>((u & ~(uintptr_t)31) + ((u & 31) >> 1));
 }
 __device__ __forceinline__ const f16* ym_p2_hi4(const P2* p) { return ym_p2_hi4(const_cast<P2*>(p)); }
+// SC1: write-through stores (sc1: the line leaves this XCD's L2 at once), for a consumer workgroup of the same
+// launch on any XCD (the persistent chain kernel, csrc/ym_conv_dma.hip; cdna_hip_programming.md §6 Guideline 16)
+template <bool SC1 = false>
 __device__ __forceinline__ void ym_p2_store4(P2* p, const float* v) {
   f16x4 h, l;
 #pragma unroll
@@ -116,8 +119,15 @@ __device__ __forceinline__ void ym_p2_store4(P2* p, const float* v) {
     l[e] = (f16)(v[e] - (float)h[e]);
   }
   f16* q = ym_p2_hi4(p);
-  *reinterpret_cast<f16x4*>(q) = h;
-  *reinterpret_cast<f16x4*>(q + 8) = l;
+  if constexpr (SC1) {
+    typedef __attribute__((address_space(1))) unsigned long long gu64;
+    __hip_atomic_store((gu64*)q, __builtin_bit_cast(unsigned long long, h), __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
+    __hip_atomic_store((gu64*)(q + 8), __builtin_bit_cast(unsigned long long, l), __ATOMIC_RELAXED,
+                       __HIP_MEMORY_SCOPE_AGENT);
+  } else {
+    *reinterpret_cast<f16x4*>(q) = h;
+    *reinterpret_cast<f16x4*>(q + 8) = l;
+  }
 }
 // v of lane ^ XOR (XOR 16 or 32): ds_bpermute (LDS crossbar), or with `vp` the VALU row swap v_permlane16_swap /
 // v_permlane32_swap with one register as both operands — the odd 16-lane rows (32: the upper half) find the partner's
@@ -143,8 +153,10 @@ __device__ __forceinline__ unsigned ym_lane_xor(unsigned v, bool vp) {
 // (tools/store_probe.hip: the 8-byte pattern of ym_p2_store4 writes HBM at 4.8-5.4 TB/s, 32-byte runs at 6.5-6.9).
 // Same stored bits as ym_p2_store4.  Both lanes of a pair must execute it (the exchange is a cross-lane read);
 // `ok` predicates only the store, and p may be any address when !ok.
-template <int XOR>
-__device__ __forceinline__ void ym_p2_store4_pair(P2* p, const float* v, bool odd, bool ok, bool vp = false) {
+// SC1: write-through (see ym_p2_store4), as a buffer store off the wave-uniform `base` (offsets < 2^31 bytes)
+template <int XOR, bool SC1 = false>
+__device__ __forceinline__ void ym_p2_store4_pair(P2* p, const float* v, bool odd, bool ok, bool vp = false,
+                                                  const void* base = nullptr) {
   f16x4 h, l;
 #pragma unroll
   for (int e = 0; e < 4; ++e) {
@@ -161,7 +173,16 @@ __device__ __forceinline__ void ym_p2_store4_pair(P2* p, const float* v, bool od
                       : f16x8{h[0], h[1], h[2], h[3], q[0], q[1], q[2], q[3]};
   if (ok) {
     const uintptr_t u = reinterpret_cast<uintptr_t>(p);
-    *reinterpret_cast<f16x8*>((u & ~(uintptr_t)31) + (odd ? 16 : 0)) = o;
+    if constexpr (SC1) {  // one 16-byte write-through store: a buffer store with the sc1 bit (aux 16)
+      const uintptr_t t = (u & ~(uintptr_t)31) + (odd ? 16 : 0);
+      const __amdgpu_buffer_rsrc_t r = __builtin_amdgcn_make_buffer_rsrc(const_cast<void*>(base), 0, 0x7FFFFFF0,
+                                                                         0x00020000);
+      typedef unsigned u32x4_t __attribute__((ext_vector_type(4)));
+      __builtin_amdgcn_raw_buffer_store_b128(__builtin_bit_cast(u32x4_t, o), r,
+                                             (unsigned)(t - reinterpret_cast<uintptr_t>(base)), 0, 16);
+    } else {
+      *reinterpret_cast<f16x8*>((u & ~(uintptr_t)31) + (odd ? 16 : 0)) = o;
+    }
   }
 }
 __device__ __forceinline__ void ym_p2_load4(const P2* p, float* v) {  // v[e] = hi + lo
@@ -457,8 +478,11 @@ hipError_t ym_launch_prep(int dtype, const PrepArgs& a, int* counts, int B, hipS
 hipError_t ym_launch_input_max(const float* x, long n, float* ctl, float* out, hipStream_t st);
 hipError_t ym_launch_decode(const DecodeArgs& a, hipStream_t st);
 hipError_t ym_launch_nms(const NmsArgs& a, hipStream_t st);
+hipError_t ym_launch_conv_dma_chain(const ConvArgs& a0, const ConvArgs& a1, int dma_cfg, int* ctl, int cap,
+                                    hipStream_t st);  // csrc/ym_conv_dma.hip: two dependent x3 convs, one launch
 int ym_debug_get(int key);  // ym_set_debug switches (ym_misc.hip)
 int ym_debug_set(int key, int value);
+void ym_debug_add(int key, int d);
 const void* ym_nms_kernel();  // the NMS kernel's function (graph replays re-point its output rows: ym_infer)
 hipError_t ym_launch_stem(int dtype, const ConvArgs& a, hipStream_t st);
 hipError_t ym_launch_letterbox(const LetterboxArgs& a, hipStream_t st);

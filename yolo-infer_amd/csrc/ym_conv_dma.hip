@@ -105,9 +105,18 @@ template <> struct Store4<P2> {
 // weight-operand layout, and the second GEMM (K = the first conv's N) runs as extra ring stages — the same fragment
 // reads and split MFMAs — before the epilogue stores the second conv's output.  The intermediate never reaches HBM and
 // the pair is one launch (the split pair wrote and read it back: model.1+cv1, the Detect cv2.l.1 -> cv2.l.2 chains).
+// The workgroup body (output tile `bid` of the launch's tile map; LDS from the caller) — the conv_dma kernel below, or
+// one work item of the persistent chain kernel conv_dma_chain.  Returns true when this workgroup stored the tile's
+// final output (false: a padding workgroup, or a split-K partial that another workgroup of the tile reduced); the
+// value is the same in every wave.  SC1OUT: the epilogue stores write through (sc1), for a consumer in the same launch.
+template <int NSTAGE, int SB, int BN, int KS2>
+struct DmaSmem {
+  static constexpr int ring = NSTAGE * SB + 16 + 256;
+  static constexpr int w2 = KS2 ? KS2 * BN * 128 : 16;
+};
 template <typename OutT, int BM, int BN, int KIND, int SPLIT, int KG, int NSTAGE, int SUB, bool X3 = false,
-          bool FUSE = false>
-__global__ __launch_bounds__(256 * KG) void conv_dma(const ConvArgs a) {
+          bool FUSE = false, bool SC1OUT = false>
+__device__ __forceinline__ bool conv_dma_body(const ConvArgs& a, const int bid, char* smem, char* w2s) {
   constexpr int NW = 4 * KG;
   constexpr int TM = BM / 64, TN = BN / 64;
   static_assert((BM / 8) % NW == 0 && (BN / 8) % NW == 0, "DMA groups must divide over the waves");
@@ -118,20 +127,16 @@ __global__ __launch_bounds__(256 * KG) void conv_dma(const ConvArgs a) {
   constexpr int NREG = TM * TN * 16;
   constexpr int SPW = 4 / KG;                        // 16-deep k sub-steps per wave per stage
   constexpr int NACC = TM * TN == 1 && SPW >= 2 ? 2 : 1;  // one 32x32 block per wave: alternate two accumulators
-  __shared__ __attribute__((aligned(16))) char smem[NSTAGE * SB + 16 + 256];  // + split-K flag, L2 warm-up scratch
+  // smem: NSTAGE * SB ring bytes + split-K flag, L2 warm-up scratch
   // FUSE: the second GEMM's K (the first conv's BN channels) in 64-deep storage sub-stages, W2 [KS2][BN rows][128 B]
   constexpr int KS2 = FUSE ? (X3 ? 2 : 1) * BN / 64 : 0;
   static_assert(!FUSE || (SPLIT == 1 && NSTAGE * SB >= KS2 * BM * 128), "fused pair: whole-K tiles, T fits the ring");
-  __shared__ __attribute__((aligned(16))) char w2s[FUSE ? KS2 * BN * 128 : 16];
   constexpr int W2P = FUSE ? KS2 * BN * 8 / (256 * KG) : 1;  // 16-byte W2 pieces per thread
   static_assert(!FUSE || (KS2 * BN * 8) % (256 * KG) == 0, "W2 pieces divide over the threads");
   // BN 128: W2 is 64 KB, 16 pieces per thread — too many registers to hold through the K loop; loaded after it
   constexpr bool W2LATE = W2P > 8;
 
   YM_STAMP(0);
-#ifndef YM_NO_WARM
-  ym_warm_kernargs<sizeof(ConvArgs)>();
-#endif
   // wid in an SGPR (uniform per wave): every LDS-DMA destination (M0) derived from it is then scalar arithmetic,
   // not a VALU address moved to M0 by v_readfirstlane before each DMA instruction
   const int tid = threadIdx.x, lane = tid & 63, wid = __builtin_amdgcn_readfirstlane(tid >> 6);
@@ -141,14 +146,13 @@ __global__ __launch_bounds__(256 * KG) void conv_dma(const ConvArgs a) {
   // tile map: every N tile and every K split of pixel tile tm share bid % 8 = one XCD (its L2 holds the pixels and
   // the split's slabs), and each XCD owns one contiguous run of pixel tiles, so the image rows a 3x3 tile shares with
   // its neighbours are fetched into one L2; padding workgroups (tm beyond M) exit before touching a counter
-  const int bid = blockIdx.x;
   int rest = bid >> 3;
   const int sp = rest % SPLIT;
   rest /= SPLIT;
   const int rq = ym_div(rest, a.fd_tn);  // rest / tiles_n
   const int tn = rest - rq * a.tiles_n;
   const int tm = (bid & 7) * a.tm_per_xcd + rq;  // (a.tm_per_xcd = gridDim.x / (8 SPLIT tiles_n))
-  if (tm * BM >= a.M) return;
+  if (tm * BM >= a.M) return false;
 
   // ---- epilogue operands first (bias, residual; wave group 0 runs the epilogue): their latency hides behind the
   // K loop.  They are older than every DMA, so the counted vmcnt waits below stay exact (loads retire in order).
@@ -561,7 +565,8 @@ __global__ __launch_bounds__(256 * KG) void conv_dma(const ConvArgs a) {
       *flag = last;
     }
     __syncthreads();
-    if (!*flag || kg != 0) return;
+    const bool last_arrival = *flag;
+    if (!last_arrival || kg != 0) return last_arrival;
     __builtin_amdgcn_fence(__ATOMIC_ACQUIRE, "wavefront");  // no instruction: keeps the sc1 loads below the ticket
     // sum every slab (this workgroup's own included) in split order — bitwise-reproducible whichever split arrived
     // last; all slabs' loads are issued together (one memory latency, not SPLIT)
@@ -636,7 +641,7 @@ __global__ __launch_bounds__(256 * KG) void conv_dma(const ConvArgs a) {
           ok ? v : u32x4{0u, 0u, 0u, 0u};
     }
     __syncthreads();
-    if (kg != 0) return;
+    if (kg != 0) return true;
     f32x16 acc2[NACC][TM][TN];
 #pragma unroll
     for (int u = 0; u < NACC; ++u)
@@ -697,7 +702,7 @@ __global__ __launch_bounds__(256 * KG) void conv_dma(const ConvArgs a) {
         if constexpr (NACC == 2) acc[0][i][j] += acc2[1][i][j];
       }
   }
-  if (kg != 0) return;
+  if (kg != 0) return true;
 
   // ---- epilogue: lane owns channels nb + 32j + 8q + 4h + {0..3} of pixel pbm + 32i + l32
   OutT* dst = static_cast<OutT*>(a.dst);
@@ -729,7 +734,10 @@ __global__ __launch_bounds__(256 * KG) void conv_dma(const ConvArgs a) {
               const int ch = n - sub * a.npr;
               o = ep_obase[i] + (size_t)((sub >> 1) * a.d_W + (sub & 1)) * a.d_ctot + ch;
             }
-            ym_p2_store4_pair<32>(dst + (okn ? o : 0), v, h, okn, a.pst & 16);
+            if constexpr (SC1OUT)
+              ym_p2_store4_pair<32, true>(dst + (okn ? o : 0), v, h, okn, a.pst & 16, a.dst);
+            else
+              ym_p2_store4_pair<32>(dst + (okn ? o : 0), v, h, okn, a.pst & 16);
             continue;
           }
         }
@@ -741,7 +749,10 @@ __global__ __launch_bounds__(256 * KG) void conv_dma(const ConvArgs a) {
                              : acc[0][i][j][4 * q + e] + bias4[j][q][e];
           v[e] = ((FUSE ? a.act2 : a.act) ? (X3 ? ym_silu_x3(x) : ym_silu_fast(x)) : x) + (float)res4[i][j][q][e];
         }
-        if (a.shuffle) {
+        if constexpr (SC1OUT) {  // (the chain kernel takes no pixel-shuffle ops)
+          static_assert(std::is_same<OutT, P2>::value, "write-through epilogue: pair-layout outputs");
+          ym_p2_store4<true>(dst + ep_obase[i] + n, v);
+        } else if (a.shuffle) {
           const int sub = n / a.npr;
           const int ch = n - sub * a.npr;
           Store4<OutT>::st(dst + ep_obase[i] + (size_t)((sub >> 1) * a.d_W + (sub & 1)) * a.d_ctot + ch, v);
@@ -751,6 +762,20 @@ __global__ __launch_bounds__(256 * KG) void conv_dma(const ConvArgs a) {
       }
   }
   YM_STAMP(3);
+  return true;
+}
+
+template <typename OutT, int BM, int BN, int KIND, int SPLIT, int KG, int NSTAGE, int SUB, bool X3 = false,
+          bool FUSE = false>
+__global__ __launch_bounds__(256 * KG) void conv_dma(const ConvArgs a) {
+  constexpr int KS2 = FUSE ? (X3 ? 2 : 1) * BN / 64 : 0;
+  typedef DmaSmem<NSTAGE, SUB * (BM + BN) * 128, BN, KS2> SM;
+  __shared__ __attribute__((aligned(16))) char smem[SM::ring];
+  __shared__ __attribute__((aligned(16))) char w2s[SM::w2];
+#ifndef YM_NO_WARM
+  ym_warm_kernargs<sizeof(ConvArgs)>();
+#endif
+  conv_dma_body<OutT, BM, BN, KIND, SPLIT, KG, NSTAGE, SUB, X3, FUSE>(a, blockIdx.x, smem, w2s);
 }
 
 struct DmaCfg {
@@ -880,7 +905,154 @@ hipError_t dispatch_fuse(const ConvArgs& a, int kind, int i, hipStream_t st) {
   return hipErrorInvalidValue;
 }
 
+// ---------------------------------------------------------------------------------------------------------------
+// Persistent chain of two dependent x3 convs in ONE launch (verdict r5 item 1: the 20² dependent chain, built and
+// measured instead of priced).  Workgroup w runs work item w of op 0 (the conv_dma_body tile map,
+// split-K included), publishes it, then runs item w of op 1, whose pixel tile first waits for the op-0 pixel tiles
+// its 3x3 window reads (per-tile ready counters, no grid barrier).  Hand-off (cdna_hip_programming.md §6 Guideline
+// 16): op 0's epilogue stores write through (sc1) → every storing wave's vmcnt(0) → workgroup barrier → one lane's
+// agent-scope counter add; the consumer's one lane polls the counters relaxed (sc1 loads + s_sleep, bounded: a give-up
+// sets `tmo`), then one agent-scope acquire (L1 invalidate) → vmcnt(0) → workgroup barrier → the ring's LDS-DMA loads.
+// The grid is at most one workgroup per CU (the 147 KB rings of these configurations admit one), so every workgroup
+// is resident once earlier kernels drain; only one chain kernel runs at a time (the runtime places chains on the main
+// stream only).  The last workgroup to finish zeroes the counters for the next launch.
+struct ChainArgs {
+  ConvArgs op[2];
+  int* ready;        // per op-0 pixel tile: (tn) tiles stored; zero at launch
+  int* done;         // workgroups finished
+  int* tmo;          // 1 when a wait gave up
+  int halo;          // op-0 output pixels an op-1 tile reads beyond its own range (Wo + 1 for a 3x3, 0 for a 1x1)
+  int tiles_m0;      // real op-0 pixel tiles
+  int ready_target;  // op 0's N tiles
+  int items0, items1;
+};
+
+template <int SPLIT>
+__device__ __forceinline__ int chain_tm(const ConvArgs& a, int bid) {  // conv_dma_body's pixel tile of item bid
+  const int rest = (bid >> 3) / SPLIT;
+  return (bid & 7) * a.tm_per_xcd + ym_div(rest, a.fd_tn);
+}
+
+template <int BM, int BN, int KA, int KB, int SPLIT, int KG, int NS, int SUB>
+__global__ __launch_bounds__(256 * KG) void conv_dma_chain(const ChainArgs c) {
+  typedef DmaSmem<NS, SUB * (BM + BN) * 128, BN, 0> SM;
+  __shared__ __attribute__((aligned(16))) char smem[SM::ring];
+  __shared__ __attribute__((aligned(16))) char w2s[SM::w2];
+#ifndef YM_NO_WARM
+  ym_warm_kernargs<sizeof(ChainArgs)>();
+#endif
+  const int G = gridDim.x, tid = threadIdx.x;
+  for (int it = blockIdx.x; it < c.items0; it += G) {
+    const bool fin = conv_dma_body<P2, BM, BN, KA, SPLIT, KG, NS, SUB, true, false, true>(c.op[0], it, smem, w2s);
+    asm volatile("s_waitcnt vmcnt(0)" ::: "memory");  // every storing wave drains its write-through stores
+    __syncthreads();
+    if (tid == 0 && fin)
+      __hip_atomic_fetch_add(c.ready + chain_tm<SPLIT>(c.op[0], it), 1, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
+  }
+  for (int it = blockIdx.x; it < c.items1; it += G) {
+    const ConvArgs& b = c.op[1];
+    const int tm = chain_tm<SPLIT>(b, it);
+    if (tm * BM < b.M) {
+      if (tid == 0) {
+        const int lo = tm * BM - c.halo <= 0 ? 0 : (tm * BM - c.halo) / BM;
+        const int hi = min(c.tiles_m0 - 1, (tm * BM + BM - 1 + c.halo) / BM);
+        bool gave_up = __hip_atomic_load(c.tmo, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT) != 0;
+        for (int t = lo; t <= hi && !gave_up; ++t) {
+          unsigned spins = 0;
+          while (__hip_atomic_load(c.ready + t, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT) < c.ready_target) {
+            __builtin_amdgcn_s_sleep(2);
+            if (++spins > (1u << 20)) {  // bounded: a missing producer ends the launch (with wrong tiles), never hangs
+              __hip_atomic_store(c.tmo, 1, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
+              gave_up = true;
+              break;
+            }
+          }
+        }
+        __builtin_amdgcn_fence(__ATOMIC_ACQUIRE, "agent");  // ONE L1 invalidate after the match
+        asm volatile("s_waitcnt vmcnt(0)" ::: "memory");
+      }
+      __syncthreads();
+    }
+    conv_dma_body<P2, BM, BN, KB, SPLIT, KG, NS, SUB, true, false, false>(b, it, smem, w2s);
+  }
+  __syncthreads();
+  if (tid == 0) {  // the last workgroup: every wait of this launch is over, zero the counters for the next one
+    const int d = __hip_atomic_fetch_add(c.done, 1, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
+    if (d == G - 1) {
+      for (int t = 0; t < c.tiles_m0; ++t) __hip_atomic_store(c.ready + t, 0, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
+      __hip_atomic_store(c.done, 0, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
+    }
+  }
+}
+
+// kind of one chain op: 1 (1x1, one source), 4 (3x3, Cin % 64 == 0 in storage chunks), 3 (other 3x3); -1: none
+inline int chain_kind(const ConvArgs& a) {
+  if (a.src1 || a.up0 || a.w2 || a.dw_w || a.shuffle || a.nchw || !a.src0) return -1;
+  if (a.k == 1 && a.s == 1) return 1;
+  if (a.k == 3) return a.Cin8 % 8 == 0 ? 4 : 3;
+  return -1;
+}
+
+template <int BM, int BN, int SPLIT, int KG, int NS, int SUB>
+hipError_t launch_chain(ConvArgs a0, ConvArgs a1, int* ctl, int cap, hipStream_t st) {
+  if ((4 / KG) % 2) return hipErrorInvalidValue;
+  ConvArgs* ops[2] = {&a0, &a1};
+  int items[2];
+  for (int i = 0; i < 2; ++i) {
+    ConvArgs& a = *ops[i];
+    const int tiles_m8 = ((a.M + BM - 1) / BM + 7) / 8 * 8;
+    a.tiles_n = (a.N + BN - 1) / BN;
+    a.fd_tn = ym_fdiv(a.tiles_n);
+    a.fd_cin8 = ym_fdiv(a.Cin8 > 0 ? a.Cin8 : 1);
+    a.tm_per_xcd = tiles_m8 / 8;
+    if (SPLIT > 1) {
+      const long tiles = (long)tiles_m8 * a.tiles_n;
+      if (tiles > a.cnt_cap || tiles * SPLIT * BM * BN * 4 > a.slab_cap || a.Kpad / DK < SPLIT) return hipErrorInvalidValue;
+    }
+    if (SUB > 1 && (a.Kpad / DK) % (SPLIT * SUB)) return hipErrorInvalidValue;
+    items[i] = tiles_m8 * a.tiles_n * SPLIT;
+  }
+  const int ka = chain_kind(a0), kb = chain_kind(a1);
+  if (ka != 4 || kb != 4) return hipErrorInvalidValue;  // (the prototype: 3x3 -> 3x3)
+  if (a1.src0 != a0.dst || a1.s0_coff != a0.d_coff || a1.s0_ctot != a0.d_ctot || a0.M != a1.M || a1.s != 1 ||
+      a0.N != a1.Cin8 * 8 / 2)
+    return hipErrorInvalidValue;
+  const int G = items[0] > items[1] ? items[0] : items[1];
+  const int tiles_m0 = (a0.M + BM - 1) / BM;
+  if (G > 256 || tiles_m0 + 2 > cap) return hipErrorInvalidValue;  // one workgroup per CU, all resident
+  ChainArgs c{};
+  c.op[0] = a0;
+  c.op[1] = a1;
+  c.ready = ctl;
+  c.done = ctl + cap - 2;
+  c.tmo = ctl + cap - 1;
+  c.halo = a1.k == 3 ? a1.Wo + 1 : 0;
+  c.tiles_m0 = tiles_m0;
+  c.ready_target = a0.tiles_n;
+  c.items0 = items[0];
+  c.items1 = items[1];
+  hipLaunchKernelGGL((conv_dma_chain<BM, BN, 4, 4, SPLIT, KG, NS, SUB>), dim3(G), dim3(256 * KG), 0, st, c);
+  return hipGetLastError();
+}
+
 }  // namespace
+
+// Two dependent x3 convs (op 1 reads op 0's output) as one persistent launch on LDS-DMA configuration i (ids as in
+// YM_DMA_CFGS; instantiated: 8, 13, 26).  ctl: `cap` zeroed ints (ready counters, done, give-up word), left zeroed.
+hipError_t ym_launch_conv_dma_chain(const ConvArgs& a0, const ConvArgs& a1, int i, int* ctl, int cap, hipStream_t st) {
+  if (!a0.x3 || !a1.x3 || a0.Kpad % DK || a1.Kpad % DK) return hipErrorInvalidValue;
+  if ((a0.N & 7) || (a1.N & 7) || (a0.d_ctot & 7) || (a0.d_coff & 7) || (a1.d_ctot & 3) || (a1.d_coff & 3))
+    return hipErrorInvalidValue;
+  const long lim = 0x7FFFFFF0L / 2;
+  if ((long)a0.N * a0.Kpad > lim || (long)a1.N * a1.Kpad > lim || a0.s0_elems > lim || a1.s0_elems > lim)
+    return hipErrorInvalidValue;
+  switch (i) {
+    case 8: return launch_chain<64, 64, 2, 2, 4, 2>(a0, a1, ctl, cap, st);
+    case 13: return launch_chain<64, 64, 2, 2, 3, 3>(a0, a1, ctl, cap, st);
+    case 26: return launch_chain<64, 64, 1, 2, 2, 2>(a0, a1, ctl, cap, st);
+  }
+  return hipErrorInvalidValue;
+}
 
 // A fused conv -> 1x1 pair (ConvArgs::w2, k2 == 1) on the LDS-DMA kernel with the second GEMM in its epilogue (x3
 // plans; i: a DMA configuration id, only YM_DMA_FUSE_CFGS are instantiated)

@@ -74,6 +74,7 @@ int fail(int code, const char* fmt, ...) {
 constexpr int32_t kMagic = 0x4C504D59;  // 'YMPL'
 constexpr int kHdr = 32, kBufRec = 8, kOpRec = 32, kNameLen = 48;
 constexpr int kSplitCounters = 16384;  // split-K tiles per conv launch (csrc/ym_conv_dma.hip)
+constexpr int kChainCtl = 4096;        // ready counters (+ done, give-up words) of the persistent chain kernel
 constexpr int kMaxLanes = 4;           // concurrent batch slices in one forward graph (<= GPU_MAX_HW_QUEUES)
 constexpr size_t kMaxGraphs = 16;      // captured forwards cached per context (the oldest is retired first)
 constexpr size_t kMiscBytes = 16384;  // ym_ctx::d_misc
@@ -202,7 +203,7 @@ struct ym_ctx {
   size_t arena_bytes = 0;
   std::vector<size_t> buf_off;
   size_t off_boxes = 0, off_scores = 0, off_cls = 0, off_keys = 0, off_counts = 0, off_ctl = 0, off_sboxes = 0,
-         off_sareas = 0, off_sup = 0, off_slab = 0, off_cnt = 0, slab_bytes = 0;
+         off_sareas = 0, off_sup = 0, off_slab = 0, off_cnt = 0, off_chain = 0, slab_bytes = 0;
   int A = 0, kstride = 0;
   int lvl_W[4] = {0}, lvl_off[4] = {0};
   hipStream_t cap_stream = nullptr;
@@ -343,6 +344,7 @@ int ensure_workspace(ym_ctx* c, int B, int H, int W) {
   c->slab_bytes = std::min<size_t>(std::max<size_t>(32u << 20, (size_t)nB << 22), 1u << 30);
   c->off_slab = off;   off = align_up(off + kMaxLanes * c->slab_bytes, 256);  // one slab region per lane
   c->off_cnt = off;    off = align_up(off + (size_t)kMaxLanes * kSplitCounters * 4, 256);
+  c->off_chain = off;  off = align_up(off + (size_t)kChainCtl * 4, 256);  // persistent chain kernel's counters
   c->arena_bytes = off;
   hipError_t e = hipMalloc(&c->d_arena, off);
   if (e != hipSuccess) {
@@ -665,7 +667,7 @@ int ym_num_conv_cfgs(int dtype) {  // public dtype codes (ym_model_desc): 1 f16,
 
 const char* ym_last_error(void) { return g_err.c_str(); }
 int ym_set_debug(int key, int value) {
-  if (key < YM_DBG_NMS || key > YM_DBG_DW_TILE) return fail(YM_EINVAL, "unknown debug key %d", key);
+  if (key < YM_DBG_NMS || key > YM_DBG_CHAIN_LAUNCHES) return fail(YM_EINVAL, "unknown debug key %d", key);
   return ym_debug_set(key, value);
 }
 
@@ -985,6 +987,32 @@ static void lane_split(const ym_infer_args* args, int B, int& L, int& Bl) {
   L = (B + Bl - 1) / Bl;
 }
 
+// YM_DBG_CHAIN = 1 (ym_set_debug, or YM_CHAIN=1 in the environment; verdict r5 item 1): op i and op i+1 as ONE persistent launch (csrc/ym_conv_dma.hip
+// conv_dma_chain) where both are x3 3x3 convs on the same LDS-DMA configuration, op i+1 reads op i's output and waits
+// for nothing else, and both run on the main stream (one chain kernel in flight at a time).  Returns 1 when launched.
+static int try_chain(ym_ctx* c, size_t i, int B, const float* d_in, const ym_infer_args* args, hipStream_t st,
+                     int& rc) {
+  rc = YM_OK;
+  if (ym_debug_get(YM_DBG_CHAIN) != 1 || c->dtype != YM_DT_X3 || i + 1 >= c->ops.size() || c->lane != 0) return 0;
+  const Op &o0 = c->ops[i], &o1 = c->ops[i + 1];
+  if (o0.r[0] != OP_CONV || o1.r[0] != OP_CONV || o0.r[30] || o1.r[30]) return 0;
+  if (c->nbr > 1 && (c->br_of[i] != 0 || c->br_of[i + 1] != 0 || !c->br_wait[i + 1].empty())) return 0;
+  const int cf0 = c->op_cfg((long)i, B), cf1 = c->op_cfg((long)i + 1, B);
+  const int dma = cf0 - 17;  // LDS-DMA ids follow the 17 first-generation configurations (csrc/ym_conv.hip)
+  if (cf0 != cf1 || (dma != 8 && dma != 13 && dma != 26)) return 0;
+  ConvArgs a0{}, a1{};
+  int f0 = 0, f1 = 0;
+  if ((rc = conv_args(c, o0, B, d_in, args->in_eps, a0, f0)) || (rc = conv_args(c, o1, B, d_in, args->in_eps, a1, f1)))
+    return 1;
+  if (f0 || f1 || a0.nchw) return 0;
+  const hipError_t e = ym_launch_conv_dma_chain(a0, a1, dma, reinterpret_cast<int*>(c->d_arena + c->off_chain),
+                                                kChainCtl, st);
+  if (e == hipErrorInvalidValue) return 0;  // shapes the chain kernel does not take: two launches
+  if (e != hipSuccess) rc = fail(YM_EHIP, "chain launch of %s + %s: %s", o0.name, o1.name, hipGetErrorString(e));
+  else ym_debug_add(YM_DBG_CHAIN_LAUNCHES, 1);
+  return 1;
+}
+
 // Launch one forward: the input statistics over the WHOLE batch (LoadTensor's /255 rule is a batch-wide max), then
 // every other op per lane on its image slice.  With fork/join events the lanes are parallel graph branches when
 // `st` is capturing; eagerly (no capture) they run on the lane streams concurrently as well.
@@ -1002,8 +1030,15 @@ static int launch_forward(ym_ctx* c, const float* d_in, int B, const ym_infer_ar
       const int s = c->br_of[i];
       for (int j : c->br_wait[i]) HIPCK(hipStreamWaitEvent(bs[s], c->op_ev[j], 0));
       c->lane = s;  // split-K slab / counter region of this stream
-      rc = launch_op(c, c->ops[i], B, d_in, args, d_dets, d_counts, bs[s]);
-      c->lane = 0;
+      if (try_chain(c, i, B, d_in, args, bs[s], rc)) {  // ops i and i + 1 in one launch
+        c->lane = 0;
+        if (rc) return rc;
+        if (c->br_rec[i]) HIPCK(hipEventRecord(c->op_ev[i], bs[s]));
+        ++i;
+      } else {
+        rc = launch_op(c, c->ops[i], B, d_in, args, d_dets, d_counts, bs[s]);
+        c->lane = 0;
+      }
       if (rc) return rc;
       if (c->br_rec[i]) HIPCK(hipEventRecord(c->op_ev[i], bs[s]));
     }
@@ -1025,8 +1060,13 @@ static int launch_forward(ym_ctx* c, const float* d_in, int B, const ym_infer_ar
     c->lane_img0 = l * Bl;
     const int nb = B - l * Bl < Bl ? B - l * Bl : Bl;
     for (size_t i = o; i < c->ops.size(); ++i) {
-      rc = launch_op(c, c->ops[i], nb, d_in + c->lane_img0 * in_img, args, d_dets + c->lane_img0 * det_img,
-                     d_counts + c->lane_img0, ls);
+      if (L == 1 && try_chain(c, i, nb, d_in, args, ls, rc)) {
+        ++i;
+        if (!rc) continue;
+      } else {
+        rc = launch_op(c, c->ops[i], nb, d_in + c->lane_img0 * in_img, args, d_dets + c->lane_img0 * det_img,
+                       d_counts + c->lane_img0, ls);
+      }
       if (rc) {
         c->lane = c->lane_img0 = 0;
         return rc;
