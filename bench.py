@@ -46,8 +46,8 @@ import torch  # noqa: E402
 import torch.distributed as dist  # noqa: E402
 
 METRIC = "images/sec @640×640 (1/2/4/8 MI355X) + mAP50-95 vs CPU ref"
-# dense MFMA peaks (MI355X_MICROARCH.md; i8 = TOP/s; f8 = the f16 peak: the fp8 plan multiplies its e4m3 codes,
-# widened exactly to fp16, on the f16 MFMA — csrc/ym_quant.h says why; the non-scaled fp8 MFMA has the same rate)
+# dense MFMA peaks (MI355X_MICROARCH.md; i8 = TOP/s; f8 = 2.5 PF: the fp8 plan runs v_mfma_f32_32x32x16_fp8_fp8, the
+# non-scaled fp8 form, at the bf16/f16 rate — the 5 PF figure is the block-scaled f8f6f4 form's)
 # x3 (fp32 storage, split-f16 MFMA): the algorithmic FLOPs against the f16 peak, although each K chunk issues three
 # f16 MFMAs (so its MFMA-issue ceiling is a third of that)
 PEAK_TFLOPS = {"f16": 2500.0, "f32": 157.3, "i8": 5000.0, "f8": 2500.0, "x3": 2500.0}
@@ -176,7 +176,7 @@ def conv_roofline(model, x, dtype, workload, reps=20):
         "traffic_note": (f"HBM-side bytes per forward of all conv launches (PMC FETCH_SIZE x2 + WRITE_SIZE, {tsrc}); "
                          f"algorithmic bytes per forward {int(by)}") if traffic else "no PMC summary for this workload",
         "kernel": "conv implicit GEMM (%s): all %d conv launches of one lane's forward (%d images), aggregated%s"
-                  % ({"i8": "conv_i8, v_mfma_i32_32x32x32_i8", "f8": "conv_i8<fp8>, e4m3 widened to f16, v_mfma_f32_32x32x16_f16",
+                  % ({"i8": "conv_i8, v_mfma_i32_32x32x32_i8", "f8": "conv_i8<fp8>, v_mfma_f32_32x32x16_fp8_fp8 (accumulation restated in oracle/quant.py)",
                       "x3": "conv_igemm/conv_lds<x3>, 3x v_mfma_f32_32x32x16_f16 per K chunk"}.get(
                       dtype, "conv_stream/conv_small/conv_dma/conv_lds/conv_bneck/conv_halo/conv_igemm"), len(conv),
                      Bl, "; int8 ops counted as FLOPs" if dtype == "i8" else ""),
@@ -255,12 +255,12 @@ def cpu_baseline(scale, task, x_gpu_dets, xs, seconds, qparams=None):
     B=1 and at B=8 (half the time budget each); also mAP of the GPU dets against the oracle's dets (and, for int8,
     against the float oracle's: the quantisation loss)."""
     from oracle.predict import OracleModel
+    from oracle.quant import Int8OracleModel
     from yolomi.metrics import evaluate
     from yolomi.synth import synth_weights
     nthreads = int(os.environ.get("OMP_NUM_THREADS", 0)) or len(os.sched_getaffinity(0))
     torch.set_num_threads(nthreads)
     if qparams is not None:
-        from oracle.quant import Int8OracleModel
         om = Int8OracleModel(scale, task, synth_weights(scale, task, 0), qparams)
     else:
         om = OracleModel(scale, task, synth_weights(scale, task, 0))
@@ -302,6 +302,14 @@ def cpu_baseline(scale, task, x_gpu_dets, xs, seconds, qparams=None):
         fl = OracleModel(scale, task, synth_weights(scale, task, 0)).predict(xs.cpu())
         mf = evaluate(x_gpu_dets, [r["boxes"].numpy() for r in fl])
         acc["vs_fp32_oracle"] = {"map50_95": round(mf["map"], 4), "map50": round(mf["map50"], 4)}
+    if fp8:  # the oracle the fp8 plan is bit-exact against: the restated fp8 MFMA accumulation (slow: image 0 only)
+        mm = Int8OracleModel(scale, task, synth_weights(scale, task, 0), qparams, accum="mfma")
+        r0 = mm.predict(xs[:1].cpu())[0]["boxes"].numpy()
+        m0 = evaluate(x_gpu_dets[:1], [r0])
+        acc["vs_fp8_mfma_oracle_image0"] = {"map50_95": round(m0["map"], 4), "dets_oracle": int(len(r0)),
+                                            "dets_gpu": int(len(x_gpu_dets[0])),
+                                            "note": "oracle/quant.py accum='mfma' (the fp8 MFMA's accumulation restated); "
+                                                    "map50_95 / gt above: the exact-sum fp8 oracle"}
     return base, acc, gts, exact
 
 

@@ -162,6 +162,32 @@ def main_f8():
         print(name, [len(x) for x in d["dets"]])
 
 
+# the fp8 plan's own accumulation (oracle/quant.py accum="mfma": the restated fp8 MFMA chain of conv_i8), with
+# det_n_f8's qparams, on 320x320 inputs (the emulated convs take ~9 s per 320² image on 8 threads)
+F8M_FIXTURES = {
+    "det_n_f8m_320": ("det_n_f8", (5501, 5502), 320),
+}
+
+
+def main_f8m():
+    for name, (base, seeds, S) in F8M_FIXTURES.items():
+        b = json.load(open(os.path.join(HERE, f"{base}.json")))
+        qp = Q.qparams_from_json(b["qparams"])
+        m = Q.Int8OracleModel(b["scale"], "detect", synth_weights(b["scale"], "detect", 0), qp, accum="mfma")
+        x = make_input("uniform", seeds, S)
+        im, y, ex = m.raw(x)
+        B = x.shape[0]
+        head = torch.cat([f.reshape(B, 144, -1) for f in ex["feats"]], 2).transpose(1, 2)
+        dets = m.predict(x, conf=b["conf"], iou=b["iou"])
+        d = {"scale": b["scale"], "task": "detect", "weights_seed": 0, "backend": "fp8", "accum": "mfma",
+             "qparams_from": base, "input": {"kind": "uniform", "seeds": list(seeds), "size": S}, "conf": b["conf"],
+             "iou": b["iou"], "max_det": 300, "qparams": b["qparams"],
+             "layers": {f"L{i}": layer_stats(ex["stored"][i].q.permute(0, 2, 3, 1)) for i in LAYERS},
+             "head": layer_stats(head), "dets": [d["boxes"].tolist() for d in dets]}
+        json.dump(d, open(os.path.join(HERE, f"{name}.json"), "w"))
+        print(name, [len(x) for x in d["dets"]])
+
+
 def main_seg():
     d = seg_fixture("s", (6001, 6002, 6003, 6004), 640)
     json.dump(d, open(os.path.join(HERE, "seg_s_uniform.json"), "w"))
@@ -192,11 +218,12 @@ def main():
 
 
 if __name__ == "__main__":
-    if len(sys.argv) > 1 and sys.argv[1] in ("i8", "seg", "f8"):
+    if len(sys.argv) > 1 and sys.argv[1] in ("i8", "seg", "f8", "f8m"):
         torch.set_num_threads(min(8, os.cpu_count() or 1))
-        {"i8": main_i8, "seg": main_seg, "f8": main_f8}[sys.argv[1]]()
+        {"i8": main_i8, "seg": main_seg, "f8": main_f8, "f8m": main_f8m}[sys.argv[1]]()
     else:
         main()
         main_seg()
         main_i8()
         main_f8()
+        main_f8m()

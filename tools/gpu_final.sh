@@ -27,6 +27,7 @@ for step in ${STEPS:-smoke suite bench_s bench_n bench_seg bench_ptq optable pro
                run bench_n_f8 400 python -u bench.py --model n --dtype f8
                run bench_n_f16 400 python -u bench.py --model n --dtype f16 --no-cpu ;;
     optable) run optable 200 python -u tools/op_table.py --model s --dtype x3 ;;
+    files) run files 900 python -u -X faulthandler -m pytest $TEST_FILES -q -p no:cacheprovider --timeout 300 --timeout-method thread ;;
     ktests) run ktests 400 python -u -X faulthandler -m pytest tests/test_gpu_kernels.py -q -p no:cacheprovider --timeout 200 --timeout-method thread ${KTESTS_K:+-k "$KTESTS_K"} ;;
     chain) for v in 0 1 0 1; do  # same-box A/B of the persistent chain kernel
              YM_CHAIN=$v run "chain_ab_$v" 300 python -u bench.py --no-cpu --no-f16 --no-roofline --steps 400; mv "$OUT/chain_ab_$v.log" "$OUT/chain_ab_${v}_$((++n))"; done

@@ -582,6 +582,20 @@ __global__ __launch_bounds__(256) void requant_copy(const ReqArgs a) {
 // ids [0, kNumCfg): conv_i8 above; then the streaming / small-M int8 kernels (csrc/ym_conv_i8_stream.hip)
 int ym_conv_i8_num_cfgs() { return kNumCfg + ym_conv_i8_stream_num_cfgs(); }
 
+// fp8 plans: one K chain per output (WK = 1), so the oracle's restated fp8 MFMA accumulation (oracle/quant.py
+// mfma_f8_conv) follows the kernel's order; the heuristic's choice among those configurations
+int choose_cfg_f8(const ConvArgs& a) {
+  const long M = a.M, N = a.N;
+  auto waves = [&](int id) {
+    const Cfg& c = kCfgs[id];
+    const long BM = c.wm * c.wtm * 32, BN = c.wn * c.wtn * 32;
+    return ((M + BM - 1) / BM) * ((N + BN - 1) / BN) * c.wm * c.wn;
+  };
+  if (N <= 32) return waves(2) >= 1024 ? 2 : 9;
+  if (N <= 64) return waves(1) >= 1024 ? 1 : (waves(5) >= 1024 ? 5 : 9);
+  return waves(0) >= 1024 ? 0 : 10;
+}
+
 hipError_t ym_launch_conv_i8(const ConvArgs& a, int cfg, hipStream_t st, bool strict, bool f8) {
   int kind;
   if (a.k == 1 && a.s == 1 && !a.src1 && !a.up0) kind = 1;
@@ -589,12 +603,16 @@ hipError_t ym_launch_conv_i8(const ConvArgs& a, int cfg, hipStream_t st, bool st
   else return hipErrorInvalidValue;
   if (a.Kpad % KSTEP || !a.q || !a.sasw || !a.biasi || (a.N & 3) || (a.s0_ctot & 15) || (a.s0_coff & 15))
     return hipErrorInvalidValue;
+  if (f8 && (cfg >= kNumCfg || (cfg >= 0 && kCfgs[cfg].wk != 1))) {  // fp8: conv_i8 with one K chain only
+    if (strict) return hipErrorInvalidValue;
+    cfg = -1;
+  }
   if (cfg >= kNumCfg) {
     const hipError_t e = ym_launch_conv_i8_stream(a, cfg - kNumCfg, st, f8);
     if (e != hipErrorInvalidValue || strict) return e;
     cfg = -1;  // a pinned table entry that does not apply: the heuristic
   }
-  return launch_id(cfg >= 0 ? cfg : choose_cfg(a), a, kind, st, f8);
+  return launch_id(cfg >= 0 ? cfg : (f8 ? choose_cfg_f8(a) : choose_cfg(a)), a, kind, st, f8);
 }
 
 hipError_t ym_launch_dwconv_i8(const DwArgs& a, hipStream_t st, bool f8) {
