@@ -40,6 +40,11 @@ for step in ${STEPS:-smoke suite bench_s bench_n bench_seg bench_ptq optable pro
         echo "[sq] rc=$rc $(date +%T)" | tee -a "$OUT/steps.log"
         if [ $rc -ne 0 ]; then exit $rc; fi ;;
     conf) run conf_timing 300 python -u tools/conf_timing.py s 8 ;;
+    profconf) (cd /tmp && CONFS=0.001 timeout -k 10 300 rocprofv3 --kernel-trace --stats --output-format csv \
+             -d "$GRAFT_REPO_ROOT/$OUT/prof_conf" -o run -- python3 "$GRAFT_REPO_ROOT/tools/conf_timing.py" s 8 \
+             > "$GRAFT_REPO_ROOT/$OUT/prof_conf.log" 2>&1); rc=$?
+          echo "[profconf] rc=$rc $(date +%T)" | tee -a "$OUT/steps.log"
+          if [ $rc -ne 0 ]; then exit $rc; fi ;;
     prof) (cd /tmp && timeout -k 10 400 rocprofv3 --kernel-trace --stats --output-format csv \
              -d "$GRAFT_REPO_ROOT/$OUT/prof" -o run -- python3 "$GRAFT_REPO_ROOT/bench.py" --steps 50 \
              --warmup 10 --no-cpu --no-f16 > "$GRAFT_REPO_ROOT/$OUT/prof_bench.log" 2>&1); rc=$?

@@ -437,6 +437,9 @@ struct NmsArgs {
   double iou;
   int dbg;  // YM_NMS_DBG: 1-7 phase ablations of the bit-matrix path, 10 the blocked path's sort alone (timing only);
             // 9 disables the blocked path
+  // multi-workgroup presort (low conf: ym_launch_nms_presort before nms_image): chunk-sorted keys, and 1 when the
+  // keys arrive sorted for the blocked path
+  unsigned long long* keys2; int presorted;
 };
 
 struct LetterboxArgs {
@@ -478,6 +481,7 @@ hipError_t ym_launch_prep(int dtype, const PrepArgs& a, int* counts, int B, hipS
 hipError_t ym_launch_input_max(const float* x, long n, float* ctl, float* out, hipStream_t st);
 hipError_t ym_launch_decode(const DecodeArgs& a, hipStream_t st);
 hipError_t ym_launch_nms(const NmsArgs& a, hipStream_t st);
+hipError_t ym_launch_nms_presort(const NmsArgs& a, hipStream_t st);  // ym_misc.hip: keys sorted by 8 WGs per image
 hipError_t ym_launch_conv_dma_chain(const ConvArgs& a0, const ConvArgs& a1, int dma_cfg, int* ctl, int cap,
                                     hipStream_t st);  // csrc/ym_conv_dma.hip: two dependent x3 convs, one launch
 int ym_debug_get(int key);  // ym_set_debug switches (ym_misc.hip)

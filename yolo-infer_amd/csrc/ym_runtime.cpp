@@ -74,7 +74,8 @@ int fail(int code, const char* fmt, ...) {
 constexpr int32_t kMagic = 0x4C504D59;  // 'YMPL'
 constexpr int kHdr = 32, kBufRec = 8, kOpRec = 32, kNameLen = 48;
 constexpr int kSplitCounters = 16384;  // split-K tiles per conv launch (csrc/ym_conv_dma.hip)
-constexpr int kChainCtl = 4096;        // ready counters (+ done, give-up words) of the persistent chain kernel
+constexpr int kChainCtl = 4096;
+constexpr float kPresortConf = 0.1f;  // NMS keys presorted over several workgroups below this conf (ym_misc.hip)        // ready counters (+ done, give-up words) of the persistent chain kernel
 constexpr int kMaxLanes = 4;           // concurrent batch slices in one forward graph (<= GPU_MAX_HW_QUEUES)
 constexpr size_t kMaxGraphs = 16;      // captured forwards cached per context (the oldest is retired first)
 constexpr size_t kMiscBytes = 16384;  // ym_ctx::d_misc
@@ -202,7 +203,7 @@ struct ym_ctx {
   char* d_arena = nullptr;
   size_t arena_bytes = 0;
   std::vector<size_t> buf_off;
-  size_t off_boxes = 0, off_scores = 0, off_cls = 0, off_keys = 0, off_counts = 0, off_ctl = 0, off_sboxes = 0,
+  size_t off_boxes = 0, off_scores = 0, off_cls = 0, off_keys = 0, off_keys2 = 0, off_counts = 0, off_ctl = 0, off_sboxes = 0,
          off_sareas = 0, off_sup = 0, off_slab = 0, off_cnt = 0, off_chain = 0, slab_bytes = 0;
   int A = 0, kstride = 0;
   int lvl_W[4] = {0}, lvl_off[4] = {0};
@@ -335,6 +336,7 @@ int ensure_workspace(ym_ctx* c, int B, int H, int W) {
   c->off_scores = off; off = align_up(off + BA * 4, 256);
   c->off_cls = off;    off = align_up(off + BA * 4, 256);
   c->off_keys = off;   off = align_up(off + (size_t)nB * c->kstride * 8, 256);
+  c->off_keys2 = off;  off = align_up(off + (size_t)nB * c->kstride * 8, 256);  // NMS presort chunks
   c->off_counts = off; off = align_up(off + (size_t)nB * 4, 256);
   c->off_ctl = off;    off = align_up(off + YM_CTL_BYTES, 256);
   c->off_sboxes = off; off = align_up(off + BA * 16, 256);
@@ -630,6 +632,14 @@ int launch_op(ym_ctx* c, const Op& op, int B, const float* d_in, const ym_infer_
       a.agnostic = args->agnostic; a.B = B; a.nc = c->nc;
       a.max_wh = args->max_wh; a.img_h = (float)c->cH; a.img_w = (float)c->cW;
       a.iou = args->iou;
+      // low conf (the validator's 0.001): thousands of candidates per image; sort their keys over several
+      // workgroups per image first (conf is part of the graph key: the predict default 0.25 never launches these)
+      if (args->conf < kPresortConf && c->kstride >= 16384) {
+        a.keys2 = c->scratch<unsigned long long>(c->off_keys2, (size_t)c->kstride * 8);
+        a.presorted = 1;
+        e = ym_launch_nms_presort(a, st);
+        if (e != hipSuccess) break;
+      }
       e = ym_launch_nms(a, st);
       break;
     }
