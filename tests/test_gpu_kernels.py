@@ -275,3 +275,42 @@ def test_chain_kernel_bitwise_equals_two_launches():
         assert torch.equal(c0, c)
         for b in range(8):
             assert torch.equal(d0[b, :int(c0[b])], d[b, :int(c0[b])])
+
+
+def test_stem_fuse_matches_the_split_launches():
+    """DESIGN.md §4.5 (verdict r5 item 5): with YM_DBG_STEMFUSE = 1 the x3 stem, model.1 and model.2.cv1 of yolo11s
+    run as ONE launch (csrc/ym_stem_fused.hip) that never stores the stem's 320x320 output.  Its stem arithmetic is
+    stem_mfma's; model.1 / cv1 sum their K in another order than the split launches, so the pair's output agrees to
+    fp32 rounding (max |diff| <= 1e-5 of its max), every later layer to 1e-4, and the detections match the split
+    launches' at 5e-4 px / 5e-5 score (the x3 plan's float64 bar), eager and graph-replayed."""
+    from core.model import YOLO11Model
+    from tests.matching import MatchReport, match_image
+    from yolomi import lib as L
+    m = YOLO11Model(task="detect", size="s", device="cuda:0", dtype="x3", verbose=False)
+    eng = m.model.engine
+    x = synthetic_batch(8, 640, 7, DEV)
+    d0, c0 = (t.clone() for t in eng.run(x, conf=0.05, use_graph=False))
+    pair = next(op for op in eng.graph.ops if op.name.startswith("model.1+"))
+    stem_out = eng.graph.ops[eng.graph.ops.index(pair) - 1].args["dst"].buf.id
+    ids = [b for b in range(len(eng.graph.buffers)) if b not in (eng.graph.input.id, stem_out)]
+    ref = {b: eng.read_buffer(b, 8) for b in ids}
+    prev = L.set_debug(L.DBG_STEMFUSE, 1)
+    try:
+        d1, c1 = (t.clone() for t in eng.run(x, conf=0.05, use_graph=False))
+        got = {b: eng.read_buffer(b, 8) for b in ids}
+        xg = x.clone()  # a new graph key: captured with the fused kernel
+        for _ in range(2):
+            d2, c2 = (t.clone() for t in eng.run(xg, conf=0.05))
+        torch.cuda.synchronize()
+    finally:
+        L.set_debug(L.DBG_STEMFUSE, prev)
+    pd = pair.args["dst"].buf.id
+    for b in ids:
+        scale = float(ref[b].abs().max()) or 1.0
+        err = float((got[b] - ref[b]).abs().max()) / scale
+        assert err <= (1e-5 if b == pd else 1e-4), (eng.graph.buffers[b].name, err)
+    for d, c in ((d1, c1), (d2, c2)):
+        rep = MatchReport()
+        for b in range(8):
+            match_image(d0[b, :int(c0[b])].cpu().numpy(), d[b, :int(c[b])].cpu().numpy(), 0.05, 0.7, 5e-4, 5e-5, rep=rep)
+        assert rep.ok and rep.matched > 0, (str(rep), rep.failures[:3])

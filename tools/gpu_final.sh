@@ -29,13 +29,17 @@ for step in ${STEPS:-smoke suite bench_s bench_n bench_seg bench_ptq optable pro
     optable) run optable 200 python -u tools/op_table.py --model s --dtype x3 ;;
     files) run files 900 python -u -X faulthandler -m pytest $TEST_FILES -q -p no:cacheprovider --timeout 300 --timeout-method thread ;;
     ktests) run ktests 400 python -u -X faulthandler -m pytest tests/test_gpu_kernels.py -q -p no:cacheprovider --timeout 200 --timeout-method thread ${KTESTS_K:+-k "$KTESTS_K"} ;;
-    chain) for v in 0 1 0 1; do  # same-box A/B of the persistent chain kernel
-             YM_CHAIN=$v run "chain_ab_$v" 300 python -u bench.py --no-cpu --no-f16 --no-roofline --steps 400; mv "$OUT/chain_ab_$v.log" "$OUT/chain_ab_${v}_$((++n))"; done
-           (cd /tmp && YM_CHAIN=1 timeout -k 10 400 rocprofv3 --kernel-trace --stats --output-format csv \
-             -d "$GRAFT_REPO_ROOT/$OUT/prof_chain" -o run -- python3 "$GRAFT_REPO_ROOT/bench.py" --steps 50 \
-             --warmup 10 --no-cpu --no-f16 --no-roofline > "$GRAFT_REPO_ROOT/$OUT/prof_chain.log" 2>&1); rc=$?
-           echo "[prof_chain] rc=$rc $(date +%T)" | tee -a "$OUT/steps.log"
-           if [ $rc -ne 0 ]; then exit $rc; fi ;;
+    ab) for v in 0 1 0 1; do  # same-box A/B of an environment switch AB_VAR (e.g. YM_CHAIN, YM_STEMFUSE)
+          export "$AB_VAR=$v"
+          run "ab_${AB_VAR}_$v" 300 python -u bench.py --no-cpu --no-f16 --no-roofline --steps 400
+          mv "$OUT/ab_${AB_VAR}_$v.log" "$OUT/ab_${AB_VAR}_${v}_$((++n))"; done
+        export "$AB_VAR=1"
+        (cd /tmp && timeout -k 10 400 rocprofv3 --kernel-trace --stats --output-format csv \
+          -d "$GRAFT_REPO_ROOT/$OUT/prof_ab" -o run -- python3 "$GRAFT_REPO_ROOT/bench.py" --steps 50 \
+          --warmup 10 --no-cpu --no-f16 --no-roofline > "$GRAFT_REPO_ROOT/$OUT/prof_ab.log" 2>&1); rc=$?
+        unset "$AB_VAR"
+        echo "[prof_ab] rc=$rc $(date +%T)" | tee -a "$OUT/steps.log"
+        if [ $rc -ne 0 ]; then exit $rc; fi ;;
     sq) bash tools/gpu_sq_table.sh "${TAG:-final}" --model s --dtype x3 > "$OUT/sq.log" 2>&1; rc=$?
         echo "[sq] rc=$rc $(date +%T)" | tee -a "$OUT/steps.log"
         if [ $rc -ne 0 ]; then exit $rc; fi ;;

@@ -484,6 +484,7 @@ hipError_t ym_launch_nms(const NmsArgs& a, hipStream_t st);
 hipError_t ym_launch_nms_presort(const NmsArgs& a, hipStream_t st);  // ym_misc.hip: keys sorted by 8 WGs per image
 hipError_t ym_launch_conv_dma_chain(const ConvArgs& a0, const ConvArgs& a1, int dma_cfg, int* ctl, int cap,
                                     hipStream_t st);  // csrc/ym_conv_dma.hip: two dependent x3 convs, one launch
+hipError_t ym_launch_stem_down_x3(const ConvArgs& s, const ConvArgs& p, hipStream_t st);  // ym_stem_fused.hip
 int ym_debug_get(int key);  // ym_set_debug switches (ym_misc.hip)
 int ym_debug_set(int key, int value);
 void ym_debug_add(int key, int d);

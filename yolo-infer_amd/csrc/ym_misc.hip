@@ -1715,10 +1715,11 @@ hipError_t ym_launch_input_max(const float* x, long n, float* ctl, float* out, h
 // against setenv and costs time on every eager forward)
 namespace {
 std::atomic<int>* dbg_slots() {
-  static std::atomic<int> v[6] = {};
+  static std::atomic<int> v[7] = {};
   static const bool init = [] {
-    const char* names[5] = {nullptr, "YM_NMS_DBG", "YM_DW_MODE", "YM_DW_TILE", "YM_CHAIN"};
-    for (int k = 1; k < 5; ++k) {
+    const char* names[7] = {nullptr, "YM_NMS_DBG", "YM_DW_MODE", "YM_DW_TILE", "YM_CHAIN", nullptr, "YM_STEMFUSE"};
+    for (int k = 1; k < 7; ++k) {
+      if (!names[k]) continue;
       const char* e = getenv(names[k]);
       v[k].store(e ? atoi(e) : 0);
     }
@@ -1729,13 +1730,13 @@ std::atomic<int>* dbg_slots() {
 }
 }  // namespace
 
-int ym_debug_get(int key) { return key > 0 && key < 6 ? dbg_slots()[key].load(std::memory_order_relaxed) : 0; }
+int ym_debug_get(int key) { return key > 0 && key < 7 ? dbg_slots()[key].load(std::memory_order_relaxed) : 0; }
 int ym_debug_set(int key, int value) {
-  if (key <= 0 || key >= 6) return -1;
+  if (key <= 0 || key >= 7) return -1;
   return dbg_slots()[key].exchange(value);
 }
 void ym_debug_add(int key, int d) {
-  if (key > 0 && key < 6) dbg_slots()[key].fetch_add(d);
+  if (key > 0 && key < 7) dbg_slots()[key].fetch_add(d);
 }
 
 hipError_t ym_launch_dwconv(int dtype, const DwArgs& a, hipStream_t st) {

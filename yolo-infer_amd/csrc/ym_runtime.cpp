@@ -677,7 +677,7 @@ int ym_num_conv_cfgs(int dtype) {  // public dtype codes (ym_model_desc): 1 f16,
 
 const char* ym_last_error(void) { return g_err.c_str(); }
 int ym_set_debug(int key, int value) {
-  if (key < YM_DBG_NMS || key > YM_DBG_CHAIN_LAUNCHES) return fail(YM_EINVAL, "unknown debug key %d", key);
+  if (key < YM_DBG_NMS || key > YM_DBG_STEMFUSE) return fail(YM_EINVAL, "unknown debug key %d", key);
   return ym_debug_set(key, value);
 }
 
@@ -1023,6 +1023,42 @@ static int try_chain(ym_ctx* c, size_t i, int B, const float* d_in, const ym_inf
   return 1;
 }
 
+// YM_DBG_STEMFUSE = 1 (verdict r5 item 5): the x3 stem (op i) and the fused 3x3 s2 -> 1x1 pair that
+// reads its output (op i + 1: model.1 -> model.2.cv1) as ONE launch (csrc/ym_stem_fused.hip): the stem's output is
+// never stored.  Only where nothing else reads that output and op i + 1 waits for nothing else.  Returns 1 when
+// launched.
+static int try_stem_fuse(ym_ctx* c, size_t i, int B, const float* d_in, const ym_infer_args* args, hipStream_t st,
+                         int& rc) {
+  rc = YM_OK;
+  if (ym_debug_get(YM_DBG_STEMFUSE) != 1 || c->dtype != YM_DT_X3 || i + 1 >= c->ops.size()) return 0;
+  const Op &o0 = c->ops[i], &o1 = c->ops[i + 1];
+  if (o0.r[0] != OP_CONV || o1.r[0] != OP_CONV || o0.r[6] != c->input_buf || !o1.r[30] || o1.r[6] != o0.r[13])
+    return 0;
+  if (c->nbr > 1 && (c->br_of[i] != c->br_of[i + 1] || !c->br_wait[i + 1].empty())) return 0;
+  const int sb = o0.r[13];
+  for (size_t j = 0; j < c->ops.size(); ++j) {  // the stem's output: op i + 1 must be its only reader
+    if (j == i + 1) continue;
+    const int32_t* r = c->ops[j].r;
+    bool reads = false;
+    switch (r[0]) {
+      case OP_CONV: reads = r[6] == sb || r[10] == sb || r[17] == sb; break;
+      case OP_DW: case OP_ATTN: case OP_REQ: reads = r[6] == sb; break;
+      case OP_SPPF: reads = r[13] == sb; break;
+      default: break;
+    }
+    if (reads) return 0;
+  }
+  ConvArgs a0{}, a1{};
+  int f0 = 0, f1 = 0;
+  if ((rc = conv_args(c, o0, B, d_in, args->in_eps, a0, f0)) || (rc = conv_args(c, o1, B, d_in, args->in_eps, a1, f1)))
+    return 1;
+  if (f0 || f1) return 0;
+  const hipError_t e = ym_launch_stem_down_x3(a0, a1, st);
+  if (e == hipErrorInvalidValue) return 0;
+  if (e != hipSuccess) rc = fail(YM_EHIP, "fused stem launch of %s + %s: %s", o0.name, o1.name, hipGetErrorString(e));
+  return 1;
+}
+
 // Launch one forward: the input statistics over the WHOLE batch (LoadTensor's /255 rule is a batch-wide max), then
 // every other op per lane on its image slice.  With fork/join events the lanes are parallel graph branches when
 // `st` is capturing; eagerly (no capture) they run on the lane streams concurrently as well.
@@ -1040,7 +1076,7 @@ static int launch_forward(ym_ctx* c, const float* d_in, int B, const ym_infer_ar
       const int s = c->br_of[i];
       for (int j : c->br_wait[i]) HIPCK(hipStreamWaitEvent(bs[s], c->op_ev[j], 0));
       c->lane = s;  // split-K slab / counter region of this stream
-      if (try_chain(c, i, B, d_in, args, bs[s], rc)) {  // ops i and i + 1 in one launch
+      if (try_stem_fuse(c, i, B, d_in, args, bs[s], rc) || try_chain(c, i, B, d_in, args, bs[s], rc)) {  // ops i, i + 1
         c->lane = 0;
         if (rc) return rc;
         if (c->br_rec[i]) HIPCK(hipEventRecord(c->op_ev[i], bs[s]));
@@ -1070,7 +1106,7 @@ static int launch_forward(ym_ctx* c, const float* d_in, int B, const ym_infer_ar
     c->lane_img0 = l * Bl;
     const int nb = B - l * Bl < Bl ? B - l * Bl : Bl;
     for (size_t i = o; i < c->ops.size(); ++i) {
-      if (L == 1 && try_chain(c, i, nb, d_in, args, ls, rc)) {
+      if (L == 1 && (try_stem_fuse(c, i, nb, d_in, args, ls, rc) || try_chain(c, i, nb, d_in, args, ls, rc))) {
         ++i;
         if (!rc) continue;
       } else {
