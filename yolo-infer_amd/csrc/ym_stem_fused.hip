@@ -130,9 +130,24 @@ __global__ __launch_bounds__(256) void stem_down_x3(const StemFuseArgs A) {
       wf[t][j] = 8 * kg + j < 27 ? (f16)wraw[t][j] : (f16)0.f;
       wfl[t][j] = 8 * kg + j < 27 ? (f16)(wraw[t][j] - (float)wf[t][j]) : (f16)0.f;
     }
-  // model.1 / cv1 epilogue operands early (their latency hides behind phases A-C)
+  // model.1 / cv1 epilogue operands and weight fragments early (their latency hides behind phases A and B): all of
+  // cv1's (4 steps) and model.1's first WPF steps, then a ring WPF steps ahead inside the K loop
   const int l32 = lane & 31, h = lane >> 5;
   const int wm = wave & 1, wn = wave >> 1;  // this wave's block: output row wm (32 pixels), channels 32 wn .. + 31
+  const f16* W1 = static_cast<const f16*>(p.w) + (size_t)(32 * wn + l32) * p.Kpad;    // this lane's weight rows
+  const f16* W2 = static_cast<const f16*>(p.w2) + (size_t)(32 * wn + l32) * p.Kpad2;
+  constexpr int KST1 = 9 * XCH / 2, KST2 = N1 / 16, WPF = 6;
+  h8 w1h[WPF], w1l[WPF], w2h[KST2], w2l[KST2];
+#pragma unroll
+  for (int t = 0; t < WPF; ++t) {
+    w1h[t] = ym_gld<h8>(W1 + 16 * (2 * t + h));
+    w1l[t] = ym_gld<h8>(W1 + 16 * (2 * t + h) + 8);
+  }
+#pragma unroll
+  for (int t = 0; t < KST2; ++t) {
+    w2h[t] = ym_gld<h8>(W2 + 16 * (2 * t + h));
+    w2l[t] = ym_gld<h8>(W2 + 16 * (2 * t + h) + 8);
+  }
   f32x4 b1[4], b2[4];
 #pragma unroll
   for (int q = 0; q < 4; ++q) {
@@ -182,19 +197,22 @@ __global__ __launch_bounds__(256) void stem_down_x3(const StemFuseArgs A) {
   __syncthreads();
 
   // ---- C: model.1 (3x3 s2 over the stem image), this wave's 32 x 32 block
-  const f16* W1 = static_cast<const f16*>(p.w) + (size_t)(32 * wn + l32) * p.Kpad;  // this lane's weight row
   f32x16 acc;
 #pragma unroll
   for (int r = 0; r < 16; ++r) acc[r] = 0.f;
-#pragma unroll 6
-  for (int t = 0; t < 9 * XCH / 2; ++t) {
+#pragma unroll
+  for (int t = 0; t < KST1; ++t) {
     const int J = 2 * t + h;  // this lane half's logical 8-channel chunk: (tap, channel chunk)
     const int tap = J / XCH, cj = J - tap * XCH;
     const int ky = tap / 3, kx = tap - ky * 3;
     const int xp = xslot(2 * wm + ky, 2 * l32 + kx);
     const int byte = xp * XPB + ((cj ^ ((xp >> 2) & (XCH - 1))) << 4);
     const h8 xh = *reinterpret_cast<const h8*>(X + byte), xl = *reinterpret_cast<const h8*>(X + XPL + byte);
-    const h8 wh = ym_gld<h8>(W1 + 16 * J), wl = ym_gld<h8>(W1 + 16 * J + 8);
+    const h8 wh = w1h[t % WPF], wl = w1l[t % WPF];
+    if (t + WPF < KST1) {  // refill the ring slot WPF steps ahead
+      w1h[t % WPF] = ym_gld<h8>(W1 + 16 * (J + 2 * WPF));
+      w1l[t % WPF] = ym_gld<h8>(W1 + 16 * (J + 2 * WPF) + 8);
+    }
     acc = __builtin_amdgcn_mfma_f32_32x32x16_f16(wh, xh, acc, 0, 0, 0);
     acc = __builtin_amdgcn_mfma_f32_32x32x16_f16(wh, xl, acc, 0, 0, 0);
     acc = __builtin_amdgcn_mfma_f32_32x32x16_f16(wl, xh, acc, 0, 0, 0);
@@ -220,16 +238,15 @@ __global__ __launch_bounds__(256) void stem_down_x3(const StemFuseArgs A) {
   __syncthreads();
 
   // ---- E: model.2.cv1 (1x1, K = N1) from the tile, then its pair-layout store
-  const f16* W2 = static_cast<const f16*>(p.w2) + (size_t)(32 * wn + l32) * p.Kpad2;
   f32x16 acc2;
 #pragma unroll
   for (int r = 0; r < 16; ++r) acc2[r] = 0.f;
 #pragma unroll
-  for (int t = 0; t < N1 / 16; ++t) {
+  for (int t = 0; t < KST2; ++t) {
     const int J = 2 * t + h;
     const int byte = tp * TPB + ((J ^ (tp & 7)) << 4);
     const h8 xh = *reinterpret_cast<const h8*>(U + byte), xl = *reinterpret_cast<const h8*>(U + TPL + byte);
-    const h8 wh = ym_gld<h8>(W2 + 16 * J), wl = ym_gld<h8>(W2 + 16 * J + 8);
+    const h8 wh = w2h[t], wl = w2l[t];
     acc2 = __builtin_amdgcn_mfma_f32_32x32x16_f16(wh, xh, acc2, 0, 0, 0);
     acc2 = __builtin_amdgcn_mfma_f32_32x32x16_f16(wh, xl, acc2, 0, 0, 0);
     acc2 = __builtin_amdgcn_mfma_f32_32x32x16_f16(wl, xh, acc2, 0, 0, 0);
