@@ -20,6 +20,8 @@
 // The stem recomputes 325 / 256 of its pixels and the patch re-reads 1.36x of the image (tile halos); both are cheap
 // against the round trip they remove.  Summation orders inside model.1 / cv1 differ from the split launches (fp32
 // rounding level; the x3 plan's bar is against float64, tests/test_gpu_kernels.py).
+#include <stdlib.h>
+
 #include "ym_common.h"
 
 namespace {
@@ -37,6 +39,8 @@ typedef float f32x16 __attribute__((ext_vector_type(16)));
 struct StemFuseArgs {
   ConvArgs s;  // the stem (nchw input)
   ConvArgs p;  // the model.1 -> cv1 pair (w2, k2 = 1)
+  int dbg;     // phase ablations for timing only (YM_STEMFUSE_DBG): 1 no patch loads, 2 no stem MFMAs, 4 no model.1
+               // MFMAs, 8 no cv1 MFMAs, 16 no stores
 };
 
 // split-column slot of stem-image column xc
@@ -82,7 +86,7 @@ __global__ __launch_bounds__(256) void stem_down_x3(const StemFuseArgs A) {
     const int c = i / (PR * PC4), r = i - c * (PR * PC4);
     const int py = r / PC4, q = r - py * PC4;
     const int iy = iy0 + py, ix = ix0 + 4 * q;
-    in[it] = i < 3 * PR * PC4 && (unsigned)iy < (unsigned)s.Hin && (unsigned)ix < (unsigned)s.Win;
+    in[it] = i < 3 * PR * PC4 && (unsigned)iy < (unsigned)s.Hin && (unsigned)ix < (unsigned)s.Win && !(A.dbg & 1);
     v[it] = in[it] ? *reinterpret_cast<const f32x4*>(img + c * HW + (size_t)iy * s.Win + ix) : f32x4{0.f, 0.f, 0.f, 0.f};
   }
   // stem weights (A = weights: lane row = channel col of a 16-channel tile, K = 8 kg .. 8 kg + 7) and biases, as
@@ -144,7 +148,7 @@ __global__ __launch_bounds__(256) void stem_down_x3(const StemFuseArgs A) {
     w1l[t] = ym_gld<h8>(W1 + 16 * (2 * t + h) + 8);
   }
 #pragma unroll
-  for (int t = 0; t < KST2; ++t) {
+  for (int t = 0; t < (A.dbg & 8 ? 0 : KST2); ++t) {
     w2h[t] = ym_gld<h8>(W2 + 16 * (2 * t + h));
     w2l[t] = ym_gld<h8>(W2 + 16 * (2 * t + h) + 8);
   }
@@ -176,9 +180,11 @@ __global__ __launch_bounds__(256) void stem_down_x3(const StemFuseArgs A) {
 #pragma unroll
     for (int t = 0; t < NT0; ++t) {
       f32x4 acc = f32x4{0.f, 0.f, 0.f, 0.f};
-      acc = __builtin_amdgcn_mfma_f32_16x16x32_f16(wfl[t], bf, acc, 0, 0, 0);
-      acc = __builtin_amdgcn_mfma_f32_16x16x32_f16(wf[t], bfl, acc, 0, 0, 0);
-      acc = __builtin_amdgcn_mfma_f32_16x16x32_f16(wf[t], bf, acc, 0, 0, 0);
+      if (!(A.dbg & 2)) {
+        acc = __builtin_amdgcn_mfma_f32_16x16x32_f16(wfl[t], bf, acc, 0, 0, 0);
+        acc = __builtin_amdgcn_mfma_f32_16x16x32_f16(wf[t], bfl, acc, 0, 0, 0);
+        acc = __builtin_amdgcn_mfma_f32_16x16x32_f16(wf[t], bf, acc, 0, 0, 0);
+      }
       f16x4 oh, ol;
 #pragma unroll
       for (int e = 0; e < 4; ++e) {
@@ -201,7 +207,7 @@ __global__ __launch_bounds__(256) void stem_down_x3(const StemFuseArgs A) {
 #pragma unroll
   for (int r = 0; r < 16; ++r) acc[r] = 0.f;
 #pragma unroll
-  for (int t = 0; t < KST1; ++t) {
+  for (int t = 0; t < (A.dbg & 4 ? 0 : KST1); ++t) {
     const int J = 2 * t + h;  // this lane half's logical 8-channel chunk: (tap, channel chunk)
     const int tap = J / XCH, cj = J - tap * XCH;
     const int ky = tap / 3, kx = tap - ky * 3;
@@ -242,7 +248,7 @@ __global__ __launch_bounds__(256) void stem_down_x3(const StemFuseArgs A) {
 #pragma unroll
   for (int r = 0; r < 16; ++r) acc2[r] = 0.f;
 #pragma unroll
-  for (int t = 0; t < KST2; ++t) {
+  for (int t = 0; t < (A.dbg & 8 ? 0 : KST2); ++t) {
     const int J = 2 * t + h;
     const int byte = tp * TPB + ((J ^ (tp & 7)) << 4);
     const h8 xh = *reinterpret_cast<const h8*>(U + byte), xl = *reinterpret_cast<const h8*>(U + TPL + byte);
@@ -261,7 +267,7 @@ __global__ __launch_bounds__(256) void stem_down_x3(const StemFuseArgs A) {
       const float x = ym_x3_pre(acc2[4 * q + e], p.wsc2, b2[q][e]);
       o[e] = p.act2 ? ym_silu_x3(x) : x;
     }
-    ym_p2_store4_pair<32>(dst + 32 * wn + 8 * q + 4 * h, o, h, true, p.pst & 16);
+    ym_p2_store4_pair<32>(dst + 32 * wn + 8 * q + 4 * h, o, h, !(A.dbg & 16), p.pst & 16);
   }
 }
 
@@ -279,7 +285,8 @@ hipError_t ym_launch_stem_down_x3(const ConvArgs& s, const ConvArgs& p, hipStrea
   if (s.Ho != 2 * p.Ho || s.Wo != 2 * p.Wo || s.Hin != 2 * s.Ho || s.Win != 2 * s.Wo || p.Wo % TW || p.Ho % RB ||
       ((p.N2 | p.d_coff | p.d_ctot) & 7) || s.M != 4 * p.M)
     return hipErrorInvalidValue;
-  StemFuseArgs A{s, p};
+  static const int dbg = [] { const char* e = getenv("YM_STEMFUSE_DBG"); return e ? atoi(e) : 0; }();
+  StemFuseArgs A{s, p, dbg};
   const int B = p.M / (p.Ho * p.Wo);
   hipLaunchKernelGGL((stem_down_x3<32, 64, 64>), dim3(B * (p.Ho / RB) * (p.Wo / TW)), dim3(256), 0, st, A);
   return hipGetLastError();
