@@ -160,7 +160,7 @@ def test_x3_segment_s_b4():
 
 # csrc/ym_conv.hip: 12 direct-to-register + 5 LDS-staged tile configurations, then the 30 LDS-DMA ones
 # (csrc/ym_conv_dma.hip) and 31 streaming ones (csrc/ym_conv_stream.hip), x3 pairing mode; then the 9 x3-only LDS-DMA
-# split-K ones (after the 116-id f16 catalogue).  The two-wave-group LDS-DMA ones run with staggered groups (STG).
+# split-K ones (after the 116-id f16 catalogue).
 X3_CFGS = list(range(17)) + list(range(17, 47)) + list(range(47, 78)) + list(range(116, 125))
 
 
