@@ -352,6 +352,10 @@ struct ConvArgs {
   // multiply-shift divisors, the pixel tiles per XCD — instead of runtime integer divisions in every workgroup's prologue
   FDiv fd_tn, fd_cin8;
   int tm_per_xcd;
+  // int8 plans on the LDS-DMA kernels (round 6): per 3x3 tap the column sums of W, [9][N] int32 — the DMA fills
+  // out-of-image taps with 0 (the stored q - 128 of q = 128), the quantized conv reads z_in there, so a border pixel's
+  // accumulator gets (z_in - 128)·Σ over its outside taps of wtap[t][n] (ym_runtime.cpp computes the table at load)
+  const int* wtap;
 };
 
 // Warm the scalar cache with every 64-byte line of a kernel's argument block in ONE round trip: the compiler loads
@@ -482,6 +486,7 @@ hipError_t ym_launch_input_max(const float* x, long n, float* ctl, float* out, h
 hipError_t ym_launch_decode(const DecodeArgs& a, hipStream_t st);
 hipError_t ym_launch_nms(const NmsArgs& a, hipStream_t st);
 hipError_t ym_launch_nms_presort(const NmsArgs& a, hipStream_t st);  // ym_misc.hip: keys sorted by 8 WGs per image
+hipError_t ym_launch_conv_dma_i8(const ConvArgs& a, int dma_cfg, hipStream_t st);  // ym_conv_dma.hip
 hipError_t ym_launch_conv_dma_chain(const ConvArgs& a0, const ConvArgs& a1, int dma_cfg, int* ctl, int cap,
                                     hipStream_t st);  // csrc/ym_conv_dma.hip: two dependent x3 convs, one launch
 hipError_t ym_launch_stem_down_x3(const ConvArgs& s, const ConvArgs& p, hipStream_t st);  // ym_stem_fused.hip

@@ -708,6 +708,8 @@ int ym_conv_num_cfgs() {
 }
 // x3 plans: + the x3-only LDS-DMA configurations, appended (the f16 ids, and so the f16 tables, are unchanged)
 int ym_conv_num_cfgs_dt(int dtype) {
+  // int8: conv_i8 / streaming ids, then the LDS-DMA configurations in their Q8 mode (round 6); fp8: conv_i8 only
+  if (dtype == YM_DT_I8) return ym_conv_i8_num_cfgs() + ym_conv_dma_num_cfgs();
   if (ym_dt_q8(dtype)) return ym_conv_i8_num_cfgs();
   return ym_conv_num_cfgs() + (dtype == YM_DT_X3 ? ym_conv_dma_x3_num_cfgs() + ym_conv_bneck_x3_num_cfgs() : 0);
 }

@@ -22,6 +22,7 @@
 #include <type_traits>
 
 #include "ym_common.h"
+#include "ym_quant.h"
 
 typedef float f32x16 __attribute__((ext_vector_type(16)));
 typedef __attribute__((address_space(3))) void lds_void_t;
@@ -42,6 +43,7 @@ __device__ unsigned long long* ym_dma_stamps;
 namespace {
 
 constexpr int DK = 64;                    // K per stage
+typedef Q8<false> Q8S;                    // the int8 scheme of csrc/ym_quant.h (Q8 mode of conv_dma_body)
 constexpr unsigned OOB = 0x80000000u;     // byte offset past num_records: the DMA deposits zeros
 
 template <int N>
@@ -109,14 +111,20 @@ template <> struct Store4<P2> {
 // one work item of the persistent chain kernel conv_dma_chain.  Returns true when this workgroup stored the tile's
 // final output (false: a padding workgroup, or a split-K partial that another workgroup of the tile reduced); the
 // value is the same in every wave.  SC1OUT: the epilogue stores write through (sc1), for a consumer in the same launch.
-template <int NSTAGE, int SB, int BN, int KS2>
+template <int NSTAGE, int SB, int BN, int KS2, bool Q8 = false>
 struct DmaSmem {
-  static constexpr int ring = NSTAGE * SB + 16 + 256;
+  static constexpr int ring = NSTAGE * SB + 16 + 256 + (Q8 ? 1024 : 0);  // Q8: + the 256-entry post table
   static constexpr int w2 = KS2 ? KS2 * BN * 128 : 16;
 };
+// Q8 (round 6): the int8 PTQ plan on the same kernel — an int8 tensor is staged as the fp16 tensor of half its
+// channels (a 16-byte chunk = 16 int8 channels, the same fragment bytes per lane), every 16-deep fp16 sub-step is one
+// v_mfma_i32_32x32x32_i8 with exact int32 sums (so tiles, K splits and wave groups never change the result), and the
+// epilogue is conv_i8's quantized one (csrc/ym_conv_i8.hip; + the padding-tap correction of ConvArgs::wtap).
 template <typename OutT, int BM, int BN, int KIND, int SPLIT, int KG, int NSTAGE, int SUB, bool X3 = false,
-          bool FUSE = false, bool SC1OUT = false>
+          bool FUSE = false, bool SC1OUT = false, bool Q8 = false>
 __device__ __forceinline__ bool conv_dma_body(const ConvArgs& a, const int bid, char* smem, char* w2s) {
+  static_assert(!Q8 || (!X3 && !FUSE && !SC1OUT), "int8: the plain GEMM only");
+  typedef typename std::conditional<Q8, i32x16, f32x16>::type ACC;
   constexpr int NW = 4 * KG;
   constexpr int TM = BM / 64, TN = BN / 64;
   static_assert((BM / 8) % NW == 0 && (BN / 8) % NW == 0, "DMA groups must divide over the waves");
@@ -180,7 +188,11 @@ __device__ __forceinline__ bool conv_dma_body(const ConvArgs& a, const int bid, 
       w2r[u] = ym_gld<u32x4>(static_cast<const f16*>(a.w2) + (ok ? (size_t)n2 * a.Kpad2 + 8 * cs : 0));
     }
   }
-  if (kg == 0) {
+  if constexpr (Q8) {  // the epilogue's requantisation table, staged once (the K loop's barriers order it)
+    float* post = reinterpret_cast<float*>(smem + NSTAGE * SB + 16 + 256);
+    for (int i = tid; i < 256; i += 256 * KG) post[i] = a.q->post[i];
+  }
+  if (kg == 0 && !Q8) {
 #pragma unroll
     for (int j = 0; j < TN; ++j)
 #pragma unroll
@@ -397,7 +409,7 @@ __device__ __forceinline__ bool conv_dma_body(const ConvArgs& a, const int bid, 
     tap = s_tap; cb = s_cb; ky = s_ky; kx = s_kx; kcur = s_k;
   }
 
-  f32x16 acc[NACC][TM][TN];
+  ACC acc[NACC][TM][TN];
 #pragma unroll
   for (int u = 0; u < NACC; ++u)
 #pragma unroll
@@ -405,7 +417,7 @@ __device__ __forceinline__ bool conv_dma_body(const ConvArgs& a, const int bid, 
 #pragma unroll
       for (int j = 0; j < TN; ++j)
 #pragma unroll
-        for (int r = 0; r < 16; ++r) acc[u][i][j][r] = 0.f;
+        for (int r = 0; r < 16; ++r) acc[u][i][j][r] = 0;
 
   const int key = (l32 >> 1) & 7;
   // this wave's k sub-steps of the stage: fragment reads first, then the MFMAs (one LDS latency per stage)
@@ -472,9 +484,15 @@ __device__ __forceinline__ bool conv_dma_body(const ConvArgs& a, const int bid, 
 #pragma unroll
           for (int i = 0; i < TM; ++i)
 #pragma unroll
-            for (int j = 0; j < TN; ++j)
-              acc[u % NACC][i][j] =
-                  __builtin_amdgcn_mfma_f32_32x32x16_f16(fa[su][u][j], fb[su][u][i], acc[u % NACC][i][j], 0, 0, 0);
+            for (int j = 0; j < TN; ++j) {
+              if constexpr (Q8)
+                acc[u % NACC][i][j] = __builtin_amdgcn_mfma_i32_32x32x32_i8(
+                    __builtin_bit_cast(i8x16, fa[su][u][j]), __builtin_bit_cast(i8x16, fb[su][u][i]),
+                    acc[u % NACC][i][j], 0, 0, 0);
+              else
+                acc[u % NACC][i][j] =
+                    __builtin_amdgcn_mfma_f32_32x32x16_f16(fa[su][u][j], fb[su][u][i], acc[u % NACC][i][j], 0, 0, 0);
+            }
     }
   };
 
@@ -515,7 +533,7 @@ __device__ __forceinline__ bool conv_dma_body(const ConvArgs& a, const int bid, 
 #pragma unroll
         for (int j = 0; j < TN; ++j)
 #pragma unroll
-          for (int r = 0; r < 16; ++r) d[((i * TN + j) * 16 + r) * 64] = acc[0][i][j][r];
+          for (int r = 0; r < 16; ++r) d[((i * TN + j) * 16 + r) * 64] = __builtin_bit_cast(float, acc[0][i][j][r]);
     }
     __syncthreads();
     if (kg == 0) {
@@ -527,7 +545,10 @@ __device__ __forceinline__ bool conv_dma_body(const ConvArgs& a, const int bid, 
 #pragma unroll
           for (int j = 0; j < TN; ++j)
 #pragma unroll
-            for (int r = 0; r < 16; ++r) acc[0][i][j][r] += q[((i * TN + j) * 16 + r) * 64];
+            for (int r = 0; r < 16; ++r) {
+              if constexpr (Q8) acc[0][i][j][r] += __builtin_bit_cast(int, q[((i * TN + j) * 16 + r) * 64]);
+              else acc[0][i][j][r] += q[((i * TN + j) * 16 + r) * 64];
+            }
       }
     }
   }
@@ -549,9 +570,11 @@ __device__ __forceinline__ bool conv_dma_body(const ConvArgs& a, const int bid, 
 #pragma unroll
           for (int q = 0; q < 4; ++q) {
             const int qq = (i * TN + j) * 4 + q;
-            const f32x4 v{acc[0][i][j][4 * q], acc[0][i][j][4 * q + 1], acc[0][i][j][4 * q + 2],
-                          acc[0][i][j][4 * q + 3]};
-            __builtin_amdgcn_raw_buffer_store_b128(__builtin_bit_cast(u32x4, v), rsl,
+            const u32x4 v{__builtin_bit_cast(unsigned, acc[0][i][j][4 * q]),
+                          __builtin_bit_cast(unsigned, acc[0][i][j][4 * q + 1]),
+                          __builtin_bit_cast(unsigned, acc[0][i][j][4 * q + 2]),
+                          __builtin_bit_cast(unsigned, acc[0][i][j][4 * q + 3])};
+            __builtin_amdgcn_raw_buffer_store_b128(v, rsl,
                                                    mine + (qq * 256u + tid) * 16u, 0, SC1);
           }
       asm volatile("s_waitcnt vmcnt(0)" ::: "memory");  // every storing wave drains its sc1 stores
@@ -586,11 +609,19 @@ __device__ __forceinline__ bool conv_dma_body(const ConvArgs& a, const int bid, 
 #pragma unroll
         for (int q = 0; q < 4; ++q) {
           const int qq = (i * TN + j) * 4 + q;
-          f32x4 v = part[0][qq];
+          if constexpr (Q8) {
+            i32x4 v = __builtin_bit_cast(i32x4, part[0][qq]);
 #pragma unroll
-          for (int s2 = 1; s2 < SPLIT; ++s2) v += part[s2][qq];
+            for (int s2 = 1; s2 < SPLIT; ++s2) v += __builtin_bit_cast(i32x4, part[s2][qq]);
 #pragma unroll
-          for (int e = 0; e < 4; ++e) acc[0][i][j][4 * q + e] = v[e];
+            for (int e = 0; e < 4; ++e) acc[0][i][j][4 * q + e] = v[e];
+          } else {
+            f32x4 v = part[0][qq];
+#pragma unroll
+            for (int s2 = 1; s2 < SPLIT; ++s2) v += part[s2][qq];
+#pragma unroll
+            for (int e = 0; e < 4; ++e) acc[0][i][j][4 * q + e] = v[e];
+          }
         }
   }
   if constexpr (FUSE) {
@@ -704,6 +735,63 @@ __device__ __forceinline__ bool conv_dma_body(const ConvArgs& a, const int bid, 
   }
   if (kg != 0) return true;
 
+  if constexpr (Q8) {
+    // ---- int8 epilogue (conv_i8's): lane owns channels nb + 32j + 8q + 4h + {0..3} of pixel pbm + 32i + l32
+    const QRec* Q = a.q;
+    const float* post = reinterpret_cast<const float*>(smem + NSTAGE * SB + 16 + 256);
+    const int mode = Q->mode;
+    const i8* res = static_cast<const i8*>(a.res);
+    const int zpad = Q->z_in - 128;  // the byte the quantized conv reads in a padding tap (the DMA read 0)
+#pragma unroll
+    for (int i = 0; i < TM; ++i) {
+      const int m = tm * BM + wm * (BM / 2) + 32 * i + l32;
+      if (m >= a.M) continue;
+      const int b = ym_div(m, a.fd_hw), rem = m - b * (a.Ho * a.Wo);
+      const int oy = ym_div(rem, a.fd_w), ox = rem - oy * a.Wo;
+      const size_t obase = (size_t)(b * a.d_P + a.d_pixoff + oy * a.d_W + ox) * a.d_ctot + a.d_coff;
+      const size_t rbase = res ? (size_t)(b * a.r_P + oy * a.Wo + ox) * a.r_ctot + a.r_coff : 0;
+      unsigned outside = 0;  // 3x3 taps of this pixel's window outside the image
+      if (a.k == 3) {
+        const int iy0 = oy * a.s - 1, ix0 = ox * a.s - 1;
+#pragma unroll
+        for (int t = 0; t < 9; ++t)
+          outside |= ((unsigned)(iy0 + t / 3) >= (unsigned)a.Hin || (unsigned)(ix0 + t % 3) >= (unsigned)a.Win) ? (1u << t)
+                                                                                                              : 0u;
+      }
+#pragma unroll
+      for (int j = 0; j < TN; ++j)
+#pragma unroll
+        for (int q = 0; q < 4; ++q) {
+          const int n = tn * BN + wn * (BN / 2) + 32 * j + 8 * q + 4 * h;
+          if (n >= a.N) continue;
+          i32x4 bi = *reinterpret_cast<const i32x4*>(a.biasi + n);
+          if (outside) {
+            for (int t = 0; t < 9; ++t)
+              if ((outside >> t) & 1u) bi += zpad * *reinterpret_cast<const i32x4*>(a.wtap + t * a.N + n);
+          }
+          const f32x4 sa = *reinterpret_cast<const f32x4*>(a.sasw + n);
+          const f32x4 bf = *reinterpret_cast<const f32x4*>(a.bias + n);
+          const int r4 = res ? *reinterpret_cast<const int*>(res + rbase + n) : 0;
+          int ov[4];
+          float fv[4];
+#pragma unroll
+          for (int e = 0; e < 4; ++e) {
+            const int qc = Q8S::code(acc[0][i][j][4 * q + e], bi[e], sa[e], bf[e], Q);
+            if (mode == 1) {
+              ov[e] = Q8S::raw_byte(qc);
+              continue;
+            }
+            float v = post[qc];
+            if (res) v = __fadd_rn(v, Q8S::dec(r4 >> (8 * e), Q->z_r, Q->s_r));
+            fv[e] = v;
+            ov[e] = Q8S::store(v, Q);
+          }
+          if (mode == 2) *reinterpret_cast<f32x4*>(static_cast<float*>(a.dst) + obase + n) = f32x4{fv[0], fv[1], fv[2], fv[3]};
+          else *reinterpret_cast<int*>(static_cast<i8*>(a.dst) + obase + n) = pack4(ov);
+        }
+    }
+    return true;
+  } else {
   // ---- epilogue: lane owns channels nb + 32j + 8q + 4h + {0..3} of pixel pbm + 32i + l32
   OutT* dst = static_cast<OutT*>(a.dst);
   // x3 pair-layout outputs: lanes l and l ^ 32 (h = 0 / 1: channels +0..3 / +4..7 of one chunk of one pixel) write
@@ -763,19 +851,20 @@ __device__ __forceinline__ bool conv_dma_body(const ConvArgs& a, const int bid, 
   }
   YM_STAMP(3);
   return true;
+  }
 }
 
 template <typename OutT, int BM, int BN, int KIND, int SPLIT, int KG, int NSTAGE, int SUB, bool X3 = false,
-          bool FUSE = false>
+          bool FUSE = false, bool Q8 = false>
 __global__ __launch_bounds__(256 * KG) void conv_dma(const ConvArgs a) {
   constexpr int KS2 = FUSE ? (X3 ? 2 : 1) * BN / 64 : 0;
-  typedef DmaSmem<NSTAGE, SUB * (BM + BN) * 128, BN, KS2> SM;
+  typedef DmaSmem<NSTAGE, SUB * (BM + BN) * 128, BN, KS2, Q8> SM;
   __shared__ __attribute__((aligned(16))) char smem[SM::ring];
   __shared__ __attribute__((aligned(16))) char w2s[SM::w2];
 #ifndef YM_NO_WARM
   ym_warm_kernargs<sizeof(ConvArgs)>();
 #endif
-  conv_dma_body<OutT, BM, BN, KIND, SPLIT, KG, NSTAGE, SUB, X3, FUSE>(a, blockIdx.x, smem, w2s);
+  conv_dma_body<OutT, BM, BN, KIND, SPLIT, KG, NSTAGE, SUB, X3, FUSE, false, Q8>(a, blockIdx.x, smem, w2s);
 }
 
 struct DmaCfg {
@@ -802,7 +891,7 @@ constexpr DmaCfg kDma[] = {
 };
 constexpr int kNumDma = sizeof(kDma) / sizeof(kDma[0]);
 
-template <typename OutT, int BM, int BN, int SPLIT, int KG, int NS, int SUB, bool X3 = false>
+template <typename OutT, int BM, int BN, int SPLIT, int KG, int NS, int SUB, bool X3 = false, bool Q8 = false>
 hipError_t launch_dma(ConvArgs a, int kind, hipStream_t st) {
   if (X3 && (4 / KG) % 2) return hipErrorInvalidValue;
   const int tiles_m8 = ((a.M + BM - 1) / BM + 7) / 8 * 8;
@@ -818,12 +907,12 @@ hipError_t launch_dma(ConvArgs a, int kind, hipStream_t st) {
   if (SUB > 1 && (a.Kpad / DK) % (SPLIT * SUB)) return hipErrorInvalidValue;  // whole stages in every split
   const dim3 grid(tiles_m8 * a.tiles_n * SPLIT), block(256 * KG);
   if (kind == 1) {
-    hipLaunchKernelGGL((conv_dma<OutT, BM, BN, 1, SPLIT, KG, NS, SUB, X3>), grid, block, 0, st, a);
+    hipLaunchKernelGGL((conv_dma<OutT, BM, BN, 1, SPLIT, KG, NS, SUB, X3, false, Q8>), grid, block, 0, st, a);
   } else if constexpr (!std::is_same<OutT, float>::value) {  // fp32 outputs: only the Detect head's 1x1 convs
     if (kind == 4)
-      hipLaunchKernelGGL((conv_dma<OutT, BM, BN, 4, SPLIT, KG, NS, SUB, X3>), grid, block, 0, st, a);
+      hipLaunchKernelGGL((conv_dma<OutT, BM, BN, 4, SPLIT, KG, NS, SUB, X3, false, Q8>), grid, block, 0, st, a);
     else
-      hipLaunchKernelGGL((conv_dma<OutT, BM, BN, 3, SPLIT, KG, NS, SUB, X3>), grid, block, 0, st, a);
+      hipLaunchKernelGGL((conv_dma<OutT, BM, BN, 3, SPLIT, KG, NS, SUB, X3, false, Q8>), grid, block, 0, st, a);
   } else {
     return hipErrorInvalidValue;
   }
@@ -1035,7 +1124,41 @@ hipError_t launch_chain(ConvArgs a0, ConvArgs a1, int* ctl, int cap, hipStream_t
   return hipGetLastError();
 }
 
+hipError_t dispatch_i8(const ConvArgs& a, int kind, int i, hipStream_t st) {
+  switch (i) {
+#define YM_X(id, bm, bn, sp, kg, ns, sub) \
+  case id: return launch_dma<i8, bm, bn, sp, kg, ns, sub, false, true>(a, kind, st);
+    YM_DMA_CFGS(YM_X)
+#undef YM_X
+  }
+  return hipErrorInvalidValue;
+}
+
 }  // namespace
+
+// The int8 PTQ plan on LDS-DMA configuration i (ids as in YM_DMA_CFGS): the int8 tensors and weight rows are described
+// to the kernel as fp16 tensors of half the channels (ctot, coff, Kpad, element counts halved; Cin8 already counts
+// 16-channel chunks), the epilogue keeps int8 units (d_*, r_*).  1x1 stride-1 single-source and 3x3 convs, whole
+// 128-byte K stages (Kpad % 128 == 0); fp8 plans stay on conv_i8 (their fp8 MFMA chain is restated per kernel).
+hipError_t ym_launch_conv_dma_i8(const ConvArgs& a0, int i, hipStream_t st) {
+  if (i < 0 || i >= kNumDma || !a0.q || !a0.sasw || !a0.biasi || a0.nchw || a0.src1 || a0.up0 || a0.shuffle || a0.w2 ||
+      a0.dw_w || !a0.src0)
+    return hipErrorInvalidValue;
+  int kind;
+  if (a0.k == 1 && a0.s == 1) kind = 1;
+  else if (a0.k == 3 && a0.wtap) kind = a0.Cin8 % 8 == 0 ? 4 : 3;
+  else return hipErrorInvalidValue;
+  if (a0.Kpad % 128 || (a0.s0_ctot | a0.s0_coff) & 15 || (a0.N & 3) || (a0.d_ctot & 3) || (a0.d_coff & 3))
+    return hipErrorInvalidValue;
+  ConvArgs a = a0;
+  a.s0_ctot /= 2;
+  a.s0_coff /= 2;
+  a.Kpad /= 2;
+  a.s0_elems /= 2;
+  const long lim = 0x7FFFFFF0L / 2;  // fp16 elements
+  if ((long)a.N * a.Kpad > lim || a.s0_elems > lim) return hipErrorInvalidValue;
+  return dispatch_i8(a, kind, i, st);
+}
 
 // Two dependent x3 convs (op 1 reads op 0's output) as one persistent launch on LDS-DMA configuration i (ids as in
 // YM_DMA_CFGS; instantiated: 8, 13, 26).  ctl: `cap` zeroed ints (ready counters, done, give-up word), left zeroed.

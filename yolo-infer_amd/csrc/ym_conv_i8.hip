@@ -607,6 +607,11 @@ hipError_t ym_launch_conv_i8(const ConvArgs& a, int cfg, hipStream_t st, bool st
     if (strict) return hipErrorInvalidValue;
     cfg = -1;
   }
+  if (!f8 && cfg >= ym_conv_i8_num_cfgs()) {  // int8: the LDS-DMA kernel's Q8 mode (csrc/ym_conv_dma.hip)
+    const hipError_t e = ym_launch_conv_dma_i8(a, cfg - ym_conv_i8_num_cfgs(), st);
+    if (e != hipErrorInvalidValue || strict) return e;
+    cfg = -1;
+  }
   if (cfg >= kNumCfg) {
     const hipError_t e = ym_launch_conv_i8_stream(a, cfg - kNumCfg, st, f8);
     if (e != hipErrorInvalidValue || strict) return e;

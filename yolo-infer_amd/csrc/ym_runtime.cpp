@@ -191,6 +191,8 @@ struct ym_ctx {
   char* d_weights = nullptr;
   std::vector<char> blob_host;  // the loaded blob as received (what ym_broadcast_weights sends from the root)
   size_t off_wstem = 0;  // stem weights re-laid out as fp32 [27][N] behind the blob's weights (ym_stem.hip)
+  size_t off_wtap0 = 0;            // int8 plans: the 3x3 convs' [9][N] int32 tap sums, behind the stem weights
+  std::vector<size_t> off_wtap;    // per op: 1 + byte offset from off_wtap0 (0: none)
   // branch schedule of a one-lane forward (ops of independent DAG branches on up to kMaxLanes streams)
   int nbr = 1;
   std::vector<int> br_of;                // per op: branch stream
@@ -397,6 +399,9 @@ int conv_args(ym_ctx* c, const Op& op, int B, const float* d_in, float in_eps, C
         a.q = c->wptr<QRec>(r[22]);
         a.sasw = c->wptr<float>(r[23]);
         a.biasi = c->wptr<int>(r[24]);
+        const size_t oi = (size_t)(&op - c->ops.data());
+        if (oi < c->off_wtap.size() && c->off_wtap[oi])
+          a.wtap = reinterpret_cast<const int*>(c->d_weights + c->off_wtap0 + (c->off_wtap[oi] - 1));
       }
       if (c->dtype == YM_DT_X3 && b0 != c->input_buf) {  // pair layout: fp16 storage chunks per tap double
         a.x3 = 1;
@@ -977,13 +982,36 @@ int ym_load_weights(ym_ctx* c, const void* blob, size_t bytes) {
       }
     break;
   }
+  // int8 plans: per 3x3 conv the [9][N] int32 tap sums of its weights (ConvArgs::wtap: the LDS-DMA kernels' padding
+  // correction), behind the stem weights
+  std::vector<int32_t> wtap;
+  c->off_wtap.assign(c->ops.size(), 0);
+  if (dtype == YM_DT_I8) {
+    for (size_t i = 0; i < c->ops.size(); ++i) {
+      const Op& o = c->ops[i];
+      if (o.r[0] != OP_CONV || o.r[6] == c->input_buf || o.r[1] != 3) continue;
+      const int N = o.r[4], Kpad = o.r[21], cin = o.r[3], cs = (cin + 15) / 16 * 16;
+      if (9 * cs > Kpad || (size_t)(uint32_t)o.r[19] + (size_t)N * Kpad > wbytes) continue;
+      const int8_t* w = reinterpret_cast<const int8_t*>(static_cast<const char*>(blob) + woff + (size_t)(uint32_t)o.r[19]);
+      c->off_wtap[i] = wtap.size() * 4 + 1;  // + 1: 0 means none (relative to off_wtap0, 4-byte units * 4)
+      for (int t = 0; t < 9; ++t)
+        for (int n = 0; n < N; ++n) {
+          int32_t sum = 0;
+          for (int k = 0; k < cs; ++k) sum += w[(size_t)n * Kpad + t * cs + k];
+          wtap.push_back(sum);
+        }
+    }
+  }
   c->off_wstem = align_up(wbytes, 256);
-  const size_t dbytes = c->off_wstem + wstem.size() * sizeof(float);
+  c->off_wtap0 = align_up(c->off_wstem + wstem.size() * sizeof(float), 256);
+  const size_t dbytes = c->off_wtap0 + wtap.size() * sizeof(int32_t);
   hipError_t e = hipMalloc(&c->d_weights, dbytes ? dbytes : 256);
   if (e != hipSuccess) return fail(YM_ENOMEM, "weights hipMalloc(%zu): %s", dbytes, hipGetErrorString(e));
   HIPCK(hipMemcpy(c->d_weights, static_cast<const char*>(blob) + woff, wbytes, hipMemcpyHostToDevice));
   if (!wstem.empty())
     HIPCK(hipMemcpy(c->d_weights + c->off_wstem, wstem.data(), wstem.size() * sizeof(float), hipMemcpyHostToDevice));
+  if (!wtap.empty())
+    HIPCK(hipMemcpy(c->d_weights + c->off_wtap0, wtap.data(), wtap.size() * sizeof(int32_t), hipMemcpyHostToDevice));
   c->wbytes = wbytes;
   c->loaded = true;
   return YM_OK;

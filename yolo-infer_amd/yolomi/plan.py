@@ -219,7 +219,8 @@ def pack_graph(g: GraphBuilder, sd: Dict[str, np.ndarray], dtype: str = "f16", q
                 C0 += pad
             N = w.shape[0]
             K = w.shape[1] * w.shape[2] * w.shape[3]
-            Kpad = (K + BK - 1) // BK * BK
+            bk = 2 * BK if dtype == "i8" else BK  # int8: whole 128-byte K stages for the LDS-DMA kernels' Q8 mode
+            Kpad = (K + bk - 1) // bk * bk
             wp = np.zeros((N, Kpad), np.int8 if quant else np.float32)
             wp[:, :K] = w.reshape(N, K)
             if dtype == "x3" and not stem:  # pair-chunk rows of W·2^s: every 8-channel K chunk as [hi x8 | lo x8]
