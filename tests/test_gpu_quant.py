@@ -102,9 +102,10 @@ def test_i8_graph_replay_bitwise_equals_eager():
 @pytest.mark.parametrize("cfg", list(range(12 + 15 + 8 + 30)))
 def test_i8_conv_tile_configs_agree(cfg):
     """Every int8 conv configuration — conv_i8 tiles (incl. intra-workgroup split-K), the streaming and the small-M
-    kernels of csrc/ym_conv_i8_stream.hip (ids 12..34) and, since round 6, the 30 LDS-DMA configurations in their
-    int8 mode (ids 35..64: csrc/ym_conv_dma.hip Q8, split-K and multi-wave-group tiles included, the padding taps
-    corrected through ConvArgs::wtap) — gives the same int8 tensors and the same fp32 head rows (integer sums)."""
+    kernels of csrc/ym_conv_i8_stream.hip (ids 12..34) and, since round 6, the LDS-DMA configurations in their
+    int8 mode (ids 35..64: csrc/ym_conv_dma.hip Q8, the padding taps corrected through ConvArgs::wtap; only the
+    unsplit one-wave-group ones are launched, the others return invalid and the op keeps its heuristic kernel) —
+    gives the same int8 tensors and the same fp32 head rows (integer sums)."""
     eng = i8_model("det_n_i8_fbgemm_320").model.engine
     x = make_input("uniform", (71,), 320).to(DEV)
     eng.run(x, use_graph=False)
