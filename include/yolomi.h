@@ -204,7 +204,8 @@ int ym_num_conv_cfgs(int dtype);
  * kernel is launched (so at graph capture for replayed forwards): YM_DBG_NMS (9 = the NMS kernel's per-box path
  * instead of the blocked one), YM_DBG_DW_MODE (depthwise variant: 0 LDS tiles, 1 rows, 2 column strips),
  * YM_DBG_DW_TILE (LDS tile shape 0..3), YM_DBG_CHAIN (1: the persistent two-conv chain kernel).
- * The environment variables YM_NMS_DBG, YM_DW_MODE, YM_DW_TILE, YM_CHAIN and YM_STEMFUSE set the initial values.  A forward graph
+ * The environment variables YM_NMS_DBG, YM_DW_MODE, YM_DW_TILE, YM_CHAIN, YM_STEMFUSE and YM_ATTN_KB set the initial
+ * values.  A forward graph
  * already captured keeps the kernels it was captured with.
  * Returns the previous value, or YM_EINVAL for an unknown key. */
 #define YM_DBG_NMS 1
@@ -213,6 +214,7 @@ int ym_num_conv_cfgs(int dtype);
 #define YM_DBG_CHAIN 4 /* 1: dependent x3 3x3 pairs on one LDS-DMA configuration as one persistent launch */
 #define YM_DBG_CHAIN_LAUNCHES 5 /* chain kernels launched since it was last set (a counter) */
 #define YM_DBG_STEMFUSE 6 /* 1: x3 stem + model.1 + model.2.cv1 as one launch (csrc/ym_stem_fused.hip); 0: three */
+#define YM_DBG_ATTN_KB 7 /* 1: x3 attention loads K fragments 8 key tiles per round trip; 0: all tiles at once */
 int ym_set_debug(int key, int value);
 
 #ifdef __cplusplus

@@ -314,3 +314,30 @@ def test_stem_fuse_matches_the_split_launches():
         for b in range(8):
             match_image(d0[b, :int(c0[b])].cpu().numpy(), d[b, :int(c[b])].cpu().numpy(), 0.05, 0.7, 5e-4, 5e-5, rep=rep)
         assert rep.ok and rep.matched > 0, (str(rep), rep.failures[:3])
+
+
+def test_attention_k_batching_is_bitwise_neutral():
+    """YM_DBG_ATTN_KB (csrc/ym_misc.hip attn_psa_x3<NKT, KB>): the x3 C2PSA attention loads the K fragments of every
+    key tile at once by default, 8 tiles per round trip with the switch at 1.  Only the load schedule differs, so
+    every tensor of the forward and the detections are bitwise equal."""
+    from core.model import YOLO11Model
+    from yolomi import lib as L
+    m = YOLO11Model(task="detect", size="s", device="cuda:0", dtype="x3", verbose=False)
+    eng = m.model.engine
+    x = synthetic_batch(8, 640, 11, DEV)
+    ids = [b for b in range(len(eng.graph.buffers)) if b != eng.graph.input.id]
+    prev = L.set_debug(L.DBG_ATTN_KB, 0)
+    try:
+        d0, c0 = (t.clone() for t in eng.run(x, conf=0.05, use_graph=False))
+        ref = {b: eng.read_buffer(b, 8) for b in ids}
+        L.set_debug(L.DBG_ATTN_KB, 1)
+        d1, c1 = (t.clone() for t in eng.run(x, conf=0.05, use_graph=False))
+        got = {b: eng.read_buffer(b, 8) for b in ids}
+    finally:
+        L.set_debug(L.DBG_ATTN_KB, prev)
+    assert any("attn" in op.name for op in eng.graph.ops)
+    for b in ids:
+        assert torch.equal(ref[b], got[b]), eng.graph.buffers[b].name
+    assert torch.equal(c0, c1)
+    for b in range(8):
+        assert torch.equal(d0[b, :int(c0[b])], d1[b, :int(c1[b])])

@@ -215,8 +215,10 @@ __device__ __forceinline__ float ord2f(int i) { return __int_as_float(i >= 0 ? i
 // The input statistics word of a forward (LoadTensor's batch max) is spread over YM_CTL_SLOTS atomicMax targets 64 B
 // apart (same-address atomics serialise at ~90 per µs); readers take the max of the slots.
 constexpr int YM_CTL_SLOTS = 16, YM_CTL_STRIDE = 16;  // ints
-// the ctl region: the slots, a ticket on its own 256-byte line, then input_stats' per-block partial maxima
-constexpr int YM_CTL_BYTES = (YM_CTL_SLOTS * YM_CTL_STRIDE + 64 + 1024) * 4;
+// the ctl region: the slots, a ticket on its own 256-byte line, input_stats' per-block partial maxima, then its
+// YM_STATS_GROUPS group tickets 128 B apart
+constexpr int YM_STATS_GROUPS = 16;
+constexpr int YM_CTL_BYTES = (YM_CTL_SLOTS * YM_CTL_STRIDE + 64 + 1024 + 32 * YM_STATS_GROUPS) * 4;
 static_assert(YM_CTL_BYTES <= 8192, "ym_input_max's region of the context scratch (ym_runtime.cpp d_misc)");
 __device__ __forceinline__ float ym_input_max(const float* ctl) {
   const int* c = reinterpret_cast<const int*>(ctl);

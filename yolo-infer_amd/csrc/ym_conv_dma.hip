@@ -533,7 +533,13 @@ __device__ __forceinline__ bool conv_dma_body(const ConvArgs& a, const int bid, 
 #pragma unroll
         for (int j = 0; j < TN; ++j)
 #pragma unroll
-          for (int r = 0; r < 16; ++r) d[((i * TN + j) * 16 + r) * 64] = __builtin_bit_cast(float, acc[0][i][j][r]);
+          for (int r = 0; r < 16; ++r) {
+            // (an element copied out first: __builtin_bit_cast straight on a vector element miscompiled — round 6,
+            // every KG 2 and split-K configuration of every plan returned wrong tiles until this was found)
+            const auto x = acc[0][i][j][r];
+            if constexpr (Q8) d[((i * TN + j) * 16 + r) * 64] = __int_as_float(x);
+            else d[((i * TN + j) * 16 + r) * 64] = x;
+          }
     }
     __syncthreads();
     if (kg == 0) {
@@ -546,7 +552,7 @@ __device__ __forceinline__ bool conv_dma_body(const ConvArgs& a, const int bid, 
           for (int j = 0; j < TN; ++j)
 #pragma unroll
             for (int r = 0; r < 16; ++r) {
-              if constexpr (Q8) acc[0][i][j][r] += __builtin_bit_cast(int, q[((i * TN + j) * 16 + r) * 64]);
+              if constexpr (Q8) acc[0][i][j][r] += __float_as_int(q[((i * TN + j) * 16 + r) * 64]);
               else acc[0][i][j][r] += q[((i * TN + j) * 16 + r) * 64];
             }
       }
@@ -570,11 +576,9 @@ __device__ __forceinline__ bool conv_dma_body(const ConvArgs& a, const int bid, 
 #pragma unroll
           for (int q = 0; q < 4; ++q) {
             const int qq = (i * TN + j) * 4 + q;
-            const u32x4 v{__builtin_bit_cast(unsigned, acc[0][i][j][4 * q]),
-                          __builtin_bit_cast(unsigned, acc[0][i][j][4 * q + 1]),
-                          __builtin_bit_cast(unsigned, acc[0][i][j][4 * q + 2]),
-                          __builtin_bit_cast(unsigned, acc[0][i][j][4 * q + 3])};
-            __builtin_amdgcn_raw_buffer_store_b128(v, rsl,
+            typedef typename std::conditional<Q8, i32x4, f32x4>::type V4;  // (whole-vector bit cast, see above)
+            const V4 v{acc[0][i][j][4 * q], acc[0][i][j][4 * q + 1], acc[0][i][j][4 * q + 2], acc[0][i][j][4 * q + 3]};
+            __builtin_amdgcn_raw_buffer_store_b128(__builtin_bit_cast(u32x4, v), rsl,
                                                    mine + (qq * 256u + tid) * 16u, 0, SC1);
           }
       asm volatile("s_waitcnt vmcnt(0)" ::: "memory");  // every storing wave drains its sc1 stores
@@ -1124,14 +1128,10 @@ hipError_t launch_chain(ConvArgs a0, ConvArgs a1, int* ctl, int cap, hipStream_t
   return hipGetLastError();
 }
 
-// int8: unsplit, one-wave-group configurations only — the split-K and KG 2 instantiations of the Q8 mode returned
-// wrong tensors on the MI355X in round 6 (tests/test_gpu_quant.py, ids 36, 38-51, 58, 61-64) and are not launched
 hipError_t dispatch_i8(const ConvArgs& a, int kind, int i, hipStream_t st) {
   switch (i) {
 #define YM_X(id, bm, bn, sp, kg, ns, sub) \
-  case id: \
-    if constexpr (sp == 1 && kg == 1) return launch_dma<i8, bm, bn, sp, kg, ns, sub, false, true>(a, kind, st); \
-    else return hipErrorInvalidValue;
+  case id: return launch_dma<i8, bm, bn, sp, kg, ns, sub, false, true>(a, kind, st);
     YM_DMA_CFGS(YM_X)
 #undef YM_X
   }

@@ -23,7 +23,10 @@ namespace {
 // aborted forward), reduces a contiguous chunk of the batch to its max and stores it write-through (sc1) into its
 // partial slot; after its `vmcnt(0)` one lane takes an agent-scope ticket, and the block whose ticket is last
 // reduces the partials (sc1 loads: the hand-off of MI355X_MICROARCH §inter-workgroup visibility, first table row),
-// writes the slots and resets the ticket.  No per-forward init kernel, no same-address atomicMax storm.  The ticket
+// writes the slots and resets the ticket.  The ticket is two-level: block b counts on group ticket b % 16 and the
+// last block of each group on the top ticket — same-address agent-scope atomics serialise at ~10 ns each, so one
+// ticket for 1,024 blocks cost ~10 us of the kernel's ~28 (tools/probe_input_stats.hip, profiles/r06j_input_stats.txt:
+// 27.9 -> 20.3 us in isolation, 17.9 with no ticket at all).  No per-forward init kernel, no same-address atomicMax storm.  The ticket
 // starts at zero (ensure_workspace zeroes the arena it lives in), and a launch can only stop part-way through a device
 // fault, which ends the context: a stale ticket cannot carry into a later forward.
 // batch_max non-null (multi-GPU shard): the slots take the given global max, x is not read.
@@ -43,6 +46,7 @@ __global__ __launch_bounds__(256) void input_stats(const float* __restrict__ x, 
   }
   int* part = slots + YM_CTL_SLOTS * YM_CTL_STRIDE + 64;  // [kStatsBlocks], after the ticket's 256-byte line
   int* ticket = slots + YM_CTL_SLOTS * YM_CTL_STRIDE;
+  int* gticket = part + kStatsBlocks;                     // [YM_STATS_GROUPS][32]
   // contiguous chunk of whole float4s per block; every round issues kStatsU 16-byte loads per lane at once, the
   // indices past the chunk clamped onto its last float4 (a duplicate cannot change a max), so there is no
   // predicated or remainder load: at B = 8, 640² (2400 float4 per block) the whole chunk is ONE round trip
@@ -78,8 +82,15 @@ __global__ __launch_bounds__(256) void input_stats(const float* __restrict__ x, 
     // kernel went 21.8 -> 52.8 us per call under rocprofv3: profiles/r04d_s_b8_x3_summary.json vs r05c.)
     __hip_atomic_store(part + blockIdx.x, f2ord(m), __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
     asm volatile("s_waitcnt vmcnt(0)" ::: "memory");
-    const int t = __hip_atomic_fetch_add(ticket, 1, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
-    last = t == (int)gridDim.x - 1;
+    const int g = blockIdx.x % YM_STATS_GROUPS, ng = ((int)gridDim.x - g + YM_STATS_GROUPS - 1) / YM_STATS_GROUPS;
+    const int t = __hip_atomic_fetch_add(gticket + 32 * g, 1, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
+    int l = 0;
+    if (t == ng - 1) {  // the group's last block: its count is complete, so every partial of the group is stored
+      __hip_atomic_store(gticket + 32 * g, 0, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
+      const int u = __hip_atomic_fetch_add(ticket, 1, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
+      l = u == min((int)gridDim.x, YM_STATS_GROUPS) - 1;
+    }
+    last = l;
   }
   __syncthreads();
   if (!last) return;
@@ -737,7 +748,7 @@ __global__ __launch_bounds__(256) void attn_psa_mfma(const AttnArgs a) {
 // (hi·hi + lo·hi + hi·lo on v_mfma_f32_16x16x32_f16, fp32 accumulation).  V^T of the (image, head) is staged in LDS
 // as hi and lo planes (the two planes of K as well would not fit beside them), K fragments stream from global
 // (32 bytes = the [hi | lo] pair of one key chunk per lane and key tile; L2-resident), P is split in registers.
-template <int NKT>
+template <int NKT, int KB>
 __global__ __launch_bounds__(256) void attn_psa_x3(const AttnArgs a) {
   extern __shared__ __attribute__((aligned(16))) f16 vt[];  // [2][64][LDV]: V^T hi, lo; then pe weights + bias f32
   constexpr int LDV = 16 * NKT + 4;
@@ -783,10 +794,10 @@ __global__ __launch_bounds__(256) void attn_psa_x3(const AttnArgs a) {
   const HL qf = ym_load_hl(qkv + (img + (q < N ? q : N - 1)) * a.q_ctot + hq + 8 * g);
   // 2. scores S^T = K·Q^T (log2 units): lane (g, c) supplies key 16t + c, logical chunk g of K.  The K fragments
   // of KB key tiles are loaded together (unconditional loads of clamped keys: rows past N only feed scores that are
-  // masked to -inf), then their MFMAs run: NKT / KB memory round trips instead of one per tile
+  // masked to -inf), then their MFMAs run: NKT / KB memory round trips instead of one per tile (KB = NKT: one; the
+  // kernel runs one wave per SIMD, so the registers are there)
   const float sl2 = a.scale * 1.4426950408889634f;
   float s[NKT][4];
-  constexpr int KB = 8;
 #pragma unroll
   for (int t0 = 0; t0 < NKT; t0 += KB) {
     HL kf[KB];
@@ -1715,10 +1726,11 @@ hipError_t ym_launch_input_max(const float* x, long n, float* ctl, float* out, h
 // against setenv and costs time on every eager forward)
 namespace {
 std::atomic<int>* dbg_slots() {
-  static std::atomic<int> v[7] = {};
+  static std::atomic<int> v[8] = {};
   static const bool init = [] {
-    const char* names[7] = {nullptr, "YM_NMS_DBG", "YM_DW_MODE", "YM_DW_TILE", "YM_CHAIN", nullptr, "YM_STEMFUSE"};
-    for (int k = 1; k < 7; ++k) {
+    const char* names[8] = {nullptr, "YM_NMS_DBG", "YM_DW_MODE", "YM_DW_TILE", "YM_CHAIN", nullptr, "YM_STEMFUSE",
+                            "YM_ATTN_KB"};
+    for (int k = 1; k < 8; ++k) {
       if (!names[k]) continue;
       const char* e = getenv(names[k]);
       v[k].store(e ? atoi(e) : 0);
@@ -1730,13 +1742,13 @@ std::atomic<int>* dbg_slots() {
 }
 }  // namespace
 
-int ym_debug_get(int key) { return key > 0 && key < 7 ? dbg_slots()[key].load(std::memory_order_relaxed) : 0; }
+int ym_debug_get(int key) { return key > 0 && key < 8 ? dbg_slots()[key].load(std::memory_order_relaxed) : 0; }
 int ym_debug_set(int key, int value) {
-  if (key <= 0 || key >= 7) return -1;
+  if (key <= 0 || key >= 8) return -1;
   return dbg_slots()[key].exchange(value);
 }
 void ym_debug_add(int key, int d) {
-  if (key > 0 && key < 7) dbg_slots()[key].fetch_add(d);
+  if (key > 0 && key < 8) dbg_slots()[key].fetch_add(d);
 }
 
 hipError_t ym_launch_dwconv(int dtype, const DwArgs& a, hipStream_t st) {
@@ -1860,7 +1872,11 @@ hipError_t launch_attn_flash(const AttnArgs& a, hipStream_t st) {
 template <int NKT>
 hipError_t launch_attn_x3(const AttnArgs& a, hipStream_t st) {
   const size_t lds = (size_t)2 * 64 * (16 * NKT + 4) * sizeof(f16) + 640 * sizeof(float);
-  hipLaunchKernelGGL((attn_psa_x3<NKT>), dim3(a.B * a.nh * ((a.N + 63) / 64)), dim3(256), lds, st, a);
+  const dim3 g(a.B * a.nh * ((a.N + 63) / 64));
+  // K fragments of every key tile in flight at once (up to 26 tiles); YM_DBG_ATTN_KB = 1: 8 tiles per round trip
+  constexpr int KBALL = NKT <= 26 ? NKT : 16;
+  if (ym_debug_get(7) == 1) hipLaunchKernelGGL((attn_psa_x3<NKT, 8>), g, dim3(256), lds, st, a);
+  else hipLaunchKernelGGL((attn_psa_x3<NKT, KBALL>), g, dim3(256), lds, st, a);
   return hipGetLastError();
 }
 

@@ -682,7 +682,7 @@ int ym_num_conv_cfgs(int dtype) {  // public dtype codes (ym_model_desc): 1 f16,
 
 const char* ym_last_error(void) { return g_err.c_str(); }
 int ym_set_debug(int key, int value) {
-  if (key < YM_DBG_NMS || key > YM_DBG_STEMFUSE) return fail(YM_EINVAL, "unknown debug key %d", key);
+  if (key < YM_DBG_NMS || key > YM_DBG_ATTN_KB) return fail(YM_EINVAL, "unknown debug key %d", key);
   return ym_debug_set(key, value);
 }
 
