@@ -204,8 +204,8 @@ int ym_num_conv_cfgs(int dtype);
  * kernel is launched (so at graph capture for replayed forwards): YM_DBG_NMS (9 = the NMS kernel's per-box path
  * instead of the blocked one), YM_DBG_DW_MODE (depthwise variant: 0 LDS tiles, 1 rows, 2 column strips),
  * YM_DBG_DW_TILE (LDS tile shape 0..3), YM_DBG_CHAIN (1: the persistent two-conv chain kernel).
- * The environment variables YM_NMS_DBG, YM_DW_MODE, YM_DW_TILE, YM_CHAIN, YM_STEMFUSE and YM_ATTN_KB set the initial
- * values.  A forward graph
+ * The environment variables YM_NMS_DBG, YM_DW_MODE, YM_DW_TILE, YM_CHAIN, YM_STEMFUSE, YM_ATTN_KB, YM_PAIRST and
+ * YM_CONV_CFG (the last two: the value itself, stored + 1) set the initial values.  A forward graph
  * already captured keeps the kernels it was captured with.
  * Returns the previous value, or YM_EINVAL for an unknown key. */
 #define YM_DBG_NMS 1
@@ -215,6 +215,8 @@ int ym_num_conv_cfgs(int dtype);
 #define YM_DBG_CHAIN_LAUNCHES 5 /* chain kernels launched since it was last set (a counter) */
 #define YM_DBG_STEMFUSE 6 /* 1: x3 stem + model.1 + model.2.cv1 as one launch (csrc/ym_stem_fused.hip); 0: three */
 #define YM_DBG_ATTN_KB 7 /* 1: x3 attention loads K fragments 8 key tiles per round trip; 0: all tiles at once */
+#define YM_DBG_PAIRST 8 /* x3 lane-pair epilogue store family mask + 1 (0: the default mask 21) */
+#define YM_DBG_CONV_CFG 9 /* a forced conv tile configuration id + 1 for untuned ops (0: the heuristic) */
 int ym_set_debug(int key, int value);
 
 #ifdef __cplusplus

@@ -252,19 +252,24 @@ def test_x3_fused_pairs_match_split(scale):
         eng.rt.set_op_cfg(B, H, W, tuned)
 
 
-def test_x3_pair_stores_bitwise_equal(monkeypatch):
-    """The lane-pair epilogue stores (csrc/ym_common.h ym_p2_store4_pair; YM_PAIRST family mask, read at graph
+def test_x3_pair_stores_bitwise_equal():
+    """The lane-pair epilogue stores (csrc/ym_common.h ym_p2_store4_pair; family mask YM_DBG_PAIRST, read at graph
     capture) write the same bits as the per-lane stores: yolo11s B=8 under the committed x3 table with every family's
     pairing off (0), on with the ds_bpermute exchange (15) and on with the v_permlane*_swap exchange (31) — the
     detection rows of all eight images are bitwise equal."""
     from core.model import YOLO11Model
+    from yolomi import lib as L
     x = make_input("uniform", list(range(8)), 640).to(DEV)
     rows = {}
-    for mask in ("0", "15", "31"):
-        monkeypatch.setenv("YM_PAIRST", mask)
-        m = YOLO11Model(task="detect", size="s", device="cuda:0", dtype="x3", verbose=False)
-        rows[mask] = [r.boxes.data.clone() for r in m.predict(x, conf=0.05)]
-        del m
+    prev = L.set_debug(L.DBG_PAIRST, 0)
+    try:
+        for mask in ("0", "15", "31"):
+            L.set_debug(L.DBG_PAIRST, int(mask) + 1)
+            m = YOLO11Model(task="detect", size="s", device="cuda:0", dtype="x3", verbose=False)
+            rows[mask] = [r.boxes.data.clone() for r in m.predict(x, conf=0.05)]
+            del m
+    finally:
+        L.set_debug(L.DBG_PAIRST, prev)
     assert sum(len(r) for r in rows["0"]) > 100
     for mask in ("15", "31"):
         for a, b in zip(rows["0"], rows[mask]):

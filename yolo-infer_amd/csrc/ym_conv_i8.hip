@@ -284,11 +284,8 @@ hipError_t launch_id(int id, const ConvArgs& a, int kind, hipStream_t st, bool f
 }
 
 int choose_cfg(const ConvArgs& a) {
-  const char* env = getenv("YM_CONV_CFG");
-  if (env && *env) {
-    const int id = atoi(env);
-    if (id >= 0 && id < kNumCfg) return id;
-  }
+  const int id = ym_debug_get(9) - 1;  // YM_DBG_CONV_CFG (value + 1): a forced tile configuration (tools/tune)
+  if (id >= 0 && id < kNumCfg) return id;
   const long M = a.M, N = a.N;
   const int steps = a.Kpad / KSTEP;
   auto waves = [&](int id) {

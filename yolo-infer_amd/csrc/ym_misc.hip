@@ -1725,15 +1725,17 @@ hipError_t ym_launch_input_max(const float* x, long n, float* ctl, float* out, h
 // the setter — a launch reads an atomic instead of calling getenv (getenv per launch is not thread-safe
 // against setenv and costs time on every eager forward)
 namespace {
+constexpr int kDbgKeys = 10;  // include/yolomi.h YM_DBG_* keys 1..9
 std::atomic<int>* dbg_slots() {
-  static std::atomic<int> v[8] = {};
+  static std::atomic<int> v[kDbgKeys] = {};
   static const bool init = [] {
-    const char* names[8] = {nullptr, "YM_NMS_DBG", "YM_DW_MODE", "YM_DW_TILE", "YM_CHAIN", nullptr, "YM_STEMFUSE",
-                            "YM_ATTN_KB"};
-    for (int k = 1; k < 8; ++k) {
+    const char* names[kDbgKeys] = {nullptr,       "YM_NMS_DBG", "YM_DW_MODE", "YM_DW_TILE", "YM_CHAIN",
+                                   nullptr,       "YM_STEMFUSE", "YM_ATTN_KB", "YM_PAIRST", "YM_CONV_CFG"};
+    for (int k = 1; k < kDbgKeys; ++k) {
       if (!names[k]) continue;
       const char* e = getenv(names[k]);
-      v[k].store(e ? atoi(e) : 0);
+      // keys 8, 9 hold value + 1 (0: unset — the pair-store default mask, no forced tile configuration)
+      v[k].store(e && *e ? atoi(e) + (k >= 8 ? 1 : 0) : 0);
     }
     return true;
   }();
@@ -1742,13 +1744,13 @@ std::atomic<int>* dbg_slots() {
 }
 }  // namespace
 
-int ym_debug_get(int key) { return key > 0 && key < 8 ? dbg_slots()[key].load(std::memory_order_relaxed) : 0; }
+int ym_debug_get(int key) { return key > 0 && key < kDbgKeys ? dbg_slots()[key].load(std::memory_order_relaxed) : 0; }
 int ym_debug_set(int key, int value) {
-  if (key <= 0 || key >= 8) return -1;
+  if (key <= 0 || key >= kDbgKeys) return -1;
   return dbg_slots()[key].exchange(value);
 }
 void ym_debug_add(int key, int d) {
-  if (key > 0 && key < 8) dbg_slots()[key].fetch_add(d);
+  if (key > 0 && key < kDbgKeys) dbg_slots()[key].fetch_add(d);
 }
 
 hipError_t ym_launch_dwconv(int dtype, const DwArgs& a, hipStream_t st) {

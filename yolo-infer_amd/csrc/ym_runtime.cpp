@@ -365,8 +365,8 @@ int conv_args(ym_ctx* c, const Op& op, int B, const float* d_in, float in_eps, C
       const int32_t* r = op.r;
       a = ConvArgs{};
       a.wsc = a.wsc2 = 1.0f;
-      const char* pst = getenv("YM_PAIRST");  // read at every capture: an A/B or test may switch it in one process
-      a.pst = pst ? atoi(pst) : 21;
+      const int pst = ym_debug_get(YM_DBG_PAIRST);  // (value + 1; 0: the default family mask 21)
+      a.pst = pst ? pst - 1 : 21;
       const int k = r[1], s = r[2], cin = r[3], cout = r[4];
       const int b0 = r[6], b1 = r[10], bd = r[13], br = r[17];
       const int up0 = r[9];
@@ -682,7 +682,7 @@ int ym_num_conv_cfgs(int dtype) {  // public dtype codes (ym_model_desc): 1 f16,
 
 const char* ym_last_error(void) { return g_err.c_str(); }
 int ym_set_debug(int key, int value) {
-  if (key < YM_DBG_NMS || key > YM_DBG_ATTN_KB) return fail(YM_EINVAL, "unknown debug key %d", key);
+  if (key < YM_DBG_NMS || key > YM_DBG_CONV_CFG) return fail(YM_EINVAL, "unknown debug key %d", key);
   return ym_debug_set(key, value);
 }
 

@@ -98,7 +98,8 @@ EXPORTED = ("ym_create", "ym_load_weights", "ym_broadcast_weights", "ym_broadcas
             "ym_num_buffers", "ym_buffer_info", "ym_read_buffer", "ym_sync", "ym_last_error", "ym_destroy",
             "ym_version", "ym_num_conv_cfgs", "ym_set_debug")
 
-DBG_NMS, DBG_DW_MODE, DBG_DW_TILE, DBG_CHAIN, DBG_CHAIN_LAUNCHES, DBG_STEMFUSE, DBG_ATTN_KB = 1, 2, 3, 4, 5, 6, 7  # ym_set_debug keys (include/yolomi.h)
+DBG_NMS, DBG_DW_MODE, DBG_DW_TILE, DBG_CHAIN, DBG_CHAIN_LAUNCHES, DBG_STEMFUSE, DBG_ATTN_KB = 1, 2, 3, 4, 5, 6, 7
+DBG_PAIRST, DBG_CONV_CFG = 8, 9  # value + 1 (0: default)  # ym_set_debug keys (include/yolomi.h)
 
 
 def set_debug(key: int, value: int) -> int:

@@ -1,4 +1,4 @@
-"""Sweep the conv tile configurations (env YM_CONV_CFG) and report per-layer device time for each.
+"""Sweep the conv tile configurations (ym_set_debug YM_DBG_CONV_CFG) and report per-layer device time for each.
 
     python -m yolomi.tune --model n --batch 8
 """
@@ -21,6 +21,7 @@ def main(argv=None):
     ap.add_argument("--reps", type=int, default=5)
     a = ap.parse_args(argv)
     os.environ["YM_AUTOTUNE"] = "0"
+    from . import lib as L
     from .engine import Engine
     from .synth import synth_weights, uniform
     dev = torch.device("cuda", 0)
@@ -30,13 +31,13 @@ def main(argv=None):
     cfgs = [int(c) for c in a.cfgs.split(",")]
     res = {}
     for c in [-1] + cfgs:
-        os.environ["YM_CONV_CFG"] = "" if c < 0 else str(c)
+        L.set_debug(L.DBG_CONV_CFG, c + 1)  # (value + 1; 0: the heuristic)
         eng.profile(x)
         t = np.zeros(len(eng.graph.ops))
         for _ in range(a.reps):
             t += np.array(eng.profile(x))
         res[c] = t / a.reps
-    os.environ["YM_CONV_CFG"] = ""
+    L.set_debug(L.DBG_CONV_CFG, 0)
     conv = [i for i, op in enumerate(eng.graph.ops) if op.kind == "conv"]
     print("op | M N K | heuristic " + " ".join(f"c{c:>5}" for c in cfgs) + " | best")
     best_sum, heur_sum = 0.0, 0.0
