@@ -274,3 +274,21 @@ def test_x3_pair_stores_bitwise_equal():
     for mask in ("15", "31"):
         for a, b in zip(rows["0"], rows[mask]):
             assert a.shape == b.shape and torch.equal(a, b), f"YM_PAIRST={mask}: detections differ from the per-lane stores"
+
+
+def test_x3_literal_bar_on_the_bench_batch():
+    """The literal north-star bar (BASELINE.json: 1e-3 on coordinates and scores, class exact, against the fp32 CPU
+    oracle — no float64 slack) on the very batch `bench.py` times and reports (`synthetic_batch(8, 640, 1000)`,
+    yolo11s x3 under the committed B=8 table), through bench.py's own `parity()`.  The bar is met on this batch
+    (8.7e-4 px) but not on every batch, since the fp32 oracle is itself up to 8e-4 px from float64: this
+    test gates the figure the bench line reports, so a table or kernel change that moves it past 1e-3 fails here."""
+    import bench
+    from core.model import YOLO11Model
+    torch.set_num_threads(min(16, os.cpu_count() or 1))
+    x = bench.synthetic_batch(8, 640, 1000, DEV)
+    m = YOLO11Model(task="detect", size="s", device="cuda:0", dtype="x3", verbose=False)
+    gdets = [r.boxes.data.cpu().numpy() for r in m.predict(x)]
+    om = OracleModel("s", "detect", synth_weights("s", "detect", 0))
+    gts = [r["boxes"].numpy() for r in om.predict(x.cpu())]
+    p = bench.parity(gdets, gts)
+    assert p["matched"] > 100 and p["meets_tolerance"], p
