@@ -176,8 +176,10 @@ def conv_roofline(model, x, dtype, workload, reps=20):
         "traffic_note": (f"HBM-side bytes per forward of all conv launches (PMC FETCH_SIZE x2 + WRITE_SIZE, {tsrc}); "
                          f"algorithmic bytes per forward {int(by)}") if traffic else "no PMC summary for this workload",
         "kernel": "conv implicit GEMM (%s): all %d conv launches of one lane's forward (%d images), aggregated%s"
-                  % ({"i8": "conv_i8, v_mfma_i32_32x32x32_i8", "f8": "conv_i8<fp8>, v_mfma_f32_32x32x16_fp8_fp8 (accumulation restated in oracle/quant.py)",
-                      "x3": "conv_igemm/conv_lds<x3>, 3x v_mfma_f32_32x32x16_f16 per K chunk"}.get(
+                  % ({"i8": "conv_i8 + conv_dma<Q8> (LDS-DMA), v_mfma_i32_32x32x32_i8",
+                      "f8": "conv_i8<fp8>, v_mfma_f32_32x32x16_fp8_fp8 (accumulation restated in oracle/quant.py)",
+                      "x3": "conv_dma (LDS-DMA ring) / conv_stream / conv_bneck / conv_dwpw on the x3 pair layout, "
+                            "3x v_mfma_f32_32x32x16_f16 per K chunk"}.get(
                       dtype, "conv_stream/conv_small/conv_dma/conv_lds/conv_bneck/conv_halo/conv_igemm"), len(conv),
                      Bl, "; int8 ops counted as FLOPs" if dtype == "i8" else ""),
         "timing": f"isolated replay: HIP events around a graph of {reps} back-to-back launches per op, on the launch "
